@@ -1,0 +1,623 @@
+// All-reduce: op orchestration (master consensus) + pipelined ring reduce-scatter/all-gather over multiplexed TCP.
+//
+// Algorithm (reference ccoip/src/cpp/reduce.cpp:528-784): chunk r = [r*base + min(r, rem), ...), ws-1 reduce-scatter
+// steps sending chunk (rank - step) and accumulating chunk (rank - step - 1), then ws-1 all-gather steps forwarding the
+// owned chunk. With quantization the owner quantizes its finished chunk once, overwrites its own copy with
+// D(Q(x)) (so every peer ends bit-identical), and received quantized chunks are forwarded verbatim.
+//
+// Two implementations of the same wire protocol:
+//  * host ring: buffers in host memory; frames are received straight into the destination (all-gather) or a pooled
+//    receive buffer (reduce-scatter); arrived elements are reduced while the rest of the chunk is still in flight.
+//  * device ring: buffers in HBM. The chunk to send is copied to pinned host memory in pieces on a HIP stream and
+//    each piece is sent as soon as its event completes; received bytes land in pinned memory and HIP kernels reduce /
+//    de-quantize them straight from pinned memory into HBM (zero-copy over PCIe), overlapped with the socket.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "../common/log.hpp"
+#include "../kernels/host_kernels.hpp"
+#include "client.hpp"
+#include "ipc.hpp"
+#include "pools.hpp"
+
+namespace pccl::client {
+
+using namespace proto;
+using namespace std::chrono_literals;
+
+BufferPool &host_pool() {
+    static BufferPool p(BufferPool::Kind::Host);
+    return p;
+}
+BufferPool &pinned_pool() {
+    static BufferPool p(BufferPool::Kind::Pinned);
+    return p;
+}
+BufferPool &device_pool() {
+    static BufferPool p(BufferPool::Kind::Device);
+    return p;
+}
+
+static std::vector<std::pair<size_t, size_t>> chunk_bounds(size_t total, size_t ws) {
+    std::vector<std::pair<size_t, size_t>> b(ws);
+    const size_t base = total / ws, rem = total % ws;
+    size_t cur = 0;
+    for (size_t r = 0; r < ws; ++r) {
+        const size_t n = base + (r < rem ? 1 : 0);
+        b[r] = {cur, cur + n};
+        cur += n;
+    }
+    return b;
+}
+
+bool Client::abort_received(uint64_t tag) {
+    auto p = master_.receive<M2CCollectiveCommsAbort>([tag](const M2CCollectiveCommsAbort &a) { return a.tag == tag; },
+                                                       0ms);
+    return p.has_value();
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// op orchestration
+// ------------------------------------------------------------------------------------------------------------------
+bool Client::all_reduce_async(const ReduceRequest &req) {
+    if (!accepted_) return false;
+    std::shared_ptr<OpState> op;
+    {
+        std::lock_guard lock(ops_mtx_);
+        auto it = ops_.find(req.tag);
+        if (it != ops_.end()) {
+            if (!it->second->done.load()) return false; // tag in use
+            if (it->second->thread.joinable()) it->second->thread.join();
+            ops_.erase(it);
+        }
+        op = std::make_shared<OpState>();
+        op->req = req;
+        op->revision_at_start = conn_revision_.load();
+        ops_[req.tag] = op;
+    }
+    op->thread = std::thread([this, op] { run_op(op); });
+    return true;
+}
+
+void Client::run_op(const std::shared_ptr<OpState> &op) {
+    const uint64_t tag = op->req.tag;
+    bool success = false, abort_seen = false;
+    uint64_t seq = 0;
+    bool commenced = false;
+    {
+        C2MCollectiveCommsInitiate init;
+        init.tag = tag;
+        init.count = op->req.count;
+        init.data_type = op->req.dtype;
+        init.op = op->req.op;
+        if (master_.send(init)) {
+            auto c = master_.receive<M2CCollectiveCommsCommence>(
+                [tag](const M2CCollectiveCommsCommence &p) { return p.tag == tag; });
+            if (c) {
+                seq = c->seq_nr;
+                commenced = true;
+            }
+        }
+    }
+    if (commenced) {
+        auto rv = ring_view(seq);
+        if (rv && rv->ring.size() >= 2) {
+            op->world = static_cast<uint32_t>(rv->ring.size());
+            // classify buffers
+            DevPtrInfo si{}, di{};
+            DeviceBackend *be = device_backend();
+            if (be) {
+                be->pointer_info(op->req.src, si);
+                be->pointer_info(op->req.dst, di);
+            }
+            const bool device = si.is_device && di.is_device && si.device == di.device;
+            std::pair<bool, bool> r{false, false};
+            bool done = false;
+            if (rv->arena) {
+                // every peer of an intra-node ring votes; the xGMI path runs only if all buffers are on GPUs
+                const int decision = rv->arena->vote(*this, *op, seq, device, device ? di.device : -1);
+                if (decision == IpcArena::kUseIpc) {
+                    r = ipc_reduce(*op, *rv, seq, di.device);
+                    done = true;
+                    if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceIpc);
+                } else if (decision == IpcArena::kAborted) {
+                    r = {false, abort_received(tag)};
+                    done = true;
+                }
+            }
+            if (!done) {
+                if (device) {
+                    r = ring_reduce_device(*op, *rv, seq, di.device);
+                    if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceRing);
+                } else if (!si.is_device && !di.is_device) {
+                    r = ring_reduce_host(*op, *rv, seq);
+                    if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::HostRing);
+                } else {
+                    LOG(ERR) << "all-reduce: send and receive buffers must both be host or both be on one GPU";
+                    r = {false, false};
+                }
+            }
+            success = r.first && !r.second;
+            abort_seen = r.second;
+        } else {
+            LOG(WARN) << "all-reduce tag " << tag << ": no usable ring (peers lost)";
+        }
+    }
+    // completion protocol: exactly one Abort(tag) packet per op, then Complete(tag)
+    bool ok = false;
+    if (commenced) {
+        C2MCollectiveCommsComplete comp;
+        comp.tag = tag;
+        comp.was_aborted = !success;
+        if (master_.send(comp)) {
+            bool aborted = abort_seen;
+            bool got_abort = abort_seen;
+            if (!got_abort) {
+                auto a = master_.receive<M2CCollectiveCommsAbort>(
+                    [tag](const M2CCollectiveCommsAbort &p) { return p.tag == tag; });
+                if (a) {
+                    got_abort = true;
+                    aborted = a->aborted;
+                }
+            }
+            auto c = master_.receive<M2CCollectiveCommsComplete>(
+                [tag](const M2CCollectiveCommsComplete &p) { return p.tag == tag; });
+            ok = got_abort && c.has_value() && !aborted && success;
+        }
+    }
+    if (!ok) LOG(WARN) << "all-reduce tag " << tag << " failed/aborted";
+    op->success = ok;
+    op->done.store(true);
+}
+
+bool Client::join_async_reduce(uint64_t tag) {
+    std::shared_ptr<OpState> op;
+    {
+        std::lock_guard lock(ops_mtx_);
+        auto it = ops_.find(tag);
+        if (it == ops_.end()) return false;
+        op = it->second;
+    }
+    if (op->thread.joinable() && op->thread.get_id() != std::this_thread::get_id()) op->thread.join();
+    if (!op->success) {
+        // Re-establish the ring once per connection revision: every peer sees the same failures, so every peer
+        // performs exactly one establishment round (several concurrent failed ops must not cascade into more).
+        // Ops still in flight keep this peer in the master's COLLECTIVE_COMMUNICATIONS_RUNNING state, where an
+        // establish vote is illegal; the last failed op to be joined performs the round instead.
+        std::lock_guard lock(establish_mtx_);
+        if (conn_revision_.load() == op->revision_at_start && !interrupted_ && !any_collective_running()) {
+            if (!request_and_establish_locked(false)) LOG(ERR) << "Failed to re-establish P2P connections after abort";
+        }
+        return false;
+    }
+    return true;
+}
+
+bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {
+    std::lock_guard lock(ops_mtx_);
+    auto it = ops_.find(tag);
+    if (it == ops_.end() || it->second->info_taken) return false;
+    out.world_size = it->second->world;
+    out.tx_bytes = it->second->tx.load();
+    out.rx_bytes = it->second->rx.load();
+    it->second->info_taken = true;
+    if (it->second->done.load()) {
+        if (it->second->thread.joinable()) it->second->thread.join();
+        ops_.erase(it);
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// shared step machinery
+// ------------------------------------------------------------------------------------------------------------------
+namespace {
+
+struct StepIo {
+    net::MuxConn *tx;
+    net::MuxConn *rx;
+    uint64_t tag;
+    uint64_t seq;
+};
+
+constexpr size_t kMetaFrameOverhead = 24;
+
+// Exchanges dequantization metadata for one step. Returns 0 ok, 1 io failure, 2 abort.
+int exchange_meta(Client *self, const StepIo &io, const QuantMeta &mine, QuantMeta &theirs, std::atomic<uint64_t> &tx,
+                  std::atomic<uint64_t> &rx, const std::function<bool()> &aborted) {
+    P2PDequantizationMeta pkt;
+    pkt.tag = io.tag;
+    pkt.meta = mine;
+    auto bytes = encode_with_id(pkt);
+    if (!io.tx->send_frame(io.tag, io.seq, bytes.data(), bytes.size())) return 1;
+    tx += bytes.size() + kMetaFrameOverhead;
+    while (true) {
+        auto m = io.rx->recv_packet<P2PDequantizationMeta>(io.tag, io.seq, 20ms);
+        if (m) {
+            theirs = m->meta;
+            rx += encode_with_id(*m).size() + kMetaFrameOverhead;
+            return 0;
+        }
+        if (!io.rx->is_open()) return 1;
+        if (aborted()) return 2;
+    }
+    (void)self;
+}
+
+} // namespace
+
+// ------------------------------------------------------------------------------------------------------------------
+// host ring
+// ------------------------------------------------------------------------------------------------------------------
+std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq) {
+    const ReduceRequest &q = op.req;
+    const size_t ws = rv.ring.size(), rank = rv.rank;
+    const size_t es = dtype_size(q.dtype);
+    const bool quant = q.qalgo != QuantAlgo::None && q.qtype != q.dtype;
+    const size_t qs = quant ? dtype_size(q.qtype) : es;
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    const size_t chunk = net::multiplex_chunk_size();
+
+    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
+    auto aborted = [&] { return abort_received(q.tag); };
+
+    Lease backup;
+    if (q.src == q.dst) {
+        backup = Lease(host_pool(), bytes);
+        std::memcpy(backup.data(), q.src, bytes);
+    } else {
+        std::memcpy(dst, q.src, bytes);
+    }
+    auto restore = [&] {
+        if (q.src == q.dst) std::memcpy(dst, backup.data(), bytes);
+    };
+
+    const auto bounds = chunk_bounds(q.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    Lease rbuf(host_pool(), max_chunk * qs + 64);
+    Lease qbuf;
+    if (quant) qbuf = Lease(host_pool(), max_chunk * qs + 64);
+
+    // Runs one full-duplex step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)` for
+    // newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
+    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
+                        const std::function<void(size_t, size_t)> &consume) -> int {
+        io.rx->post_sink(q.tag, seq, sink, rx_bytes);
+        size_t sent = 0, done_el = 0;
+        const size_t rx_el = rx_bytes / qs;
+        auto drain = [&](size_t have) {
+            const size_t el = have / qs;
+            if (el > done_el) {
+                consume(done_el, el);
+                done_el = el;
+            }
+        };
+        while (sent < tx_bytes) {
+            const size_t n = std::min(chunk, tx_bytes - sent);
+            if (!io.tx->send_frame(q.tag, seq, payload + sent, n)) {
+                io.rx->remove_sink(q.tag);
+                return 1;
+            }
+            sent += n;
+            op.tx += n;
+            drain(io.rx->sink_progress(q.tag));
+        }
+        size_t idle = 0;
+        while (done_el < rx_el) {
+            const size_t have = io.rx->wait_sink(q.tag, rx_bytes, 20ms);
+            const size_t before = done_el;
+            drain(have);
+            if (done_el != before) {
+                idle = 0;
+                continue;
+            }
+            if (!io.rx->is_open()) {
+                io.rx->remove_sink(q.tag);
+                return 1;
+            }
+            if (++idle % 2 == 0 && aborted()) {
+                io.rx->remove_sink(q.tag);
+                return 2;
+            }
+        }
+        op.rx += rx_bytes;
+        io.rx->remove_sink(q.tag);
+        return 0;
+    };
+    auto fail = [&](int code) -> std::pair<bool, bool> {
+        restore();
+        return {code == 2, code == 2};
+    };
+
+    // ---- reduce-scatter
+    for (size_t step = 0; step + 1 < ws; ++step) {
+        const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
+        const auto [ts, te] = bounds[tx_idx];
+        const auto [rs, re] = bounds[rx_idx];
+        const uint8_t *payload = dst + ts * es;
+        QuantMeta mine, theirs;
+        if (quant) {
+            if (te > ts) mine = kernels::host_quantize(qbuf.data(), dst + ts * es, te - ts, q.dtype, q.qtype, q.qalgo);
+            else mine = kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
+            payload = qbuf.data();
+            if (int rc = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(rc);
+        }
+        uint8_t *rx_region = dst + rs * es;
+        const int rc = run_step(payload, (te - ts) * qs, rbuf.data(), (re - rs) * qs, [&](size_t a, size_t b) {
+            if (quant)
+                kernels::host_dequant_reduce(rx_region + a * es, rbuf.data() + a * qs, b - a, q.dtype, q.qtype, q.op, theirs);
+            else
+                kernels::host_reduce(rx_region + a * es, rbuf.data() + a * es, b - a, q.dtype, q.op);
+        });
+        if (rc) return fail(rc);
+    }
+
+    // ---- all-gather
+    Lease ag[2];
+    if (quant) {
+        ag[0] = Lease(host_pool(), max_chunk * qs + 64);
+        ag[1] = Lease(host_pool(), max_chunk * qs + 64);
+    }
+    QuantMeta prev_meta;
+    size_t cur = (rank + 1) % ws;
+    for (size_t step = 0; step + 1 < ws; ++step) {
+        const size_t inc = (cur + ws - 1) % ws;
+        const auto [ts, te] = bounds[cur];
+        const auto [rs, re] = bounds[inc];
+        uint8_t *rx_region = dst + rs * es;
+        int rc;
+        if (quant) {
+            QuantMeta mine, theirs;
+            const uint8_t *payload;
+            if (step == 0) {
+                if (te > ts) {
+                    mine = kernels::host_quantize(qbuf.data(), dst + ts * es, te - ts, q.dtype, q.qtype, q.qalgo);
+                    // parity: our own copy becomes exactly what the other peers will de-quantize
+                    kernels::host_dequant_reduce(dst + ts * es, qbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set, mine);
+                } else {
+                    mine = kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
+                }
+                payload = qbuf.data();
+            } else {
+                mine = prev_meta;
+                payload = ag[(step - 1) % 2].data();
+            }
+            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
+            uint8_t *sink = ag[step % 2].data();
+            rc = run_step(payload, (te - ts) * qs, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+                kernels::host_dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, theirs);
+            });
+            prev_meta = theirs;
+        } else {
+            rc = run_step(dst + ts * es, (te - ts) * es, rx_region, (re - rs) * es, [](size_t, size_t) {});
+        }
+        if (rc) return fail(rc);
+        cur = inc;
+    }
+    if (q.op == ReduceOp::Avg) kernels::host_finalize_avg(dst, q.count, q.dtype, ws);
+    return {true, false};
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// device ring (HBM buffers, pinned staging, HIP kernels)
+// ------------------------------------------------------------------------------------------------------------------
+std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    DeviceBackend *be = device_backend();
+    const ReduceRequest &q = op.req;
+    const size_t ws = rv.ring.size(), rank = rv.rank;
+    const size_t es = dtype_size(q.dtype);
+    const bool quant = q.qalgo != QuantAlgo::None && q.qtype != q.dtype;
+    const size_t qs = quant ? dtype_size(q.qtype) : es;
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    const size_t chunk = net::multiplex_chunk_size();
+    const size_t piece = std::max<size_t>(1 << 20, std::min(chunk, env_size("PCCL_DEVICE_PIECE_BYTES", 4u << 20)));
+
+    be->set_device(device);
+    DevStream st = be->create_stream();
+    if (!st) return {false, false};
+    struct StreamGuard {
+        DeviceBackend *be;
+        DevStream s;
+        ~StreamGuard() { be->destroy_stream(s); }
+    } sg{be, st};
+
+    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
+    auto aborted = [&] { return abort_received(q.tag); };
+
+    Lease backup;
+    if (q.src == q.dst) {
+        backup = Lease(device_pool(), bytes, device);
+        if (!backup.ok()) return {false, false};
+        be->memcpy_async(backup.data(), q.src, bytes, st);
+    } else {
+        be->memcpy_async(dst, q.src, bytes, st);
+    }
+    auto restore = [&] {
+        be->stream_sync(st);
+        if (q.src == q.dst) {
+            be->memcpy_async(dst, backup.data(), bytes, st);
+            be->stream_sync(st);
+        }
+    };
+
+    const auto bounds = chunk_bounds(q.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t stage_bytes = max_chunk * std::max(qs, es) + 64;
+    Lease txbuf(pinned_pool(), stage_bytes), rxa(pinned_pool(), stage_bytes), rxb(pinned_pool(), stage_bytes);
+    Lease mm(pinned_pool(), 64);
+    if (!txbuf.ok() || !rxa.ok() || !rxb.ok() || !mm.ok()) return {false, false};
+    uint8_t *rxbuf[2] = {rxa.data(), rxb.data()};
+    auto *minmax_out = reinterpret_cast<double *>(mm.data());
+
+    std::vector<DevEvent> events;
+    auto ev = [&](size_t i) {
+        while (events.size() <= i) events.push_back(be->create_event());
+        return events[i];
+    };
+    struct EvGuard {
+        DeviceBackend *be;
+        std::vector<DevEvent> *e;
+        ~EvGuard() {
+            for (auto x : *e) be->destroy_event(x);
+        }
+    } eg{be, &events};
+
+    // quantize `n` elements at device `src` into pinned txbuf; returns meta
+    auto quantize_to_pinned = [&](const uint8_t *src, size_t n) -> QuantMeta {
+        if (n == 0) return kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
+        be->minmax(src, n, q.dtype, minmax_out, st);
+        be->stream_sync(st);
+        QuantMeta m = kernels::make_meta(q.qalgo, q.dtype, q.qtype, minmax_out[0], minmax_out[1]);
+        be->quantize(txbuf.data(), src, n, q.dtype, q.qtype, kernels::make_params(m, q.qtype), st);
+        be->stream_sync(st);
+        return m;
+    };
+
+    // one full-duplex step. `tx_ready(piece_idx)` blocks until that piece of the payload may be sent.
+    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
+                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume) -> int {
+        io.rx->post_sink(q.tag, seq, sink, rx_bytes);
+        size_t sent = 0, done_el = 0, k = 0;
+        const size_t rx_el = rx_bytes / qs;
+        auto drain = [&](size_t have) {
+            const size_t el = have / qs;
+            if (el > done_el) {
+                consume(done_el, el);
+                done_el = el;
+            }
+        };
+        while (sent < tx_bytes) {
+            const size_t n = std::min(piece, tx_bytes - sent);
+            if (!tx_ready(k++)) {
+                io.rx->remove_sink(q.tag);
+                return 1;
+            }
+            if (!io.tx->send_frame(q.tag, seq, payload + sent, n)) {
+                io.rx->remove_sink(q.tag);
+                return 1;
+            }
+            sent += n;
+            op.tx += n;
+            drain(io.rx->sink_progress(q.tag));
+        }
+        size_t idle = 0;
+        while (done_el < rx_el) {
+            const size_t have = io.rx->wait_sink(q.tag, rx_bytes, 20ms);
+            const size_t before = done_el;
+            drain(have);
+            if (done_el != before) {
+                idle = 0;
+                continue;
+            }
+            if (!io.rx->is_open()) {
+                io.rx->remove_sink(q.tag);
+                return 1;
+            }
+            if (++idle % 2 == 0 && aborted()) {
+                io.rx->remove_sink(q.tag);
+                return 2;
+            }
+        }
+        op.rx += rx_bytes;
+        io.rx->remove_sink(q.tag);
+        be->stream_sync(st); // everything consumed from `sink` has landed in HBM
+        return 0;
+    };
+    auto always_ready = [](size_t) { return true; };
+    // stage device bytes to pinned txbuf in pieces; tx_ready waits for the piece's event
+    auto stage_d2h = [&](const uint8_t *src, size_t n) {
+        size_t k = 0;
+        for (size_t off = 0; off < n; off += piece, ++k) {
+            be->memcpy_async(txbuf.data() + off, src + off, std::min(piece, n - off), st);
+            be->event_record(ev(k), st);
+        }
+    };
+    auto d2h_ready = [&](size_t k) { return be->event_sync(ev(k)); };
+    auto fail = [&](int code) -> std::pair<bool, bool> {
+        restore();
+        return {code == 2, code == 2};
+    };
+
+    // ---- reduce-scatter
+    for (size_t step = 0; step + 1 < ws; ++step) {
+        const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
+        const auto [ts, te] = bounds[tx_idx];
+        const auto [rs, re] = bounds[rx_idx];
+        uint8_t *rx_region = dst + rs * es;
+        uint8_t *sink = rxbuf[step % 2];
+        int rc;
+        if (quant) {
+            QuantMeta theirs;
+            const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts);
+            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
+            const auto params = kernels::make_params(theirs, q.qtype);
+            rc = run_step(txbuf.data(), (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+                be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, q.op, params, st);
+            });
+        } else {
+            stage_d2h(dst + ts * es, (te - ts) * es);
+            rc = run_step(txbuf.data(), (te - ts) * es, d2h_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
+                be->reduce(rx_region + a * es, sink + a * es, b - a, q.dtype, q.op, st);
+            });
+        }
+        if (rc) return fail(rc);
+    }
+
+    // ---- all-gather
+    QuantMeta prev_meta;
+    size_t cur = (rank + 1) % ws;
+    for (size_t step = 0; step + 1 < ws; ++step) {
+        const size_t inc = (cur + ws - 1) % ws;
+        const auto [ts, te] = bounds[cur];
+        const auto [rs, re] = bounds[inc];
+        uint8_t *rx_region = dst + rs * es;
+        uint8_t *sink = rxbuf[step % 2];
+        const uint8_t *payload;
+        int rc;
+        if (quant) {
+            QuantMeta mine, theirs;
+            if (step == 0) {
+                mine = quantize_to_pinned(dst + ts * es, te - ts);
+                if (te > ts) { // parity: own chunk := D(Q(x))
+                    be->dequant_reduce(dst + ts * es, txbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set,
+                                       kernels::make_params(mine, q.qtype), st);
+                }
+                payload = txbuf.data();
+            } else {
+                mine = prev_meta;
+                payload = rxbuf[(step - 1) % 2];
+            }
+            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
+            const auto params = kernels::make_params(theirs, q.qtype);
+            rc = run_step(payload, (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+                be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, params, st);
+            });
+            prev_meta = theirs;
+        } else {
+            if (step == 0) {
+                stage_d2h(dst + ts * es, (te - ts) * es);
+                payload = txbuf.data();
+                rc = run_step(payload, (te - ts) * es, d2h_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
+                    be->memcpy_async(rx_region + a * es, sink + a * es, (b - a) * es, st);
+                });
+            } else {
+                payload = rxbuf[(step - 1) % 2]; // forward what we received last step, verbatim from pinned memory
+                rc = run_step(payload, (te - ts) * es, always_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
+                    be->memcpy_async(rx_region + a * es, sink + a * es, (b - a) * es, st);
+                });
+            }
+        }
+        if (rc) return fail(rc);
+        cur = inc;
+    }
+    if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
+    if (!be->stream_sync(st)) return {false, false};
+    return {true, false};
+}
+
+} // namespace pccl::client

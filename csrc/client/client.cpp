@@ -1,0 +1,466 @@
+#include "client.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <csignal>
+#include <cstring>
+#include <list>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include "../common/log.hpp"
+#include "../net/socket.hpp"
+#include "benchmark.hpp"
+#include "ipc.hpp"
+
+namespace pccl::client {
+
+using namespace proto;
+using namespace std::chrono_literals;
+
+Client::Client(const ClientConfig &cfg) : cfg_(cfg), master_(cfg.master) { std::signal(SIGPIPE, SIG_IGN); }
+
+Client::~Client() {
+    interrupt();
+    join();
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// listeners
+// ------------------------------------------------------------------------------------------------------------------
+bool Client::start_listeners() {
+    const auto proto = cfg_.master.inet.protocol;
+    p2p_listener_ = std::make_unique<net::Listener>(proto, cfg_.p2p_port);
+    ss_listener_ = std::make_unique<net::Listener>(proto, cfg_.ss_port);
+    bm_listener_ = std::make_unique<net::Listener>(proto, cfg_.bm_port);
+    if (!p2p_listener_->listen() || !ss_listener_->listen() || !bm_listener_->listen()) {
+        LOG(ERR) << "Failed to bind peer listeners";
+        return false;
+    }
+    p2p_listener_->run_async([this](int fd, const SockAddr &a) { on_p2p_accept(fd, a); });
+    ss_listener_->run_async([this](int fd, const SockAddr &a) { on_ss_accept(fd, a); });
+    bm_listener_->run_async([this](int fd, const SockAddr &a) { on_bm_accept(fd, a); });
+    LOG(INFO) << "Peer listening: p2p " << p2p_listener_->port() << ", shared state " << ss_listener_->port()
+              << ", benchmark " << bm_listener_->port();
+    return true;
+}
+
+void Client::on_p2p_accept(int fd, const SockAddr &peer) {
+    timeval tv{10, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    auto hello = net::recv_packet<P2PHello>(fd);
+    if (!hello) {
+        LOG(WARN) << "P2P: no hello from " << sockaddr_str(peer);
+        ::close(fd);
+        return;
+    }
+    timeval none{0, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+    auto conn = std::make_shared<net::MuxConn>(fd, net::MuxConn::Mode::Rx, peer);
+    conn->start();
+    {
+        std::lock_guard lock(p2p_mtx_);
+        auto &pool = rx_[hello->peer_uuid];
+        if (pool.size() <= hello->connection_nr) pool.resize(hello->connection_nr + 1);
+        if (pool[hello->connection_nr]) pool[hello->connection_nr]->interrupt();
+        pool[hello->connection_nr] = conn;
+    }
+    // ack only after the RX side is registered: an op may use it as soon as the connector reports success
+    if (!net::send_packet(fd, P2PHelloAck{})) {
+        LOG(WARN) << "P2P: failed to ack " << sockaddr_str(peer);
+        conn->interrupt();
+        return;
+    }
+    LOG(DEBUG) << "P2P RX connection #" << hello->connection_nr << " from " << hello->peer_uuid.str();
+}
+
+void Client::on_bm_accept(int fd, const SockAddr &peer) {
+    timeval tv{10, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    auto hello = net::recv_packet<C2BHello>(fd);
+    if (!hello) {
+        ::close(fd);
+        return;
+    }
+    std::lock_guard lock(bm_mtx_);
+    // one benchmarked peer at a time (its parallel connections are all admitted)
+    if (bm_running_.load() > 0 && bm_peer_ && *bm_peer_ != hello->peer_uuid) {
+        net::send_packet(fd, B2CBenchmarkServerIsBusy{true});
+        ::close(fd);
+        return;
+    }
+    for (auto it = bm_threads_.begin(); bm_running_.load() == 0 && it != bm_threads_.end();) {
+        if (it->joinable()) it->join();
+        it = bm_threads_.erase(it);
+    }
+    net::send_packet(fd, B2CBenchmarkServerIsBusy{false});
+    bm_peer_ = hello->peer_uuid;
+    bm_running_++;
+    bm_threads_.emplace_back([this, fd, peer] {
+        benchmark_receive(fd, peer);
+        bm_running_--;
+    });
+}
+
+void Client::on_ss_accept(int fd, const SockAddr &peer) {
+    std::lock_guard lock(ss_mtx_);
+    ss_threads_.emplace_back([this, fd, peer] { serve_shared_state(fd, peer); });
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// connect / establish
+// ------------------------------------------------------------------------------------------------------------------
+bool Client::connect() {
+    if (accepted_) {
+        LOG(WARN) << "connect() called twice";
+        return false;
+    }
+    if (!start_listeners()) return false;
+    if (!master_.connect()) return false;
+
+    C2MRequestSessionRegistration reg;
+    reg.peer_group = cfg_.peer_group;
+    reg.use_explicit_addresses = cfg_.explicit_addresses;
+    if (cfg_.explicit_addresses) {
+        reg.advertised_p2p = cfg_.adv_p2p;
+        reg.advertised_ss = cfg_.adv_ss;
+        reg.advertised_bm = cfg_.adv_bm;
+    } else {
+        reg.p2p_port = p2p_listener_->port();
+        reg.ss_port = ss_listener_->port();
+        reg.bm_port = bm_listener_->port();
+    }
+    if (!master_.send(reg)) return false;
+    auto resp = master_.receive<M2CSessionRegistrationResponse>();
+    if (!resp) {
+        LOG(ERR) << "No registration response from master";
+        return false;
+    }
+    if (!resp->accepted) {
+        LOG(ERR) << "Master rejected registration";
+        return false;
+    }
+    uuid_ = resp->assigned_uuid;
+    LOG(INFO) << "Registered with master as " << uuid_.str();
+    const EstablishResult r = establish();
+    if (r == EstablishResult::Failed) return false;
+    accepted_ = true;
+    if (r == EstablishResult::Retry) {
+        // we were accepted even though the round failed: retry like every other peer
+        if (!request_and_establish(true)) return false;
+        return true;
+    }
+    conn_revision_++;
+    return true;
+}
+
+bool Client::connect_pool(const PeerInfo &peer, std::vector<std::shared_ptr<net::MuxConn>> &pool) {
+    pool.clear();
+    for (uint32_t nr = 0; nr < cfg_.pool_size; ++nr) {
+        const int fd = net::connect_tcp(peer.p2p_listen_addr, 5000);
+        if (fd < 0) {
+            LOG(WARN) << "P2P connect to " << sockaddr_str(peer.p2p_listen_addr) << " failed";
+            for (auto &c : pool) c->interrupt();
+            pool.clear();
+            return false;
+        }
+        P2PHello hello;
+        hello.peer_uuid = uuid_;
+        hello.connection_nr = nr;
+        timeval tv{10, 0};
+        setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        if (!net::send_packet(fd, hello) || !net::recv_packet<P2PHelloAck>(fd)) {
+            LOG(WARN) << "P2P handshake with " << peer.peer_uuid.str() << " failed";
+            ::close(fd);
+            for (auto &c : pool) c->interrupt();
+            pool.clear();
+            return false;
+        }
+        timeval none{0, 0};
+        setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+        auto conn = std::make_shared<net::MuxConn>(fd, net::MuxConn::Mode::Tx, peer.p2p_listen_addr);
+        conn->start();
+        pool.push_back(std::move(conn));
+    }
+    return true;
+}
+
+Client::EstablishResult Client::establish() {
+    auto info = master_.receive<M2CP2PConnectionInfo>();
+    if (!info) {
+        LOG(ERR) << "Failed to receive P2P connection info";
+        return EstablishResult::Failed;
+    }
+    global_ws_ = info->global_world_size;
+    local_ws_ = info->local_world_size;
+    n_groups_ = info->num_distinct_peer_groups;
+    largest_group_ = info->largest_peer_group_world_size;
+
+    std::vector<PeerInfo> neighbors;
+    {
+        std::lock_guard lock(p2p_mtx_);
+        if (!info->unchanged) neighbors_ = info->all_peers;
+        neighbors = neighbors_;
+    }
+    bool ok = true;
+    std::vector<Uuid> failed;
+    for (const auto &n : neighbors) {
+        bool healthy = false;
+        {
+            std::lock_guard lock(p2p_mtx_);
+            auto it = tx_.find(n.peer_uuid);
+            if (it != tx_.end() && it->second.size() == cfg_.pool_size)
+                healthy = std::all_of(it->second.begin(), it->second.end(), [](auto &c) { return c && c->is_open(); });
+        }
+        if (healthy) continue;
+        std::vector<std::shared_ptr<net::MuxConn>> pool;
+        if (!connect_pool(n, pool)) {
+            ok = false;
+            failed.push_back(n.peer_uuid);
+            break;
+        }
+        std::lock_guard lock(p2p_mtx_);
+        auto &slot = tx_[n.peer_uuid];
+        for (auto &c : slot)
+            if (c) c->interrupt();
+        slot = std::move(pool);
+    }
+    {
+        // drop TX pools to non-neighbours and RX pools from non-neighbours / dead RX connections
+        std::lock_guard lock(p2p_mtx_);
+        auto is_nb = [&](const Uuid &u) {
+            return std::any_of(neighbors.begin(), neighbors.end(), [&](const PeerInfo &p) { return p.peer_uuid == u; });
+        };
+        for (auto it = tx_.begin(); it != tx_.end();) {
+            if (!is_nb(it->first)) {
+                for (auto &c : it->second)
+                    if (c) c->interrupt();
+                it = tx_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        for (auto it = rx_.begin(); it != rx_.end();) {
+            if (!is_nb(it->first)) {
+                for (auto &c : it->second)
+                    if (c) c->interrupt();
+                it = rx_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+    C2MP2PConnectionsEstablished est;
+    est.success = ok;
+    est.failed_peers = failed;
+    if (!master_.send(est)) return EstablishResult::Failed;
+    auto resp = master_.receive<M2CP2PConnectionsEstablished>();
+    if (!resp) {
+        LOG(ERR) << "Failed to receive P2P established response";
+        return EstablishResult::Failed;
+    }
+    if (!resp->success) {
+        LOG(INFO) << "P2P establishment round failed (peer churn); retrying";
+        return EstablishResult::Retry;
+    }
+    std::shared_ptr<IpcArena> old_arena;
+    {
+        std::lock_guard lock(p2p_mtx_);
+        ring_ = resp->ring_order;
+        old_arena = arena_;
+    }
+    // Intra-node fast path: every peer of a loopback run lives on this host (the master enforces loopback
+    // exclusivity), so the ring can rendezvous in shared memory and exchange device buffers over xGMI.
+    std::shared_ptr<IpcArena> arena;
+    if (resp->ring_order.size() >= 2 && sockaddr_is_loopback(cfg_.master) && !env_flag("PCCL_DISABLE_IPC", false) &&
+        device_backend_available()) {
+        if (old_arena && old_arena->matches(resp->ring_order)) {
+            arena = old_arena;
+        } else {
+            arena = IpcArena::create(*this, resp->ring_order, cfg_.master.port, cfg_.peer_group);
+        }
+    }
+    {
+        std::lock_guard lock(p2p_mtx_);
+        arena_ = arena;
+    }
+    return EstablishResult::Success;
+}
+
+bool Client::request_and_establish(bool accept_new) {
+    std::lock_guard lock(establish_mtx_);
+    return request_and_establish_locked(accept_new);
+}
+
+bool Client::request_and_establish_locked(bool accept_new) {
+    if (!accepted_) return false;
+    if (!master_.is_open()) {
+        LOG(ERR) << "Master connection closed (kicked?)";
+        return false;
+    }
+    EstablishResult r;
+    do {
+        C2MRequestEstablishP2PConnections pkt;
+        pkt.accept_new_peers = accept_new;
+        if (!master_.send(pkt)) return false;
+        r = establish();
+    } while (r == EstablishResult::Retry);
+    if (r == EstablishResult::Failed) return false;
+    conn_revision_++;
+    return true;
+}
+
+bool Client::update_topology() {
+    if (any_collective_running()) return false;
+    return request_and_establish(true);
+}
+
+bool Client::are_peers_pending(bool &pending) {
+    if (!accepted_ || !master_.is_open()) return false;
+    if (!master_.send(C2MCheckPeersPending{})) return false;
+    auto r = master_.receive<M2CPeersPendingResponse>();
+    if (!r) return false;
+    pending = r->peers_pending;
+    return true;
+}
+
+int Client::ring_rank() {
+    std::lock_guard lock(p2p_mtx_);
+    for (size_t i = 0; i < ring_.size(); ++i)
+        if (ring_[i] == uuid_) return static_cast<int>(i);
+    return -1;
+}
+
+std::optional<Client::RingView> Client::ring_view(uint64_t seq) {
+    std::lock_guard lock(p2p_mtx_);
+    RingView rv;
+    rv.ring = ring_;
+    auto it = std::find(ring_.begin(), ring_.end(), uuid_);
+    if (it == ring_.end()) return std::nullopt;
+    rv.rank = static_cast<size_t>(it - ring_.begin());
+    rv.arena = arena_;
+    if (ring_.size() < 2) return rv;
+    const Uuid next = ring_[(rv.rank + 1) % ring_.size()];
+    const Uuid prev = ring_[(rv.rank + ring_.size() - 1) % ring_.size()];
+    auto t = tx_.find(next);
+    auto r = rx_.find(prev);
+    if (t == tx_.end() || r == rx_.end() || t->second.empty() || r->second.empty()) return std::nullopt;
+    rv.tx = t->second;
+    rv.rx = r->second;
+    (void)seq;
+    return rv;
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// topology optimization (bandwidth benchmarks + ATSP on the master)
+// ------------------------------------------------------------------------------------------------------------------
+bool Client::optimize_topology() {
+    if (!accepted_ || !master_.is_open()) return false;
+    bool complete = false;
+    do {
+        if (!master_.send(C2MOptimizeTopology{})) return false;
+        auto resp = master_.receive<M2COptimizeTopologyResponse>();
+        if (!resp) return false;
+        std::list<BenchmarkRequest> todo(resp->requests.begin(), resp->requests.end());
+        std::map<Uuid, std::chrono::steady_clock::time_point> last_attempt;
+        while (!todo.empty()) {
+            bool progressed = false;
+            for (auto it = todo.begin(); it != todo.end();) {
+                auto la = last_attempt.find(it->to_peer);
+                if (la != last_attempt.end() && std::chrono::steady_clock::now() - la->second < 1s) {
+                    ++it;
+                    continue;
+                }
+                double mbps = 0;
+                const BenchResult r = benchmark_send(uuid_, it->to_peer_endpoint, mbps);
+                if (r == BenchResult::Success) {
+                    C2MReportPeerBandwidth rep;
+                    rep.to_peer = it->to_peer;
+                    rep.bandwidth_mbps = mbps;
+                    if (!master_.send(rep)) return false;
+                    LOG(INFO) << "Bandwidth to " << it->to_peer.str() << ": " << mbps << " Mbit/s";
+                    it = todo.erase(it);
+                    progressed = true;
+                } else if (r == BenchResult::Busy || r == BenchResult::SendFailure) {
+                    last_attempt[it->to_peer] = std::chrono::steady_clock::now();
+                    ++it;
+                } else {
+                    LOG(WARN) << "Benchmark to " << sockaddr_str(it->to_peer_endpoint) << " failed; skipping";
+                    it = todo.erase(it);
+                    progressed = true;
+                }
+            }
+            if (!progressed && !todo.empty()) std::this_thread::sleep_for(250ms);
+        }
+        if (!master_.send(C2MOptimizeTopologyWorkComplete{})) return false;
+        auto done = master_.receive<M2COptimizeTopologyComplete>();
+        if (!done) return false;
+        complete = done->success;
+    } while (!complete);
+    // rewire to the (possibly) new ring order
+    return request_and_establish(false);
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// lifecycle
+// ------------------------------------------------------------------------------------------------------------------
+bool Client::any_collective_running() {
+    std::lock_guard lock(ops_mtx_);
+    for (auto &[_, op] : ops_)
+        if (!op->done.load()) return true;
+    return false;
+}
+
+bool Client::interrupt() {
+    if (interrupted_.exchange(true)) return true;
+    master_.interrupt();
+    {
+        std::lock_guard lock(p2p_mtx_);
+        for (auto &[_, pool] : tx_)
+            for (auto &c : pool)
+                if (c) c->interrupt();
+        for (auto &[_, pool] : rx_)
+            for (auto &c : pool)
+                if (c) c->interrupt();
+    }
+    if (p2p_listener_) p2p_listener_->interrupt();
+    if (ss_listener_) ss_listener_->interrupt();
+    if (bm_listener_) bm_listener_->interrupt();
+    return true;
+}
+
+bool Client::join() {
+    std::vector<std::shared_ptr<OpState>> ops;
+    {
+        std::lock_guard lock(ops_mtx_);
+        for (auto &[_, op] : ops_) ops.push_back(op);
+    }
+    for (auto &op : ops)
+        if (op->thread.joinable()) op->thread.join();
+    if (p2p_listener_) p2p_listener_->join();
+    if (ss_listener_) ss_listener_->join();
+    if (bm_listener_) bm_listener_->join();
+    master_.join();
+    {
+        std::lock_guard lock(p2p_mtx_);
+        tx_.clear();
+        rx_.clear();
+        arena_.reset();
+    }
+    std::vector<std::thread> ss, bm;
+    {
+        std::lock_guard lock(ss_mtx_);
+        ss.swap(ss_threads_);
+    }
+    for (auto &t : ss)
+        if (t.joinable()) t.join();
+    {
+        std::lock_guard lock(bm_mtx_);
+        bm.swap(bm_threads_);
+    }
+    for (auto &t : bm)
+        if (t.joinable()) t.join();
+    return true;
+}
+
+} // namespace pccl::client

@@ -1,0 +1,181 @@
+// Peer (client) protocol engine: connection management, phase votes, collectives and shared state
+// (reference behaviour: ccoip/src/cpp/ccoip_client_handler.cpp, ccoip_client_state.cpp, reduce.cpp).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../common/device_backend.hpp"
+#include "../common/types.hpp"
+#include "../net/listener.hpp"
+#include "../net/master_conn.hpp"
+#include "../net/mux.hpp"
+
+namespace pccl::client {
+
+struct ClientConfig {
+    SockAddr master{};
+    uint32_t peer_group = 0;
+    uint32_t pool_size = 1;
+    uint16_t p2p_port = 48149, ss_port = 48150, bm_port = 48151;
+    bool explicit_addresses = false;
+    SockAddr adv_p2p{}, adv_ss{}, adv_bm{};
+};
+
+struct SSEntry {
+    std::string key;
+    DType dtype = DType::F32;
+    DeviceType device = DeviceType::Cpu;
+    void *data = nullptr;
+    size_t count = 0;
+    size_t bytes = 0;
+    bool allow_content_inequality = false;
+};
+
+struct SharedState {
+    uint64_t revision = 0;
+    SyncStrategy strategy = SyncStrategy::EnforcePopular;
+    std::vector<SSEntry> entries;
+};
+
+struct SSInfo {
+    uint64_t tx_bytes = 0;
+    uint64_t rx_bytes = 0;
+};
+
+struct ReduceInfo {
+    uint32_t world_size = 0;
+    uint64_t tx_bytes = 0;
+    uint64_t rx_bytes = 0;
+};
+
+struct ReduceRequest {
+    const void *src = nullptr;
+    void *dst = nullptr;
+    size_t count = 0;
+    DType dtype = DType::F32;
+    DType qtype = DType::F32;
+    QuantAlgo qalgo = QuantAlgo::None;
+    ReduceOp op = ReduceOp::Sum;
+    uint64_t tag = 0;
+};
+
+class IpcArena; // intra-node shared-memory + IPC rendezvous (ipc.cpp)
+
+class Client {
+public:
+    explicit Client(const ClientConfig &cfg);
+    ~Client();
+
+    bool connect();
+    bool interrupt();
+    bool join();
+
+    bool update_topology();                         // accept new peers + (re)establish ring
+    bool request_and_establish(bool accept_new);
+    bool are_peers_pending(bool &pending);
+    bool optimize_topology();
+    bool sync_shared_state(SharedState &ss, SSInfo &info);
+
+    bool all_reduce_async(const ReduceRequest &req);
+    bool join_async_reduce(uint64_t tag);           // true on success
+    bool get_reduce_info(uint64_t tag, ReduceInfo &out);
+    bool any_collective_running();
+
+    size_t global_world_size() const { return global_ws_.load(); }
+    size_t local_world_size() const { return local_ws_.load(); }
+    size_t num_distinct_groups() const { return n_groups_.load(); }
+    size_t largest_group_size() const { return largest_group_.load(); }
+    uint64_t connection_revision() const { return conn_revision_.load(); }
+    int ring_rank();
+    int last_reduce_path() const { return last_path_.load(); }
+    const Uuid &uuid() const { return uuid_; }
+
+private:
+    friend class IpcArena;
+    enum class EstablishResult { Success, Retry, Failed };
+
+    struct OpState {
+        ReduceRequest req;
+        std::thread thread;
+        std::atomic<bool> done{false};
+        bool success = false;
+        bool info_taken = false;
+        uint64_t revision_at_start = 0;
+        std::atomic<uint64_t> tx{0}, rx{0};
+        uint32_t world = 0;
+    };
+
+    struct RingView { // immutable snapshot used by an op thread
+        std::vector<Uuid> ring;
+        size_t rank = 0;
+        std::vector<std::shared_ptr<net::MuxConn>> tx; // pool to next
+        std::vector<std::shared_ptr<net::MuxConn>> rx; // pool from prev
+        std::shared_ptr<IpcArena> arena;
+    };
+
+    // connection management
+    bool start_listeners();
+    void on_p2p_accept(int fd, const SockAddr &peer);
+    void on_ss_accept(int fd, const SockAddr &peer);
+    void on_bm_accept(int fd, const SockAddr &peer);
+    EstablishResult establish();
+    bool request_and_establish_locked(bool accept_new);
+    bool connect_pool(const proto::PeerInfo &peer, std::vector<std::shared_ptr<net::MuxConn>> &pool);
+    std::optional<RingView> ring_view(uint64_t seq);
+
+    // collectives
+    void run_op(const std::shared_ptr<OpState> &op);
+    // returns {success, abort_received}
+    std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);
+    std::pair<bool, bool> ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device);
+    std::pair<bool, bool> ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
+    bool abort_received(uint64_t tag);
+
+    // shared state
+    void serve_shared_state(int fd, SockAddr peer);
+    bool hash_entry(const SSEntry &e, uint64_t &hash, HashType &type);
+
+    ClientConfig cfg_;
+    net::MasterConnection master_;
+    std::unique_ptr<net::Listener> p2p_listener_, ss_listener_, bm_listener_;
+    Uuid uuid_;
+    std::atomic<bool> accepted_{false};
+    std::atomic<bool> interrupted_{false};
+
+    std::mutex p2p_mtx_;
+    std::map<Uuid, std::vector<std::shared_ptr<net::MuxConn>>> tx_;
+    std::map<Uuid, std::vector<std::shared_ptr<net::MuxConn>>> rx_;
+    std::vector<proto::PeerInfo> neighbors_;
+    std::vector<Uuid> ring_;
+    std::shared_ptr<IpcArena> arena_;
+    std::mutex establish_mtx_; // serializes concurrent re-establishment attempts
+
+    std::atomic<uint64_t> conn_revision_{0};
+    std::atomic<size_t> global_ws_{0}, local_ws_{0}, n_groups_{0}, largest_group_{0};
+    std::atomic<int> last_path_{0};
+
+    std::mutex ops_mtx_;
+    std::map<uint64_t, std::shared_ptr<OpState>> ops_;
+
+    // shared-state distribution (server side)
+    std::mutex ss_mtx_;
+    SharedState *serving_ = nullptr;
+    std::atomic<uint64_t> ss_tx_bytes_{0};
+    std::vector<std::thread> ss_threads_;
+
+    // benchmark server
+    std::mutex bm_mtx_;
+    std::optional<Uuid> bm_peer_;
+    std::atomic<int> bm_running_{0};
+    std::vector<std::thread> bm_threads_;
+};
+
+} // namespace pccl::client

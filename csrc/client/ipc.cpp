@@ -1,0 +1,492 @@
+#include "ipc.hpp"
+
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <tuple>
+
+#include "../common/log.hpp"
+#include "client.hpp"
+
+namespace pccl::client {
+
+using namespace std::chrono;
+
+namespace {
+constexpr uint64_t kMagic = 0x5043434c49504331ull; // "PCCLIPC1"
+constexpr uint32_t kClosed = 0x80000000u;
+constexpr uint32_t kSlots = 256;
+constexpr uint32_t kMaxWorld = 16;
+
+constexpr uint32_t PH_VOTED = 1, PH_COPIED = 2, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
+
+uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const auto *b = static_cast<const uint8_t *>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+} // namespace
+
+struct alignas(64) PeerSlotShm {
+    std::atomic<uint32_t> present;
+    int32_t pid;
+    uint32_t can_ipc;
+    uint8_t uuid[16];
+};
+
+struct alignas(64) OpPeerShm {
+    std::atomic<uint64_t> phase; // (seq + 1) << 8 | phase
+    uint32_t vote;
+    int32_t device;
+    uint64_t bytes;
+    uint64_t buf_id;
+    uint64_t buf_cap;
+    uint32_t dtype;
+    uint32_t op;
+    uint8_t handle[kIpcHandleBytes];
+};
+
+struct ArenaShm {
+    std::atomic<uint64_t> magic;
+    std::atomic<uint32_t> join;
+    std::atomic<uint32_t> unlinked;
+    uint32_t world;
+    uint32_t pad[11];
+    PeerSlotShm *peers() { return reinterpret_cast<PeerSlotShm *>(reinterpret_cast<uint8_t *>(this) + 64); }
+    OpPeerShm *op(uint32_t slot, uint32_t peer) {
+        auto *base = reinterpret_cast<uint8_t *>(this) + 64 + sizeof(PeerSlotShm) * kMaxWorld;
+        return reinterpret_cast<OpPeerShm *>(base) + slot * kMaxWorld + peer;
+    }
+    static size_t bytes() { return 64 + sizeof(PeerSlotShm) * kMaxWorld + sizeof(OpPeerShm) * kSlots * kMaxWorld; }
+};
+
+struct OpCtx {
+    void *mine_in = nullptr;
+    std::vector<void *> peer_base;
+    size_t bytes = 0;
+};
+
+// per-process bookkeeping
+static std::mutex g_ctx_mtx;
+static std::map<std::pair<const IpcArena *, uint64_t>, OpCtx> g_ctx;
+static std::mutex g_attempt_mtx;
+static std::map<uint64_t, int> g_attempts;
+
+std::shared_ptr<IpcArena> IpcArena::create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
+                                           uint32_t group) {
+    const size_t W = ring.size();
+    if (W < 2 || W > kMaxWorld) return nullptr;
+    auto it = std::find(ring.begin(), ring.end(), c.uuid());
+    if (it == ring.end()) return nullptr;
+    const size_t rank = static_cast<size_t>(it - ring.begin());
+
+    uint64_t h = fnv1a(&group, sizeof(group));
+    h = fnv1a(&master_port, sizeof(master_port), h);
+    for (const auto &u : ring) h = fnv1a(u.data.data(), 16, h);
+    int attempt;
+    {
+        std::lock_guard l(g_attempt_mtx);
+        attempt = g_attempts[h]++;
+    }
+    char nbuf[96];
+    std::snprintf(nbuf, sizeof(nbuf), "/pccl_arena_%016llx_%d", static_cast<unsigned long long>(h), attempt);
+    const std::string name(nbuf);
+    const size_t bytes = ArenaShm::bytes();
+    const int timeout_ms = static_cast<int>(env_size("PCCL_IPC_RENDEZVOUS_MS", 15000));
+    const auto t0 = steady_clock::now();
+    auto elapsed_ms = [&] { return duration_cast<milliseconds>(steady_clock::now() - t0).count(); };
+
+    int fd = -1;
+    if (rank == 0) {
+        shm_unlink(name.c_str());
+        fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+            LOG(WARN) << "IPC arena: cannot create " << name << ": " << std::strerror(errno);
+            if (fd >= 0) close(fd);
+            return nullptr;
+        }
+    } else {
+        while (true) {
+            fd = shm_open(name.c_str(), O_RDWR, 0600);
+            if (fd >= 0) {
+                struct stat st{};
+                if (fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes) break;
+                close(fd);
+                fd = -1;
+            }
+            if (elapsed_ms() > timeout_ms) {
+                LOG(WARN) << "IPC arena: rendezvous " << name << " timed out (peers not on this host?)";
+                return nullptr;
+            }
+            std::this_thread::sleep_for(milliseconds(1));
+        }
+    }
+    void *mem = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (mem == MAP_FAILED) return nullptr;
+    auto *shm = static_cast<ArenaShm *>(mem);
+    if (rank == 0) {
+        shm->world = static_cast<uint32_t>(W);
+        shm->magic.store(kMagic, std::memory_order_release);
+    } else {
+        while (shm->magic.load(std::memory_order_acquire) != kMagic) {
+            if (elapsed_ms() > timeout_ms) {
+                munmap(mem, bytes);
+                return nullptr;
+            }
+            std::this_thread::sleep_for(milliseconds(1));
+        }
+    }
+    PeerSlotShm &me = shm->peers()[rank];
+    me.pid = static_cast<int32_t>(getpid());
+    me.can_ipc = device_backend_available() ? 1 : 0;
+    std::memcpy(me.uuid, c.uuid().data.data(), 16);
+    me.present.store(1, std::memory_order_release);
+    // join unless the rendezvous was closed by a peer that gave up
+    uint32_t v = shm->join.load();
+    bool joined = false;
+    while (!(v & kClosed)) {
+        if (shm->join.compare_exchange_weak(v, v + 1)) {
+            joined = true;
+            break;
+        }
+    }
+    bool ok = false;
+    if (joined) {
+        while (true) {
+            v = shm->join.load(std::memory_order_acquire);
+            if ((v & ~kClosed) == W) {
+                ok = true;
+                break;
+            }
+            if (v & kClosed) break;
+            if (elapsed_ms() > timeout_ms) {
+                uint32_t expect = v;
+                if (shm->join.compare_exchange_strong(expect, v | kClosed)) break;
+                continue; // the last peer joined concurrently: re-read
+            }
+            std::this_thread::sleep_for(milliseconds(1));
+        }
+    }
+    if (ok) {
+        if (shm->unlinked.fetch_add(1) + 1 == W) shm_unlink(name.c_str());
+        for (size_t k = 0; k < W; ++k)
+            if (!shm->peers()[k].can_ipc) ok = false; // consistent: every peer reads the same slots
+    } else {
+        shm_unlink(name.c_str());
+    }
+    if (!ok) {
+        munmap(mem, bytes);
+        LOG(INFO) << "IPC arena not used for this ring";
+        return nullptr;
+    }
+    auto arena = std::shared_ptr<IpcArena>(new IpcArena());
+    arena->ring_ = ring;
+    arena->rank_ = rank;
+    arena->name_ = name;
+    arena->shm_ = shm;
+    arena->shm_bytes_ = bytes;
+    for (size_t k = 0; k < W; ++k) arena->pids_.push_back(shm->peers()[k].pid);
+    LOG(INFO) << "IPC arena established (" << W << " peers on this host, rank " << rank << ")";
+    return arena;
+}
+
+IpcArena::~IpcArena() {
+    DeviceBackend *be = device_backend();
+    if (be) {
+        const int cur = be->current_device();
+        for (auto &[key, p] : mappings_) {
+            be->set_device(std::get<2>(key));
+            be->ipc_close(p);
+        }
+        for (auto &b : bufs_) {
+            be->set_device(b->device);
+            be->free_device(b->ptr);
+        }
+        if (cur >= 0) be->set_device(cur);
+    }
+    if (shm_) munmap(shm_, shm_bytes_);
+}
+
+IpcArena::CommBuf *IpcArena::acquire_buffer(size_t bytes, int device) {
+    std::lock_guard l(mtx_);
+    CommBuf *best = nullptr;
+    for (auto &b : bufs_)
+        if (!b->busy && b->device == device && b->cap >= bytes && (!best || b->cap < best->cap)) best = b.get();
+    if (best) {
+        best->busy = true;
+        return best;
+    }
+    DeviceBackend *be = device_backend();
+    auto b = std::make_unique<CommBuf>();
+    b->cap = std::max<size_t>(bytes, 1 << 20);
+    b->device = device;
+    be->set_device(device);
+    b->ptr = be->alloc_device(b->cap);
+    if (!b->ptr || !be->ipc_export(b->ptr, b->handle)) {
+        if (b->ptr) be->free_device(b->ptr);
+        LOG(ERR) << "IPC arena: failed to allocate/export " << b->cap << " bytes";
+        return nullptr;
+    }
+    b->id = next_buf_id_++;
+    b->busy = true;
+    bufs_.push_back(std::move(b));
+    return bufs_.back().get();
+}
+
+void IpcArena::release_buffer(CommBuf *b) {
+    if (!b) return;
+    std::lock_guard l(mtx_);
+    b->busy = false;
+}
+
+void *IpcArena::peer_mapping(int peer, uint64_t buf_id, const uint8_t *handle, int my_device) {
+    std::lock_guard l(mtx_);
+    const auto key = std::make_tuple(peer, buf_id, my_device);
+    auto it = mappings_.find(key);
+    if (it != mappings_.end()) return it->second;
+    DeviceBackend *be = device_backend();
+    be->set_device(my_device);
+    void *p = be->ipc_open(handle);
+    if (p) mappings_[key] = p;
+    return p;
+}
+
+void IpcArena::set_phase(uint64_t seq, uint32_t phase) {
+    shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_))
+        ->phase.store(((seq + 1) << 8) | phase, std::memory_order_release);
+}
+
+static bool pid_alive(int pid) { return kill(pid, 0) == 0 || errno == EPERM; }
+
+int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    const auto t0 = steady_clock::now();
+    const auto timeout = milliseconds(env_size("PCCL_IPC_TIMEOUT_MS", 60000));
+    auto last_check = t0;
+    uint64_t spins = 0;
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        if (k == rank_) continue;
+        OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        while (true) {
+            const uint64_t v = p->phase.load(std::memory_order_acquire);
+            const uint64_t vs = v >> 8;
+            const uint32_t vp = static_cast<uint32_t>(v & 0xff);
+            if (vs == seq + 1) {
+                if (vp == PH_ABORTED) return 1;
+                if (vp >= phase) break;
+            } else if (vs > seq + 1) {
+                return 1;
+            }
+            if (++spins < 4096) {
+                cpu_relax();
+                continue;
+            }
+            std::this_thread::sleep_for(microseconds(spins < 20000 ? 5 : 50));
+            const auto now = steady_clock::now();
+            if (now - last_check > milliseconds(10)) {
+                last_check = now;
+                if (c.abort_received(tag)) return 2;
+                if (!pid_alive(pids_[k])) {
+                    LOG(WARN) << "IPC: peer process " << pids_[k] << " died";
+                    return 1;
+                }
+                if (!c.master_.is_open()) return 1;
+                if (now - t0 > timeout) {
+                    LOG(WARN) << "IPC: barrier timeout (seq " << seq << ", phase " << phase << ")";
+                    return 1;
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    const auto t0 = steady_clock::now();
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        while (true) {
+            const uint64_t v = p->phase.load(std::memory_order_acquire);
+            const uint32_t vp = static_cast<uint32_t>(v & 0xff);
+            if (v == 0 || (v >> 8) >= seq + 1 || vp == PH_RELEASED || vp == PH_ABORTED) break;
+            std::this_thread::sleep_for(microseconds(20));
+            if (steady_clock::now() - t0 > seconds(30) || !pid_alive(pids_[k]) || !c.master_.is_open()) return false;
+        }
+    }
+    return true;
+}
+
+int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
+                        ReduceOp op) {
+    if (!wait_slot_free(c, seq)) return kAborted;
+    CommBuf *buf = nullptr;
+    if (device_ok) {
+        buf = acquire_buffer(2 * bytes, device);
+        if (!buf) device_ok = false;
+    }
+    OpPeerShm *mine = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    mine->vote = device_ok ? 1 : 0;
+    mine->device = device;
+    mine->bytes = bytes;
+    mine->dtype = static_cast<uint32_t>(dtype);
+    mine->op = static_cast<uint32_t>(op);
+    if (buf) {
+        mine->buf_id = buf->id;
+        mine->buf_cap = buf->cap;
+        std::memcpy(mine->handle, buf->handle, kIpcHandleBytes);
+    }
+    set_phase(seq, PH_VOTED);
+    const int rc = barrier(c, tag, seq, PH_VOTED);
+    if (rc != 0) {
+        set_phase(seq, PH_ABORTED);
+        release_buffer(buf);
+        return kAborted;
+    }
+    bool all = true;
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        all = all && p->vote == 1 && p->bytes == bytes && p->dtype == static_cast<uint32_t>(dtype) &&
+              p->op == static_cast<uint32_t>(op);
+    }
+    if (!all) {
+        set_phase(seq, PH_RELEASED);
+        release_buffer(buf);
+        return kUseRing;
+    }
+    OpCtx ctx;
+    ctx.bytes = bytes;
+    ctx.mine_in = buf->ptr;
+    ctx.peer_base.resize(ring_.size());
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        if (k == rank_) {
+            ctx.peer_base[k] = buf->ptr;
+            continue;
+        }
+        const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        ctx.peer_base[k] = peer_mapping(static_cast<int>(k), p->buf_id, p->handle, device);
+        if (!ctx.peer_base[k]) {
+            LOG(ERR) << "IPC: cannot map buffer of peer " << k;
+            set_phase(seq, PH_ABORTED);
+            release_buffer(buf);
+            return kAborted;
+        }
+    }
+    {
+        std::lock_guard l(g_ctx_mtx);
+        g_ctx[{this, seq}] = std::move(ctx);
+    }
+    // stash the buffer pointer for release in run()
+    {
+        std::lock_guard l(mtx_);
+        (void)buf;
+    }
+    return kUseIpc;
+}
+
+std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
+                                    DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
+                                    std::atomic<uint64_t> &rx) {
+    OpCtx ctx;
+    {
+        std::lock_guard l(g_ctx_mtx);
+        auto it = g_ctx.find({this, seq});
+        if (it == g_ctx.end()) return {false, false};
+        ctx = std::move(it->second);
+        g_ctx.erase(it);
+    }
+    CommBuf *mybuf = nullptr;
+    {
+        std::lock_guard l(mtx_);
+        for (auto &b : bufs_)
+            if (b->ptr == ctx.mine_in) mybuf = b.get();
+    }
+    DeviceBackend *be = device_backend();
+    be->set_device(device);
+    DevStream st = be->create_stream();
+    const size_t W = ring_.size();
+    const size_t es = dtype_size(dtype);
+    const size_t bytes = ctx.bytes;
+    auto *my_in = static_cast<uint8_t *>(ctx.mine_in);
+    auto *my_out = my_in + bytes;
+    bool dst_touched = false;
+
+    auto finish = [&](int rc) -> std::pair<bool, bool> {
+        if (rc != 0) {
+            set_phase(seq, PH_ABORTED);
+            be->stream_sync(st);
+            if (dst_touched && src == dst) { // restore the caller's buffer from the copied-in original
+                be->memcpy_async(dst, my_in, bytes, st);
+                be->stream_sync(st);
+            }
+        } else {
+            set_phase(seq, PH_RELEASED);
+        }
+        be->destroy_stream(st);
+        release_buffer(mybuf);
+        return {rc == 2, rc == 2};
+    };
+    if (!st) return finish(1);
+
+    // 1. copy-in
+    if (!be->memcpy_async(my_in, src, bytes, st) || !be->stream_sync(st)) return finish(1);
+    set_phase(seq, PH_COPIED);
+    if (int rc = barrier(c, tag, seq, PH_COPIED)) return finish(rc);
+
+    // shard bounds: 256-byte aligned so every peer's shard is 16-byte-vector aligned
+    const size_t align_el = std::max<size_t>(1, 256 / es);
+    const size_t per = ((count + W - 1) / W + align_el - 1) / align_el * align_el;
+    std::vector<size_t> lo(W), n(W);
+    for (size_t k = 0; k < W; ++k) {
+        lo[k] = std::min(k * per, count);
+        n[k] = std::min(lo[k] + per, count) - lo[k];
+    }
+
+    // 2. reduce-scatter: read shard `rank` from every peer over xGMI, reduce in fixed peer order
+    std::vector<const void *> srcs(W);
+    for (size_t k = 0; k < W; ++k) srcs[k] = static_cast<const uint8_t *>(ctx.peer_base[k]) + lo[rank_] * es;
+    dst_touched = true;
+    if (!be->multi_reduce(my_out + lo[rank_] * es, static_cast<uint8_t *>(dst) + lo[rank_] * es, srcs.data(),
+                          static_cast<int>(W), n[rank_], dtype, op, st) ||
+        !be->stream_sync(st))
+        return finish(1);
+    set_phase(seq, PH_REDUCED);
+    if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
+
+    // 3. all-gather: pull every other peer's reduced shard straight into the receive buffer
+    std::vector<const void *> gsrc(W);
+    for (size_t k = 0; k < W; ++k) gsrc[k] = static_cast<const uint8_t *>(ctx.peer_base[k]) + bytes + lo[k] * es;
+    if (!be->multi_gather(dst, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_), dtype,
+                          st) ||
+        !be->stream_sync(st))
+        return finish(1);
+    set_phase(seq, PH_GATHERED);
+    if (int rc = barrier(c, tag, seq, PH_GATHERED)) return finish(rc);
+
+    const uint64_t moved = static_cast<uint64_t>(bytes) * (W - 1) / W;
+    tx += 2 * moved;
+    rx += 2 * moved;
+    return finish(0);
+}
+
+std::pair<bool, bool> Client::ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    return rv.arena->run(*this, op.req.tag, seq, op.req.src, op.req.dst, op.req.count, op.req.dtype, op.req.op, device,
+                         op.tx, op.rx);
+}
+
+} // namespace pccl::client

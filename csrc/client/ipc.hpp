@@ -1,0 +1,97 @@
+// Intra-node xGMI fast path.
+//
+// When every peer of a ring runs on this host (loopback run), the peers rendezvous in a POSIX shared-memory arena
+// and each exports HBM communication buffers through HIP IPC. An all-reduce whose buffers are on GPUs at every peer
+// then runs as a "two-shot" direct-access collective instead of a TCP ring:
+//   1. copy-in: each peer copies its send buffer into its exported comm buffer (local HBM)
+//   2. reduce-scatter: peer r owns shard r and reduces it by reading shard r from *all* peers' comm buffers at once
+//      (one fused kernel, 16-byte loads, fixed peer order -> every peer gets bit-identical results); the result goes
+//      to its own output region and straight into the user's receive buffer
+//   3. all-gather: each peer reads the other peers' reduced shards directly into its receive buffer
+// A ring moves data over one xGMI link per GPU; this uses all W-1 links of the fully connected MI355X node
+// concurrently and needs 3 kernel launches instead of 2(W-1) dependent ring steps.
+//
+// Synchronization is a per-op barrier in shared memory keyed by the master-assigned sequence number (so concurrent
+// ops with different tags proceed independently). Every wait is bounded and also watches the master's abort packet
+// and the liveness of the peer processes, so a peer dying mid-collective aborts the op on all survivors
+// (fault tolerance is preserved); a vote at the start of each op lets all peers agree on the data path.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../common/device_backend.hpp"
+#include "../common/types.hpp"
+
+namespace pccl::client {
+
+class Client;
+struct ArenaShm;
+
+class IpcArena {
+public:
+    static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1;
+
+    static std::shared_ptr<IpcArena> create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
+                                            uint32_t group);
+    ~IpcArena();
+
+    bool matches(const std::vector<Uuid> &ring) const { return ring == ring_; }
+    size_t world() const { return ring_.size(); }
+    size_t rank() const { return rank_; }
+
+    template<typename Op>
+    int vote(Client &c, Op &op, uint64_t seq, bool device_ok, int device);
+
+    // Runs the IPC all-reduce for a voted op. Returns {success, aborted}.
+    std::pair<bool, bool> run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
+                              DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
+                              std::atomic<uint64_t> &rx);
+
+    // internal (exposed for the vote template)
+    int vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
+                  ReduceOp op);
+
+private:
+    IpcArena() = default;
+    struct CommBuf {
+        uint64_t id = 0;
+        void *ptr = nullptr;
+        size_t cap = 0;
+        int device = -1;
+        uint8_t handle[kIpcHandleBytes]{};
+        bool busy = false;
+    };
+    CommBuf *acquire_buffer(size_t bytes, int device);
+    void release_buffer(CommBuf *b);
+    void *peer_mapping(int peer, uint64_t buf_id, const uint8_t *handle, int my_device);
+    // waits until every peer reached `phase` for `seq`; 0 ok, 1 failure (peer dead/aborted/timeout), 2 master abort
+    int barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase);
+    void set_phase(uint64_t seq, uint32_t phase);
+    bool wait_slot_free(Client &c, uint64_t seq);
+
+    std::vector<Uuid> ring_;
+    size_t rank_ = 0;
+    std::string name_;
+    ArenaShm *shm_ = nullptr;
+    size_t shm_bytes_ = 0;
+    std::vector<int> pids_;
+
+    std::mutex mtx_;
+    std::vector<std::unique_ptr<CommBuf>> bufs_;
+    uint64_t next_buf_id_ = 1;
+    std::map<std::tuple<int, uint64_t, int>, void *> mappings_; // (peer, buf id, my device) -> mapped ptr
+};
+
+template<typename Op>
+int IpcArena::vote(Client &c, Op &op, uint64_t seq, bool device_ok, int device) {
+    return vote_impl(c, op.req.tag, seq, device_ok, device, op.req.count * dtype_size(op.req.dtype), op.req.dtype,
+                     op.req.op);
+}
+
+} // namespace pccl::client

@@ -1,0 +1,122 @@
+// Reusable buffer pools (pinned host / device / plain host) so collectives never allocate on the hot path.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdlib>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../common/device_backend.hpp"
+
+namespace pccl::client {
+
+class BufferPool {
+public:
+    enum class Kind { Host, Pinned, Device };
+    explicit BufferPool(Kind k) : kind_(k) {}
+    ~BufferPool() {
+        for (auto &b : free_) release(b);
+    }
+
+    struct Buf {
+        void *p = nullptr;
+        size_t cap = 0;
+        int device = -1;
+    };
+
+    Buf get(size_t n, int device = -1) {
+        {
+            std::lock_guard l(mtx_);
+            size_t best = SIZE_MAX;
+            size_t bi = 0;
+            for (size_t i = 0; i < free_.size(); ++i)
+                if (free_[i].cap >= n && free_[i].device == device && free_[i].cap < best) {
+                    best = free_[i].cap;
+                    bi = i;
+                }
+            if (best != SIZE_MAX) {
+                Buf b = free_[bi];
+                free_.erase(free_.begin() + static_cast<long>(bi));
+                return b;
+            }
+        }
+        Buf b;
+        b.cap = n < 4096 ? 4096 : n;
+        b.device = device;
+        switch (kind_) {
+            case Kind::Host: b.p = std::aligned_alloc(4096, (b.cap + 4095) / 4096 * 4096); break;
+            case Kind::Pinned: b.p = device_backend() ? device_backend()->alloc_pinned(b.cap) : nullptr; break;
+            case Kind::Device: b.p = device_backend() ? device_backend()->alloc_device(b.cap) : nullptr; break;
+        }
+        if (b.p == nullptr) b.cap = 0;
+        return b;
+    }
+
+    void put(const Buf &b) {
+        if (b.p == nullptr) return;
+        std::lock_guard l(mtx_);
+        free_.push_back(b);
+        if (free_.size() > 32) {
+            release(free_.front());
+            free_.erase(free_.begin());
+        }
+    }
+
+private:
+    void release(const Buf &b) {
+        if (!b.p) return;
+        switch (kind_) {
+            case Kind::Host: std::free(b.p); break;
+            case Kind::Pinned:
+                if (device_backend()) device_backend()->free_pinned(b.p);
+                break;
+            case Kind::Device:
+                if (device_backend()) {
+                    const int cur = device_backend()->current_device();
+                    if (b.device >= 0) device_backend()->set_device(b.device);
+                    device_backend()->free_device(b.p);
+                    if (cur >= 0) device_backend()->set_device(cur);
+                }
+                break;
+        }
+    }
+    Kind kind_;
+    std::mutex mtx_;
+    std::vector<Buf> free_;
+};
+
+// RAII lease of a pooled buffer.
+class Lease {
+public:
+    Lease() = default;
+    Lease(BufferPool &pool, size_t n, int device = -1) : pool_(&pool), buf_(pool.get(n, device)) {}
+    ~Lease() {
+        if (pool_) pool_->put(buf_);
+    }
+    Lease(const Lease &) = delete;
+    Lease &operator=(const Lease &) = delete;
+    Lease(Lease &&o) noexcept : pool_(o.pool_), buf_(o.buf_) { o.pool_ = nullptr; }
+    Lease &operator=(Lease &&o) noexcept {
+        if (this != &o) {
+            if (pool_) pool_->put(buf_);
+            pool_ = o.pool_;
+            buf_ = o.buf_;
+            o.pool_ = nullptr;
+        }
+        return *this;
+    }
+    uint8_t *data() const { return static_cast<uint8_t *>(buf_.p); }
+    bool ok() const { return buf_.p != nullptr; }
+
+private:
+    BufferPool *pool_ = nullptr;
+    BufferPool::Buf buf_{};
+};
+
+BufferPool &host_pool();
+BufferPool &pinned_pool();
+BufferPool &device_pool();
+
+} // namespace pccl::client

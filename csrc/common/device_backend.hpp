@@ -1,0 +1,88 @@
+// Device backend interface. The HIP implementation lives in a separately built plugin (libpccl_hip.so, sources in
+// csrc/hip/) that libpccl.so loads with dlopen at pcclInit, so that CPU-only hosts never initialize a GPU runtime and
+// so that an application which already loaded PyTorch's HIP runtime shares it (same SONAME) instead of loading a
+// second copy. All kernel entry points are asynchronous on the given stream.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../kernels/quant_common.hpp"
+#include "types.hpp"
+
+namespace pccl {
+
+using DevStream = void *; // hipStream_t
+using DevEvent = void *;  // hipEvent_t
+
+constexpr size_t kIpcHandleBytes = 64;
+
+struct DevPtrInfo {
+    bool is_device = false; // device (or managed) memory addressable by kernels
+    int device = -1;
+};
+
+class DeviceBackend {
+public:
+    virtual ~DeviceBackend() = default;
+
+    virtual int device_count() = 0;
+    virtual bool pointer_info(const void *p, DevPtrInfo &out) = 0;
+    virtual bool set_device(int dev) = 0;
+    virtual int current_device() = 0;
+
+    // memory
+    virtual void *alloc_device(size_t n) = 0;
+    virtual void free_device(void *p) = 0;
+    virtual void *alloc_pinned(size_t n) = 0; // host memory, device-mapped (kernels may read/write it)
+    virtual void free_pinned(void *p) = 0;
+    virtual bool ipc_export(void *dev_ptr, uint8_t handle[kIpcHandleBytes]) = 0;
+    virtual void *ipc_open(const uint8_t handle[kIpcHandleBytes]) = 0;
+    virtual void ipc_close(void *mapped) = 0;
+
+    // streams / events
+    virtual DevStream create_stream() = 0; // non-blocking stream on the current device
+    virtual void destroy_stream(DevStream s) = 0;
+    virtual bool stream_sync(DevStream s) = 0;
+    virtual DevEvent create_event() = 0;
+    virtual void destroy_event(DevEvent e) = 0;
+    virtual bool event_record(DevEvent e, DevStream s) = 0;
+    virtual int event_query(DevEvent e) = 0; // 1 complete, 0 pending, -1 error
+    virtual bool event_sync(DevEvent e) = 0;
+    virtual bool memcpy_async(void *dst, const void *src, size_t n, DevStream s) = 0; // any direction
+    virtual bool memcpy_sync(void *dst, const void *src, size_t n) = 0;
+    virtual bool device_sync() = 0;
+
+    // kernels
+    virtual bool reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, DevStream s) = 0;
+    virtual bool dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                                const kernels::QuantParams &p, DevStream s) = 0;
+    virtual bool quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
+                          const kernels::QuantParams &p, DevStream s) = 0;
+    // writes {min, max} as two doubles to `out2` (pinned host or device memory)
+    virtual bool minmax(const void *src, size_t count, DType vtype, double *out2, DevStream s) = 0;
+    virtual bool finalize_avg(void *dst, size_t count, DType t, size_t world_size, DevStream s) = 0;
+
+    // Intra-node xGMI kernels. srcs[k] points to shard `count` elements in peer k's buffer (IPC-mapped);
+    // dst0/dst1 receive op(srcs[0..n)) reduced in order 0..n-1 (dst1 may be null). Avg divides by n at the end.
+    virtual bool multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t,
+                              ReduceOp op, DevStream s) = 0;
+    // dst regions gathered from n sources: dst[k*stride ...] = srcs[k] for k != skip (count elements each,
+    // segment k has counts[k] elements at element offset offsets[k]).
+    virtual bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
+                              int skip, DType t, DevStream s) = 0;
+
+    // Simple hash of device memory (bit-identical to kernels::simplehash_host). Synchronous.
+    virtual uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) = 0;
+    // Fills device memory with the reference test pattern (random_init_kernel of the reference tests).
+    virtual bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) = 0;
+};
+
+// Returns the process-wide backend (nullptr if HIP is unavailable). Loaded lazily and thread-safely.
+DeviceBackend *device_backend();
+bool device_backend_available();
+
+} // namespace pccl
+
+// Plugin entry point (exported by libpccl_hip.so).
+extern "C" pccl::DeviceBackend *pccl_create_hip_backend();

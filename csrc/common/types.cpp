@@ -1,0 +1,129 @@
+#include "types.hpp"
+
+#include <arpa/inet.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fcntl.h>
+#include <random>
+#include <unistd.h>
+
+namespace pccl {
+
+const char *dtype_name(DType t) {
+    switch (t) {
+        case DType::U8: return "uint8";
+        case DType::I8: return "int8";
+        case DType::U16: return "uint16";
+        case DType::U32: return "uint32";
+        case DType::I16: return "int16";
+        case DType::I32: return "int32";
+        case DType::U64: return "uint64";
+        case DType::I64: return "int64";
+        case DType::F16: return "float16";
+        case DType::BF16: return "bfloat16";
+        case DType::F32: return "float32";
+        case DType::F64: return "float64";
+        case DType::F8E4M3: return "float8_e4m3";
+        case DType::F8E5M2: return "float8_e5m2";
+    }
+    return "?";
+}
+
+std::string Uuid::str() const {
+    char buf[40];
+    int p = 0;
+    for (size_t i = 0; i < 16; ++i) {
+        if (i == 4 || i == 6 || i == 8 || i == 10) buf[p++] = '-';
+        p += std::snprintf(buf + p, sizeof(buf) - p, "%02x", data[i]);
+    }
+    return std::string(buf, p);
+}
+
+Uuid Uuid::random() {
+    // UUIDv4 from the kernel CSPRNG (fallback: random_device)
+    Uuid u;
+    bool ok = false;
+    const int fd = ::open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+    if (fd >= 0) {
+        ok = ::read(fd, u.data.data(), 16) == 16;
+        ::close(fd);
+    }
+    if (!ok) {
+        std::random_device rd;
+        for (auto &b : u.data) b = static_cast<uint8_t>(rd());
+    }
+    u.data[6] = (u.data[6] & 0x0f) | 0x40;
+    u.data[8] = (u.data[8] & 0x3f) | 0x80;
+    return u;
+}
+
+std::string sockaddr_str(const SockAddr &a) {
+    char buf[INET6_ADDRSTRLEN + 16];
+    if (a.inet.protocol == inetIPv4) {
+        inet_ntop(AF_INET, a.inet.ipv4.data, buf, sizeof(buf));
+        return std::string(buf) + ":" + std::to_string(a.port);
+    }
+    inet_ntop(AF_INET6, a.inet.ipv6.data, buf, sizeof(buf));
+    return "[" + std::string(buf) + "]:" + std::to_string(a.port);
+}
+
+bool sockaddr_equal(const SockAddr &a, const SockAddr &b) { return SockAddrKey::of(a) == SockAddrKey::of(b); }
+
+bool sockaddr_is_loopback(const SockAddr &a) {
+    if (a.inet.protocol == inetIPv4) return a.inet.ipv4.data[0] == 127;
+    for (int i = 0; i < 15; ++i)
+        if (a.inet.ipv6.data[i] != 0) return false;
+    return a.inet.ipv6.data[15] == 1;
+}
+
+bool sockaddr_is_zero(const SockAddr &a) {
+    if (a.port != 0) return false;
+    if (a.inet.protocol == inetIPv4) {
+        for (auto b : a.inet.ipv4.data)
+            if (b) return false;
+        return true;
+    }
+    for (auto b : a.inet.ipv6.data)
+        if (b) return false;
+    return true;
+}
+
+SockAddr make_sockaddr_v4(uint8_t a, uint8_t b, uint8_t c, uint8_t d, uint16_t port) {
+    SockAddr s{};
+    s.inet.protocol = inetIPv4;
+    s.inet.ipv4.data[0] = a;
+    s.inet.ipv4.data[1] = b;
+    s.inet.ipv4.data[2] = c;
+    s.inet.ipv4.data[3] = d;
+    s.port = port;
+    return s;
+}
+
+SockAddrKey SockAddrKey::of(const SockAddr &a) {
+    SockAddrKey k;
+    k.v4 = a.inet.protocol == inetIPv4;
+    if (k.v4)
+        std::memcpy(k.ip.data(), a.inet.ipv4.data, 4);
+    else
+        std::memcpy(k.ip.data(), a.inet.ipv6.data, 16);
+    k.port = a.port;
+    return k;
+}
+
+size_t env_size(const char *name, size_t dflt) {
+    const char *v = std::getenv(name);
+    if (v == nullptr || *v == 0) return dflt;
+    char *end = nullptr;
+    const unsigned long long x = std::strtoull(v, &end, 10);
+    if (end == v) return dflt;
+    return static_cast<size_t>(x);
+}
+
+bool env_flag(const char *name, bool dflt) {
+    const char *v = std::getenv(name);
+    if (v == nullptr || *v == 0) return dflt;
+    return !(v[0] == '0' || v[0] == 'f' || v[0] == 'F' || v[0] == 'n' || v[0] == 'N');
+}
+
+} // namespace pccl

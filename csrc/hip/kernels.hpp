@@ -1,0 +1,417 @@
+// HIP/CDNA4 kernels of pccl-amd. Header-only templates included by hip_backend.hip (single translation unit).
+//
+// Design notes (MI355X / gfx950):
+//  * wave64, 256-thread workgroups (4 waves), grid-stride loops with the grid capped at 256 CUs x 8 WGs.
+//  * Bit-exactness first: every arithmetic expression comes from csrc/common/numeric.hpp, csrc/kernels/elem.hpp and
+//    csrc/kernels/quant_common.hpp, compiled with -ffp-contract=off exactly like the host SIMD loops, so a peer
+//    reducing on the CPU and a peer reducing on an MI355X produce identical bytes.
+//  * Ring/TCP-path kernels (reduce, dequant_reduce, quantize) read or write pinned host memory directly (zero-copy
+//    over PCIe) — no staging H2D/D2H memcpy — and are bound by the network, so they use coalesced scalar element
+//    access which works for the arbitrary (unaligned) chunk offsets of the ring.
+//  * Intra-node xGMI kernels (multi_reduce / multi_gather) are bandwidth-critical: 16-byte vector loads
+//    (global_load_dwordx4) from up to 16 IPC-mapped peer buffers per thread, two vectors in flight per source,
+//    fp32 accumulation in fixed peer order, one rounding at the end.
+//  * simplehash emulates the reference's 32-lane warp tree inside wave64 with __shfl_down(width=32).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../common/numeric.hpp"
+#include "../common/types.hpp"
+#include "../kernels/elem.hpp"
+#include "../kernels/quant_common.hpp"
+
+namespace pccl::hipk {
+
+using namespace pccl::kernels;
+
+constexpr int kBlock = 256;
+constexpr int kMaxGrid = 2048;
+constexpr int kMaxSrc = 16;
+
+inline int grid_for(size_t work_items, int per_thread = 1) {
+    const size_t threads = (work_items + per_thread - 1) / per_thread;
+    size_t g = (threads + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > static_cast<size_t>(kMaxGrid)) g = kMaxGrid;
+    return static_cast<int>(g);
+}
+
+// ---------------------------------------------------------------- elementwise reduce (ring path)
+template<typename E, typename Op>
+__global__ __launch_bounds__(kBlock) void k_reduce(typename E::S *__restrict__ dst, const typename E::S *__restrict__ src,
+                                                   size_t n) {
+    using C = typename E::C;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), E::ld(src[i])));
+}
+
+// ---------------------------------------------------------------- fused dequant + reduce
+template<typename Q>
+struct QInt {
+    using T = Q;
+    static __device__ __forceinline__ double deq_d(T q, const QuantParams &p) {
+        return dq_minmax_int(static_cast<double>(q), p);
+    }
+};
+
+template<typename E, typename Op, typename Q>
+__global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
+                                                      QuantParams p) {
+    using C = typename E::C;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const C v = static_cast<C>(dq_minmax_int(static_cast<double>(src[i]), p));
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
+    }
+}
+
+template<typename E, typename Op, bool E4M3>
+__global__ __launch_bounds__(kBlock) void k_dq_fp8(typename E::S *__restrict__ dst, const uint8_t *__restrict__ src, size_t n,
+                                                   QuantParams p) {
+    using C = typename E::C;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const float f = (E4M3 ? num::fp8e4m3_to_f32(src[i]) : num::fp8e5m2_to_f32(src[i])) * p.f8_inv;
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
+    }
+}
+
+template<typename E, typename Op, typename Q>
+__global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
+                                                   QuantParams p) {
+    using C = typename E::C;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const float f = dq_zps(static_cast<int64_t>(src[i]), p);
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
+    }
+}
+
+// ---------------------------------------------------------------- quantize
+template<typename E, typename Q>
+__global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+                                                     QuantParams p) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const double q = q_minmax_int(static_cast<double>(E::ld(src[i])), p);
+        if constexpr (sizeof(Q) == 8 && !__is_signed(Q)) {
+            dst[i] = q >= 18446744073709551615.0 ? ~0ull : static_cast<uint64_t>(q);
+        } else if constexpr (sizeof(Q) == 8) {
+            dst[i] = q >= 9223372036854775807.0 ? INT64_MAX : static_cast<int64_t>(q);
+        } else {
+            dst[i] = static_cast<Q>(static_cast<int64_t>(q));
+        }
+    }
+}
+
+template<typename E, bool E4M3>
+__global__ __launch_bounds__(kBlock) void k_q_fp8(uint8_t *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+                                                  QuantParams p) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const float x = static_cast<float>(E::ld(src[i])) * p.f8_scale;
+        dst[i] = E4M3 ? num::f32_to_fp8e4m3(x) : num::f32_to_fp8e5m2(x);
+    }
+}
+
+template<typename E, typename Q>
+__global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+                                                  QuantParams p) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+        dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p));
+}
+
+// ---------------------------------------------------------------- min / max (two pass, exact)
+__device__ __forceinline__ void wave_minmax(double &lo, double &hi) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double l2 = __shfl_xor(lo, off, 64);
+        const double h2 = __shfl_xor(hi, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+}
+
+template<typename E>
+__global__ __launch_bounds__(kBlock) void k_minmax_partial(const typename E::S *__restrict__ src, size_t n,
+                                                           double *__restrict__ partial) {
+    __shared__ double s_lo[kBlock / 64], s_hi[kBlock / 64];
+    double lo = __builtin_inf(), hi = -__builtin_inf();
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const double v = static_cast<double>(E::ld(src[i]));
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    wave_minmax(lo, hi);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            lo = s_lo[k] < lo ? s_lo[k] : lo;
+            hi = s_hi[k] > hi ? s_hi[k] : hi;
+        }
+        partial[2 * blockIdx.x] = lo;
+        partial[2 * blockIdx.x + 1] = hi;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_minmax_final(const double *__restrict__ partial, int nblocks, size_t n,
+                                                         double *__restrict__ out) {
+    __shared__ double s_lo[kBlock / 64], s_hi[kBlock / 64];
+    double lo = __builtin_inf(), hi = -__builtin_inf();
+    for (int i = threadIdx.x; i < nblocks; i += kBlock) {
+        lo = partial[2 * i] < lo ? partial[2 * i] : lo;
+        hi = partial[2 * i + 1] > hi ? partial[2 * i + 1] : hi;
+    }
+    wave_minmax(lo, hi);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            lo = s_lo[k] < lo ? s_lo[k] : lo;
+            hi = s_hi[k] > hi ? s_hi[k] : hi;
+        }
+        out[0] = n ? lo : 0.0;
+        out[1] = n ? hi : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- AVG finalize
+template<typename E>
+__global__ __launch_bounds__(kBlock) void k_avg(typename E::S *__restrict__ dst, size_t n, size_t ws) {
+    using C = typename E::C;
+    const C w = static_cast<C>(ws);
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+        dst[i] = E::st(static_cast<C>(E::ld(dst[i]) / w));
+}
+
+// ---------------------------------------------------------------- xGMI multi-source reduce
+struct SrcList {
+    const void *p[kMaxSrc];
+};
+
+// One 16-byte vector holds VEC elements of storage type S.
+template<typename E>
+struct Vec {
+    using S = typename E::S;
+    static constexpr int N = 16 / sizeof(S);
+};
+
+template<typename E, typename Op, bool AVG, int MAXN>
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(typename E::S *__restrict__ dst0, typename E::S *__restrict__ dst1,
+                                                             SrcList srcs, int nsrc, size_t nvec) {
+    using S = typename E::S;
+    using C = typename E::C;
+    constexpr int V = Vec<E>::N;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    for (size_t i = tid; i < nvec; i += 2 * stride) {
+        const size_t j = i + stride;
+        const bool has2 = j < nvec;
+        C acc0[V], acc1[V];
+        uint4 in0[MAXN], in1[MAXN];
+        // issue every load first: 2 * nsrc independent 16-byte loads in flight over the xGMI links
+#pragma unroll
+        for (int k = 0; k < MAXN; ++k) {
+            if (k < nsrc) {
+                in0[k] = reinterpret_cast<const uint4 *>(srcs.p[k])[i];
+                if (has2) in1[k] = reinterpret_cast<const uint4 *>(srcs.p[k])[j];
+            }
+        }
+        {
+            const S *s0 = reinterpret_cast<const S *>(&in0[0]);
+            const S *s1 = reinterpret_cast<const S *>(&in1[0]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                acc0[e] = E::ld(s0[e]);
+                acc1[e] = has2 ? E::ld(s1[e]) : C(0);
+            }
+        }
+#pragma unroll
+        for (int k = 1; k < MAXN; ++k) {
+            if (k < nsrc) {
+                const S *s0 = reinterpret_cast<const S *>(&in0[k]);
+                const S *s1 = reinterpret_cast<const S *>(&in1[k]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    acc0[e] = apply_op<Op, C>(acc0[e], E::ld(s0[e]));
+                    if (has2) acc1[e] = apply_op<Op, C>(acc1[e], E::ld(s1[e]));
+                }
+            }
+        }
+        uint4 out0, out1;
+        S *o0 = reinterpret_cast<S *>(&out0);
+        S *o1 = reinterpret_cast<S *>(&out1);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            if (AVG) {
+                acc0[e] = static_cast<C>(acc0[e] / static_cast<C>(nsrc));
+                acc1[e] = static_cast<C>(acc1[e] / static_cast<C>(nsrc));
+            }
+            o0[e] = E::st(acc0[e]);
+            o1[e] = E::st(acc1[e]);
+        }
+        reinterpret_cast<uint4 *>(dst0)[i] = out0;
+        if (dst1) reinterpret_cast<uint4 *>(dst1)[i] = out0;
+        if (has2) {
+            reinterpret_cast<uint4 *>(dst0)[j] = out1;
+            if (dst1) reinterpret_cast<uint4 *>(dst1)[j] = out1;
+        }
+    }
+}
+
+template<typename E, typename Op, bool AVG>
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(typename E::S *__restrict__ dst0, typename E::S *__restrict__ dst1,
+                                                                SrcList srcs, int nsrc, size_t n, size_t begin) {
+    using S = typename E::S;
+    using C = typename E::C;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = begin + static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        C acc = E::ld(static_cast<const S *>(srcs.p[0])[i]);
+        for (int k = 1; k < nsrc; ++k) acc = apply_op<Op, C>(acc, E::ld(static_cast<const S *>(srcs.p[k])[i]));
+        if (AVG) acc = static_cast<C>(acc / static_cast<C>(nsrc));
+        const S v = E::st(acc);
+        dst0[i] = v;
+        if (dst1) dst1[i] = v;
+    }
+}
+
+// ---------------------------------------------------------------- xGMI multi-source gather (all-gather phase)
+struct GatherList {
+    const void *src[kMaxSrc];
+    size_t off[kMaxSrc];   // destination byte offset of segment k
+    size_t bytes[kMaxSrc]; // bytes of segment k
+};
+
+__global__ __launch_bounds__(kBlock) void k_multi_gather(uint8_t *__restrict__ dst, GatherList g, int n, int skip) {
+    // blockIdx.y selects the segment: every peer's segment is streamed concurrently over its own xGMI link
+    const int k = blockIdx.y;
+    if (k >= n || k == skip) return;
+    const uint8_t *src = static_cast<const uint8_t *>(g.src[k]);
+    uint8_t *d = dst + g.off[k];
+    const size_t bytes = g.bytes[k];
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (aligned) {
+        const size_t nvec = bytes / 16;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(d);
+        size_t i = tid;
+        for (; i + 3 * stride < nvec; i += 4 * stride) {
+            const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], e = s4[i + 3 * stride];
+            d4[i] = a;
+            d4[i + stride] = b;
+            d4[i + 2 * stride] = c;
+            d4[i + 3 * stride] = e;
+        }
+        for (; i < nvec; i += stride) d4[i] = s4[i];
+        for (size_t b = nvec * 16 + tid; b < bytes; b += stride) d[b] = src[b];
+    } else {
+        for (size_t b = tid; b < bytes; b += stride) d[b] = src[b];
+    }
+}
+
+// ---------------------------------------------------------------- simplehash
+__device__ __forceinline__ uint32_t hcomb(uint32_t a, uint32_t b) {
+    a ^= b + 0x9e3779b1u;
+    a = (a << 7) | (a >> 25);
+    return a * 0x85ebca6bu;
+}
+
+// 256-thread block reduction with the reference's exact 32-lane tree (8 groups of 32, then 8 partials + 24 zeros).
+__device__ __forceinline__ uint32_t block_tree256(uint32_t v, uint32_t *lds8) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) v = hcomb(v, __shfl_down(v, off, 32));
+    const int t = threadIdx.x;
+    if ((t & 31) == 0) lds8[t >> 5] = v;
+    __syncthreads();
+    uint32_t r = 0;
+    if (t < 32) {
+        r = t < 8 ? lds8[t] : 0u;
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) r = hcomb(r, __shfl_down(r, off, 32));
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_hash_big(const uint4 *__restrict__ d4, uint32_t *__restrict__ partial,
+                                                     size_t n_vec, size_t vpb) {
+    __shared__ uint32_t lds8[8];
+    const size_t start = static_cast<size_t>(blockIdx.x) * vpb;
+    size_t end = start + vpb;
+    if (end > n_vec) end = n_vec;
+    uint32_t h = 0;
+    size_t i = start + threadIdx.x;
+    // software pipeline: 8 independent 16-byte loads in flight ahead of the serial hash chain
+    constexpr int D = 8;
+    for (; i + (D - 1) * kBlock < end; i += D * kBlock) {
+        uint4 v[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[k] = d4[i + k * kBlock];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            h = hcomb(h, v[k].x);
+            h = hcomb(h, v[k].y);
+            h = hcomb(h, v[k].z);
+            h = hcomb(h, v[k].w);
+        }
+    }
+    for (; i < end; i += kBlock) {
+        const uint4 v = d4[i];
+        h = hcomb(h, v.x);
+        h = hcomb(h, v.y);
+        h = hcomb(h, v.z);
+        h = hcomb(h, v.w);
+    }
+    const uint32_t r = block_tree256(h, lds8);
+    if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
+// final pass + tail words/bytes handled on device; writes the 32-bit hash to out[0]
+__global__ __launch_bounds__(kBlock) void k_hash_final(const uint32_t *__restrict__ partial, int nblocks,
+                                                       const uint8_t *__restrict__ data, size_t n_bytes,
+                                                       uint32_t *__restrict__ out) {
+    __shared__ uint32_t lds8[8];
+    uint32_t h = 0;
+    for (int i = threadIdx.x; i < nblocks; i += kBlock) h = hcomb(h, partial[i]);
+    uint32_t r = block_tree256(h, lds8);
+    if (nblocks == 0) r = 0;
+    if (threadIdx.x == 0) {
+        const size_t n_words = n_bytes / 4;
+        const size_t n_vec = n_words / 4;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(data);
+        for (size_t k = n_vec * 4; k < n_words; ++k) r = hcomb(r, w[k]);
+        const size_t tail = n_bytes % 4;
+        if (tail) {
+            uint32_t v = 0;
+            for (size_t k = 0; k < tail; ++k) v |= static_cast<uint32_t>(data[n_words * 4 + k]) << (8 * k);
+            r = hcomb(r, v);
+        }
+        out[0] = r;
+    }
+}
+
+// reference test pattern (ccoip/tests/unit_tests/simple_hash/simplehash_cpu_test.cu:17-23), launched <<<8, 256>>>
+__global__ void k_test_pattern(uint64_t *data, size_t N) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nt = blockDim.x * gridDim.x;
+    for (size_t i = tid; i < N; i += nt) data[i] = ((tid * nt) ^ (i & N)) * 0xaabaababab1ull;
+}
+
+} // namespace pccl::hipk

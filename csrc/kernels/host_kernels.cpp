@@ -1,0 +1,433 @@
+#include "host_kernels.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <vector>
+
+#include "../common/log.hpp"
+#include "elem.hpp"
+
+namespace pccl::kernels {
+
+// ------------------------------------------------------------------------------------------------------------------
+// reduce
+// ------------------------------------------------------------------------------------------------------------------
+template<typename E, typename Op>
+static void reduce_loop(void *dst_v, const void *src_v, size_t n) {
+    using S = typename E::S;
+    using C = typename E::C;
+    auto *__restrict dst = static_cast<S *>(dst_v);
+    const auto *__restrict src = static_cast<const S *>(src_v);
+    for (size_t i = 0; i < n; ++i) dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), E::ld(src[i])));
+}
+
+template<typename E>
+static bool reduce_op(void *dst, const void *src, size_t n, ReduceOp op) {
+    switch (op) {
+        case ReduceOp::Set: std::memmove(dst, src, n * sizeof(typename E::S)); return true;
+        case ReduceOp::Sum:
+        case ReduceOp::Avg: reduce_loop<E, OpSum>(dst, src, n); return true;
+        case ReduceOp::Prod: reduce_loop<E, OpProd>(dst, src, n); return true;
+        case ReduceOp::Max: reduce_loop<E, OpMax>(dst, src, n); return true;
+        case ReduceOp::Min: reduce_loop<E, OpMin>(dst, src, n); return true;
+    }
+    return false;
+}
+
+bool host_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op) {
+    switch (t) {
+        case DType::F32: return reduce_op<EF32>(dst, src, count, op);
+        case DType::F64: return reduce_op<EF64>(dst, src, count, op);
+        case DType::BF16: return reduce_op<EBF16>(dst, src, count, op);
+        case DType::F16: return reduce_op<EF16>(dst, src, count, op);
+        case DType::U8: return reduce_op<EInt<uint8_t>>(dst, src, count, op);
+        case DType::I8: return reduce_op<EInt<int8_t>>(dst, src, count, op);
+        case DType::U16: return reduce_op<EInt<uint16_t>>(dst, src, count, op);
+        case DType::I16: return reduce_op<EInt<int16_t>>(dst, src, count, op);
+        case DType::U32: return reduce_op<EInt<uint32_t>>(dst, src, count, op);
+        case DType::I32: return reduce_op<EInt<int32_t>>(dst, src, count, op);
+        case DType::U64: return reduce_op<EInt<uint64_t>>(dst, src, count, op);
+        case DType::I64: return reduce_op<EInt<int64_t>>(dst, src, count, op);
+        default: break;
+    }
+    LOG(ERR) << "host_reduce: unsupported dtype " << dtype_name(t);
+    return false;
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// min / max
+// ------------------------------------------------------------------------------------------------------------------
+template<typename E>
+static void minmax_loop(const void *src_v, size_t n, double &mn, double &mx) {
+    using S = typename E::S;
+    const auto *src = static_cast<const S *>(src_v);
+    double lo = std::numeric_limits<double>::infinity(), hi = -std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < n; ++i) {
+        const double v = static_cast<double>(E::ld(src[i]));
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    mn = n ? lo : 0.0;
+    mx = n ? hi : 0.0;
+}
+
+void host_minmax(const void *src, size_t count, DType vtype, double &mn, double &mx) {
+    switch (vtype) {
+        case DType::F32: minmax_loop<EF32>(src, count, mn, mx); return;
+        case DType::F64: minmax_loop<EF64>(src, count, mn, mx); return;
+        case DType::BF16: minmax_loop<EBF16>(src, count, mn, mx); return;
+        case DType::F16: minmax_loop<EF16>(src, count, mn, mx); return;
+        default: mn = mx = 0; return;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// quantize / dequantize
+// ------------------------------------------------------------------------------------------------------------------
+template<typename E, typename Q>
+static void quant_minmax_int(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    const auto *src = static_cast<const typename E::S *>(src_v);
+    auto *dst = static_cast<Q *>(dst_v);
+    for (size_t i = 0; i < n; ++i) {
+        const double q = q_minmax_int(static_cast<double>(E::ld(src[i])), p);
+        if constexpr (std::is_same_v<Q, uint64_t>) {
+            dst[i] = q >= 18446744073709551615.0 ? ~0ull : static_cast<uint64_t>(q);
+        } else if constexpr (std::is_same_v<Q, int64_t>) {
+            dst[i] = q >= 9223372036854775807.0 ? INT64_MAX : static_cast<int64_t>(q);
+        } else {
+            dst[i] = static_cast<Q>(static_cast<int64_t>(q));
+        }
+    }
+}
+
+template<typename E, bool E4M3>
+static void quant_fp8(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    const auto *src = static_cast<const typename E::S *>(src_v);
+    auto *dst = static_cast<uint8_t *>(dst_v);
+    for (size_t i = 0; i < n; ++i) {
+        const float x = static_cast<float>(E::ld(src[i])) * p.f8_scale;
+        dst[i] = E4M3 ? num::f32_to_fp8e4m3(x) : num::f32_to_fp8e5m2(x);
+    }
+}
+
+template<typename E, typename Q>
+static void quant_zps(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    const auto *src = static_cast<const typename E::S *>(src_v);
+    auto *dst = static_cast<Q *>(dst_v);
+    for (size_t i = 0; i < n; ++i) dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p));
+}
+
+template<typename E, typename Op, typename Q>
+static void dq_minmax_int_loop(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    using C = typename E::C;
+    auto *dst = static_cast<typename E::S *>(dst_v);
+    const auto *src = static_cast<const Q *>(src_v);
+    for (size_t i = 0; i < n; ++i) {
+        const C v = static_cast<C>(dq_minmax_int(static_cast<double>(src[i]), p));
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
+    }
+}
+
+template<typename E, typename Op, bool E4M3>
+static void dq_fp8_loop(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    using C = typename E::C;
+    auto *dst = static_cast<typename E::S *>(dst_v);
+    const auto *src = static_cast<const uint8_t *>(src_v);
+    for (size_t i = 0; i < n; ++i) {
+        const float f = (E4M3 ? num::fp8e4m3_to_f32(src[i]) : num::fp8e5m2_to_f32(src[i])) * p.f8_inv;
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
+    }
+}
+
+template<typename E, typename Op, typename Q>
+static void dq_zps_loop(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
+    using C = typename E::C;
+    auto *dst = static_cast<typename E::S *>(dst_v);
+    const auto *src = static_cast<const Q *>(src_v);
+    for (size_t i = 0; i < n; ++i) {
+        const float f = dq_zps(static_cast<int64_t>(src[i]), p);
+        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
+    }
+}
+
+template<typename E>
+static bool quantize_v(void *dst_q, const void *src, size_t n, DType qtype, const QuantParams &p) {
+    if (p.algo == QuantAlgo::MinMax) {
+        switch (qtype) {
+            case DType::U8: quant_minmax_int<E, uint8_t>(dst_q, src, n, p); return true;
+            case DType::I8: quant_minmax_int<E, int8_t>(dst_q, src, n, p); return true;
+            case DType::U16: quant_minmax_int<E, uint16_t>(dst_q, src, n, p); return true;
+            case DType::I16: quant_minmax_int<E, int16_t>(dst_q, src, n, p); return true;
+            case DType::U32: quant_minmax_int<E, uint32_t>(dst_q, src, n, p); return true;
+            case DType::I32: quant_minmax_int<E, int32_t>(dst_q, src, n, p); return true;
+            case DType::U64: quant_minmax_int<E, uint64_t>(dst_q, src, n, p); return true;
+            case DType::I64: quant_minmax_int<E, int64_t>(dst_q, src, n, p); return true;
+            case DType::F8E4M3: quant_fp8<E, true>(dst_q, src, n, p); return true;
+            case DType::F8E5M2: quant_fp8<E, false>(dst_q, src, n, p); return true;
+            default: return false;
+        }
+    }
+    if (p.algo == QuantAlgo::ZeroPointScale) {
+        switch (qtype) {
+            case DType::U8: quant_zps<E, uint8_t>(dst_q, src, n, p); return true;
+            case DType::I8: quant_zps<E, int8_t>(dst_q, src, n, p); return true;
+            case DType::U16: quant_zps<E, uint16_t>(dst_q, src, n, p); return true;
+            case DType::I16: quant_zps<E, int16_t>(dst_q, src, n, p); return true;
+            case DType::U32: quant_zps<E, uint32_t>(dst_q, src, n, p); return true;
+            case DType::I32: quant_zps<E, int32_t>(dst_q, src, n, p); return true;
+            default: return false;
+        }
+    }
+    return false;
+}
+
+proto::QuantMeta host_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, QuantAlgo algo) {
+    double mn = 0, mx = 0;
+    host_minmax(src, count, vtype, mn, mx);
+    proto::QuantMeta meta = make_meta(algo, vtype, qtype, mn, mx);
+    const QuantParams p = make_params(meta, qtype);
+    bool ok = false;
+    switch (vtype) {
+        case DType::F32: ok = quantize_v<EF32>(dst_q, src, count, qtype, p); break;
+        case DType::F64: ok = quantize_v<EF64>(dst_q, src, count, qtype, p); break;
+        case DType::BF16: ok = quantize_v<EBF16>(dst_q, src, count, qtype, p); break;
+        case DType::F16: ok = quantize_v<EF16>(dst_q, src, count, qtype, p); break;
+        default: break;
+    }
+    if (!ok) LOG(ERR) << "host_quantize: unsupported combination " << dtype_name(vtype) << " -> " << dtype_name(qtype);
+    return meta;
+}
+
+template<typename E, typename Op>
+static bool dequant_v(void *dst, const void *src_q, size_t n, DType qtype, const QuantParams &p) {
+    if (p.algo == QuantAlgo::MinMax) {
+        switch (qtype) {
+            case DType::U8: dq_minmax_int_loop<E, Op, uint8_t>(dst, src_q, n, p); return true;
+            case DType::I8: dq_minmax_int_loop<E, Op, int8_t>(dst, src_q, n, p); return true;
+            case DType::U16: dq_minmax_int_loop<E, Op, uint16_t>(dst, src_q, n, p); return true;
+            case DType::I16: dq_minmax_int_loop<E, Op, int16_t>(dst, src_q, n, p); return true;
+            case DType::U32: dq_minmax_int_loop<E, Op, uint32_t>(dst, src_q, n, p); return true;
+            case DType::I32: dq_minmax_int_loop<E, Op, int32_t>(dst, src_q, n, p); return true;
+            case DType::U64: dq_minmax_int_loop<E, Op, uint64_t>(dst, src_q, n, p); return true;
+            case DType::I64: dq_minmax_int_loop<E, Op, int64_t>(dst, src_q, n, p); return true;
+            case DType::F8E4M3: dq_fp8_loop<E, Op, true>(dst, src_q, n, p); return true;
+            case DType::F8E5M2: dq_fp8_loop<E, Op, false>(dst, src_q, n, p); return true;
+            default: return false;
+        }
+    }
+    if (p.algo == QuantAlgo::ZeroPointScale) {
+        switch (qtype) {
+            case DType::U8: dq_zps_loop<E, Op, uint8_t>(dst, src_q, n, p); return true;
+            case DType::I8: dq_zps_loop<E, Op, int8_t>(dst, src_q, n, p); return true;
+            case DType::U16: dq_zps_loop<E, Op, uint16_t>(dst, src_q, n, p); return true;
+            case DType::I16: dq_zps_loop<E, Op, int16_t>(dst, src_q, n, p); return true;
+            case DType::U32: dq_zps_loop<E, Op, uint32_t>(dst, src_q, n, p); return true;
+            case DType::I32: dq_zps_loop<E, Op, int32_t>(dst, src_q, n, p); return true;
+            default: return false;
+        }
+    }
+    return false;
+}
+
+template<typename E>
+static bool dequant_op(void *dst, const void *src_q, size_t n, DType qtype, ReduceOp op, const QuantParams &p) {
+    switch (op) {
+        case ReduceOp::Set: return dequant_v<E, OpSet>(dst, src_q, n, qtype, p);
+        case ReduceOp::Sum:
+        case ReduceOp::Avg: return dequant_v<E, OpSum>(dst, src_q, n, qtype, p);
+        case ReduceOp::Prod: return dequant_v<E, OpProd>(dst, src_q, n, qtype, p);
+        case ReduceOp::Max: return dequant_v<E, OpMax>(dst, src_q, n, qtype, p);
+        case ReduceOp::Min: return dequant_v<E, OpMin>(dst, src_q, n, qtype, p);
+    }
+    return false;
+}
+
+bool host_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                         const proto::QuantMeta &meta) {
+    const QuantParams p = make_params(meta, qtype);
+    switch (vtype) {
+        case DType::F32: return dequant_op<EF32>(dst, src_q, count, qtype, op, p);
+        case DType::F64: return dequant_op<EF64>(dst, src_q, count, qtype, op, p);
+        case DType::BF16: return dequant_op<EBF16>(dst, src_q, count, qtype, op, p);
+        case DType::F16: return dequant_op<EF16>(dst, src_q, count, qtype, op, p);
+        default: return false;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// AVG finalization
+// ------------------------------------------------------------------------------------------------------------------
+template<typename E>
+static void avg_loop(void *dst_v, size_t n, size_t ws) {
+    using C = typename E::C;
+    auto *dst = static_cast<typename E::S *>(dst_v);
+    const C w = static_cast<C>(ws);
+    for (size_t i = 0; i < n; ++i) dst[i] = E::st(static_cast<C>(E::ld(dst[i]) / w));
+}
+
+bool host_finalize_avg(void *dst, size_t count, DType t, size_t ws) {
+    if (ws == 0) return false;
+    switch (t) {
+        case DType::F32: avg_loop<EF32>(dst, count, ws); return true;
+        case DType::F64: avg_loop<EF64>(dst, count, ws); return true;
+        case DType::BF16: avg_loop<EBF16>(dst, count, ws); return true;
+        case DType::F16: avg_loop<EF16>(dst, count, ws); return true;
+        case DType::U8: avg_loop<EInt<uint8_t>>(dst, count, ws); return true;
+        case DType::I8: avg_loop<EInt<int8_t>>(dst, count, ws); return true;
+        case DType::U16: avg_loop<EInt<uint16_t>>(dst, count, ws); return true;
+        case DType::I16: avg_loop<EInt<int16_t>>(dst, count, ws); return true;
+        case DType::U32: avg_loop<EInt<uint32_t>>(dst, count, ws); return true;
+        case DType::I32: avg_loop<EInt<int32_t>>(dst, count, ws); return true;
+        case DType::U64: avg_loop<EInt<uint64_t>>(dst, count, ws); return true;
+        case DType::I64: avg_loop<EInt<int64_t>>(dst, count, ws); return true;
+        default: return false;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// simplehash (host emulation of the 960 x 256 launch, 32-lane shuffle trees)
+// ------------------------------------------------------------------------------------------------------------------
+static inline uint32_t hc(uint32_t a, uint32_t b) {
+    a ^= b + 0x9e3779b1u;
+    a = (a << 7) | (a >> 25);
+    return a * 0x85ebca6bu;
+}
+
+static uint32_t tree32(uint32_t *t) { // in-place 32-lane shuffle-down tree; returns lane 0
+    for (int off = 16; off > 0; off >>= 1)
+        for (int i = 0; i < off; ++i) t[i] = hc(t[i], t[i + off]);
+    return t[0];
+}
+
+static uint32_t tree256(const uint32_t *acc) {
+    uint32_t warps[32] = {0};
+    uint32_t tmp[32];
+    for (int w = 0; w < 8; ++w) {
+        std::memcpy(tmp, acc + w * 32, sizeof(tmp));
+        warps[w] = tree32(tmp);
+    }
+    return tree32(warps);
+}
+
+static uint32_t hash_block(const uint32_t *words, size_t n_vec, size_t vpb, size_t b) {
+    const size_t start = b * vpb;
+    const size_t end = std::min(start + vpb, n_vec);
+    uint32_t acc[256] = {0};
+    for (size_t i = start; i < end; i += 256) {
+        const size_t m = std::min<size_t>(256, end - i);
+        const uint32_t *v = words + i * 4;
+        for (size_t t = 0; t < m; ++t) {
+            uint32_t a = acc[t];
+            a = hc(a, v[t * 4 + 0]);
+            a = hc(a, v[t * 4 + 1]);
+            a = hc(a, v[t * 4 + 2]);
+            a = hc(a, v[t * 4 + 3]);
+            acc[t] = a;
+        }
+    }
+    return tree256(acc);
+}
+
+uint32_t simplehash_host(const void *data, size_t n_bytes) {
+    if (n_bytes == 0) return 0;
+    const auto *words = static_cast<const uint32_t *>(data);
+    const size_t n_words = n_bytes / 4;
+    const size_t n_vec = n_words / 4;
+    size_t grid = (n_vec + 255) / 256;
+    if (grid > 960) grid = 960;
+    uint32_t h = 0;
+    if (grid > 0) {
+        const size_t vpb = (n_vec + grid - 1) / grid;
+        std::vector<uint32_t> partial(grid);
+        const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency() / 2);
+        const size_t n_threads = n_bytes >= (32u << 20) ? std::min<size_t>(hw, grid) : 1;
+        if (n_threads <= 1) {
+            for (size_t b = 0; b < grid; ++b) partial[b] = hash_block(words, n_vec, vpb, b);
+        } else {
+            std::vector<std::thread> ts;
+            for (size_t t = 0; t < n_threads; ++t)
+                ts.emplace_back([&, t] {
+                    for (size_t b = t; b < grid; b += n_threads) partial[b] = hash_block(words, n_vec, vpb, b);
+                });
+            for (auto &t : ts) t.join();
+        }
+        uint32_t fin[256] = {0};
+        for (size_t b = 0; b < grid; ++b) fin[b % 256] = hc(fin[b % 256], partial[b]);
+        h = tree256(fin);
+    }
+    for (size_t i = n_vec * 4; i < n_words; ++i) h = hc(h, words[i]);
+    const size_t tail = n_bytes % 4;
+    if (tail) {
+        const auto *bytes = static_cast<const uint8_t *>(data) + n_words * 4;
+        uint32_t v = 0;
+        for (size_t i = 0; i < tail; ++i) v |= static_cast<uint32_t>(bytes[i]) << (8 * i);
+        h = hc(h, v);
+    }
+    return h;
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// CRC-32C
+// ------------------------------------------------------------------------------------------------------------------
+static uint32_t g_crc_table[8][256];
+static bool g_crc_init = false;
+static bool g_spoof_no_hw = false;
+
+static void crc_init() {
+    if (g_crc_init) return;
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+        g_crc_table[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+        for (int t = 1; t < 8; ++t) g_crc_table[t][i] = (g_crc_table[t - 1][i] >> 8) ^ g_crc_table[0][g_crc_table[t - 1][i] & 0xff];
+    g_crc_init = true;
+}
+
+uint32_t crc32c_sw(const void *data, size_t n) {
+    crc_init();
+    const auto *p = static_cast<const uint8_t *>(data);
+    uint32_t c = 0xffffffffu;
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        v ^= c;
+        c = g_crc_table[7][v & 0xff] ^ g_crc_table[6][(v >> 8) & 0xff] ^ g_crc_table[5][(v >> 16) & 0xff] ^
+            g_crc_table[4][(v >> 24) & 0xff] ^ g_crc_table[3][(v >> 32) & 0xff] ^ g_crc_table[2][(v >> 40) & 0xff] ^
+            g_crc_table[1][(v >> 48) & 0xff] ^ g_crc_table[0][v >> 56];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) c = (c >> 8) ^ g_crc_table[0][(c ^ *p++) & 0xff];
+    return ~c;
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(const void *data, size_t n) {
+    const auto *p = static_cast<const uint8_t *>(data);
+    uint64_t c = 0xffffffffu;
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        c = __builtin_ia32_crc32di(c, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t c32 = static_cast<uint32_t>(c);
+    while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+    return ~c32;
+}
+
+bool crc32c_has_hw() {
+    if (g_spoof_no_hw) return false;
+    return __builtin_cpu_supports("sse4.2");
+}
+
+void crc32c_spoof_no_hw(bool no_hw) { g_spoof_no_hw = no_hw; }
+
+uint32_t crc32c(const void *data, size_t n) { return crc32c_has_hw() ? crc32c_hw(data, n) : crc32c_sw(data, n); }
+
+} // namespace pccl::kernels

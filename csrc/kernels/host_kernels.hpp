@@ -1,0 +1,41 @@
+// Host (CPU) reduce / quantize / hash kernels. These serve host-memory collectives and are the bit-exact reference
+// for the HIP kernels (csrc/hip/*.hip), which must produce identical bytes.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../common/types.hpp"
+#include "../proto/packets.hpp"
+#include "quant_common.hpp"
+
+namespace pccl::kernels {
+
+// dst[i] = dst[i] (op) src[i] for `count` elements of `t`. op Set copies. Avg accumulates like Sum.
+bool host_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op);
+
+// dst[i] = dst[i] (op) dequant(src_q[i]) — fused de-quantization + accumulation (op Set = plain dequant).
+bool host_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                         const proto::QuantMeta &meta);
+
+// Computes metadata over src and quantizes into dst_q.
+proto::QuantMeta host_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, QuantAlgo algo);
+
+// min / max of a chunk as double.
+void host_minmax(const void *src, size_t count, DType vtype, double &mn, double &mx);
+
+// AVG finalization: dst[i] /= world_size (integer division for integer types).
+bool host_finalize_avg(void *dst, size_t count, DType t, size_t world_size);
+
+// "simplehash": non-associative 32-bit hash whose reduction tree emulates a 960x256 GPU launch with a 32-lane
+// shuffle tree (definition: reference ccoip/src/cuda/simplehash_cuda.cu). Requires 16-byte aligned data.
+uint32_t simplehash_host(const void *data, size_t n_bytes);
+
+// CRC-32C (Castagnoli). Uses SSE4.2 when available (and not spoofed off), otherwise slicing-by-8 tables.
+uint32_t crc32c(const void *data, size_t n_bytes);
+uint32_t crc32c_sw(const void *data, size_t n_bytes);
+uint32_t crc32c_hw(const void *data, size_t n_bytes);
+void crc32c_spoof_no_hw(bool no_hw); // test hook: force the software path
+bool crc32c_has_hw();
+
+} // namespace pccl::kernels

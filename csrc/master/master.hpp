@@ -1,0 +1,164 @@
+// Master coordinator: authoritative per-peer state machine + micro-consensus for every phase change
+// (reference behaviour: ccoip/src/cpp/ccoip_master_state.cpp and ccoip_master_handler.cpp).
+//
+// All state lives on the EventServer loop thread; the only other thread is the asynchronous "moonshot" ATSP
+// search, which hands its result back through `pending_rings_` and is applied at the start of the next P2P
+// establishment round (never in the middle of one).
+//
+// Deliberate divergences from the reference:
+//  * reachable-ring search uses mutual *reachability* as adjacency (reference used the unreachable set, #5)
+//  * topology task result is applied when it improved the tour (reference returned early on improvement, #4) and
+//    M2COptimizeTopologyComplete carries the ring order
+//  * revision-legality check of an unknown client cannot dereference an end iterator (#6)
+//  * a peer group whose latest-revision holders all died re-baselines instead of failing with "no distributor"
+//  * a mixed round of accept-new / no-new establish votes proceeds as "no new peers" instead of deadlocking
+//  * ring order survives membership changes (members keep their relative order, new peers are appended) instead of
+//    falling back to UUID order, so an optimized ring is not thrown away on every join/leave
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "../common/types.hpp"
+#include "../net/event_server.hpp"
+#include "../proto/packets.hpp"
+#include "topology.hpp"
+
+namespace pccl::master {
+
+enum class Phase { Registered, Accepted };
+
+enum class State {
+    Idle,
+    VoteAcceptNewPeers,
+    VoteNoNewPeersEstablishP2P,
+    ConnectingToPeers,
+    ConnectingToPeersFailed,
+    WaitingForOtherPeers,
+    VoteOptimizeTopology,
+    OptimizeTopology,
+    OptimizeTopologyFailed,
+    VoteCompleteTopologyOptimization,
+    VoteSyncSharedState,
+    DistributeSharedState,
+    RequestSharedState,
+    VoteCompleteSharedStateSync,
+    CollectiveCommsRunning
+};
+
+enum class CollState { VoteInitiate, Perform, VoteComplete };
+
+enum class SSStatus { Match, KeySetMismatch, ContentHashMismatch, RevisionOutdated, RevisionIncrementViolation };
+
+struct ClientInfo {
+    Uuid uuid;
+    SockAddr addr{};
+    Phase phase = Phase::Registered;
+    State state = State::Idle;
+    bool voted_pending_query = false;
+    std::map<uint64_t, CollState> colls;
+    uint32_t group = 0;
+    SockAddr p2p{}, ss{}, bm{};
+    uint64_t ss_revision = 0; // revision announced in the current shared-state round
+};
+
+struct GroupState {
+    std::vector<Uuid> ring;
+    bool ring_optimal = false;
+    bool optimized_once = false;
+    BandwidthStore bw;
+    uint64_t next_revision = 0;
+    // shared-state round
+    std::vector<std::pair<Uuid, std::vector<proto::SharedStateHashEntry>>> candidates, entries;
+    std::vector<proto::SharedStateHashEntry> mask;
+    std::map<Uuid, SSStatus> statuses;
+    std::map<std::string, uint64_t> hashes;
+    std::map<std::string, HashType> hash_types;
+    std::map<Uuid, std::vector<std::string>> dirty_keys;
+    std::map<Uuid, SyncStrategy> strategies;
+    std::map<uint64_t, bool> aborted; // per tag
+};
+
+class Master {
+public:
+    explicit Master(const SockAddr &listen_addr);
+    ~Master();
+
+    bool launch();    // listen + start loop thread (non-blocking)
+    bool interrupt(); // stop loop
+    bool join();      // wait for loop thread
+    uint16_t port() const { return server_.port(); }
+
+private:
+    // dispatch
+    void on_packet(const SockAddr &addr, uint16_t id, const uint8_t *payload, size_t n);
+    void on_disconnect(const SockAddr &addr);
+    void kick(const SockAddr &addr);
+
+    // handlers
+    void handle_join(const SockAddr &addr, const proto::C2MRequestSessionRegistration &p);
+    void handle_request_establish(const SockAddr &addr, bool accept_new);
+    void handle_p2p_established(const SockAddr &addr, const proto::C2MP2PConnectionsEstablished &p);
+    void handle_check_pending(const SockAddr &addr);
+    void handle_optimize(const SockAddr &addr);
+    void handle_report_bw(const SockAddr &addr, const proto::C2MReportPeerBandwidth &p);
+    void handle_optimize_work_complete(const SockAddr &addr);
+    void handle_sync_shared_state(const SockAddr &addr, const proto::C2MSyncSharedState &p);
+    void handle_dist_complete(const SockAddr &addr);
+    void handle_coll_initiate(const SockAddr &addr, const proto::C2MCollectiveCommsInitiate &p);
+    void handle_coll_complete(const SockAddr &addr, const proto::C2MCollectiveCommsComplete &p);
+
+    // consensus checks
+    void check_establish_consensus();
+    bool check_p2p_established();
+    void check_pending_query_consensus();
+    void check_optimize_consensus();
+    void check_optimize_complete_consensus();
+    bool check_sync_consensus(uint32_t group);
+    void check_sync_complete_consensus(uint32_t group);
+    void check_coll_initiate_consensus(uint32_t group, uint64_t tag);
+    void check_coll_complete_consensus(uint32_t group, uint64_t tag);
+    void send_abort(uint32_t group, uint64_t tag, bool aborted);
+
+    // helpers
+    ClientInfo *client_by_addr(const SockAddr &addr);
+    ClientInfo *client_by_uuid(const Uuid &u);
+    void on_peer_accepted(ClientInfo &c);
+    std::vector<Uuid> ring_of(uint32_t group, bool include_registered);
+    std::optional<std::vector<Uuid>> reachable_ring(uint32_t group);
+    uint64_t local_world_size(uint32_t group, bool include_registered) const;
+    uint64_t num_groups(bool include_registered) const;
+    uint64_t largest_group(bool include_registered) const;
+    void send_connection_info(bool include_registered);
+    void transition_to_establish(bool accept_new);
+    void apply_pending_rings();
+    void run_topology_optimization(uint32_t group);
+    SSStatus revision_status(ClientInfo &c, uint64_t revision);
+    bool elect_mask(uint32_t group);
+    void compute_mismatches(uint32_t group);
+    void end_sync_phase(uint32_t group);
+
+    net::EventServer server_;
+    std::map<Uuid, ClientInfo> clients_;
+    std::unordered_map<SockAddrKey, Uuid, SockAddrKeyHash> by_addr_;
+    std::map<uint32_t, GroupState> groups_;
+    uint64_t dist_rr_ = 0; // round-robin cursor over shared-state distributors
+    std::map<Uuid, std::set<Uuid>> unreachable_;
+    std::map<Uuid, std::vector<Uuid>> prev_neighbors_;
+    uint64_t next_seq_ = 0;
+    bool peer_dropped_ = false;
+    bool running_ = false;
+
+    // async moonshot optimization
+    std::mutex pending_mtx_;
+    std::map<uint32_t, std::pair<std::vector<Uuid>, bool>> pending_rings_;
+    std::vector<std::thread> optimizer_threads_;
+    std::atomic<bool> stopping_{false};
+};
+
+} // namespace pccl::master

@@ -1,0 +1,99 @@
+#include "master_conn.hpp"
+
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include "../common/log.hpp"
+#include "socket.hpp"
+
+namespace pccl::net {
+
+MasterConnection::MasterConnection(const SockAddr &master) : master_(master) {}
+
+MasterConnection::~MasterConnection() {
+    interrupt();
+    join();
+}
+
+bool MasterConnection::connect() {
+    fd_ = connect_tcp(master_, 5000);
+    if (fd_ < 0) {
+        LOG(ERR) << "Failed to connect to master " << sockaddr_str(master_);
+        return false;
+    }
+    timeval tv{10, 0}; // bounded sends (reference: SO_SNDTIMEO 10 s)
+    setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    open_ = true;
+    rx_thread_ = std::thread([this] { rx_loop(); });
+    return true;
+}
+
+void MasterConnection::interrupt() {
+    interrupted_ = true;
+    if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+    open_ = false;
+    q_cv_.notify_all();
+}
+
+void MasterConnection::join() {
+    if (rx_thread_.joinable()) rx_thread_.join();
+    if (fd_ >= 0) {
+        ::close(fd_);
+        fd_ = -1;
+    }
+}
+
+bool MasterConnection::send_raw(uint16_t id, const std::vector<uint8_t> &payload) {
+    if (!open_) return false;
+    std::lock_guard lock(send_mtx_);
+    if (!send_ltv(fd_, id, payload.data(), payload.size())) {
+        LOG(WARN) << "Failed to send packet " << id << " to master";
+        return false;
+    }
+    return true;
+}
+
+void MasterConnection::rx_loop() {
+    while (!interrupted_) {
+        auto pkt = recv_ltv(fd_);
+        if (!pkt) break;
+        {
+            std::lock_guard lock(q_mtx_);
+            queue_.push_back(Item{pkt->id, std::move(pkt->payload)});
+        }
+        q_cv_.notify_all();
+    }
+    open_ = false;
+    q_cv_.notify_all();
+    LOG(DEBUG) << "Master connection RX loop ended";
+}
+
+bool MasterConnection::take(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match,
+                            std::chrono::milliseconds timeout) {
+    std::unique_lock lock(q_mtx_);
+    const auto deadline = std::chrono::steady_clock::now() + timeout;
+    while (true) {
+        for (auto it = queue_.begin(); it != queue_.end(); ++it) {
+            if (match(it->id, it->payload)) {
+                queue_.erase(it);
+                return true;
+            }
+        }
+        if (!open_) return false;
+        if (timeout.count() == 0) return false;
+        if (timeout.count() < 0) {
+            q_cv_.wait(lock);
+        } else if (q_cv_.wait_until(lock, deadline) == std::cv_status::timeout) {
+            // one final scan happens on next loop iteration only if time remains
+            for (auto it = queue_.begin(); it != queue_.end(); ++it) {
+                if (match(it->id, it->payload)) {
+                    queue_.erase(it);
+                    return true;
+                }
+            }
+            return false;
+        }
+    }
+}
+
+} // namespace pccl::net

@@ -1,0 +1,78 @@
+// Client-side connection to the master: a blocking TCP socket with a dedicated RX thread that parses LTV packets
+// into a queue. Consumers wait for a packet by id (+ optional predicate), so concurrent collective worker threads
+// never steal each other's Commence/Abort/Complete packets (same contract as the reference QueuedSocket,
+// tinysockets/src/queued_client_socket.cpp:332-424).
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <optional>
+#include <thread>
+#include <vector>
+
+#include "../common/types.hpp"
+#include "../proto/packets.hpp"
+
+namespace pccl::net {
+
+class MasterConnection {
+public:
+    explicit MasterConnection(const SockAddr &master);
+    ~MasterConnection();
+
+    bool connect();
+    void interrupt();
+    void join();
+    bool is_open() const { return open_.load(); }
+
+    template<typename P>
+    bool send(const P &p) {
+        proto::WBuf w;
+        p.encode(w);
+        return send_raw(P::kId, w.data);
+    }
+
+    // Blocks until a packet of type P (matching pred) arrives; nullopt if the connection closed or timeout elapsed.
+    // timeout < 0 waits forever; timeout == 0 polls without blocking.
+    template<typename P>
+    std::optional<P> receive(std::function<bool(const P &)> pred = nullptr,
+                             std::chrono::milliseconds timeout = std::chrono::milliseconds(-1)) {
+        std::optional<P> result;
+        auto match = [&](uint16_t id, const std::vector<uint8_t> &payload) -> bool {
+            if (id != P::kId) return false;
+            auto p = proto::decode_payload<P>(payload.data(), payload.size());
+            if (!p) return false;
+            if (pred && !pred(*p)) return false;
+            result = std::move(p);
+            return true;
+        };
+        if (!take(match, timeout)) return std::nullopt;
+        return result;
+    }
+
+private:
+    bool send_raw(uint16_t id, const std::vector<uint8_t> &payload);
+    bool take(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match,
+              std::chrono::milliseconds timeout);
+    void rx_loop();
+
+    SockAddr master_;
+    int fd_ = -1;
+    std::thread rx_thread_;
+    std::atomic<bool> open_{false};
+    std::atomic<bool> interrupted_{false};
+    std::mutex send_mtx_;
+    std::mutex q_mtx_;
+    std::condition_variable q_cv_;
+    struct Item {
+        uint16_t id;
+        std::vector<uint8_t> payload;
+    };
+    std::deque<Item> queue_;
+};
+
+} // namespace pccl::net

@@ -1,0 +1,249 @@
+#include "mux.hpp"
+
+#include <cerrno>
+#include <cstring>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include "../common/log.hpp"
+#include "socket.hpp"
+
+namespace pccl::net {
+
+size_t multiplex_chunk_size() {
+    static const size_t v = env_size("PCCL_MULTIPLEX_CHUNK_SIZE", 16ull << 20);
+    return v == 0 ? (16ull << 20) : v;
+}
+
+static constexpr size_t kMaxFrame = 1ull << 30;
+
+MuxConn::MuxConn(int fd, Mode mode, const SockAddr &peer_addr) : fd_(fd), mode_(mode), peer_addr_(peer_addr) {}
+
+MuxConn::~MuxConn() {
+    interrupt();
+    join();
+    if (fd_ >= 0) {
+        ::close(fd_);
+        fd_ = -1;
+    }
+}
+
+bool MuxConn::start() {
+    open_.store(true, std::memory_order_release);
+    if (mode_ == Mode::Rx) rx_thread_ = std::thread([this] { rx_loop(); });
+    return true;
+}
+
+void MuxConn::interrupt() {
+    stop_ = true;
+    if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+    open_.store(false, std::memory_order_release);
+    {
+        std::lock_guard l(mtx_);
+    }
+    cv_.notify_all();
+}
+
+void MuxConn::join() {
+    if (rx_thread_.joinable()) rx_thread_.join();
+}
+
+bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n) {
+    if (!is_open()) return false;
+    uint8_t hdr[24];
+    const uint64_t vals[3] = {n + 16, tag, ctr};
+    for (int v = 0; v < 3; ++v)
+        for (int i = 0; i < 8; ++i) hdr[v * 8 + i] = static_cast<uint8_t>(vals[v] >> (8 * (7 - i)));
+    iovec iov[2] = {{hdr, 24}, {const_cast<void *>(data), n}};
+    std::lock_guard lock(tx_mtx_);
+    if (!sendv_all(fd_, iov, n ? 2 : 1)) {
+        open_.store(false, std::memory_order_release);
+        return false;
+    }
+    return true;
+}
+
+bool MuxConn::read_into(uint8_t *dst, size_t n, Sink *progress_sink) {
+    constexpr size_t kPiece = 1 << 20;
+    size_t done = 0;
+    while (done < n) {
+        const size_t want = std::min(kPiece, n - done);
+        const ssize_t k = ::recv(fd_, dst + done, want, 0);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        if (k == 0) return false;
+        done += static_cast<size_t>(k);
+        rx_total_.fetch_add(static_cast<uint64_t>(k), std::memory_order_relaxed);
+        if (progress_sink != nullptr) {
+            progress_sink->received.fetch_add(static_cast<size_t>(k), std::memory_order_release);
+            {
+                std::lock_guard l(mtx_);
+            }
+            cv_.notify_all();
+        }
+    }
+    return true;
+}
+
+void MuxConn::rx_loop() {
+    while (!stop_) {
+        uint8_t hdr[24];
+        if (!recv_all(fd_, hdr, 24)) break;
+        uint64_t vals[3] = {0, 0, 0};
+        for (int v = 0; v < 3; ++v)
+            for (int i = 0; i < 8; ++i) vals[v] = (vals[v] << 8) | hdr[v * 8 + i];
+        const uint64_t len = vals[0], tag = vals[1], ctr = vals[2];
+        if (len < 16 || len - 16 > kMaxFrame) {
+            LOG(WARN) << "MuxConn: invalid frame length " << len << " from " << sockaddr_str(peer_addr_);
+            break;
+        }
+        const size_t n = len - 16;
+        Sink *sink = nullptr;
+        size_t offset = 0;
+        {
+            std::lock_guard l(mtx_);
+            auto it = sinks_.find(tag);
+            if (it != sinks_.end() && it->second->ctr == ctr &&
+                it->second->received.load(std::memory_order_relaxed) + n <= it->second->capacity) {
+                // only deliver directly if nothing for this tag/ctr is still queued ahead of us (FIFO)
+                auto qit = queued_.find(tag);
+                bool queued_ahead = false;
+                if (qit != queued_.end())
+                    for (const auto &f : qit->second)
+                        if (f.ctr == ctr) queued_ahead = true;
+                if (!queued_ahead) {
+                    sink = it->second.get();
+                    sink->busy = true;
+                    offset = sink->received.load(std::memory_order_relaxed);
+                }
+            }
+        }
+        if (sink != nullptr) {
+            const bool ok = read_into(sink->dst + offset, n, sink);
+            {
+                std::lock_guard l(mtx_);
+                sink->busy = false;
+            }
+            cv_.notify_all();
+            if (!ok) break;
+            continue;
+        }
+        std::vector<uint8_t> buf(n);
+        if (n > 0 && !read_into(buf.data(), n, nullptr)) break;
+        {
+            std::lock_guard l(mtx_);
+            auto it = sinks_.find(tag);
+            if (it != sinks_.end() && ctr < it->second->ctr) {
+                // stale frame of an aborted earlier op with the same tag
+            } else if (it != sinks_.end() && it->second->ctr == ctr && !it->second->busy &&
+                       it->second->received.load(std::memory_order_relaxed) + n <= it->second->capacity &&
+                       (queued_.find(tag) == queued_.end() || queued_[tag].empty())) {
+                // the sink was posted while we were reading this frame: deliver it now (keeps FIFO order)
+                Sink *s = it->second.get();
+                const size_t off = s->received.load(std::memory_order_relaxed);
+                std::memcpy(s->dst + off, buf.data(), n);
+                s->received.store(off + n, std::memory_order_release);
+            } else {
+                queued_[tag].push_back(Frame{ctr, std::move(buf)});
+            }
+        }
+        cv_.notify_all();
+    }
+    open_.store(false, std::memory_order_release);
+    {
+        std::lock_guard l(mtx_);
+    }
+    cv_.notify_all();
+}
+
+std::optional<std::vector<uint8_t>> MuxConn::recv_frame(uint64_t tag, uint64_t ctr, std::chrono::milliseconds timeout) {
+    std::unique_lock l(mtx_);
+    const auto deadline = std::chrono::steady_clock::now() + timeout;
+    while (true) {
+        auto it = queued_.find(tag);
+        if (it != queued_.end()) {
+            auto &q = it->second;
+            while (!q.empty() && q.front().ctr < ctr) q.pop_front();
+            if (!q.empty() && q.front().ctr == ctr) {
+                auto data = std::move(q.front().data);
+                q.pop_front();
+                if (q.empty()) queued_.erase(it);
+                return data;
+            }
+        }
+        if (!is_open()) return std::nullopt;
+        if (cv_.wait_until(l, deadline) == std::cv_status::timeout) {
+            // re-check once
+            auto it2 = queued_.find(tag);
+            if (it2 != queued_.end() && !it2->second.empty() && it2->second.front().ctr == ctr) continue;
+            return std::nullopt;
+        }
+    }
+}
+
+void MuxConn::post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n) {
+    std::lock_guard l(mtx_);
+    auto s = std::make_unique<Sink>();
+    s->ctr = ctr;
+    s->dst = dst;
+    s->capacity = n;
+    auto it = queued_.find(tag);
+    if (it != queued_.end()) {
+        auto &q = it->second;
+        while (!q.empty() && q.front().ctr < ctr) q.pop_front();
+        while (!q.empty() && q.front().ctr == ctr) {
+            const auto &f = q.front().data;
+            const size_t have = s->received.load(std::memory_order_relaxed);
+            if (have + f.size() > n) break;
+            std::memcpy(dst + have, f.data(), f.size());
+            s->received.store(have + f.size(), std::memory_order_release);
+            q.pop_front();
+        }
+        if (q.empty()) queued_.erase(it);
+    }
+    sinks_[tag] = std::move(s);
+}
+
+size_t MuxConn::sink_progress(uint64_t tag) {
+    std::lock_guard l(mtx_);
+    auto it = sinks_.find(tag);
+    if (it == sinks_.end()) return 0;
+    return it->second->received.load(std::memory_order_acquire);
+}
+
+size_t MuxConn::wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout) {
+    std::unique_lock l(mtx_);
+    const auto deadline = std::chrono::steady_clock::now() + timeout;
+    while (true) {
+        auto it = sinks_.find(tag);
+        if (it == sinks_.end()) return 0;
+        const size_t have = it->second->received.load(std::memory_order_acquire);
+        if (have >= want || !is_open()) return have;
+        if (cv_.wait_until(l, deadline) == std::cv_status::timeout)
+            return it->second->received.load(std::memory_order_acquire);
+    }
+}
+
+void MuxConn::remove_sink(uint64_t tag) {
+    std::unique_lock l(mtx_);
+    auto it = sinks_.find(tag);
+    if (it == sinks_.end()) return;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    bool interrupted = false;
+    while (it->second->busy) {
+        cv_.wait_for(l, std::chrono::milliseconds(50));
+        if (std::chrono::steady_clock::now() > deadline && !interrupted) {
+            LOG(WARN) << "MuxConn: sink still being written after 10 s; interrupting connection";
+            interrupted = true;
+            if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+        }
+        it = sinks_.find(tag);
+        if (it == sinks_.end()) return;
+    }
+    sinks_.erase(it);
+}
+
+} // namespace pccl::net

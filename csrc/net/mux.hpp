@@ -1,0 +1,107 @@
+// Multiplexed P2P data connection (one TCP stream carrying frames of many concurrent collectives).
+//
+// Frame format (reference tinysockets multiplexed socket): u64 BE length(= payload + 16) | u64 BE tag |
+// u64 BE stream_ctr | payload. A collective op is identified by its tag; stream_ctr is the master-assigned sequence
+// number so that frames of an aborted earlier op with the same tag are discarded.
+//
+// Design (differs from the reference's TX-thread + SPSC-queue design):
+//   * TX: the sending op thread writes whole frames directly with sendmsg under a per-connection mutex; no copy,
+//     no extra thread hop.
+//   * RX: one thread per connection reads frame headers; if the owning op has posted a *sink* (destination memory —
+//     user host memory or a pinned staging buffer for the HIP path) the payload is received straight into it
+//     (zero copy) in pieces, publishing progress after every piece so the consumer can pipeline reduction/H2D behind
+//     the socket. Frames without a matching sink (early arrivals, packet frames) are queued per tag.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <optional>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../common/types.hpp"
+#include "../proto/packets.hpp"
+
+namespace pccl::net {
+
+class MuxConn {
+public:
+    enum class Mode { Tx, Rx };
+    MuxConn(int fd, Mode mode, const SockAddr &peer_addr);
+    ~MuxConn();
+
+    bool start();
+    void interrupt();
+    void join();
+    bool is_open() const { return open_.load(std::memory_order_acquire); }
+    const SockAddr &peer_addr() const { return peer_addr_; }
+
+    // ---- TX side ----
+    bool send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n);
+    template<typename P>
+    bool send_packet(uint64_t tag, uint64_t ctr, const P &p) {
+        auto bytes = proto::encode_with_id(p);
+        return send_frame(tag, ctr, bytes.data(), bytes.size());
+    }
+
+    // ---- RX side ----
+    // Next queued frame for (tag, ctr); frames for the tag with an older ctr are dropped. Waits up to `timeout`.
+    std::optional<std::vector<uint8_t>> recv_frame(uint64_t tag, uint64_t ctr, std::chrono::milliseconds timeout);
+    template<typename P>
+    std::optional<P> recv_packet(uint64_t tag, uint64_t ctr, std::chrono::milliseconds timeout) {
+        auto f = recv_frame(tag, ctr, timeout);
+        if (!f || f->size() < 2) return std::nullopt;
+        const uint16_t id = static_cast<uint16_t>(((*f)[0] << 8) | (*f)[1]);
+        if (id != P::kId) return std::nullopt;
+        return proto::decode_payload<P>(f->data() + 2, f->size() - 2);
+    }
+
+    // Posts a sink of exactly `n` bytes at `dst` for (tag, ctr). Already-queued matching frames are copied in.
+    void post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n);
+    // Bytes delivered into the sink so far (acquire). 0 if no sink.
+    size_t sink_progress(uint64_t tag);
+    // Waits until progress >= want, the connection closed, or timeout. Returns current progress.
+    size_t wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout);
+    // Removes the sink; waits for an in-flight write into it to finish (interrupts the connection if it hangs).
+    void remove_sink(uint64_t tag);
+
+    uint64_t rx_bytes_total() const { return rx_total_.load(std::memory_order_relaxed); }
+
+private:
+    struct Sink {
+        uint64_t ctr = 0;
+        uint8_t *dst = nullptr;
+        size_t capacity = 0;
+        std::atomic<size_t> received{0};
+        bool busy = false; // RX thread is writing into dst
+    };
+    struct Frame {
+        uint64_t ctr;
+        std::vector<uint8_t> data;
+    };
+    void rx_loop();
+    bool read_into(uint8_t *dst, size_t n, Sink *progress_sink);
+
+    int fd_;
+    Mode mode_;
+    SockAddr peer_addr_;
+    std::atomic<bool> open_{false};
+    std::atomic<bool> stop_{false};
+    std::thread rx_thread_;
+    std::mutex tx_mtx_;
+
+    std::mutex mtx_;
+    std::condition_variable cv_;
+    std::unordered_map<uint64_t, std::unique_ptr<Sink>> sinks_;
+    std::unordered_map<uint64_t, std::deque<Frame>> queued_;
+    std::atomic<uint64_t> rx_total_{0};
+};
+
+size_t multiplex_chunk_size();
+
+} // namespace pccl::net

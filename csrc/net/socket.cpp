@@ -1,0 +1,252 @@
+#include "socket.hpp"
+
+#include <arpa/inet.h>
+#include <cerrno>
+#include <cstring>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include "../common/log.hpp"
+
+namespace pccl::net {
+
+bool to_native(const SockAddr &a, sockaddr_storage &ss, socklen_t &len) {
+    std::memset(&ss, 0, sizeof(ss));
+    if (a.inet.protocol == inetIPv4) {
+        auto *s4 = reinterpret_cast<sockaddr_in *>(&ss);
+        s4->sin_family = AF_INET;
+        s4->sin_port = htons(a.port);
+        std::memcpy(&s4->sin_addr, a.inet.ipv4.data, 4);
+        len = sizeof(sockaddr_in);
+        return true;
+    }
+    auto *s6 = reinterpret_cast<sockaddr_in6 *>(&ss);
+    s6->sin6_family = AF_INET6;
+    s6->sin6_port = htons(a.port);
+    std::memcpy(&s6->sin6_addr, a.inet.ipv6.data, 16);
+    len = sizeof(sockaddr_in6);
+    return true;
+}
+
+SockAddr from_native(const sockaddr_storage &ss) {
+    SockAddr a{};
+    if (ss.ss_family == AF_INET) {
+        const auto *s4 = reinterpret_cast<const sockaddr_in *>(&ss);
+        a.inet.protocol = inetIPv4;
+        std::memcpy(a.inet.ipv4.data, &s4->sin_addr, 4);
+        a.port = ntohs(s4->sin_port);
+    } else if (ss.ss_family == AF_INET6) {
+        const auto *s6 = reinterpret_cast<const sockaddr_in6 *>(&ss);
+        // map v4-mapped v6 addresses back to v4
+        const uint8_t *b = reinterpret_cast<const uint8_t *>(&s6->sin6_addr);
+        static const uint8_t prefix[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff};
+        if (std::memcmp(b, prefix, 12) == 0) {
+            a.inet.protocol = inetIPv4;
+            std::memcpy(a.inet.ipv4.data, b + 12, 4);
+        } else {
+            a.inet.protocol = inetIPv6;
+            std::memcpy(a.inet.ipv6.data, b, 16);
+        }
+        a.port = ntohs(s6->sin6_port);
+    }
+    return a;
+}
+
+void tune_socket(int fd, bool bulk) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    setsockopt(fd, SOL_SOCKET, SO_KEEPALIVE, &one, sizeof(one));
+    int idle = 30, intvl = 5, cnt = 4;
+    setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &idle, sizeof(idle));
+    setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl));
+    setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt));
+    if (bulk) {
+        int sz = 8 << 20;
+        setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+        setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+    }
+}
+
+int connect_tcp(const SockAddr &addr, int timeout_ms) {
+    sockaddr_storage ss{};
+    socklen_t len{};
+    to_native(addr, ss, len);
+    const int fd = ::socket(ss.ss_family, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    if (fd < 0) return -1;
+    int rc = ::connect(fd, reinterpret_cast<sockaddr *>(&ss), len);
+    if (rc != 0 && errno != EINPROGRESS) {
+        ::close(fd);
+        return -1;
+    }
+    if (rc != 0) {
+        pollfd p{fd, POLLOUT, 0};
+        rc = ::poll(&p, 1, timeout_ms);
+        int err = 0;
+        socklen_t el = sizeof(err);
+        if (rc <= 0 || getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el) != 0 || err != 0) {
+            ::close(fd);
+            return -1;
+        }
+    }
+    // back to blocking
+    const int flags = fcntl(fd, F_GETFL, 0);
+    fcntl(fd, F_SETFL, flags & ~O_NONBLOCK);
+    tune_socket(fd, true);
+    return fd;
+}
+
+int listen_tcp(ccoip_inet_protocol_t proto, uint16_t port, bool bump, uint16_t &bound_port, int backlog) {
+    for (int attempt = 0; attempt < 2048; ++attempt) {
+        const uint16_t try_port = static_cast<uint16_t>(port == 0 ? 0 : port + attempt);
+        const int fam = proto == inetIPv4 ? AF_INET : AF_INET6;
+        const int fd = ::socket(fam, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        if (fd < 0) return -1;
+        int one = 1;
+        setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+        sockaddr_storage ss{};
+        socklen_t len;
+        if (fam == AF_INET) {
+            auto *s4 = reinterpret_cast<sockaddr_in *>(&ss);
+            s4->sin_family = AF_INET;
+            s4->sin_addr.s_addr = htonl(INADDR_ANY);
+            s4->sin_port = htons(try_port);
+            len = sizeof(sockaddr_in);
+        } else {
+            auto *s6 = reinterpret_cast<sockaddr_in6 *>(&ss);
+            s6->sin6_family = AF_INET6;
+            s6->sin6_addr = in6addr_any;
+            s6->sin6_port = htons(try_port);
+            int off = 0;
+            setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &off, sizeof(off));
+            len = sizeof(sockaddr_in6);
+        }
+        if (::bind(fd, reinterpret_cast<sockaddr *>(&ss), len) == 0 && ::listen(fd, backlog) == 0) {
+            sockaddr_storage got{};
+            socklen_t gl = sizeof(got);
+            getsockname(fd, reinterpret_cast<sockaddr *>(&got), &gl);
+            bound_port = from_native(got).port;
+            return fd;
+        }
+        ::close(fd);
+        if (!bump || port == 0) return -1;
+    }
+    return -1;
+}
+
+bool send_all(int fd, const void *data, size_t n) {
+    const auto *p = static_cast<const uint8_t *>(data);
+    while (n > 0) {
+        const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        p += k;
+        n -= static_cast<size_t>(k);
+    }
+    return true;
+}
+
+bool sendv_all(int fd, iovec *iov, int iovcnt) {
+    while (iovcnt > 0) {
+        msghdr msg{};
+        msg.msg_iov = iov;
+        msg.msg_iovlen = static_cast<size_t>(iovcnt);
+        ssize_t k = ::sendmsg(fd, &msg, MSG_NOSIGNAL);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        while (k > 0 && iovcnt > 0) {
+            if (static_cast<size_t>(k) >= iov->iov_len) {
+                k -= static_cast<ssize_t>(iov->iov_len);
+                ++iov;
+                --iovcnt;
+            } else {
+                iov->iov_base = static_cast<uint8_t *>(iov->iov_base) + k;
+                iov->iov_len -= static_cast<size_t>(k);
+                k = 0;
+            }
+        }
+        while (iovcnt > 0 && iov->iov_len == 0) {
+            ++iov;
+            --iovcnt;
+        }
+    }
+    return true;
+}
+
+bool recv_all(int fd, void *data, size_t n) {
+    auto *p = static_cast<uint8_t *>(data);
+    while (n > 0) {
+        const ssize_t k = ::recv(fd, p, n, 0);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        if (k == 0) return false;
+        p += k;
+        n -= static_cast<size_t>(k);
+    }
+    return true;
+}
+
+int wait_readable(int fd, int timeout_ms) {
+    pollfd p{fd, POLLIN, 0};
+    const int rc = ::poll(&p, 1, timeout_ms);
+    if (rc < 0) return errno == EINTR ? 0 : -1;
+    if (rc == 0) return 0;
+    if (p.revents & POLLIN) return 1;
+    return -1;
+}
+
+std::vector<uint8_t> ltv_header(uint16_t id, size_t payload_len) {
+    std::vector<uint8_t> h(10);
+    const uint64_t len = payload_len + 2;
+    for (int i = 0; i < 8; ++i) h[i] = static_cast<uint8_t>(len >> (8 * (7 - i)));
+    h[8] = static_cast<uint8_t>(id >> 8);
+    h[9] = static_cast<uint8_t>(id);
+    return h;
+}
+
+bool send_ltv(int fd, uint16_t id, const uint8_t *payload, size_t n) {
+    auto h = ltv_header(id, n);
+    iovec iov[2] = {{h.data(), h.size()}, {const_cast<uint8_t *>(payload), n}};
+    return sendv_all(fd, iov, n ? 2 : 1);
+}
+
+std::optional<LtvPacket> recv_ltv(int fd, size_t max_len) {
+    uint8_t h[10];
+    if (!recv_all(fd, h, 10)) return std::nullopt;
+    uint64_t len = 0;
+    for (int i = 0; i < 8; ++i) len = (len << 8) | h[i];
+    if (len < 2 || len - 2 > max_len) return std::nullopt;
+    LtvPacket p;
+    p.id = static_cast<uint16_t>((h[8] << 8) | h[9]);
+    p.payload.resize(len - 2);
+    if (len > 2 && !recv_all(fd, p.payload.data(), len - 2)) return std::nullopt;
+    return p;
+}
+
+void close_fd(int &fd) {
+    if (fd >= 0) {
+        ::shutdown(fd, SHUT_RDWR);
+        ::close(fd);
+        fd = -1;
+    }
+}
+
+bool is_connected(int fd) {
+    if (fd < 0) return false;
+    char c;
+    const ssize_t k = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    if (k == 0) return false;
+    if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return false;
+    return true;
+}
+
+} // namespace pccl::net

@@ -1,0 +1,404 @@
+// CCoIP packet definitions. Wire layouts follow SURVEY Appendix A (reference ccoip/src/cpp/ccoip_packets.cpp);
+// this is an independent implementation of the same byte format.
+//
+// Framing on control sockets (master, shared-state, benchmark, p2p hello): u64 length(payload+2) | u16 id | payload.
+// Packets carried inside multiplexed P2P frames: u16 id | payload (no length; the frame carries it).
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "../common/types.hpp"
+#include "buffer.hpp"
+
+namespace pccl::proto {
+
+using PacketId = uint16_t;
+
+// ---- client -> master ----
+constexpr PacketId C2M_REQUEST_SESSION_REGISTRATION = 1;
+constexpr PacketId C2M_REQUEST_ESTABLISH_P2P_CONNECTIONS = 2;
+constexpr PacketId C2M_P2P_CONNECTIONS_ESTABLISHED = 3;
+constexpr PacketId C2M_CHECK_PEERS_PENDING = 4;
+constexpr PacketId C2M_OPTIMIZE_TOPOLOGY = 5;
+constexpr PacketId C2M_REPORT_PEER_BANDWIDTH = 6;
+constexpr PacketId C2M_OPTIMIZE_TOPOLOGY_WORK_COMPLETE = 7;
+constexpr PacketId C2M_SYNC_SHARED_STATE = 8;
+constexpr PacketId C2M_DIST_SHARED_STATE_COMPLETE = 9;
+constexpr PacketId C2M_COLLECTIVE_COMMS_INITIATE = 10;
+constexpr PacketId C2M_COLLECTIVE_COMMS_COMPLETE = 11;
+// ---- master -> client ----
+constexpr PacketId M2C_SESSION_REGISTRATION_RESPONSE = 1;
+constexpr PacketId M2C_P2P_CONNECTION_INFO = 2;
+constexpr PacketId M2C_P2P_CONNECTIONS_ESTABLISHED = 3;
+constexpr PacketId M2C_PEERS_PENDING_RESPONSE = 4;
+constexpr PacketId M2C_OPTIMIZE_TOPOLOGY_RESPONSE = 5;
+constexpr PacketId M2C_OPTIMIZE_TOPOLOGY_COMPLETE = 6;
+constexpr PacketId M2C_SYNC_SHARED_STATE = 7;
+constexpr PacketId M2C_SYNC_SHARED_STATE_COMPLETE = 8;
+constexpr PacketId M2C_COLLECTIVE_COMMS_COMMENCE = 9;
+constexpr PacketId M2C_COLLECTIVE_COMMS_COMPLETE = 10;
+constexpr PacketId M2C_COLLECTIVE_COMMS_ABORT = 11;
+// ---- peer <-> peer ----
+constexpr PacketId P2P_HELLO = 1;
+constexpr PacketId P2P_HELLO_ACK = 2;
+constexpr PacketId P2P_DEQUANTIZATION_META = 3;
+// ---- shared state client <-> server ----
+constexpr PacketId C2S_REQUEST_SHARED_STATE = 1;
+constexpr PacketId S2C_SHARED_STATE_RESPONSE = 1;
+// ---- benchmark ----
+constexpr PacketId C2B_HELLO = 1;
+constexpr PacketId B2C_BENCHMARK_SERVER_IS_BUSY = 1;
+
+struct Empty {
+    void encode(WBuf &) const {}
+    bool decode(RBuf &) { return true; }
+};
+
+struct C2MRequestSessionRegistration {
+    static constexpr PacketId kId = C2M_REQUEST_SESSION_REGISTRATION;
+    uint32_t peer_group = 0;
+    bool use_explicit_addresses = false;
+    SockAddr advertised_p2p{}, advertised_ss{}, advertised_bm{};
+    uint16_t p2p_port = 0, ss_port = 0, bm_port = 0;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct C2MRequestEstablishP2PConnections {
+    static constexpr PacketId kId = C2M_REQUEST_ESTABLISH_P2P_CONNECTIONS;
+    bool accept_new_peers = false;
+    void encode(WBuf &w) const { w.boolean(accept_new_peers); }
+    bool decode(RBuf &r) {
+        accept_new_peers = r.boolean();
+        return r.ok();
+    }
+};
+
+struct C2MP2PConnectionsEstablished {
+    static constexpr PacketId kId = C2M_P2P_CONNECTIONS_ESTABLISHED;
+    bool success = false;
+    std::vector<Uuid> failed_peers;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct C2MCheckPeersPending : Empty {
+    static constexpr PacketId kId = C2M_CHECK_PEERS_PENDING;
+};
+struct C2MOptimizeTopology : Empty {
+    static constexpr PacketId kId = C2M_OPTIMIZE_TOPOLOGY;
+};
+struct C2MOptimizeTopologyWorkComplete : Empty {
+    static constexpr PacketId kId = C2M_OPTIMIZE_TOPOLOGY_WORK_COMPLETE;
+};
+
+struct C2MReportPeerBandwidth {
+    static constexpr PacketId kId = C2M_REPORT_PEER_BANDWIDTH;
+    Uuid to_peer;
+    double bandwidth_mbps = 0;
+    void encode(WBuf &w) const {
+        w.uuid(to_peer);
+        w.f64(bandwidth_mbps);
+    }
+    bool decode(RBuf &r) {
+        to_peer = r.uuid();
+        bandwidth_mbps = r.f64();
+        return r.ok();
+    }
+};
+
+struct SharedStateHashEntry {
+    std::string key;
+    uint64_t hash = 0;
+    HashType hash_type = HashType::Simple;
+    uint64_t num_elements = 0;
+    DType data_type = DType::F32;
+    bool allow_content_inequality = false;
+    bool operator==(const SharedStateHashEntry &o) const {
+        return key == o.key && hash == o.hash && hash_type == o.hash_type && num_elements == o.num_elements &&
+               data_type == o.data_type && allow_content_inequality == o.allow_content_inequality;
+    }
+};
+
+struct C2MSyncSharedState {
+    static constexpr PacketId kId = C2M_SYNC_SHARED_STATE;
+    uint64_t revision = 0;
+    SyncStrategy strategy = SyncStrategy::EnforcePopular;
+    std::vector<SharedStateHashEntry> entries;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct C2MDistSharedStateComplete : Empty {
+    static constexpr PacketId kId = C2M_DIST_SHARED_STATE_COMPLETE;
+};
+
+struct C2MCollectiveCommsInitiate {
+    static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_INITIATE;
+    uint64_t tag = 0;
+    uint64_t count = 0;
+    DType data_type = DType::F32;
+    ReduceOp op = ReduceOp::Sum;
+    void encode(WBuf &w) const {
+        w.u64(tag);
+        w.u64(count);
+        w.u8(static_cast<uint8_t>(data_type));
+        w.u8(static_cast<uint8_t>(op));
+    }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        count = r.u64();
+        data_type = static_cast<DType>(r.u8());
+        op = static_cast<ReduceOp>(r.u8());
+        return r.ok();
+    }
+};
+
+struct C2MCollectiveCommsComplete {
+    static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_COMPLETE;
+    uint64_t tag = 0;
+    bool was_aborted = false;
+    void encode(WBuf &w) const {
+        w.u64(tag);
+        w.boolean(was_aborted);
+    }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        was_aborted = r.boolean();
+        return r.ok();
+    }
+};
+
+struct M2CSessionRegistrationResponse {
+    static constexpr PacketId kId = M2C_SESSION_REGISTRATION_RESPONSE;
+    bool accepted = false;
+    Uuid assigned_uuid;
+    void encode(WBuf &w) const {
+        w.boolean(accepted);
+        w.uuid(assigned_uuid);
+    }
+    bool decode(RBuf &r) {
+        accepted = r.boolean();
+        assigned_uuid = r.uuid();
+        return r.ok();
+    }
+};
+
+struct PeerInfo {
+    SockAddr p2p_listen_addr{};
+    Uuid peer_uuid;
+};
+
+struct M2CP2PConnectionInfo {
+    static constexpr PacketId kId = M2C_P2P_CONNECTION_INFO;
+    bool unchanged = false;
+    uint64_t global_world_size = 0;
+    uint64_t local_world_size = 0;
+    uint64_t num_distinct_peer_groups = 0;
+    uint64_t largest_peer_group_world_size = 0;
+    std::vector<PeerInfo> all_peers;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct M2CP2PConnectionsEstablished {
+    static constexpr PacketId kId = M2C_P2P_CONNECTIONS_ESTABLISHED;
+    bool success = false;
+    std::vector<Uuid> ring_order;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct M2CPeersPendingResponse {
+    static constexpr PacketId kId = M2C_PEERS_PENDING_RESPONSE;
+    bool peers_pending = false;
+    void encode(WBuf &w) const { w.boolean(peers_pending); }
+    bool decode(RBuf &r) {
+        peers_pending = r.boolean();
+        return r.ok();
+    }
+};
+
+struct BenchmarkRequest {
+    Uuid from_peer;
+    Uuid to_peer;
+    SockAddr to_peer_endpoint{};
+};
+
+struct M2COptimizeTopologyResponse {
+    static constexpr PacketId kId = M2C_OPTIMIZE_TOPOLOGY_RESPONSE;
+    std::vector<BenchmarkRequest> requests;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct M2COptimizeTopologyComplete {
+    static constexpr PacketId kId = M2C_OPTIMIZE_TOPOLOGY_COMPLETE;
+    bool success = false;
+    std::vector<Uuid> ring_order;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct M2CSyncSharedState {
+    static constexpr PacketId kId = M2C_SYNC_SHARED_STATE;
+    bool is_outdated = false;
+    SockAddr distributor{};
+    std::vector<std::string> outdated_keys;
+    std::vector<uint64_t> expected_hashes;
+    std::vector<HashType> expected_hash_types;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct M2CSyncSharedStateComplete : Empty {
+    static constexpr PacketId kId = M2C_SYNC_SHARED_STATE_COMPLETE;
+};
+
+struct M2CCollectiveCommsCommence {
+    static constexpr PacketId kId = M2C_COLLECTIVE_COMMS_COMMENCE;
+    uint64_t tag = 0;
+    uint64_t seq_nr = 0;
+    void encode(WBuf &w) const {
+        w.u64(tag);
+        w.u64(seq_nr);
+    }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        seq_nr = r.u64();
+        return r.ok();
+    }
+};
+
+struct M2CCollectiveCommsComplete {
+    static constexpr PacketId kId = M2C_COLLECTIVE_COMMS_COMPLETE;
+    uint64_t tag = 0;
+    void encode(WBuf &w) const { w.u64(tag); }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        return r.ok();
+    }
+};
+
+struct M2CCollectiveCommsAbort {
+    static constexpr PacketId kId = M2C_COLLECTIVE_COMMS_ABORT;
+    uint64_t tag = 0;
+    bool aborted = false;
+    void encode(WBuf &w) const {
+        w.u64(tag);
+        w.boolean(aborted);
+    }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        aborted = r.boolean();
+        return r.ok();
+    }
+};
+
+struct P2PHello {
+    static constexpr PacketId kId = P2P_HELLO;
+    Uuid peer_uuid;
+    uint32_t connection_nr = 0;
+    void encode(WBuf &w) const {
+        w.uuid(peer_uuid);
+        w.u32(connection_nr);
+    }
+    bool decode(RBuf &r) {
+        peer_uuid = r.uuid();
+        connection_nr = r.u32();
+        return r.ok();
+    }
+};
+
+struct P2PHelloAck : Empty {
+    static constexpr PacketId kId = P2P_HELLO_ACK;
+};
+
+// De-quantization metadata exchanged per ring step (values kept as double/int64 in memory; encoded in the
+// reference's byte layout: MIN_MAX -> u8 dtype + min bytes + max bytes (floats little-endian host order, ints
+// big-endian), ZERO_POINT_SCALE -> u8 zp dtype + zp bytes + u8 scale dtype + scale bytes).
+struct QuantMeta {
+    QuantAlgo algo = QuantAlgo::None; // MinMax or ZeroPointScale
+    DType value_type = DType::F32;    // dtype of min/max (== the unquantized data type)
+    double min_value = 0, max_value = 0;
+    int64_t zero_point = 0;
+    float scale = 1.0f;
+    bool operator==(const QuantMeta &o) const {
+        return algo == o.algo && value_type == o.value_type && min_value == o.min_value &&
+               max_value == o.max_value && zero_point == o.zero_point && scale == o.scale;
+    }
+};
+
+struct P2PDequantizationMeta {
+    static constexpr PacketId kId = P2P_DEQUANTIZATION_META;
+    uint64_t tag = 0;
+    QuantMeta meta;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct C2SRequestSharedState {
+    static constexpr PacketId kId = C2S_REQUEST_SHARED_STATE;
+    std::vector<std::string> keys;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+enum class SharedStateStatus : uint8_t { Success = 1, NotDistributed = 2, NotInMode = 3, UnknownKey = 4 };
+
+struct SharedStateEntryInfo {
+    std::string key;
+    uint64_t size_bytes = 0;
+};
+
+struct S2CSharedStateResponse {
+    static constexpr PacketId kId = S2C_SHARED_STATE_RESPONSE;
+    SharedStateStatus status = SharedStateStatus::Success;
+    uint64_t revision = 0;
+    std::vector<SharedStateEntryInfo> entries;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct C2BHello {
+    static constexpr PacketId kId = C2B_HELLO;
+    Uuid peer_uuid;
+    void encode(WBuf &w) const { w.uuid(peer_uuid); }
+    bool decode(RBuf &r) {
+        peer_uuid = r.uuid();
+        return r.ok();
+    }
+};
+
+struct B2CBenchmarkServerIsBusy {
+    static constexpr PacketId kId = B2C_BENCHMARK_SERVER_IS_BUSY;
+    bool is_busy = false;
+    void encode(WBuf &w) const { w.boolean(is_busy); }
+    bool decode(RBuf &r) {
+        is_busy = r.boolean();
+        return r.ok();
+    }
+};
+
+// Serialize a packet as u16 id + payload (used inside multiplexed frames and after the LTV length prefix).
+template<typename P>
+std::vector<uint8_t> encode_with_id(const P &p) {
+    WBuf w;
+    w.u16(P::kId);
+    p.encode(w);
+    return std::move(w.data);
+}
+
+// Parse payload (after the id) into a packet; returns nullopt on malformed input.
+template<typename P>
+std::optional<P> decode_payload(const uint8_t *data, size_t n) {
+    RBuf r(data, n);
+    P p{};
+    if (!p.decode(r) || !r.ok()) return std::nullopt;
+    return p;
+}
+
+} // namespace pccl::proto

@@ -1,0 +1,122 @@
+"""Thin wrappers over the ``pcclx*`` kernel entry points of libpccl.so.
+
+Each op runs either the HIP kernel (tensor on a GPU) or the host SIMD twin (CPU tensor); both produce identical bytes.
+On a GPU box these calls fail loudly if the HIP plugin is missing instead of silently falling back to the host path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from .._native import C
+
+# torch dtype -> CCoIP wire dtype code (pccl::DType)
+WIRE_DTYPE = {torch.uint8: 0, torch.int8: 1, torch.int16: 4, torch.int32: 5, torch.int64: 7, torch.float16: 8,
+              torch.bfloat16: 9, torch.float32: 10, torch.float64: 11}
+for _name, _code in (("uint16", 2), ("uint32", 3), ("uint64", 6), ("float8_e4m3fn", 12), ("float8_e5m2", 13)):
+    if hasattr(torch, _name):
+        WIRE_DTYPE[getattr(torch, _name)] = _code
+
+OPS = {"set": 0, "sum": 1, "avg": 2, "prod": 3, "max": 4, "min": 5}
+ALGOS = {"none": 0, "min_max": 1, "zero_point_scale": 2}
+
+
+def hip_device_count() -> int:
+    return int(C.pcclxHipDeviceCount())
+
+
+def _on_device(t: torch.Tensor) -> int:
+    if t.device.type == "cuda":
+        if hip_device_count() == 0:
+            raise RuntimeError("pccl-amd HIP backend (libpccl_hip.so) is not loaded but a GPU tensor was passed")
+        torch.cuda.current_stream(t.device).synchronize()
+        return 1
+    return 0
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+def simplehash(t: torch.Tensor) -> int:
+    assert t.is_contiguous()
+    return int(C.pcclxSimpleHash(t.data_ptr(), t.numel() * t.element_size(), _on_device(t)))
+
+
+def crc32c(t: torch.Tensor, force_software: bool = False) -> int:
+    assert t.device.type == "cpu" and t.is_contiguous()
+    return int(C.pcclxCrc32c(t.data_ptr(), t.numel() * t.element_size(), int(force_software)))
+
+
+def crc32c_has_hw() -> bool:
+    return bool(C.pcclxCrc32cHasHw())
+
+
+def fill_test_pattern(t: torch.Tensor):
+    """Reference test pattern (random_init_kernel<<<8,256>>>) on a GPU uint8/uint64 buffer."""
+    assert t.device.type == "cuda"
+    _check(C.pcclxFillTestPattern(t.data_ptr(), t.numel() * t.element_size() // 8), "fill_test_pattern")
+
+
+def reduce_(dst: torch.Tensor, src: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """dst = dst (op) src in place, with the library's exact accumulation/rounding rules."""
+    assert dst.dtype == src.dtype and dst.numel() == src.numel() and dst.device == src.device
+    _check(C.pcclxReduce(dst.data_ptr(), src.data_ptr(), dst.numel(), WIRE_DTYPE[dst.dtype], OPS[op], _on_device(dst)),
+           "reduce")
+    return dst
+
+
+def finalize_avg(dst: torch.Tensor, world_size: int) -> torch.Tensor:
+    _check(C.pcclxFinalizeAvg(dst.data_ptr(), dst.numel(), WIRE_DTYPE[dst.dtype], world_size, _on_device(dst)),
+           "finalize_avg")
+    return dst
+
+
+def quantize(src: torch.Tensor, qdtype: torch.dtype, algo: str = "min_max") -> Tuple[torch.Tensor, List[float]]:
+    """Quantizes src -> (q, meta) where meta = [min, max, zero_point, scale]."""
+    out = torch.empty(src.shape, dtype=qdtype, device=src.device)
+    meta = (ctypes.c_double * 4)()
+    _check(C.pcclxQuantize(out.data_ptr(), src.data_ptr(), src.numel(), WIRE_DTYPE[src.dtype], WIRE_DTYPE[qdtype],
+                           ALGOS[algo], _on_device(src), meta), "quantize")
+    return out, list(meta)
+
+
+def dequant_reduce(dst: torch.Tensor, q: torch.Tensor, meta: Sequence[float], algo: str = "min_max",
+                   op: str = "sum") -> torch.Tensor:
+    m = (ctypes.c_double * 4)(*meta)
+    _check(C.pcclxDequantReduce(dst.data_ptr(), q.data_ptr(), dst.numel(), WIRE_DTYPE[dst.dtype], WIRE_DTYPE[q.dtype],
+                                ALGOS[algo], OPS[op], m, _on_device(dst)), "dequant_reduce")
+    return dst
+
+
+def multi_reduce(srcs: Sequence[torch.Tensor], op: str = "sum", out: Optional[torch.Tensor] = None,
+                 out2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = op(srcs[0], ..., srcs[n-1]) in fixed order (the xGMI reduce-scatter kernel; GPU only)."""
+    s0 = srcs[0]
+    out = torch.empty_like(s0) if out is None else out
+    _on_device(s0)
+    arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    _check(C.pcclxMultiReduce(out.data_ptr(), out2.data_ptr() if out2 is not None else None, arr, len(srcs),
+                              s0.numel(), WIRE_DTYPE[s0.dtype], OPS[op]), "multi_reduce")
+    return out
+
+
+def multi_gather(dst: torch.Tensor, srcs: Sequence[torch.Tensor], offsets: Sequence[int], skip: int = -1):
+    """dst[offsets[k] : offsets[k] + srcs[k].numel()] = srcs[k] for k != skip (the xGMI all-gather kernel)."""
+    _on_device(dst)
+    arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    offs = (ctypes.c_size_t * len(srcs))(*offsets)
+    cnts = (ctypes.c_size_t * len(srcs))(*[s.numel() for s in srcs])
+    _check(C.pcclxMultiGather(dst.data_ptr(), arr, offs, cnts, len(srcs), skip, WIRE_DTYPE[dst.dtype]),
+           "multi_gather")
+    return dst
+
+
+def bench_kernel(which: str, dst: torch.Tensor, src: torch.Tensor, n: int = 1, iters: int = 20) -> float:
+    """Average microseconds per launch of a device kernel ('reduce', 'hash', 'multi_reduce', 'quantize')."""
+    w = {"reduce": 0, "hash": 1, "multi_reduce": 2, "quantize": 3}[which]
+    _on_device(src)
+    return float(C.pcclxBenchKernel(w, dst.data_ptr(), src.data_ptr(), src.numel(), WIRE_DTYPE[src.dtype], n, iters))
