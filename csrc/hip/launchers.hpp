@@ -1,0 +1,36 @@
+// Host-side launch functions of the HIP kernels, one translation unit per kernel family so that the (heavily
+// templated) device code compiles in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../common/types.hpp"
+#include "../kernels/quant_common.hpp"
+
+namespace pccl::hipk {
+
+// hip_reduce.hip
+bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, hipStream_t s);
+bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_t s);
+
+// hip_quant.hip
+bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                           const kernels::QuantParams &p, hipStream_t s);
+bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
+                     const kernels::QuantParams &p, hipStream_t s);
+bool launch_minmax(const void *src, size_t count, DType vtype, double *partial_scratch, double *out2, hipStream_t s);
+
+// hip_ipc.hip
+bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
+                         hipStream_t s);
+bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
+                         int skip, DType t, hipStream_t s);
+
+// hip_hash.hip
+bool launch_simplehash(const void *dev_ptr, size_t n_bytes, uint32_t *partial_scratch, uint32_t *out, hipStream_t s);
+bool launch_test_pattern(void *dev_ptr, size_t n_u64, hipStream_t s);
+
+} // namespace pccl::hipk
