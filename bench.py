@@ -1,0 +1,156 @@
+"""Flagship benchmark: ring all-reduce of a 1 GiB bf16 HIP device buffer per peer (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024]
+
+N == 1 : two peers (threads of this process) share cuda:0 — an all-reduce needs >= 2 peers.
+N  > 1 : launched by torch.distributed.run, one peer per GPU (LOCAL_RANK); rank 0 also hosts the CCoIP master.
+         torch.distributed (gloo) is used only for the bench's own barriers / max-over-ranks and to share the port.
+
+Each timed step is one pcclAllReduce(SUM) of the whole buffer on every peer. Peers on one host rendezvous in shared
+memory and reduce over xGMI (DEVICE_IPC path); the ring over loopback TCP is the fallback (PCCL_DISABLE_IPC=1).
+
+Reported: ``value`` = whole-job aggregate bus bandwidth = n_peers x busBW, with the nccl-tests convention
+busBW = (bytes / t) x 2 (n - 1) / n. ``extra`` carries per-peer busBW/algBW and the reference's own metric,
+(rx_bytes + tx_bytes) / t per peer (reference tests/basic_reduce_test/main.cpp:141-143).
+vs_baseline = value / 5.625 GB/s (the reference's best published all-reduce throughput, 45 Gbit/s,
+docs/md/01_Introduction.md:8).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_GBPS = 45e9 / 8 / 1e9  # 45 Gbit/s
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mib", type=int, default=1024, help="buffer size per peer in MiB (flagship: 1024)")
+    ap.add_argument("--peers-per-gpu", type=int, default=0, help="N==1 only: peers sharing cuda:0 (default 2)")
+    return ap.parse_args()
+
+
+def _peer_loop(comm, x, y, steps, warmup, sync_all, torch, pccl):
+    """Runs warmup + timed steps; sync_all() is the cross-peer barrier. Returns (seconds, tx, rx, path)."""
+    for s in range(warmup):
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=s)
+    torch.cuda.synchronize()
+    sync_all()
+    t0 = time.perf_counter()
+    tx = rx = 0
+    for s in range(steps):
+        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=warmup + s)
+        tx += info.tx_bytes
+        rx += info.rx_bytes
+    torch.cuda.synchronize()
+    sync_all()
+    dt = time.perf_counter() - t0
+    return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+
+def _report(n_gpus, n_peers, steps, warmup, nbytes, dt, tx, rx, path, parallelism):
+    import pccl_amd as pccl
+    t = dt / steps
+    alg = nbytes / t / 1e9
+    bus = alg * 2 * (n_peers - 1) / n_peers
+    value = bus * n_peers
+    line = {
+        "metric": "all-reduce bus BW (GB/s) vs tensor bytes, 2/4/8 peers; peer-rejoin latency",
+        "value": round(value, 3), "unit": "GB/s", "n_gpus": n_gpus, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_GBPS, 3), "dtype": "bf16",
+        "data": "synthetic (torch.randn bf16 on device)",
+        "config": {"model": "8-peer ring all-reduce, 1 GiB bf16 HIP device buffer per MI355X, loopback TCP",
+                   "global_batch": n_peers, "seq_len": nbytes // 2, "parallelism": parallelism,
+                   "tensor_bytes": nbytes, "n_peers": n_peers},
+        "extra": {"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
+                  "ref_metric_rx_plus_tx_per_peer_GBps": round((tx + rx) / steps / t / 1e9, 3),
+                  "reduce_path": pccl.ReducePath(path).name,
+                  "baseline_note": "vs_baseline divides the aggregate value by the reference's 45 Gbit/s "
+                                   "per-run WAN figure (no like-for-like MI355X number is published)"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+def bench_single_gpu(a):
+    import torch
+
+    import pccl_amd as pccl
+    from pccl_amd.utils import local_master, run_threaded_peers
+    n_peers = a.peers_per_gpu or 2
+    nbytes = a.mib << 20
+    n = nbytes // 2
+    dev = torch.device("cuda:0")
+    bar = threading.Barrier(n_peers)
+
+    def fn(rank, comm):
+        torch.cuda.set_device(dev)
+        g = torch.Generator(device=dev).manual_seed(rank)
+        x = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
+        y = torch.empty_like(x)
+        return _peer_loop(comm, x, y, a.steps, a.warmup, bar.wait, torch, pccl)
+
+    with local_master() as addr:
+        res = run_threaded_peers(n_peers, fn, address=addr, timeout=1800)
+    dt = max(r[0] for r in res)
+    _report(1, n_peers, a.steps, a.warmup, nbytes, dt, res[0][1], res[0][2], res[0][3], f"{n_peers} peers on 1 GPU")
+
+
+def bench_multi_gpu(a):
+    import torch
+    import torch.distributed as dist
+
+    import pccl_amd as pccl
+    from pccl_amd.utils import free_port, wait_for_world
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    master = None
+    port = [free_port() if rank == 0 else 0]
+    if rank == 0:
+        master = pccl.MasterNode(f"127.0.0.1:{port[0]}")
+        master.run()
+    dist.broadcast_object_list(port, src=0)
+    comm = pccl.Communicator(f"127.0.0.1:{port[0]}", 0)
+    comm.connect(n_attempts=30)
+    wait_for_world(comm, world, timeout=300)
+    nbytes = a.mib << 20
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(nbytes // 2, device=dev, dtype=torch.bfloat16, generator=g)
+    y = torch.empty_like(x)
+    dt, tx, rx, path = _peer_loop(comm, x, y, a.steps, a.warmup, dist.barrier, torch, pccl)
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        _report(world, world, a.steps, a.warmup, nbytes, float(t.item()), tx, rx, path, f"dp{world} (1 peer/GPU)")
+    dist.barrier()
+    comm.destroy()
+    if master is not None:
+        master.interrupt()
+        master.await_termination()
+    dist.destroy_process_group()
+
+
+def main():
+    a = _args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        bench_multi_gpu(a)
+    else:
+        bench_single_gpu(a)
+
+
+if __name__ == "__main__":
+    main()

@@ -56,6 +56,7 @@ struct alignas(64) OpPeerShm {
     uint64_t buf_cap;
     uint32_t dtype;
     uint32_t op;
+    uint64_t raw_ptr; // valid only inside the exporting process (peers that share a process skip the IPC mapping)
     uint8_t handle[kIpcHandleBytes];
 };
 
@@ -99,7 +100,8 @@ std::shared_ptr<IpcArena> IpcArena::create(Client &c, const std::vector<Uuid> &r
     int attempt;
     {
         std::lock_guard l(g_attempt_mtx);
-        attempt = g_attempts[h]++;
+        // counted per (ring, peer) so that threaded peers sharing a process agree on the attempt number
+        attempt = g_attempts[fnv1a(c.uuid().data.data(), 16, h)]++;
     }
     char nbuf[96];
     std::snprintf(nbuf, sizeof(nbuf), "/pccl_arena_%016llx_%d", static_cast<unsigned long long>(h), attempt);
@@ -348,6 +350,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     if (buf) {
         mine->buf_id = buf->id;
         mine->buf_cap = buf->cap;
+        mine->raw_ptr = reinterpret_cast<uint64_t>(buf->ptr);
         std::memcpy(mine->handle, buf->handle, kIpcHandleBytes);
     }
     set_phase(seq, PH_VOTED);
@@ -379,6 +382,10 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
             continue;
         }
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        if (pids_[k] == pids_[rank_]) { // same process (threaded peers): the pointer is directly usable
+            ctx.peer_base[k] = reinterpret_cast<void *>(p->raw_ptr);
+            continue;
+        }
         ctx.peer_base[k] = peer_mapping(static_cast<int>(k), p->buf_id, p->handle, device);
         if (!ctx.peer_base[k]) {
             LOG(ERR) << "IPC: cannot map buffer of peer " << k;
@@ -390,11 +397,6 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     {
         std::lock_guard l(g_ctx_mtx);
         g_ctx[{this, seq}] = std::move(ctx);
-    }
-    // stash the buffer pointer for release in run()
-    {
-        std::lock_guard l(mtx_);
-        (void)buf;
     }
     return kUseIpc;
 }

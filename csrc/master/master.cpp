@@ -627,8 +627,13 @@ bool Master::elect_mask(uint32_t group) {
         size_t first = 0;
     };
     std::vector<Cand> cands;
+    // SEND_ONLY peers declare their state to be the correct one: if any voted, only they are electable (documented
+    // semantics of PCCL_SHARED_STATE_SYNC_STRATEGY_SEND_ONLY; the reference elects purely by popularity).
+    bool any_tx_only = false;
+    for (const auto &[u, _] : gs.candidates) any_tx_only = any_tx_only || gs.strategies[u] == SyncStrategy::TxOnly;
     for (size_t i = 0; i < gs.candidates.size(); ++i) {
         const auto &[u, entries] = gs.candidates[i];
+        if (any_tx_only && gs.strategies[u] != SyncStrategy::TxOnly) continue;
         int prio = -1;
         auto st = gs.statuses.find(u);
         if (st != gs.statuses.end()) prio = st->second == SSStatus::Match ? 1 : st->second == SSStatus::RevisionOutdated ? -2 : -1;

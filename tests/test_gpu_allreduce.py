@@ -1,0 +1,141 @@
+"""All-reduce of HIP device tensors on an MI355X: xGMI IPC path, device ring path, quantized, shared state.
+
+Multi-peer cases share cuda:0 (the GPU box has one GPU); the IPC path is exercised both between threads of one
+process and between two processes (real hipIpc export/open).
+"""
+import json
+import os
+import subprocess
+
+import pytest
+import torch
+
+import pccl_amd as pccl
+from pccl_amd.utils import local_master, run_threaded_peers, spawn_python
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _run(world, fn):
+    with local_master() as addr:
+        return run_threaded_peers(world, fn, address=addr, timeout=180)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float16])
+@pytest.mark.parametrize("disable_ipc", [False, True])
+def test_device_all_reduce_two_peers(hip, dtype, disable_ipc, monkeypatch):
+    if disable_ipc:
+        monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    n = (1 << 22) + 5
+    gen = [torch.Generator().manual_seed(k) for k in range(2)]
+    inputs = [torch.randn(n, generator=g).to(dtype) for g in gen]
+    expect = (inputs[0].float() + inputs[1].float()).to(dtype)
+
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        y = torch.empty_like(x)
+        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        torch.cuda.synchronize()
+        return y.cpu(), info, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    res = _run(2, fn)
+    want_path = pccl.ReducePath.DEVICE_RING if disable_ipc else pccl.ReducePath.DEVICE_IPC
+    for y, info, path in res:
+        assert path == want_path.value
+        assert torch.equal(y, expect)
+
+
+def test_device_avg_three_peers_in_place(hip):
+    n = 1_000_003
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(3 * rank), device=hip)
+        comm.all_reduce(x, x, op=pccl.ReduceOp.AVG, tag=0)
+        torch.cuda.synchronize()
+        return x.cpu()
+
+    for y in _run(3, fn):
+        assert torch.all(y == 3.0)
+
+
+@pytest.mark.parametrize("disable_ipc", [False, True])
+def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
+    if disable_ipc:
+        monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    n, k = 1 << 20, 6
+
+    def fn(rank, comm):
+        xs = [torch.full((n,), float(rank + j), device=hip, dtype=torch.bfloat16) for j in range(k)]
+        ys = [torch.empty_like(x) for x in xs]
+        hs = [comm.all_reduce_async(xs[j], ys[j], op=pccl.ReduceOp.SUM, tag=j) for j in range(k)]
+        for h in hs:
+            ok, _, _ = h.wait()
+            assert ok
+        torch.cuda.synchronize()
+        return [y.float().cpu() for y in ys]
+
+    for ys in _run(2, fn):
+        for j, y in enumerate(ys):
+            assert torch.all(y == float(1 + 2 * j))
+
+
+@pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
+def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
+    n = (1 << 20) + 3
+    inputs = [torch.randn(n, generator=torch.Generator().manual_seed(40 + r)) for r in range(3)]
+
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        y = torch.empty_like(x)
+        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0, quantization_options=pccl.QuantizationOptions(
+            qdtype, pccl.QuantizationAlgorithm.MIN_MAX))
+        torch.cuda.synchronize()
+        return y.cpu(), info
+
+    res = _run(3, fn)
+    expect = inputs[0] + inputs[1] + inputs[2]
+    for y, info in res:
+        assert torch.equal(y, res[0][0])
+        assert info.tx_bytes < n * 4
+        err = (y - expect).abs()
+        bound = 3 * (max(float(t.max() - t.min()) for t in inputs) / 255) if qdtype == pccl.DataType.UINT8 else None
+        if bound is not None:
+            assert err.max().item() <= bound
+        else:
+            assert (err <= expect.abs() * 0.2 + 0.05).all()
+
+
+def test_device_shared_state(hip):
+    n = (1 << 22) + 1
+
+    def fn(rank, comm):
+        w = torch.full((n,), 1.0 if rank == 1 else 2.0, device=hip)
+        m = torch.arange(1000, device=hip, dtype=torch.bfloat16)
+        st = pccl.SharedState([pccl.TensorInfo.from_torch(w, "w"), pccl.TensorInfo.from_torch(m, "m")])
+        info = comm.sync_shared_state(st)
+        torch.cuda.synchronize()
+        return w.cpu(), info.rx_bytes
+
+    res = _run(3, fn)
+    for w, _ in res:
+        assert torch.all(w == 2.0)
+    assert [r[1] for r in res] == [0, n * 4, 0]
+
+
+def test_two_process_ipc(hip, tmp_path):
+    """Two processes on cuda:0 exchange device buffers through hipIpc handles (the intra-node xGMI path)."""
+    with local_master() as addr:
+        procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, "2", str(r), "--n",
+                               str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3"],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+        outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
+        assert len(lines) == 3
+        for ln in lines:
+            expect = float(1 + 2 + 2 * ln["step"])
+            assert ln["lo"] == ln["hi"] == expect
+            assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value

@@ -1,0 +1,106 @@
+"""HIP/CDNA4 kernels on an MI355X vs plain PyTorch fp32 references and vs the host twins (bit-exact).
+
+Reference parity: simplehash CUDA == CPU goldens (ccoip/tests/unit_tests/simple_hash/simplehash_cuda_test.cpp),
+random_init_kernel golden 1054399963 (simplehash_cpu_test.cu:106).
+"""
+import numpy as np
+import pytest
+import torch
+
+from pccl_amd.ops import kernels as K
+from tests._util import lcg_bytes
+from tests.test_hash import reference_test_pattern
+from tests.test_host_kernels import FLOATS, INTS, _rand, _ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,golden", [(154533888, 3391090508), (1, 344386053), (4, 3765247898), (25, 3651434421)])
+def test_device_simplehash_goldens(hip, n, golden):
+    x = torch.from_numpy(lcg_bytes(n)).to(hip)
+    assert K.simplehash(x) == golden
+
+
+def test_device_test_pattern_golden(hip):
+    n = 154533888
+    x = torch.empty(n, dtype=torch.uint8, device=hip)
+    K.fill_test_pattern(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x.cpu(), torch.from_numpy(reference_test_pattern(n)))
+    assert K.simplehash(x) == 1054399963
+
+
+@pytest.mark.parametrize("n", [16, 17, 1000, 4096 + 5, (1 << 22) + 9, 960 * 256 * 16 * 3 + 48])
+def test_device_hash_equals_host(hip, n):
+    x = torch.from_numpy(lcg_bytes(n, seed=n))
+    assert K.simplehash(x.to(hip)) == K.simplehash(x)
+
+
+@pytest.mark.parametrize("dtype", FLOATS + INTS)
+@pytest.mark.parametrize("op", ["sum", "prod", "max", "min", "set"])
+@pytest.mark.parametrize("n", [1, 4099, (1 << 20) + 3])
+def test_device_reduce_matches_torch(hip, dtype, op, n):
+    a, b = _rand(n, dtype, 11), _rand(n, dtype, 12)
+    expect = _ref(a, b, op)
+    got = K.reduce_(a.to(hip), b.to(hip), op)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), expect)
+
+
+@pytest.mark.parametrize("dtype", FLOATS + [torch.int32, torch.int64])
+def test_device_finalize_avg(hip, dtype):
+    x = _rand(100_003, dtype, 13)
+    assert torch.equal(K.finalize_avg(x.to(hip), 3).cpu(), K.finalize_avg(x.clone(), 3))
+
+
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("qdtype", [torch.uint8, torch.int8, torch.int16, getattr(torch, "float8_e4m3fn", None),
+                                    getattr(torch, "float8_e5m2", None)])
+@pytest.mark.parametrize("algo", ["min_max", "zero_point_scale"])
+def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
+    if qdtype is None:
+        pytest.skip("no fp8 dtype")
+    if algo == "zero_point_scale" and qdtype not in (torch.uint8, torch.int8):
+        pytest.skip("zps is 8-bit integer only")
+    x = _rand((1 << 20) + 7, vdtype, 14)
+    qh, mh = K.quantize(x, qdtype, algo)
+    qd, md = K.quantize(x.to(hip), qdtype, algo)
+    torch.cuda.synchronize()
+    assert mh == md
+    assert torch.equal(qd.cpu().view(torch.uint8), qh.view(torch.uint8))
+    acc = _rand(x.numel(), vdtype, 15)
+    rh = K.dequant_reduce(acc.clone(), qh, mh, algo, "sum")
+    rd = K.dequant_reduce(acc.to(hip), qd, md, algo, "sum")
+    torch.cuda.synchronize()
+    assert torch.equal(rd.cpu(), rh)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32])
+@pytest.mark.parametrize("nsrc", [2, 3, 5, 8, 16])
+@pytest.mark.parametrize("op", ["sum", "avg", "max"])
+def test_multi_reduce(hip, dtype, nsrc, op):
+    n = (1 << 18) + 13
+    srcs = [_rand(n, dtype, 20 + k) for k in range(nsrc)]
+    # the kernel accumulates in the compute type (fp32 for 16-bit floats) in fixed source order, rounds once
+    ct = {torch.bfloat16: torch.float32, torch.float16: torch.float32}.get(dtype, dtype)
+    acc = srcs[0].to(ct)
+    for s in srcs[1:]:
+        acc = torch.maximum(acc, s.to(ct)) if op == "max" else acc + s.to(ct)
+    if op == "avg":
+        acc = acc / nsrc if dtype.is_floating_point else torch.div(acc, nsrc, rounding_mode="trunc")
+    ref = acc.to(dtype)
+    out2 = torch.empty(n, dtype=dtype, device=hip)
+    got = K.multi_reduce([s.to(hip) for s in srcs], op, out2=out2)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref)
+    assert torch.equal(out2.cpu(), ref)
+
+
+def test_multi_gather(hip):
+    parts = [torch.randn(n, device=hip) for n in (1000, 0, 4099, 17)]
+    offs = [0, 1000, 1000, 5099]
+    dst = torch.zeros(5116, device=hip)
+    K.multi_gather(dst, parts, offs, skip=2)
+    torch.cuda.synchronize()
+    expect = torch.cat([parts[0], parts[1], torch.zeros(4099, device=hip), parts[3]])
+    assert torch.equal(dst, expect)

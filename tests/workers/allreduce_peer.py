@@ -1,0 +1,68 @@
+"""Standalone peer process used by the multi-process tests (CPU and GPU).
+
+usage: allreduce_peer.py MASTER WORLD RANK --n N --dtype bf16 --device cpu|cuda:0 --steps K [--die-at STEP]
+Each step all-reduces (rank+1+step) and checks the exact sum; prints one JSON line per step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+import torch  # noqa: E402
+
+import pccl_amd as pccl  # noqa: E402
+from pccl_amd.utils import wait_for_world  # noqa: E402
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "i32": torch.int32}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("master")
+    ap.add_argument("world", type=int)
+    ap.add_argument("rank", type=int)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--device", default="cpu")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--die-at", type=int, default=-1)
+    ap.add_argument("--min-world", type=int, default=0)
+    a = ap.parse_args()
+    dev = torch.device(a.device)
+    comm = pccl.Communicator(a.master, 0)
+    comm.connect(n_attempts=30)
+    wait_for_world(comm, a.world, timeout=120)
+    step = 0
+    while step < a.steps:
+        if step > 0 and comm.are_peers_pending():
+            comm.update_topology()
+        ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
+        if a.min_world and ws < a.min_world:
+            time.sleep(0.05)
+            continue
+        x = torch.full((a.n,), float(a.rank + 1 + step), dtype=DT[a.dtype], device=dev)
+        y = torch.empty_like(x)
+        if step == a.die_at:
+            os._exit(17)  # simulated crash (no clean disconnect)
+        t0 = time.perf_counter()
+        try:
+            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=step)
+        except pccl.PCCLError as e:
+            print(json.dumps({"rank": a.rank, "step": step, "error": e.result.name}), flush=True)
+            continue  # retry the step with the new world
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        lo, hi = float(y.float().min()), float(y.float().max())
+        print(json.dumps({"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
+                          "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt,
+                          "tx": info.tx_bytes, "rx": info.rx_bytes}), flush=True)
+        step += 1
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    main()
