@@ -288,9 +288,13 @@ int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
             const uint64_t vs = v >> 8;
             const uint32_t vp = static_cast<uint32_t>(v & 0xff);
             if (vs == seq + 1) {
-                if (vp == PH_ABORTED) return 1;
+                if (vp == PH_ABORTED) {
+                    LOG(WARN) << "IPC: peer " << k << " aborted op seq " << seq << " (phase " << phase << ")";
+                    return 1;
+                }
                 if (vp >= phase) break;
             } else if (vs > seq + 1) {
+                LOG(WARN) << "IPC: peer " << k << " is ahead (seq " << vs - 1 << " > " << seq << ")";
                 return 1;
             }
             if (++spins < 4096) {
@@ -335,7 +339,10 @@ bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
 
 int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
                         ReduceOp op) {
-    if (!wait_slot_free(c, seq)) return kAborted;
+    if (!wait_slot_free(c, seq)) {
+        LOG(WARN) << "IPC: slot of op seq " << seq << " not released by a peer";
+        return kAborted;
+    }
     CommBuf *buf = nullptr;
     if (device_ok) {
         buf = acquire_buffer(2 * bytes, device);
@@ -356,6 +363,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     set_phase(seq, PH_VOTED);
     const int rc = barrier(c, tag, seq, PH_VOTED);
     if (rc != 0) {
+        LOG(WARN) << "IPC: vote barrier failed (rc " << rc << ")";
         set_phase(seq, PH_ABORTED);
         release_buffer(buf);
         return kAborted;
@@ -408,7 +416,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     {
         std::lock_guard l(g_ctx_mtx);
         auto it = g_ctx.find({this, seq});
-        if (it == g_ctx.end()) return {false, false};
+        if (it == g_ctx.end()) {
+            LOG(ERR) << "IPC: no context for op seq " << seq;
+            return {false, false};
+        }
         ctx = std::move(it->second);
         g_ctx.erase(it);
     }
@@ -441,12 +452,18 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         }
         be->destroy_stream(st);
         release_buffer(mybuf);
-        return {rc == 2, rc == 2};
+        return {rc == 0, rc == 2};
     };
-    if (!st) return finish(1);
+    if (!st) {
+        LOG(ERR) << "IPC: cannot create a stream on device " << device;
+        return finish(1);
+    }
 
     // 1. copy-in
-    if (!be->memcpy_async(my_in, src, bytes, st) || !be->stream_sync(st)) return finish(1);
+    if (!be->memcpy_async(my_in, src, bytes, st) || !be->stream_sync(st)) {
+        LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
+        return finish(1);
+    }
     set_phase(seq, PH_COPIED);
     if (int rc = barrier(c, tag, seq, PH_COPIED)) return finish(rc);
 
@@ -465,8 +482,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     dst_touched = true;
     if (!be->multi_reduce(my_out + lo[rank_] * es, static_cast<uint8_t *>(dst) + lo[rank_] * es, srcs.data(),
                           static_cast<int>(W), n[rank_], dtype, op, st) ||
-        !be->stream_sync(st))
+        !be->stream_sync(st)) {
+        LOG(ERR) << "IPC: multi-source reduce failed";
         return finish(1);
+    }
     set_phase(seq, PH_REDUCED);
     if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
 
@@ -475,8 +494,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     for (size_t k = 0; k < W; ++k) gsrc[k] = static_cast<const uint8_t *>(ctx.peer_base[k]) + bytes + lo[k] * es;
     if (!be->multi_gather(dst, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_), dtype,
                           st) ||
-        !be->stream_sync(st))
+        !be->stream_sync(st)) {
+        LOG(ERR) << "IPC: gather failed";
         return finish(1);
+    }
     set_phase(seq, PH_GATHERED);
     if (int rc = barrier(c, tag, seq, PH_GATHERED)) return finish(rc);
 

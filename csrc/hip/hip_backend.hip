@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 
 #include "../common/device_backend.hpp"
@@ -140,7 +141,12 @@ public:
         return hipk::launch_quantize(dst_q, src, count, vtype, qtype, p, static_cast<hipStream_t>(s));
     }
     bool minmax(const void *src, size_t count, DType vtype, double *out2, DevStream s) override {
-        return hipk::launch_minmax(src, count, vtype, scratch_for(s).dev, out2, static_cast<hipStream_t>(s));
+        // the partials scratch is per stream; threads sharing a stream (e.g. the null stream) take turns until the
+        // result has landed, so interleaved launches can never mix their partials
+        Scratch &sc = scratch_for(s);
+        std::lock_guard l(*sc.mtx);
+        return hipk::launch_minmax(src, count, vtype, sc.dev, out2, static_cast<hipStream_t>(s)) &&
+               hipStreamSynchronize(static_cast<hipStream_t>(s)) == hipSuccess;
     }
     bool finalize_avg(void *dst, size_t count, DType t, size_t ws, DevStream s) override {
         return hipk::launch_finalize_avg(dst, count, t, ws, static_cast<hipStream_t>(s));
@@ -156,6 +162,7 @@ public:
     uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) override {
         if (n_bytes == 0) return 0;
         Scratch &sc = scratch_for(s);
+        std::lock_guard l(*sc.mtx);
         auto *out = reinterpret_cast<uint32_t *>(sc.host);
         if (!hipk::launch_simplehash(dev_ptr, n_bytes, reinterpret_cast<uint32_t *>(sc.dev), out,
                                      static_cast<hipStream_t>(s)) ||
@@ -173,6 +180,7 @@ private:
     struct Scratch {
         double *dev = nullptr;  // 2 x 1024 doubles: min/max partials, or 960 hash partials
         double *host = nullptr; // pinned result words
+        std::shared_ptr<std::mutex> mtx = std::make_shared<std::mutex>();
     };
     Scratch &scratch_for(DevStream s) {
         std::lock_guard l(scratch_mtx_);

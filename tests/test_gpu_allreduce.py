@@ -104,7 +104,9 @@ def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
         if bound is not None:
             assert err.max().item() <= bound
         else:
-            assert (err <= expect.abs() * 0.2 + 0.05).all()
+            # partial sums are re-quantized at every ring hop: error scales with sum(|x_r|), not |sum(x_r)|
+            mag = inputs[0].abs() + inputs[1].abs() + inputs[2].abs()
+            assert (err <= mag * 0.15 + 0.05).all()
 
 
 def test_device_shared_state(hip):

@@ -35,7 +35,7 @@ def main():
     comm = pccl.Communicator(a.master, 0)
     comm.connect(n_attempts=30)
     wait_for_world(comm, a.world, timeout=120)
-    step = 0
+    step, failures = 0, 0
     while step < a.steps:
         if step > 0 and comm.are_peers_pending():
             comm.update_topology()
@@ -52,6 +52,9 @@ def main():
             info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=step)
         except pccl.PCCLError as e:
             print(json.dumps({"rank": a.rank, "step": step, "error": e.result.name}), flush=True)
+            failures += 1
+            if failures > 20:
+                sys.exit(3)
             continue  # retry the step with the new world
         if dev.type == "cuda":
             torch.cuda.synchronize()
