@@ -6,6 +6,7 @@
 
 #include "../common/device_backend.hpp"
 #include "../kernels/host_kernels.hpp"
+#include "../kernels/optim_common.hpp"
 
 using namespace pccl;
 
@@ -148,4 +149,30 @@ PCCLX_EXPORT double pcclxBenchKernel(int which, void *dst, const void *src, size
     be->destroy_event(e1);
     be->destroy_stream(st);
     return us;
+}
+
+PCCLX_EXPORT int pcclxPseudoGrad(float *pg, const float *outer, const void *local, size_t count, int local_dtype,
+                                 int on_device) {
+    const auto lt = static_cast<DType>(local_dtype);
+    if (!on_device) return kernels::host_pseudo_grad(pg, outer, local, count, lt) ? 0 : -1;
+    DeviceBackend *be = device_backend();
+    if (!be) return -1;
+    return be->pseudo_grad(pg, outer, local, count, lt, nullptr) && be->device_sync() ? 0 : -1;
+}
+
+PCCLX_EXPORT int pcclxOuterSgd(float *outer, float *mom, const float *pg, void *local, size_t count, int local_dtype,
+                               float lr, float momentum, float dampening, float weight_decay, int nesterov, int first,
+                               int on_device) {
+    kernels::OuterSgdParams p;
+    p.lr = lr;
+    p.momentum = momentum;
+    p.dampening = dampening;
+    p.weight_decay = weight_decay;
+    p.nesterov = nesterov;
+    p.first = first;
+    const auto lt = static_cast<DType>(local_dtype);
+    if (!on_device) return kernels::host_outer_sgd(outer, mom, pg, local, count, lt, p) ? 0 : -1;
+    DeviceBackend *be = device_backend();
+    if (!be) return -1;
+    return be->outer_sgd(outer, mom, pg, local, count, lt, p, nullptr) && be->device_sync() ? 0 : -1;
 }

@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "../kernels/optim_common.hpp"
 #include "../kernels/quant_common.hpp"
 #include "types.hpp"
 
@@ -76,6 +77,12 @@ public:
     virtual uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) = 0;
     // Fills device memory with the reference test pattern (random_init_kernel of the reference tests).
     virtual bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) = 0;
+
+    // fused DiLoCo outer step (csrc/kernels/optim_common.hpp); outer/mom/pg fp32, local F32/BF16/F16
+    virtual bool pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType local_t,
+                             DevStream s) = 0;
+    virtual bool outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType local_t,
+                           const kernels::OuterSgdParams &p, DevStream s) = 0;
 };
 
 // Returns the process-wide backend (nullptr if HIP is unavailable). Loaded lazily and thread-safely.

@@ -175,6 +175,13 @@ public:
     bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) override {
         return hipk::launch_test_pattern(dev_ptr, n_u64, static_cast<hipStream_t>(s));
     }
+    bool pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType lt, DevStream s) override {
+        return hipk::launch_pseudo_grad(pg, outer, local, count, lt, static_cast<hipStream_t>(s));
+    }
+    bool outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType lt,
+                   const kernels::OuterSgdParams &p, DevStream s) override {
+        return hipk::launch_outer_sgd(outer, mom, pg, local, count, lt, p, static_cast<hipStream_t>(s));
+    }
 
 private:
     struct Scratch {

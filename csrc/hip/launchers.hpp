@@ -8,6 +8,7 @@
 #include <cstdint>
 
 #include "../common/types.hpp"
+#include "../kernels/optim_common.hpp"
 #include "../kernels/quant_common.hpp"
 
 namespace pccl::hipk {
@@ -28,6 +29,11 @@ bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n,
                          hipStream_t s);
 bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
                          int skip, DType t, hipStream_t s);
+
+// hip_optim.hip
+bool launch_pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType lt, hipStream_t s);
+bool launch_outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType lt,
+                      const kernels::OuterSgdParams &p, hipStream_t s);
 
 // hip_hash.hip
 bool launch_simplehash(const void *dev_ptr, size_t n_bytes, uint32_t *partial_scratch, uint32_t *out, hipStream_t s);

@@ -9,6 +9,7 @@
 
 #include "../common/log.hpp"
 #include "elem.hpp"
+#include "optim_common.hpp"
 
 namespace pccl::kernels {
 
@@ -429,5 +430,65 @@ bool crc32c_has_hw() {
 void crc32c_spoof_no_hw(bool no_hw) { g_spoof_no_hw = no_hw; }
 
 uint32_t crc32c(const void *data, size_t n) { return crc32c_has_hw() ? crc32c_hw(data, n) : crc32c_sw(data, n); }
+
+
+// ------------------------------------------------------------------------------------------------------------------
+// DiLoCo outer step (host twin of hip_optim.hip)
+// ------------------------------------------------------------------------------------------------------------------
+template<typename F>
+static void host_parallel(size_t count, F &&body) {
+    constexpr size_t kMinPerThread = 1 << 20;
+    const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+    const size_t nt = std::min(hw, std::max<size_t>(1, count / kMinPerThread));
+    if (nt <= 1) {
+        body(size_t{0}, count);
+        return;
+    }
+    std::vector<std::thread> ts;
+    const size_t per = (count + nt - 1) / nt;
+    for (size_t k = 0; k < nt; ++k) {
+        const size_t lo = k * per, hi = std::min(count, lo + per);
+        if (lo < hi) ts.emplace_back([&, lo, hi] { body(lo, hi); });
+    }
+    for (auto &th : ts) th.join();
+}
+
+template<typename E>
+static void pg_loop(float *pg, const float *outer, const void *local, size_t count) {
+    const auto *l = static_cast<const typename E::S *>(local);
+    host_parallel(count, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) pg[i] = outer[i] - static_cast<float>(E::ld(l[i]));
+    });
+}
+
+template<typename E>
+static void sgd_loop(float *outer, float *mom, const float *pg, void *local, size_t count, const OuterSgdParams &p) {
+    auto *l = static_cast<typename E::S *>(local);
+    host_parallel(count, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            outer_sgd_elem(outer[i], mom[i], pg[i], p);
+            l[i] = E::st(outer[i]);
+        }
+    });
+}
+
+bool host_pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType local_t) {
+    switch (local_t) {
+        case DType::F32: pg_loop<EF32>(pg, outer, local, count); return true;
+        case DType::BF16: pg_loop<EBF16>(pg, outer, local, count); return true;
+        case DType::F16: pg_loop<EF16>(pg, outer, local, count); return true;
+        default: return false;
+    }
+}
+
+bool host_outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType local_t,
+                    const OuterSgdParams &p) {
+    switch (local_t) {
+        case DType::F32: sgd_loop<EF32>(outer, mom, pg, local, count, p); return true;
+        case DType::BF16: sgd_loop<EBF16>(outer, mom, pg, local, count, p); return true;
+        case DType::F16: sgd_loop<EF16>(outer, mom, pg, local, count, p); return true;
+        default: return false;
+    }
+}
 
 } // namespace pccl::kernels

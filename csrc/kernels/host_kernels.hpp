@@ -7,6 +7,7 @@
 
 #include "../common/types.hpp"
 #include "../proto/packets.hpp"
+#include "optim_common.hpp"
 #include "quant_common.hpp"
 
 namespace pccl::kernels {
@@ -30,6 +31,13 @@ bool host_finalize_avg(void *dst, size_t count, DType t, size_t world_size);
 // "simplehash": non-associative 32-bit hash whose reduction tree emulates a 960x256 GPU launch with a 32-lane
 // shuffle tree (definition: reference ccoip/src/cuda/simplehash_cuda.cu). Requires 16-byte aligned data.
 uint32_t simplehash_host(const void *data, size_t n_bytes);
+
+// DiLoCo outer step (optim_common.hpp): pg = outer - local; outer/mom SGD update and local = cast(outer).
+// outer, mom, pg are fp32; local is F32 / BF16 / F16.
+
+bool host_pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType local_t);
+bool host_outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType local_t,
+                    const OuterSgdParams &p);
 
 // CRC-32C (Castagnoli). Uses SSE4.2 when available (and not spoofed off), otherwise slicing-by-8 tables.
 uint32_t crc32c(const void *data, size_t n_bytes);

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import importlib.util
 import os
-from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint16, c_uint32,
+from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_size_t, c_uint8, c_uint16, c_uint32,
                     c_uint64, c_void_p)
 
 if importlib.util.find_spec("torch") is not None:  # share torch's HIP runtime with the plugin
@@ -143,6 +143,9 @@ def _load() -> ctypes.CDLL:
         "pcclxMultiReduce": ([c_void_p, c_void_p, p(c_void_p), c_int, c_size_t, c_int, c_int], c_int),
         "pcclxMultiGather": ([c_void_p, p(c_void_p), p(c_size_t), p(c_size_t), c_int, c_int, c_int], c_int),
         "pcclxBenchKernel": ([c_int, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int], c_double),
+        "pcclxPseudoGrad": ([c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int], c_int),
+        "pcclxOuterSgd": ([c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_float, c_float, c_float, c_float,
+                           c_int, c_int, c_int], c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

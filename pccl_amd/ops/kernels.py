@@ -120,3 +120,30 @@ def bench_kernel(which: str, dst: torch.Tensor, src: torch.Tensor, n: int = 1, i
     w = {"reduce": 0, "hash": 1, "multi_reduce": 2, "quantize": 3}[which]
     _on_device(src)
     return float(C.pcclxBenchKernel(w, dst.data_ptr(), src.data_ptr(), src.numel(), WIRE_DTYPE[src.dtype], n, iters))
+
+
+def _local_code(t: torch.Tensor) -> int:
+    if t.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        raise TypeError(f"DiLoCo local parameters must be fp32/bf16/fp16, got {t.dtype}")
+    return WIRE_DTYPE[t.dtype]
+
+
+def pseudo_grad(pg: torch.Tensor, outer: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
+    """pg = outer - local (fp32 outer/pg; local fp32/bf16/fp16), fused HIP kernel on GPU tensors."""
+    assert pg.dtype == outer.dtype == torch.float32 and pg.numel() == outer.numel() == local.numel()
+    assert pg.is_contiguous() and outer.is_contiguous() and local.is_contiguous()
+    _check(C.pcclxPseudoGrad(pg.data_ptr(), outer.data_ptr(), local.data_ptr(), pg.numel(), _local_code(local),
+                             _on_device(pg)), "pseudo_grad")
+    return pg
+
+
+def outer_sgd(outer: torch.Tensor, momentum_buf: torch.Tensor, pg: torch.Tensor, local: torch.Tensor, *, lr: float,
+              momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+              first: bool = False) -> None:
+    """One fused pass: SGD(+momentum/nesterov) update of ``outer`` with gradient ``pg``, then local = cast(outer)."""
+    for t in (outer, momentum_buf, pg):
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == local.numel()
+    assert local.is_contiguous()
+    _check(C.pcclxOuterSgd(outer.data_ptr(), momentum_buf.data_ptr(), pg.data_ptr(), local.data_ptr(), outer.numel(),
+                           _local_code(local), lr, momentum, dampening, weight_decay, int(nesterov), int(first),
+                           _on_device(outer)), "outer_sgd")
