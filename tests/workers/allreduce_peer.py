@@ -1,7 +1,10 @@
 """Standalone peer process used by the multi-process tests (CPU and GPU).
 
-usage: allreduce_peer.py MASTER WORLD RANK --n N --dtype bf16 --device cpu|cuda:0 --steps K [--die-at STEP]
-Each step all-reduces (rank+1+step) and checks the exact sum; prints one JSON line per step.
+usage: allreduce_peer.py MASTER WORLD RANK [--n N] [--dtype f32|bf16|f16|i32] [--device cpu|cuda:0] [--steps K]
+                         [--die-at STEP] [--const] [--no-wait]
+Each step all-reduces a tensor and checks the result; prints one JSON line per attempt.
+  default: x = rank + 1 + step, tag = step (all peers start together)
+  --const: x = 1, tag 0, result must equal the op's world size (membership may change between steps)
 """
 import argparse
 import json
@@ -29,41 +32,55 @@ def main():
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--die-at", type=int, default=-1)
-    ap.add_argument("--min-world", type=int, default=0)
+    ap.add_argument("--const", action="store_true")
+    ap.add_argument("--no-wait", action="store_true", help="do not wait for WORLD peers (late joiner)")
+    ap.add_argument("--step-sleep", type=float, default=0.0)
     a = ap.parse_args()
     dev = torch.device(a.device)
+    t_start = time.perf_counter()
     comm = pccl.Communicator(a.master, 0)
     comm.connect(n_attempts=30)
-    wait_for_world(comm, a.world, timeout=120)
-    step, failures = 0, 0
+    if not a.no_wait:
+        wait_for_world(comm, a.world, timeout=120)
+    step, failures, first_ok = 0, 0, None
+    it = 0
     while step < a.steps:
-        if step > 0 and comm.are_peers_pending():
+        if it > 0 and comm.are_peers_pending():
             comm.update_topology()
+        it += 1
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
-        if a.min_world and ws < a.min_world:
+        if ws < 2:
             time.sleep(0.05)
             continue
-        x = torch.full((a.n,), float(a.rank + 1 + step), dtype=DT[a.dtype], device=dev)
+        val = 1.0 if a.const else float(a.rank + 1 + step)
+        x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
         y = torch.empty_like(x)
         if step == a.die_at:
             os._exit(17)  # simulated crash (no clean disconnect)
         t0 = time.perf_counter()
         try:
-            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=step)
+            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0 if a.const else step)
         except pccl.PCCLError as e:
             print(json.dumps({"rank": a.rank, "step": step, "error": e.result.name}), flush=True)
             failures += 1
-            if failures > 20:
+            if failures > 50:
                 sys.exit(3)
             continue  # retry the step with the new world
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if first_ok is None:
+            first_ok = time.perf_counter() - t_start
         lo, hi = float(y.float().min()), float(y.float().max())
-        print(json.dumps({"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
-                          "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt,
-                          "tx": info.tx_bytes, "rx": info.rx_bytes}), flush=True)
+        rec = {"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
+               "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
+               "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
+        if a.const and not (lo == hi == float(info.local_world_size)):
+            rec["bad"] = True
+        print(json.dumps(rec), flush=True)
         step += 1
+        if a.step_sleep:
+            time.sleep(a.step_sleep)
     comm.destroy()
 
 
