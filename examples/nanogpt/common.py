@@ -47,8 +47,8 @@ def parser(desc: str) -> argparse.ArgumentParser:
 
 
 def device_of(a) -> torch.device:
-    if a.device == "cuda" and "LOCAL_RANK" in os.environ:
-        return torch.device("cuda", int(os.environ["LOCAL_RANK"]))
+    if a.device == "cuda":
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     return torch.device(a.device)
 
 

@@ -85,6 +85,7 @@ def test_sync_diloco_two_peers(momentum):
 
 
 def test_async_diloco_two_peers():
+    _make_model(0)
     world, rounds = 2, 4
 
     def fn(rank, comm):
@@ -128,6 +129,8 @@ def test_outer_kernels_gpu_match_host(hip, local_dtype):
 
 @pytest.mark.gpu
 def test_sync_diloco_gpu(hip):
+    _make_model(0)  # build the shared init in the main thread
+
     def fn(rank, comm):
         model = _make_model(0, hip)
         d = DiLoCo(model, comm, outer_lr=0.7, outer_momentum=0.9, nesterov=True)
