@@ -18,6 +18,7 @@
 #include "../common/log.hpp"
 #include "../kernels/host_kernels.hpp"
 #include "client.hpp"
+#include "../common/trace.hpp"
 #include "ipc.hpp"
 #include "pools.hpp"
 
@@ -82,6 +83,8 @@ bool Client::all_reduce_async(const ReduceRequest &req) {
 
 void Client::run_op(const std::shared_ptr<OpState> &op) {
     const uint64_t tag = op->req.tag;
+    OpTrace trace;
+    current_trace() = trace_ops_enabled() ? &trace : nullptr;
     bool success = false, abort_seen = false;
     uint64_t seq = 0;
     bool commenced = false;
@@ -97,6 +100,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
             if (c) {
                 seq = c->seq_nr;
                 commenced = true;
+                trace_mark("commence");
             }
         }
     }
@@ -117,6 +121,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
             if (rv->arena) {
                 // every peer of an intra-node ring votes; the xGMI path runs only if all buffers are on GPUs
                 const int decision = rv->arena->vote(*this, *op, seq, device, device ? di.device : -1);
+                trace_mark("vote");
                 if (decision == IpcArena::kUseIpc) {
                     r = ipc_reduce(*op, *rv, seq, di.device);
                     done = true;
@@ -167,6 +172,15 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
         }
     }
     if (!ok) LOG(WARN) << "all-reduce tag " << tag << " failed/aborted";
+    if (current_trace()) {
+        trace.mark("complete");
+        static const char *names[] = {"none", "host_ring", "device_ring", "ipc"};
+        std::fprintf(stderr, "[pccl-trace] tag %llu seq %llu bytes %zu world %u path %s %s%s\n",
+                     static_cast<unsigned long long>(tag), static_cast<unsigned long long>(seq),
+                     op->req.count * dtype_size(op->req.dtype), op->world, names[last_path_.load() & 3],
+                     ok ? "ok" : "FAILED", trace.str().c_str());
+        current_trace() = nullptr;
+    }
     op->success = ok;
     op->done.store(true);
 }

@@ -15,6 +15,7 @@
 
 #include "../common/log.hpp"
 #include "client.hpp"
+#include "../common/trace.hpp"
 
 namespace pccl::client {
 
@@ -464,8 +465,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
         return finish(1);
     }
+    trace_mark("copy_in");
     set_phase(seq, PH_COPIED);
     if (int rc = barrier(c, tag, seq, PH_COPIED)) return finish(rc);
+    trace_mark("copied_barrier");
 
     // shard bounds: 256-byte aligned so every peer's shard is 16-byte-vector aligned
     const size_t align_el = std::max<size_t>(1, 256 / es);
@@ -486,8 +489,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         LOG(ERR) << "IPC: multi-source reduce failed";
         return finish(1);
     }
+    trace_mark("reduce");
     set_phase(seq, PH_REDUCED);
     if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
+    trace_mark("reduced_barrier");
 
     // 3. all-gather: pull every other peer's reduced shard straight into the receive buffer
     std::vector<const void *> gsrc(W);
@@ -498,8 +503,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         LOG(ERR) << "IPC: gather failed";
         return finish(1);
     }
+    trace_mark("gather");
     set_phase(seq, PH_GATHERED);
     if (int rc = barrier(c, tag, seq, PH_GATHERED)) return finish(rc);
+    trace_mark("gathered_barrier");
 
     const uint64_t moved = static_cast<uint64_t>(bytes) * (W - 1) / W;
     tx += 2 * moved;

@@ -62,3 +62,19 @@ LogLine::~LogLine() {
 }
 
 } // namespace pccl
+
+#include "trace.hpp"
+
+namespace pccl {
+bool trace_ops_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("PCCL_TRACE_OPS");
+        return e != nullptr && e[0] != '\0' && e[0] != '0';
+    }();
+    return v;
+}
+OpTrace *&current_trace() {
+    thread_local OpTrace *t = nullptr;
+    return t;
+}
+} // namespace pccl

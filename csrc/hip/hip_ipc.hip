@@ -28,7 +28,7 @@ bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n,
             using O = decltype(o);
             bool ok = true;
             if (nvec > 0) {
-                const int grid = grid_for(nvec, 2);
+                const int grid = std::min(grid_for(nvec, 2), 1024); // 4 WGs / CU measured best (kbench)
                 ok = launch_ok([&] {
                     if constexpr (std::is_same_v<O, OpSum>) {
                         if (avg) {
