@@ -27,6 +27,15 @@ namespace pccl::client {
 using namespace proto;
 using namespace std::chrono_literals;
 
+StreamPool &stream_pool() {
+    static auto *p = new StreamPool(); // never destroyed: streams may outlive static destruction order
+    return *p;
+}
+EventPool &event_pool() {
+    static auto *p = new EventPool();
+    return *p;
+}
+
 BufferPool &host_pool() {
     static BufferPool p(BufferPool::Kind::Host);
     return p;
@@ -369,6 +378,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
         if (rc) return fail(rc);
     }
 
+    trace_mark("reduce_scatter");
     // ---- all-gather
     Lease ag[2];
     if (quant) {
@@ -431,13 +441,9 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     const size_t piece = std::max<size_t>(1 << 20, std::min(chunk, env_size("PCCL_DEVICE_PIECE_BYTES", 4u << 20)));
 
     be->set_device(device);
-    DevStream st = be->create_stream();
+    StreamLease stream(device);
+    DevStream st = stream.get();
     if (!st) return {false, false};
-    struct StreamGuard {
-        DeviceBackend *be;
-        DevStream s;
-        ~StreamGuard() { be->destroy_stream(s); }
-    } sg{be, st};
 
     StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
     auto aborted = [&] { return abort_received(q.tag); };
@@ -470,16 +476,18 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
 
     std::vector<DevEvent> events;
     auto ev = [&](size_t i) {
-        while (events.size() <= i) events.push_back(be->create_event());
+        while (events.size() <= i) events.push_back(event_pool().get());
         return events[i];
     };
-    struct EvGuard {
+    struct EvGuard { // drains the op's stream before its events / staging buffers are recycled
         DeviceBackend *be;
+        DevStream s;
         std::vector<DevEvent> *e;
         ~EvGuard() {
-            for (auto x : *e) be->destroy_event(x);
+            be->stream_sync(s);
+            for (auto x : *e) event_pool().put(x);
         }
-    } eg{be, &events};
+    } eg{be, st, &events};
 
     // quantize `n` elements at device `src` into pinned txbuf; returns meta
     auto quantize_to_pinned = [&](const uint8_t *src, size_t n) -> QuantMeta {
@@ -582,6 +590,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         if (rc) return fail(rc);
     }
 
+    trace_mark("reduce_scatter");
     // ---- all-gather
     QuantMeta prev_meta;
     size_t cur = (rank + 1) % ws;

@@ -15,6 +15,7 @@
 
 #include "../common/log.hpp"
 #include "client.hpp"
+#include "pools.hpp"
 #include "../common/trace.hpp"
 
 namespace pccl::client {
@@ -432,7 +433,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     }
     DeviceBackend *be = device_backend();
     be->set_device(device);
-    DevStream st = be->create_stream();
+    StreamLease stream(device);
+    DevStream st = stream.get();
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
@@ -451,7 +453,6 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         } else {
             set_phase(seq, PH_RELEASED);
         }
-        be->destroy_stream(st);
         release_buffer(mybuf);
         return {rc == 0, rc == 2};
     };

@@ -4,6 +4,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -113,6 +114,78 @@ public:
 private:
     BufferPool *pool_ = nullptr;
     BufferPool::Buf buf_{};
+};
+
+// Reusable HIP streams / events per device: creating and destroying them per collective costs 10s-100s of us
+// (hipStreamDestroy synchronises), which is visible on every op of the latency-bound paths.
+class StreamPool {
+public:
+    DevStream get(int device) {
+        {
+            std::lock_guard l(mtx_);
+            auto &v = free_[device];
+            if (!v.empty()) {
+                DevStream s = v.back();
+                v.pop_back();
+                return s;
+            }
+        }
+        DeviceBackend *be = device_backend();
+        if (!be) return nullptr;
+        be->set_device(device);
+        return be->create_stream();
+    }
+    void put(int device, DevStream s) {
+        if (!s) return;
+        std::lock_guard l(mtx_);
+        free_[device].push_back(s);
+    }
+
+private:
+    std::mutex mtx_;
+    std::map<int, std::vector<DevStream>> free_;
+};
+
+class EventPool {
+public:
+    DevEvent get() {
+        {
+            std::lock_guard l(mtx_);
+            if (!free_.empty()) {
+                DevEvent e = free_.back();
+                free_.pop_back();
+                return e;
+            }
+        }
+        DeviceBackend *be = device_backend();
+        return be ? be->create_event() : nullptr;
+    }
+    void put(DevEvent e) {
+        if (!e) return;
+        std::lock_guard l(mtx_);
+        free_.push_back(e);
+    }
+
+private:
+    std::mutex mtx_;
+    std::vector<DevEvent> free_;
+};
+
+StreamPool &stream_pool();
+EventPool &event_pool();
+
+// RAII stream lease (the stream is synchronised by its user before it is returned)
+class StreamLease {
+public:
+    explicit StreamLease(int device) : device_(device), s_(stream_pool().get(device)) {}
+    ~StreamLease() { stream_pool().put(device_, s_); }
+    StreamLease(const StreamLease &) = delete;
+    StreamLease &operator=(const StreamLease &) = delete;
+    DevStream get() const { return s_; }
+
+private:
+    int device_;
+    DevStream s_;
 };
 
 BufferPool &host_pool();

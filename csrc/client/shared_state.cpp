@@ -152,10 +152,11 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             if (be) be->pointer_info(dst.data, pi);
             if (pi.is_device) {
                 be->set_device(pi.device);
-                DevStream st = be->create_stream();
+                StreamLease stream(pi.device);
+                DevStream st = stream.get();
                 Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
                 uint8_t *stage[2] = {a.data(), b.data()};
-                DevEvent evs[2] = {be->create_event(), be->create_event()};
+                DevEvent evs[2] = {event_pool().get(), event_pool().get()};
                 bool ok = a.ok() && b.ok();
                 size_t off = 0, k = 0;
                 while (ok && off < dst.bytes) {
@@ -169,9 +170,8 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                     ++k;
                 }
                 be->stream_sync(st);
-                be->destroy_event(evs[0]);
-                be->destroy_event(evs[1]);
-                be->destroy_stream(st);
+                event_pool().put(evs[0]);
+                event_pool().put(evs[1]);
                 if (!ok) {
                     LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
                     return false;
@@ -245,10 +245,11 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         if (be) be->pointer_info(e.data, pi);
         if (pi.is_device) {
             be->set_device(pi.device);
-            DevStream st = be->create_stream();
+            StreamLease stream(pi.device);
+            DevStream st = stream.get();
             Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
             uint8_t *stage[2] = {a.data(), b.data()};
-            DevEvent evs[2] = {be->create_event(), be->create_event()};
+            DevEvent evs[2] = {event_pool().get(), event_pool().get()};
             bool ok = a.ok() && b.ok();
             const size_t npieces = (e.bytes + kStagePiece - 1) / kStagePiece;
             auto issue = [&](size_t k) {
@@ -267,9 +268,8 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
                 if (ok) ss_tx_bytes_ += n;
             }
             be->stream_sync(st);
-            be->destroy_event(evs[0]);
-            be->destroy_event(evs[1]);
-            be->destroy_stream(st);
+            event_pool().put(evs[0]);
+            event_pool().put(evs[1]);
             if (!ok) {
                 LOG(WARN) << "Shared state: streaming " << e.key << " to " << sockaddr_str(peer) << " failed";
                 return;
