@@ -37,6 +37,9 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mib", type=int, default=1024, help="buffer size per peer in MiB (flagship: 1024)")
     ap.add_argument("--peers-per-gpu", type=int, default=0, help="N==1 only: peers sharing cuda:0 (default 2)")
+    ap.add_argument("--path", default="auto", choices=["auto", "ring"],
+                    help="auto: xGMI IPC between same-host peers; ring: force the pipelined TCP ring")
+    ap.add_argument("--pool", type=int, default=4, help="P2P connections per neighbour (ring stripes)")
     return ap.parse_args()
 
 
@@ -101,7 +104,8 @@ def bench_single_gpu(a):
         return _peer_loop(comm, x, y, a.steps, a.warmup, bar.wait, torch, pccl)
 
     with local_master() as addr:
-        res = run_threaded_peers(n_peers, fn, address=addr, timeout=1800)
+        res = run_threaded_peers(n_peers, fn, address=addr, timeout=1800,
+                                 comm_kwargs={"p2p_connection_pool_size": a.pool})
     dt = max(r[0] for r in res)
     _report(1, n_peers, a.steps, a.warmup, nbytes, dt, res[0][1], res[0][2], res[0][3], f"{n_peers} peers on 1 GPU")
 
@@ -124,7 +128,7 @@ def bench_multi_gpu(a):
         master = pccl.MasterNode(f"127.0.0.1:{port[0]}")
         master.run()
     dist.broadcast_object_list(port, src=0)
-    comm = pccl.Communicator(f"127.0.0.1:{port[0]}", 0)
+    comm = pccl.Communicator(f"127.0.0.1:{port[0]}", 0, p2p_connection_pool_size=a.pool)
     comm.connect(n_attempts=30)
     wait_for_world(comm, world, timeout=300)
     nbytes = a.mib << 20
@@ -146,6 +150,8 @@ def bench_multi_gpu(a):
 
 def main():
     a = _args()
+    if a.path == "ring":
+        os.environ["PCCL_DISABLE_IPC"] = "1"
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         bench_multi_gpu(a)
     else:

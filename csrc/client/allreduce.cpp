@@ -12,6 +12,8 @@
 //    each piece is sent as soon as its event completes; received bytes land in pinned memory and HIP kernels reduce /
 //    de-quantize them straight from pinned memory into HBM (zero-copy over PCIe), overlapped with the socket.
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <chrono>
 #include <cstring>
 
@@ -180,7 +182,9 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
             ok = got_abort && c.has_value() && !aborted && success;
         }
     }
-    if (!ok) LOG(WARN) << "all-reduce tag " << tag << " failed/aborted";
+    if (!ok) {
+        LOG(WARN) << "all-reduce tag " << tag << " failed/aborted";
+    }
     if (current_trace()) {
         trace.mark("complete");
         static const char *names[] = {"none", "host_ring", "device_ring", "ipc"};
@@ -210,7 +214,9 @@ bool Client::join_async_reduce(uint64_t tag) {
         // establish vote is illegal; the last failed op to be joined performs the round instead.
         std::lock_guard lock(establish_mtx_);
         if (conn_revision_.load() == op->revision_at_start && !interrupted_ && !any_collective_running()) {
-            if (!request_and_establish_locked(false)) LOG(ERR) << "Failed to re-establish P2P connections after abort";
+            if (!request_and_establish_locked(false)) {
+                LOG(ERR) << "Failed to re-establish P2P connections after abort";
+            }
         }
         return false;
     }
@@ -268,6 +274,121 @@ int exchange_meta(Client *self, const StepIo &io, const QuantMeta &mine, QuantMe
     (void)self;
 }
 
+// Striping: a large ring-step payload is split into up to PCCL_RING_STRIPES contiguous stripes, each sent on its own
+// pooled TCP connection by its own thread (one loopback/WAN TCP stream tops out well below the NIC / memory
+// bandwidth). Stripe boundaries depend only on (bytes, connection count, alignment), so sender and receiver derive
+// the same plan: the sender's pool to `next` is exactly the receiver's RX pool from `prev`.
+struct StripePlan {
+    std::vector<size_t> off, len;
+};
+
+// (read per step: cheap next to a ring step, and lets tests / tuning change them at runtime)
+size_t ring_stripes() { return std::max<size_t>(1, std::min<size_t>(16, env_size("PCCL_RING_STRIPES", 4))); }
+size_t stripe_min_bytes() { return std::max<size_t>(1 << 20, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20)); }
+constexpr size_t kStripeAlign = 1 << 20; // multiple of every element size and of the device staging piece
+
+StripePlan plan_stripes(size_t bytes, size_t conns) {
+    StripePlan s;
+    size_t p = std::min({ring_stripes(), std::max<size_t>(1, conns), std::max<size_t>(1, bytes / stripe_min_bytes())});
+    const size_t per = (bytes / p + kStripeAlign - 1) / kStripeAlign * kStripeAlign;
+    size_t off = 0;
+    for (size_t k = 0; k < p && (off < bytes || k == 0); ++k) {
+        const size_t n = (k + 1 == p) ? bytes - off : std::min(per, bytes - off);
+        s.off.push_back(off);
+        s.len.push_back(n);
+        off += n;
+    }
+    return s;
+}
+
+// One full-duplex ring step over the striped connections. `tx_ready(end)` blocks until payload bytes [0, end) may be
+// sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any order across
+// stripes, in order within a stripe). Returns 0 ok, 1 io failure, 2 abort.
+int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
+                 const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
+                 const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
+                 size_t rx_bytes, size_t elem, size_t frame, const std::function<void(size_t, size_t)> &consume,
+                 const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr) {
+    const StripePlan tp = plan_stripes(tx_bytes, txs.size());
+    const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
+    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
+    auto tx_conn = [&](size_t k) { return txs[(seq + k) % txs.size()].get(); };
+    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    auto remove_sinks = [&] {
+        for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->remove_sink(tag);
+    };
+
+    std::atomic<int> send_rc{0};
+    auto send_stripe = [&](size_t k) {
+        net::MuxConn *c = tx_conn(k);
+        const size_t base = tp.off[k], len = tp.len[k];
+        for (size_t sent = 0; sent < len && send_rc.load(std::memory_order_relaxed) == 0;) {
+            const size_t n = std::min(frame, len - sent);
+            if (!tx_ready(base + sent + n) || !c->send_frame(tag, seq, payload + base + sent, n)) {
+                send_rc.store(1);
+                return;
+            }
+            sent += n;
+            tx_ctr += n;
+        }
+    };
+    std::vector<std::thread> senders;
+    senders.reserve(tp.off.size());
+    for (size_t k = 0; k < tp.off.size(); ++k)
+        if (tp.len[k] > 0) senders.emplace_back(send_stripe, k);
+
+    std::vector<size_t> done(rp.off.size(), 0); // elements consumed per stripe
+    size_t remaining = rp.off.size();
+    for (size_t k = 0; k < rp.off.size(); ++k)
+        if (rp.len[k] == 0) --remaining;
+    int rc = 0;
+    size_t idle = 0, rr = 0;
+    while (remaining > 0) {
+        bool progress = false;
+        for (size_t k = 0; k < rp.off.size(); ++k) {
+            const size_t want = rp.len[k] / elem;
+            if (done[k] >= want) continue;
+            const size_t have = rx_conn(k)->sink_progress(tag) / elem;
+            if (have > done[k]) {
+                const size_t e0 = rp.off[k] / elem;
+                consume(e0 + done[k], e0 + have);
+                done[k] = have;
+                progress = true;
+                if (done[k] >= want) --remaining;
+            }
+        }
+        if (remaining == 0 || progress) {
+            idle = 0;
+            continue;
+        }
+        // block on one unfinished stripe (round robin) for a short while
+        size_t k = rr++ % rp.off.size();
+        while (done[k] >= rp.len[k] / elem) k = rr++ % rp.off.size();
+        net::MuxConn *c = rx_conn(k);
+        c->wait_sink(tag, rp.len[k], 5ms);
+        if (!c->is_open() || send_rc.load() != 0) {
+            rc = 1;
+            break;
+        }
+        if (++idle % 8 == 0 && aborted()) {
+            rc = 2;
+            break;
+        }
+    }
+    if (rc != 0) {
+        send_rc.store(rc);
+        // unblock senders stuck in send() on a dead peer: the connection is being torn down anyway
+        for (auto &t : senders) t.join();
+        remove_sinks();
+        return rc;
+    }
+    for (auto &t : senders) t.join();
+    remove_sinks();
+    if (send_rc.load() != 0) return 1;
+    rx_ctr += rx_bytes;
+    return 0;
+}
+
 } // namespace
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -304,51 +425,12 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     Lease qbuf;
     if (quant) qbuf = Lease(host_pool(), max_chunk * qs + 64);
 
-    // Runs one full-duplex step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)` for
-    // newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
+    // One full-duplex (striped) step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)`
+    // for newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
                         const std::function<void(size_t, size_t)> &consume) -> int {
-        io.rx->post_sink(q.tag, seq, sink, rx_bytes);
-        size_t sent = 0, done_el = 0;
-        const size_t rx_el = rx_bytes / qs;
-        auto drain = [&](size_t have) {
-            const size_t el = have / qs;
-            if (el > done_el) {
-                consume(done_el, el);
-                done_el = el;
-            }
-        };
-        while (sent < tx_bytes) {
-            const size_t n = std::min(chunk, tx_bytes - sent);
-            if (!io.tx->send_frame(q.tag, seq, payload + sent, n)) {
-                io.rx->remove_sink(q.tag);
-                return 1;
-            }
-            sent += n;
-            op.tx += n;
-            drain(io.rx->sink_progress(q.tag));
-        }
-        size_t idle = 0;
-        while (done_el < rx_el) {
-            const size_t have = io.rx->wait_sink(q.tag, rx_bytes, 20ms);
-            const size_t before = done_el;
-            drain(have);
-            if (done_el != before) {
-                idle = 0;
-                continue;
-            }
-            if (!io.rx->is_open()) {
-                io.rx->remove_sink(q.tag);
-                return 1;
-            }
-            if (++idle % 2 == 0 && aborted()) {
-                io.rx->remove_sink(q.tag);
-                return 2;
-            }
-        }
-        op.rx += rx_bytes;
-        io.rx->remove_sink(q.tag);
-        return 0;
+        return striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes,
+                            qs, chunk, consume, aborted, op.tx, op.rx);
     };
     auto fail = [&](int code) -> std::pair<bool, bool> {
         restore();
@@ -500,55 +582,13 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         return m;
     };
 
-    // one full-duplex step. `tx_ready(piece_idx)` blocks until that piece of the payload may be sent.
+    // one full-duplex (striped) step. `tx_ready(end)` blocks until payload bytes [0, end) may be sent.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
                         uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume) -> int {
-        io.rx->post_sink(q.tag, seq, sink, rx_bytes);
-        size_t sent = 0, done_el = 0, k = 0;
-        const size_t rx_el = rx_bytes / qs;
-        auto drain = [&](size_t have) {
-            const size_t el = have / qs;
-            if (el > done_el) {
-                consume(done_el, el);
-                done_el = el;
-            }
-        };
-        while (sent < tx_bytes) {
-            const size_t n = std::min(piece, tx_bytes - sent);
-            if (!tx_ready(k++)) {
-                io.rx->remove_sink(q.tag);
-                return 1;
-            }
-            if (!io.tx->send_frame(q.tag, seq, payload + sent, n)) {
-                io.rx->remove_sink(q.tag);
-                return 1;
-            }
-            sent += n;
-            op.tx += n;
-            drain(io.rx->sink_progress(q.tag));
-        }
-        size_t idle = 0;
-        while (done_el < rx_el) {
-            const size_t have = io.rx->wait_sink(q.tag, rx_bytes, 20ms);
-            const size_t before = done_el;
-            drain(have);
-            if (done_el != before) {
-                idle = 0;
-                continue;
-            }
-            if (!io.rx->is_open()) {
-                io.rx->remove_sink(q.tag);
-                return 1;
-            }
-            if (++idle % 2 == 0 && aborted()) {
-                io.rx->remove_sink(q.tag);
-                return 2;
-            }
-        }
-        op.rx += rx_bytes;
-        io.rx->remove_sink(q.tag);
-        be->stream_sync(st); // everything consumed from `sink` has landed in HBM
-        return 0;
+        const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs, piece,
+                                    consume, aborted, op.tx, op.rx);
+        if (rc == 0) be->stream_sync(st); // everything consumed from `sink` has landed in HBM
+        return rc;
     };
     auto always_ready = [](size_t) { return true; };
     // stage device bytes to pinned txbuf in pieces; tx_ready waits for the piece's event
@@ -559,7 +599,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
             be->event_record(ev(k), st);
         }
     };
-    auto d2h_ready = [&](size_t k) { return be->event_sync(ev(k)); };
+    auto d2h_ready = [&](size_t end) { return end == 0 || be->event_sync(ev((end - 1) / piece)); };
     auto fail = [&](int code) -> std::pair<bool, bool> {
         restore();
         return {code == 2, code == 2};

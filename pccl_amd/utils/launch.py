@@ -75,7 +75,8 @@ def wait_for_world(comm, world_size: int, timeout: float = 60.0, poll: float = 0
 
 
 def run_threaded_peers(n: int, fn: Callable[[int, object], object], *, address: str, timeout: float = 120.0,
-                       peer_group: int = 0, connect_stagger: float = 0.0) -> List[object]:
+                       peer_group: int = 0, connect_stagger: float = 0.0,
+                       comm_kwargs: Optional[Dict[str, object]] = None) -> List[object]:
     """Runs ``fn(rank, communicator)`` on n peers, one thread each, all connected to ``address``.
 
     Each peer waits until the world has n members before calling ``fn``. Exceptions are re-raised in the caller.
@@ -88,7 +89,7 @@ def run_threaded_peers(n: int, fn: Callable[[int, object], object], *, address: 
 
     def body(r: int):
         try:
-            c = Communicator(address, peer_group, **ports[r])
+            c = Communicator(address, peer_group, **ports[r], **(comm_kwargs or {}))
             comms[r] = c
             c.connect(n_attempts=10)
             wait_for_world(c, n, timeout=timeout)

@@ -194,3 +194,26 @@ def test_single_peer_too_few_peers():
     with local_master() as addr:
         res = run_threaded_peers(1, fn, address=addr)
     assert res[0] == pccl.Result.TOO_FEW_PEERS
+
+
+@pytest.mark.parametrize("world,pool", [(2, 4), (3, 3), (3, 8)])
+@pytest.mark.parametrize("quant", [False, True])
+def test_striped_large_all_reduce(world, pool, quant, monkeypatch):
+    """Large chunks are striped over the connection pool (PCCL_STRIPE_MIN_BYTES lowered to exercise uneven plans)."""
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
+    n = 3_000_017
+    inputs = [_peer_tensor(r, n, torch.float32) for r in range(world)]
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if quant else None
+
+    def fn(rank, comm):
+        out = torch.empty(n)
+        comm.all_reduce(inputs[rank], out, op=pccl.ReduceOp.SUM, tag=0, quantization_options=qopt)
+        return out
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, comm_kwargs={"p2p_connection_pool_size": pool})
+    for out in res[1:]:
+        assert torch.equal(out, res[0])
+    expect = _expected(inputs, pccl.ReduceOp.SUM).float()
+    tol = 3 * world * max(float(t.max() - t.min()) for t in inputs) / 255 if quant else 1e-4
+    assert (res[0] - expect).abs().max().item() <= tol
