@@ -278,7 +278,9 @@ pcclResult_t pcclAllReduceMultipleWithRetry(const pcclReduceOpDescriptor_t *desc
                 any_failed = true;
             }
         }
-        if (any_failed) LOG(WARN) << "pcclAllReduceMultipleWithRetry: retrying failed all-reduces";
+        if (any_failed) {
+            LOG(WARN) << "pcclAllReduceMultipleWithRetry: retrying failed all-reduces";
+        }
     }
     if (info_out != nullptr) {
         info_out->local_world_size = static_cast<uint32_t>(c.local_world_size());

@@ -49,17 +49,24 @@ struct alignas(64) PeerSlotShm {
     uint8_t uuid[16];
 };
 
+// Per (op slot, peer) record. Every peer publishes where its op *input* (read by the reduce-scatter) and *output*
+// (written by its own reduce, read by the all-gather) live:
+//   zero-copy (out-of-place device buffers): input = the caller's send buffer, output = the caller's receive buffer
+//   staged (in-place or export failure):     input / output = the two halves of a pooled, exported comm buffer
+// Peers may mix the two modes. *_raw are usable directly by peers in the same process (threaded peers).
 struct alignas(64) OpPeerShm {
     std::atomic<uint64_t> phase; // (seq + 1) << 8 | phase
     uint32_t vote;
     int32_t device;
     uint64_t bytes;
-    uint64_t buf_id;
-    uint64_t buf_cap;
     uint32_t dtype;
     uint32_t op;
-    uint64_t raw_ptr; // valid only inside the exporting process (peers that share a process skip the IPC mapping)
-    uint8_t handle[kIpcHandleBytes];
+    uint32_t zero_copy;
+    uint32_t pad;
+    uint64_t in_raw, out_raw;
+    uint64_t in_off, out_off;
+    uint8_t in_handle[kIpcHandleBytes];
+    uint8_t out_handle[kIpcHandleBytes];
 };
 
 struct ArenaShm {
@@ -77,8 +84,10 @@ struct ArenaShm {
 };
 
 struct OpCtx {
-    void *mine_in = nullptr;
-    std::vector<void *> peer_base;
+    bool zero_copy = false;
+    void *comm = nullptr;          // staged mode: my comm buffer (input half | output half)
+    void *my_out = nullptr;        // where my reduce writes shard `rank` (peers gather from here)
+    std::vector<const uint8_t *> peer_in, peer_out;
     size_t bytes = 0;
 };
 
@@ -257,16 +266,52 @@ void IpcArena::release_buffer(CommBuf *b) {
     b->busy = false;
 }
 
-void *IpcArena::peer_mapping(int peer, uint64_t buf_id, const uint8_t *handle, int my_device) {
+void *IpcArena::peer_mapping(int peer, const uint8_t *handle, int my_device) {
     std::lock_guard l(mtx_);
-    const auto key = std::make_tuple(peer, buf_id, my_device);
+    std::array<uint8_t, kIpcHandleBytes> hb;
+    std::memcpy(hb.data(), handle, kIpcHandleBytes);
+    const auto key = std::make_tuple(peer, hb, my_device);
     auto it = mappings_.find(key);
-    if (it != mappings_.end()) return it->second;
+    if (it != mappings_.end()) {
+        auto pos = std::find(mapping_lru_.begin(), mapping_lru_.end(), key); // touch (most recently used last)
+        if (pos != mapping_lru_.end() && pos + 1 != mapping_lru_.end()) {
+            mapping_lru_.erase(pos);
+            mapping_lru_.push_back(key);
+        }
+        return it->second;
+    }
     DeviceBackend *be = device_backend();
     be->set_device(my_device);
     void *p = be->ipc_open(handle);
-    if (p) mappings_[key] = p;
+    if (!p) return nullptr;
+    mappings_[key] = p;
+    mapping_lru_.push_back(key);
+    // bound the number of open mappings (user allocations come and go); never evict entries of in-flight ops:
+    // those were (re)inserted at the back by this call or by the vote of the op that uses them
+    constexpr size_t kMaxMappings = 256;
+    while (mapping_lru_.size() > kMaxMappings) {
+        auto old = mapping_lru_.front();
+        mapping_lru_.erase(mapping_lru_.begin());
+        auto mit = mappings_.find(old);
+        if (mit != mappings_.end()) {
+            be->set_device(std::get<2>(old));
+            be->ipc_close(mit->second);
+            mappings_.erase(mit);
+        }
+    }
+    be->set_device(my_device);
     return p;
+}
+
+bool IpcArena::export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset) {
+    DeviceBackend *be = device_backend();
+    void *base = nullptr;
+    size_t size = 0;
+    if (!be->address_range(p, &base, &size) || base == nullptr) return false;
+    be->set_device(device);
+    if (!be->ipc_export(base, handle)) return false; // e.g. VMM / expandable-segment memory: use the staged mode
+    offset = static_cast<uint64_t>(static_cast<uint8_t *>(p) - static_cast<uint8_t *>(base));
+    return true;
 }
 
 void IpcArena::set_phase(uint64_t seq, uint32_t phase) {
@@ -340,28 +385,43 @@ bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
 }
 
 int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
-                        ReduceOp op) {
+                        ReduceOp op, const void *src, void *dst) {
     if (!wait_slot_free(c, seq)) {
         LOG(WARN) << "IPC: slot of op seq " << seq << " not released by a peer";
         return kAborted;
     }
-    CommBuf *buf = nullptr;
-    if (device_ok) {
-        buf = acquire_buffer(2 * bytes, device);
-        if (!buf) device_ok = false;
-    }
     OpPeerShm *mine = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    CommBuf *buf = nullptr;
+    bool zero_copy = false;
+    if (device_ok) {
+        // zero-copy needs distinct send / receive buffers (in-place ops keep the staged copy as their abort backup)
+        if (src != dst && !env_flag("PCCL_IPC_NO_ZERO_COPY", false)) {
+            zero_copy = export_user(const_cast<void *>(src), device, mine->in_handle, mine->in_off) &&
+                        export_user(dst, device, mine->out_handle, mine->out_off);
+        }
+        if (zero_copy) {
+            mine->in_raw = reinterpret_cast<uint64_t>(src);
+            mine->out_raw = reinterpret_cast<uint64_t>(dst);
+        } else {
+            buf = acquire_buffer(2 * bytes, device);
+            if (!buf) {
+                device_ok = false;
+            } else {
+                std::memcpy(mine->in_handle, buf->handle, kIpcHandleBytes);
+                std::memcpy(mine->out_handle, buf->handle, kIpcHandleBytes);
+                mine->in_off = 0;
+                mine->out_off = bytes;
+                mine->in_raw = reinterpret_cast<uint64_t>(buf->ptr);
+                mine->out_raw = reinterpret_cast<uint64_t>(static_cast<uint8_t *>(buf->ptr) + bytes);
+            }
+        }
+    }
     mine->vote = device_ok ? 1 : 0;
+    mine->zero_copy = zero_copy ? 1 : 0;
     mine->device = device;
     mine->bytes = bytes;
     mine->dtype = static_cast<uint32_t>(dtype);
     mine->op = static_cast<uint32_t>(op);
-    if (buf) {
-        mine->buf_id = buf->id;
-        mine->buf_cap = buf->cap;
-        mine->raw_ptr = reinterpret_cast<uint64_t>(buf->ptr);
-        std::memcpy(mine->handle, buf->handle, kIpcHandleBytes);
-    }
     set_phase(seq, PH_VOTED);
     const int rc = barrier(c, tag, seq, PH_VOTED);
     if (rc != 0) {
@@ -384,25 +444,28 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     }
     OpCtx ctx;
     ctx.bytes = bytes;
-    ctx.mine_in = buf->ptr;
-    ctx.peer_base.resize(ring_.size());
+    ctx.zero_copy = zero_copy;
+    ctx.comm = buf ? buf->ptr : nullptr;
+    ctx.my_out = zero_copy ? dst : static_cast<uint8_t *>(buf->ptr) + bytes;
+    ctx.peer_in.resize(ring_.size());
+    ctx.peer_out.resize(ring_.size());
     for (size_t k = 0; k < ring_.size(); ++k) {
-        if (k == rank_) {
-            ctx.peer_base[k] = buf->ptr;
-            continue;
-        }
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
-        if (pids_[k] == pids_[rank_]) { // same process (threaded peers): the pointer is directly usable
-            ctx.peer_base[k] = reinterpret_cast<void *>(p->raw_ptr);
+        if (k == rank_ || pids_[k] == pids_[rank_]) { // same process (threaded peers): raw pointers are usable
+            ctx.peer_in[k] = reinterpret_cast<const uint8_t *>(p->in_raw);
+            ctx.peer_out[k] = reinterpret_cast<const uint8_t *>(p->out_raw);
             continue;
         }
-        ctx.peer_base[k] = peer_mapping(static_cast<int>(k), p->buf_id, p->handle, device);
-        if (!ctx.peer_base[k]) {
-            LOG(ERR) << "IPC: cannot map buffer of peer " << k;
+        auto *in_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->in_handle, device));
+        auto *out_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->out_handle, device));
+        if (!in_base || !out_base) {
+            LOG(ERR) << "IPC: cannot map the buffers of peer " << k;
             set_phase(seq, PH_ABORTED);
             release_buffer(buf);
             return kAborted;
         }
+        ctx.peer_in[k] = in_base + p->in_off;
+        ctx.peer_out[k] = out_base + p->out_off;
     }
     {
         std::lock_guard l(g_ctx_mtx);
@@ -426,10 +489,10 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         g_ctx.erase(it);
     }
     CommBuf *mybuf = nullptr;
-    {
+    if (ctx.comm) {
         std::lock_guard l(mtx_);
         for (auto &b : bufs_)
-            if (b->ptr == ctx.mine_in) mybuf = b.get();
+            if (b->ptr == ctx.comm) mybuf = b.get();
     }
     DeviceBackend *be = device_backend();
     be->set_device(device);
@@ -438,16 +501,15 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
-    auto *my_in = static_cast<uint8_t *>(ctx.mine_in);
-    auto *my_out = my_in + bytes;
+    auto *my_out = static_cast<uint8_t *>(ctx.my_out);
     bool dst_touched = false;
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
             set_phase(seq, PH_ABORTED);
             be->stream_sync(st);
-            if (dst_touched && src == dst) { // restore the caller's buffer from the copied-in original
-                be->memcpy_async(dst, my_in, bytes, st);
+            if (dst_touched && src == dst && ctx.comm) { // restore the caller's buffer from the staged original
+                be->memcpy_async(dst, ctx.comm, bytes, st);
                 be->stream_sync(st);
             }
         } else {
@@ -457,14 +519,16 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         return {rc == 0, rc == 2};
     };
     if (!st) {
-        LOG(ERR) << "IPC: cannot create a stream on device " << device;
+        LOG(ERR) << "IPC: no stream on device " << device;
         return finish(1);
     }
 
-    // 1. copy-in
-    if (!be->memcpy_async(my_in, src, bytes, st) || !be->stream_sync(st)) {
-        LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
-        return finish(1);
+    // 1. staged mode: copy-in (zero-copy peers expose the caller's send buffer directly)
+    if (!ctx.zero_copy) {
+        if (!be->memcpy_async(ctx.comm, src, bytes, st) || !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
+            return finish(1);
+        }
     }
     trace_mark("copy_in");
     set_phase(seq, PH_COPIED);
@@ -480,12 +544,13 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         n[k] = std::min(lo[k] + per, count) - lo[k];
     }
 
-    // 2. reduce-scatter: read shard `rank` from every peer over xGMI, reduce in fixed peer order
+    // 2. reduce-scatter: read shard `rank` of every peer's input over xGMI, reduce in fixed peer order; the result
+    //    lands in my output (= the caller's receive buffer in zero-copy mode, else the comm buffer + caller's buffer)
     std::vector<const void *> srcs(W);
-    for (size_t k = 0; k < W; ++k) srcs[k] = static_cast<const uint8_t *>(ctx.peer_base[k]) + lo[rank_] * es;
+    for (size_t k = 0; k < W; ++k) srcs[k] = ctx.peer_in[k] + lo[rank_] * es;
     dst_touched = true;
-    if (!be->multi_reduce(my_out + lo[rank_] * es, static_cast<uint8_t *>(dst) + lo[rank_] * es, srcs.data(),
-                          static_cast<int>(W), n[rank_], dtype, op, st) ||
+    void *dst1 = ctx.zero_copy ? nullptr : static_cast<uint8_t *>(dst) + lo[rank_] * es;
+    if (!be->multi_reduce(my_out + lo[rank_] * es, dst1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st) ||
         !be->stream_sync(st)) {
         LOG(ERR) << "IPC: multi-source reduce failed";
         return finish(1);
@@ -497,7 +562,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
 
     // 3. all-gather: pull every other peer's reduced shard straight into the receive buffer
     std::vector<const void *> gsrc(W);
-    for (size_t k = 0; k < W; ++k) gsrc[k] = static_cast<const uint8_t *>(ctx.peer_base[k]) + bytes + lo[k] * es;
+    for (size_t k = 0; k < W; ++k) gsrc[k] = ctx.peer_out[k] + lo[k] * es;
     if (!be->multi_gather(dst, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_), dtype,
                           st) ||
         !be->stream_sync(st)) {

@@ -17,6 +17,7 @@
 // (fault tolerance is preserved); a vote at the start of each op lets all peers agree on the data path.
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <cstdint>
 #include <map>
@@ -55,7 +56,7 @@ public:
 
     // internal (exposed for the vote template)
     int vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
-                  ReduceOp op);
+                  ReduceOp op, const void *src, void *dst);
 
 private:
     IpcArena() = default;
@@ -69,7 +70,9 @@ private:
     };
     CommBuf *acquire_buffer(size_t bytes, int device);
     void release_buffer(CommBuf *b);
-    void *peer_mapping(int peer, uint64_t buf_id, const uint8_t *handle, int my_device);
+    void *peer_mapping(int peer, const uint8_t *handle, int my_device);
+    // exports the allocation holding a user device buffer (zero-copy path); cached per allocation base
+    bool export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset);
     // waits until every peer reached `phase` for `seq`; 0 ok, 1 failure (peer dead/aborted/timeout), 2 master abort
     int barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase);
     void set_phase(uint64_t seq, uint32_t phase);
@@ -85,13 +88,16 @@ private:
     std::mutex mtx_;
     std::vector<std::unique_ptr<CommBuf>> bufs_;
     uint64_t next_buf_id_ = 1;
-    std::map<std::tuple<int, uint64_t, int>, void *> mappings_; // (peer, buf id, my device) -> mapped ptr
+    // (peer, handle bytes, my device) -> mapped allocation base; handles identify allocations uniquely (a freed and
+    // re-allocated block at the same address gets a new handle), so stale entries are merely unused
+    std::map<std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>, void *> mappings_;
+    std::vector<std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>> mapping_lru_;
 };
 
 template<typename Op>
 int IpcArena::vote(Client &c, Op &op, uint64_t seq, bool device_ok, int device) {
     return vote_impl(c, op.req.tag, seq, device_ok, device, op.req.count * dtype_size(op.req.dtype), op.req.dtype,
-                     op.req.op);
+                     op.req.op, op.req.src, op.req.dst);
 }
 
 } // namespace pccl::client

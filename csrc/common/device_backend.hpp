@@ -40,6 +40,8 @@ public:
     virtual bool ipc_export(void *dev_ptr, uint8_t handle[kIpcHandleBytes]) = 0;
     virtual void *ipc_open(const uint8_t handle[kIpcHandleBytes]) = 0;
     virtual void ipc_close(void *mapped) = 0;
+    // allocation containing `p` (IPC handles always map the allocation base; offsets travel separately)
+    virtual bool address_range(const void *p, void **base, size_t *size) = 0;
 
     // streams / events
     virtual DevStream create_stream() = 0; // non-blocking stream on the current device

@@ -81,6 +81,17 @@ public:
     void ipc_close(void *mapped) override {
         if (mapped) (void)hipIpcCloseMemHandle(mapped);
     }
+    bool address_range(const void *p, void **base, size_t *size) override {
+        hipDeviceptr_t b = nullptr;
+        size_t n = 0;
+        if (hipMemGetAddressRange(&b, &n, const_cast<void *>(p)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        *base = reinterpret_cast<void *>(b);
+        *size = n;
+        return true;
+    }
 
     DevStream create_stream() override {
         hipStream_t s = nullptr;

@@ -126,11 +126,16 @@ def test_device_shared_state(hip):
     assert [r[1] for r in res] == [0, n * 4, 0]
 
 
-def test_two_process_ipc(hip, tmp_path):
-    """Two processes on cuda:0 exchange device buffers through hipIpc handles (the intra-node xGMI path)."""
+@pytest.mark.parametrize("mode", ["zero_copy", "inplace", "mixed"])
+def test_two_process_ipc(hip, mode):
+    """Two processes on cuda:0 exchange device buffers through hipIpc handles (the intra-node xGMI path):
+    out-of-place ops export the caller's buffers (zero-copy, interior offsets), in-place ops a staged comm buffer."""
+    def extra(r):
+        return ["--inplace"] if mode == "inplace" or (mode == "mixed" and r == 1) else []
     with local_master() as addr:
         procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, "2", str(r), "--n",
-                               str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3"],
+                               str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3",
+                               *extra(r)],
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
         outs = [p.communicate(timeout=240) for p in procs]
     for p, (o, e) in zip(procs, outs):
@@ -141,3 +146,25 @@ def test_two_process_ipc(hip, tmp_path):
             expect = float(1 + 2 + 2 * ln["step"])
             assert ln["lo"] == ln["hi"] == expect
             assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value
+
+
+@pytest.mark.parametrize("inplace", [(False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("no_zc", [False, True])
+def test_device_ipc_modes(hip, inplace, no_zc, monkeypatch):
+    """Zero-copy and staged peers mixed in one op; interior (offset) views of larger allocations."""
+    if no_zc:
+        monkeypatch.setenv("PCCL_IPC_NO_ZERO_COPY", "1")
+    n = 3_000_001
+    big = [torch.randn(n + 1000, device=hip) for _ in range(2)]
+
+    def fn(rank, comm):
+        x = big[rank][777:777 + n]  # interior view: the IPC handle maps the allocation base
+        expect = (big[0][777:777 + n] + big[1][777:777 + n]).clone()
+        y = x if inplace[rank] else torch.empty_like(x)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        torch.cuda.synchronize()
+        return y.cpu(), expect.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    for y, expect, path in _run(2, fn):
+        assert path == pccl.ReducePath.DEVICE_IPC.value
+        assert torch.equal(y, expect)

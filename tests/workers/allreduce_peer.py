@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--const", action="store_true")
     ap.add_argument("--no-wait", action="store_true", help="do not wait for WORLD peers (late joiner)")
     ap.add_argument("--step-sleep", type=float, default=0.0)
+    ap.add_argument("--inplace", action="store_true")
     a = ap.parse_args()
     dev = torch.device(a.device)
     t_start = time.perf_counter()
@@ -54,7 +55,7 @@ def main():
             continue
         val = 1.0 if a.const else float(a.rank + 1 + step)
         x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
-        y = torch.empty_like(x)
+        y = x if a.inplace else torch.empty_like(x)
         if step == a.die_at:
             os._exit(17)  # simulated crash (no clean disconnect)
         t0 = time.perf_counter()
