@@ -1,0 +1,89 @@
+"""Native (C/C++) tests: internal unit tests, C-API peers against the standalone ccoip_master executable
+(reference tests/basic_reduce_test + tests/concurrent_reduce_test), C99 header compatibility, sanitizer build."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from pccl_amd.utils import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "build")
+MASTER = os.path.join(ROOT, "pccl_amd", "lib", "ccoip_master")
+
+
+def _ensure_built():
+    need = [os.path.join(BUILD, "tests", "pccl_unit_tests"), os.path.join(BUILD, "tests", "pccl_reduce_peer"), MASTER]
+    if not all(os.path.exists(p) for p in need):
+        import __graft_entry__
+        __graft_entry__.build()
+    return need
+
+
+def test_unit_tests():
+    unit, _, _ = _ensure_built()
+    r = subprocess.run([unit], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failure(s)" in r.stdout
+
+
+@pytest.mark.parametrize("world,num_ops,n,pool,inflight", [(2, 4, 1 << 20, 1, 4), (3, 8, 100_003, 2, 3),
+                                                           (4, 16, 65_536, 4, 16)])
+def test_c_api_peers_with_standalone_master(world, num_ops, n, pool, inflight):
+    _, peer, master = _ensure_built()
+    port = free_port()
+    m = subprocess.Popen([master, "--port", str(port)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        assert "listening" in m.stdout.readline()
+        peers = [subprocess.Popen([peer, str(port), str(world), "3", str(num_ops), str(n), str(pool), str(inflight)],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(world)]
+        outs = [p.communicate(timeout=180) for p in peers]
+        for p, (o, e) in zip(peers, outs):
+            assert p.returncode == 0, e[-2000:]
+            steps = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
+            assert len(steps) == 3 and all(s["world"] == world for s in steps)
+    finally:
+        m.terminate()
+        m.wait(timeout=30)
+    assert m.returncode == 0  # SIGTERM -> clean interrupt + await termination
+
+
+def test_c99_header_compat(tmp_path):
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = os.path.join(ROOT, "tests", "native", "c99_compat.c")
+    r = subprocess.run([cc, "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        "-c", src, "-o", str(tmp_path / "c99.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.skipif(os.environ.get("PCCL_TEST_SANITIZE") != "1", reason="set PCCL_TEST_SANITIZE=1 (slow build)")
+def test_sanitizer_build_unit_and_peers():
+    """ASan + UBSan build of the host library (reference PCCL_SANITIZE_TESTS); runs the unit tests and a 3-peer
+    C-API reduce with the sanitized library."""
+    bdir = os.path.join(ROOT, "build-asan")
+    out = os.path.join(bdir, "lib")
+    subprocess.run(["cmake", "-S", ROOT, "-B", bdir, "-G", "Ninja", "-DPCCL_SANITIZE=ON", "-DPCCL_BUILD_HIP_SUPPORT=OFF",
+                    f"-DPCCL_OUTPUT_DIR={out}", "-DCMAKE_BUILD_TYPE=RelWithDebInfo"], check=True, capture_output=True)
+    subprocess.run(["ninja", "-C", bdir, "-j", "8"], check=True, capture_output=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(bdir, "tests", "pccl_unit_tests")], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    port = free_port()
+    m = subprocess.Popen([os.path.join(out, "ccoip_master"), "--port", str(port)], stdout=subprocess.PIPE, text=True,
+                         env=env)
+    try:
+        m.stdout.readline()
+        peers = [subprocess.Popen([os.path.join(bdir, "tests", "pccl_reduce_peer"), str(port), "3", "3", "4",
+                                   "200003", "2"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                 for _ in range(3)]
+        for p in peers:
+            o, e = p.communicate(timeout=300)
+            assert p.returncode == 0, e[-3000:]
+    finally:
+        m.terminate()
+        m.wait(timeout=60)
