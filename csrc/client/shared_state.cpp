@@ -108,14 +108,12 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         LOG(ERR) << "Shared state sync: no response from master (kicked?)";
         return false;
     }
-    if (resp->is_outdated) {
-        if (sockaddr_is_zero(resp->distributor)) {
-            LOG(ERR) << "Shared state sync: master assigned no distributor";
-            return false;
-        }
-        const int fd = net::connect_tcp(resp->distributor, 10000);
+    // Fetches the outdated entries from one distributor; false if it failed or died mid-transfer (partially written
+    // entries are overwritten by the next attempt, and every entry is hash-verified at the end).
+    auto fetch_from = [&](const SockAddr &distributor) -> bool {
+        const int fd = net::connect_tcp(distributor, 10000);
         if (fd < 0) {
-            LOG(ERR) << "Shared state sync: cannot reach distributor " << sockaddr_str(resp->distributor);
+            LOG(WARN) << "Shared state sync: cannot reach distributor " << sockaddr_str(distributor);
             return false;
         }
         struct FdGuard {
@@ -127,7 +125,7 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         if (!net::send_packet(fd, req)) return false;
         auto sresp = net::recv_packet<S2CSharedStateResponse>(fd);
         if (!sresp || sresp->status != SharedStateStatus::Success) {
-            LOG(ERR) << "Shared state sync: distributor refused (status "
+            LOG(WARN) << "Shared state sync: distributor refused (status "
                      << (sresp ? static_cast<int>(sresp->status) : -1) << ")";
             return false;
         }
@@ -193,10 +191,28 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 }
             }
         }
+        return true;
+    };
+    bool fetched = !resp->is_outdated;
+    if (resp->is_outdated) {
+        std::vector<SockAddr> sources;
+        if (!sockaddr_is_zero(resp->distributor)) sources.push_back(resp->distributor);
+        for (const auto &f : resp->fallback_distributors) sources.push_back(f);
+        if (sources.empty()) LOG(ERR) << "Shared state sync: master assigned no distributor";
+        for (const auto &src : sources) {
+            info.rx_bytes = 0;
+            if ((fetched = fetch_from(src))) break;
+            LOG(WARN) << "Shared state sync: distributor " << sockaddr_str(src) << " failed; trying the next one";
+        }
     }
+    // complete the round even if nothing could be fetched: the other peers must not wait for us forever
     if (!master_.send(C2MDistSharedStateComplete{})) return false;
     if (!master_.receive<M2CSyncSharedStateComplete>()) {
         LOG(ERR) << "Shared state sync: no completion from master";
+        return false;
+    }
+    if (!fetched) {
+        LOG(ERR) << "Shared state sync: no distributor could deliver the shared state";
         return false;
     }
     info.tx_bytes = ss_tx_bytes_.exchange(0);

@@ -12,6 +12,7 @@ using namespace proto;
 Master::Master(const SockAddr &listen_addr) : server_(listen_addr, false) {
     server_.on_read([this](const SockAddr &a, uint16_t id, const uint8_t *p, size_t n) { on_packet(a, id, p, n); });
     server_.on_close([this](const SockAddr &a) { on_disconnect(a); });
+    server_.on_tick([this] { on_tick(); });
 }
 
 Master::~Master() {
@@ -162,7 +163,12 @@ void Master::send_connection_info(bool include_registered) {
     for (auto &[u, c] : clients_) {
         if (c.state != State::ConnectingToPeers) continue;
         M2CP2PConnectionInfo info;
-        info.global_world_size = clients_.size();
+        // peers still waiting for admission are not part of the run yet (the reference counts every registered
+        // client here, which makes a lone peer with a pending newcomer believe it has company: ops then fail with
+        // pcclTooFewPeers forever)
+        info.global_world_size = 0;
+        for (const auto &[_, o] : clients_)
+            if (include_registered || o.phase == Phase::Accepted) ++info.global_world_size;
         info.local_world_size = local_world_size(c.group, include_registered);
         info.num_distinct_peer_groups = num_groups(include_registered);
         info.largest_peer_group_world_size = largest_group(include_registered);
@@ -756,8 +762,14 @@ bool Master::check_sync_consensus(uint32_t group) {
         M2CSyncSharedState resp;
         resp.is_outdated = c.state == State::RequestSharedState;
         if (resp.is_outdated) {
-            if (!distributors.empty()) resp.distributor = distributors[dist_rr_++ % distributors.size()]->ss;
-            else LOG(ERR) << "Master: no shared state distributor for " << u.str();
+            if (!distributors.empty()) {
+                const size_t first = dist_rr_++ % distributors.size();
+                resp.distributor = distributors[first]->ss;
+                for (size_t k = 1; k < distributors.size(); ++k)
+                    resp.fallback_distributors.push_back(distributors[(first + k) % distributors.size()]->ss);
+            } else {
+                LOG(ERR) << "Master: no shared state distributor for " << u.str();
+            }
             resp.outdated_keys = gs.dirty_keys[u];
             for (const auto &k : resp.outdated_keys) {
                 resp.expected_hashes.push_back(gs.hashes[k]);
@@ -961,6 +973,56 @@ void Master::on_disconnect(const SockAddr &addr) {
         check_coll_initiate_consensus(info.group, tag);
         check_coll_complete_consensus(info.group, tag);
     }
+    maybe_bootstrap_orphans();
+}
+
+// PCCL_MASTER_DUMP_SEC=N: log the full consensus state every N seconds (diagnosing stuck runs)
+void Master::on_tick() {
+    static const size_t every = env_size("PCCL_MASTER_DUMP_SEC", 0);
+    if (every == 0) return;
+    const auto now = std::chrono::steady_clock::now();
+    if (now - last_dump_ < std::chrono::seconds(every)) return;
+    last_dump_ = now;
+    LOG(WARN) << "Master state:\n" << dump_state();
+}
+
+std::string Master::dump_state() const {
+    static const char *phases[] = {"registered", "accepted"};
+    static const char *states[] = {"idle", "vote_accept_new", "vote_no_new", "connecting", "connecting_failed",
+                                   "waiting_for_others", "vote_optimize", "optimize", "optimize_failed",
+                                   "vote_optimize_complete", "vote_sync_ss", "distribute_ss", "request_ss",
+                                   "vote_ss_complete", "collectives_running"};
+    static const char *colls[] = {"vote_initiate", "perform", "vote_complete"};
+    std::string s;
+    for (const auto &[u, c] : clients_) {
+        s += "  " + u.str().substr(0, 8) + " " + sockaddr_str(c.addr) + " group " + std::to_string(c.group) + " " +
+             phases[static_cast<int>(c.phase)] + " " + states[static_cast<int>(c.state)] +
+             (c.voted_pending_query ? " (voted pending query)" : "");
+        for (const auto &[tag, cs] : c.colls) s += " tag" + std::to_string(tag) + ":" + colls[static_cast<int>(cs)];
+        s += "\n";
+    }
+    return s;
+}
+
+// Newcomers are admitted by a vote of the accepted peers. If every accepted peer left while newcomers were waiting,
+// nobody would ever vote: bootstrap them like the very first peer of a run.
+void Master::maybe_bootstrap_orphans() {
+    bool any_accepted = false, any_waiting = false, any_connecting = false;
+    for (const auto &[_, c] : clients_) {
+        any_accepted = any_accepted || c.phase == Phase::Accepted;
+        any_waiting = any_waiting || (c.phase == Phase::Registered && c.state == State::Idle);
+        any_connecting = any_connecting || c.state == State::ConnectingToPeers || c.state == State::WaitingForOtherPeers;
+    }
+    if (any_accepted || !any_waiting || any_connecting) return;
+    LOG(INFO) << "Master: no accepted peers left; admitting the waiting newcomers";
+    for (auto &[_, c] : clients_) {
+        if (c.phase == Phase::Registered && c.state == State::Idle) {
+            c.phase = Phase::Accepted;
+            on_peer_accepted(c);
+            break;
+        }
+    }
+    transition_to_establish(true);
 }
 
 } // namespace pccl::master

@@ -98,6 +98,14 @@ private:
     // dispatch
     void on_packet(const SockAddr &addr, uint16_t id, const uint8_t *payload, size_t n);
     void on_disconnect(const SockAddr &addr);
+    void maybe_bootstrap_orphans();
+    void on_tick();
+    std::chrono::steady_clock::time_point last_dump_{};
+
+public:
+    std::string dump_state() const;
+
+private:
     void kick(const SockAddr &addr);
 
     // handlers

@@ -91,6 +91,7 @@ void EventServer::loop() {
             if (!c.closing && (events[i].events & EPOLLOUT)) flush(c);
         }
         process_pending_closes();
+        if (tick_cb_ && !stop_) tick_cb_();
     }
     // shutdown: close all clients (no callbacks on interrupt)
     for (auto &[fd, c] : clients_by_fd_) ::close(fd);

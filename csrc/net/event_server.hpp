@@ -27,6 +27,8 @@ public:
 
     void on_read(ReadCb cb) { read_cb_ = std::move(cb); }
     void on_close(CloseCb cb) { close_cb_ = std::move(cb); }
+    // called on the loop thread after every wake-up (at least every 500 ms)
+    void on_tick(std::function<void()> cb) { tick_cb_ = std::move(cb); }
     void on_join(JoinCb cb) { join_cb_ = std::move(cb); }
 
     bool listen();
@@ -81,6 +83,7 @@ private:
     std::vector<int> pending_close_;
     ReadCb read_cb_;
     CloseCb close_cb_;
+    std::function<void()> tick_cb_;
     JoinCb join_cb_;
 };
 

@@ -162,6 +162,8 @@ void M2CSyncSharedState::encode(WBuf &w) const {
     for (size_t i = 0; i < outdated_keys.size(); ++i) w.u64(i < expected_hashes.size() ? expected_hashes[i] : 0);
     for (size_t i = 0; i < outdated_keys.size(); ++i)
         w.u8(static_cast<uint8_t>(i < expected_hash_types.size() ? expected_hash_types[i] : HashType::Simple));
+    w.u64(fallback_distributors.size());
+    for (const auto &a : fallback_distributors) w.sockaddr(a);
 }
 
 bool M2CSyncSharedState::decode(RBuf &r) {
@@ -175,6 +177,13 @@ bool M2CSyncSharedState::decode(RBuf &r) {
     for (auto &h : expected_hashes) h = r.u64();
     expected_hash_types.resize(n);
     for (auto &t : expected_hash_types) t = static_cast<HashType>(r.u8());
+    fallback_distributors.clear();
+    if (r.ok() && r.remaining() >= 8) {
+        const uint64_t m = r.u64();
+        if (!r.plausible_count(m, 7)) return false;
+        fallback_distributors.resize(m);
+        for (auto &a : fallback_distributors) a = r.sockaddr();
+    }
     return r.ok();
 }
 

@@ -250,6 +250,9 @@ struct M2CSyncSharedState {
     std::vector<std::string> outdated_keys;
     std::vector<uint64_t> expected_hashes;
     std::vector<HashType> expected_hash_types;
+    // [pccl-amd extension, appended] other peers holding the elected state: tried in order if the distributor
+    // dies mid-transfer (absent in reference-encoded packets)
+    std::vector<SockAddr> fallback_distributors;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };

@@ -56,7 +56,8 @@ def all_reduce_multiple_with_retry(comm: Communicator, tensors: Sequence[torch.T
         return comm.all_reduce_async(t, outs[i], op=op, tag=tag_base + i, operand_descriptor=desc,
                                      quantization_options=q)
 
-    while ws > 1 and not all(done):
+    too_few = False
+    while ws > 1 and not all(done) and not too_few:
         failed = False
         in_flight: List[int] = []
         pending = [i for i in range(n) if not done[i]]
@@ -67,8 +68,8 @@ def all_reduce_multiple_with_retry(comm: Communicator, tensors: Sequence[torch.T
                 try:
                     handles[i] = launch(i)
                 except PCCLError as e:
-                    if e.result == Result.TOO_FEW_PEERS:
-                        failed = True
+                    if e.result == Result.TOO_FEW_PEERS:  # alone (the ring shrank to this peer)
+                        failed = too_few = True
                         break
                     raise
                 in_flight.append(i)
@@ -95,7 +96,7 @@ def all_reduce_multiple_with_retry(comm: Communicator, tensors: Sequence[torch.T
                     rx += info.rx_bytes
             retries += 1
         ws = world_size(comm)
-    return RetryResult(all(done), tx, rx, retries, ws)
+    return RetryResult(all(done) and not too_few, tx, rx, retries, ws)
 
 
 def maybe_update_topology(comm: Communicator, iteration: int, *, retries: int = 10) -> bool:
