@@ -23,7 +23,7 @@ if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
   step_dir=$GRAFT_REPO_ROOT/gpurun_out
   echo "=== prof" | tee -a $step_dir/steps.log
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $step_dir/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 > $step_dir/prof.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $step_dir/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 > $step_dir/prof.log 2>&1
   echo "=== prof rc=$?" | tee -a $step_dir/steps.log
 fi
 exit 0
