@@ -119,6 +119,9 @@ def bench_multi_gpu(a):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    # rehearsal on a 1-GPU box: PCCL_BENCH_SAME_GPU=1 puts every rank on cuda:0 (the real run uses one GPU per rank)
+    if os.environ.get("PCCL_BENCH_SAME_GPU") == "1":
+        local_rank = 0
     dist.init_process_group("gloo")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
