@@ -58,7 +58,9 @@ class DiLoCo:
     def __init__(self, model: torch.nn.Module, comm: Communicator, *, outer_lr: float = 0.7,
                  outer_momentum: float = 0.0, nesterov: bool = False, weight_decay: float = 0.0,
                  quantization: Optional[QuantizationOptions] = None, bucket_bytes: int = 1 << 30,
-                 max_in_flight: int = 8, tag_base: int = 2 << 20):
+                 max_in_flight: int = 8, tag_base: int = 2 << 20, tensors: Optional[List[torch.Tensor]] = None):
+        """``tensors``: explicit local parameter tensors (e.g. FSDP2 shards, ``p.to_local()``) instead of flattening
+        ``model``'s parameters; each must be contiguous and stay the live storage of its parameter."""
         self.model = model
         self.comm = comm
         self.lr, self.momentum, self.nesterov, self.wd = outer_lr, outer_momentum, nesterov, weight_decay
@@ -66,8 +68,13 @@ class DiLoCo:
         self.bucket_bytes = bucket_bytes
         self.max_in_flight = max_in_flight
         self.tag_base = tag_base
-        self.params = FlatParams(model)
-        self.local = self.params.buffers()
+        if tensors is None:
+            self.params = FlatParams(model)
+            self.local = self.params.buffers()
+        else:
+            assert all(t.is_contiguous() for t in tensors), "DiLoCo local tensors must be contiguous"
+            self.params = None
+            self.local = [t.view(-1) for t in tensors]
         self.outer = [b.detach().float().clone() for b in self.local]
         self.mom = [torch.zeros_like(o) for o in self.outer]
         self.pg = [torch.empty_like(o) for o in self.outer]

@@ -3,6 +3,7 @@ and finish with identical model state on both peers (tiny preset, CPU; GPU varia
 import json
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -19,7 +20,12 @@ def _run(script, extra, device="cpu", world=2, timeout=300):
         procs = [spawn_python([os.path.join(EX, script), "--master", addr, *base, *extra],
                               env={"OMP_NUM_THREADS": "2"}, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for _ in range(world)]
-        outs = [p.communicate(timeout=timeout) for p in procs]
+        try:
+            outs = [p.communicate(timeout=timeout) for p in procs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
     done = []
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
@@ -53,3 +59,49 @@ def test_train_pccl_ddp_gpu(hip):
 def test_diloco_gpu(hip, extra):
     res = _run("sync_diloco.py", ["--max-iters", "12", "--inner-steps", "3", *extra], device="cuda")
     assert res[0]["outer_sum"] == res[1]["outer_sum"]
+
+
+def test_diloco_fsdp_two_nodes():
+    """Two simulated nodes (torchrun x 2, gloo FSDP2 with 2 ranks each) x PCCL peer group per local rank."""
+    from pccl_amd.utils import free_ports
+    ports = free_ports(2)
+    with local_master() as addr:
+        nodes = [spawn_python(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+                               "127.0.0.1", "--master-port", str(ports[k]), os.path.join(EX, "sync_diloco_fsdp.py"),
+                               "--preset", "tiny", "--device", "cpu", "--dtype", "float32",
+                               "--batch-size", "2", "--max-iters", "6", "--inner-steps", "3", "--seed", str(1337 + k)],
+                              env={"OMP_NUM_THREADS": "1", "PCCL_MASTER": addr}, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+                 for k in range(2)]
+        try:
+            outs = [p.communicate(timeout=300) for p in nodes]
+        finally:
+            for p in nodes:
+                if p.poll() is None:
+                    p.kill()
+    done = {}
+    for p, (o, e) in zip(nodes, outs):
+        assert p.returncode == 0, e[-3000:]
+        for ln in o.splitlines():
+            if ln.startswith("{") and '"done"' in ln:
+                r = json.loads(ln)
+                done.setdefault(r["group"], []).append(r)
+    assert sorted(done) == [0, 1]
+    for g, rs in done.items():
+        assert len(rs) == 2 and rs[0]["outer_sum"] == rs[1]["outer_sum"] and rs[0]["outer_steps"] == 2, rs
+
+
+def test_prepare_data_and_rccl_baseline(tmp_path):
+    """Data prep -> uint16 memmap; the plain-DDP (RCCL/gloo) baseline trainer runs on it under torchrun."""
+    from pccl_amd.utils import free_port
+    r = subprocess.run([sys.executable, os.path.join(EX, "prepare_data.py"), "--out-dir", str(tmp_path),
+                        "--synthetic-bytes", "200000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    p = spawn_python(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+                      "127.0.0.1", "--master-port", str(free_port()), os.path.join(EX, "train_rccl.py"), "--preset",
+                      "tiny", "--device", "cpu", "--dtype", "float32", "--max-iters", "3", "--batch-size", "2",
+                      "--data", str(tmp_path / "train.bin")], env={"OMP_NUM_THREADS": "1"},
+                     stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    o, e = p.communicate(timeout=300)
+    assert p.returncode == 0, e[-3000:]
+    assert len([ln for ln in o.splitlines() if ln.startswith('{"iter"')]) == 3

@@ -71,3 +71,47 @@ def test_mnist_ddp_gpu(hip, world):
 @pytest.mark.gpu
 def test_mnist_ddp_gpu_late_joiner(hip):
     _check(_run(3, device="cuda", late_joiner=True), 60)
+
+
+DILOCO_PEER = os.path.join(ROOT, "examples", "mnist_diloco", "mnist_diloco_peer.py")
+
+
+def _run_diloco(world, device="cpu", late_joiner=False):
+    with local_master() as addr:
+        procs = []
+        n0 = world - 1 if late_joiner else world
+        extra = ["--min-world", str(world)] if late_joiner else []
+        for r in range(n0):
+            procs.append(spawn_python([DILOCO_PEER, "--master", addr, "--rank", str(r), "--device", device, *extra],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        if late_joiner:
+            time.sleep(2.0)
+            procs.append(spawn_python([DILOCO_PEER, "--master", addr, "--rank", str(world - 1), "--device", device],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        try:
+            outs = [p.communicate(timeout=300) for p in procs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+    res = []
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]))
+    assert len({r["hash"] for r in res}) == 1, res
+    assert all(r["outer_steps"] == 10 for r in res)
+    return res
+
+
+def test_mnist_diloco():
+    res = _run_diloco(2)
+    assert all(r["loss_last"] < r["loss_first"] for r in res)
+
+
+def test_mnist_diloco_late_joiner():
+    _run_diloco(3, late_joiner=True)
+
+
+@pytest.mark.gpu
+def test_mnist_diloco_gpu(hip):
+    _run_diloco(2, device="cuda")
