@@ -40,6 +40,7 @@ def _args():
     ap.add_argument("--path", default="auto", choices=["auto", "ring"],
                     help="auto: xGMI IPC between same-host peers; ring: force the pipelined TCP ring")
     ap.add_argument("--pool", type=int, default=4, help="P2P connections per neighbour (ring stripes)")
+    ap.add_argument("--rejoin", type=int, default=1, help="N==1: also measure peer-rejoin latency after the timed steps")
     return ap.parse_args()
 
 
@@ -61,7 +62,7 @@ def _peer_loop(comm, x, y, steps, warmup, sync_all, torch, pccl):
     return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
 
 
-def _report(n_gpus, n_peers, steps, warmup, nbytes, dt, tx, rx, path, parallelism):
+def _report(n_gpus, n_peers, steps, warmup, nbytes, dt, tx, rx, path, parallelism, rejoin_s=None):
     import pccl_amd as pccl
     t = dt / steps
     alg = nbytes / t / 1e9
@@ -79,10 +80,45 @@ def _report(n_gpus, n_peers, steps, warmup, nbytes, dt, tx, rx, path, parallelis
         "extra": {"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
                   "ref_metric_rx_plus_tx_per_peer_GBps": round((tx + rx) / steps / t / 1e9, 3),
                   "reduce_path": pccl.ReducePath(path).name,
+                  "peer_rejoin_latency_ms": round(rejoin_s * 1e3, 1) if rejoin_s else None,
                   "baseline_note": "vs_baseline divides the aggregate value by the reference's 45 Gbit/s "
                                    "per-run WAN figure (no like-for-like MI355X number is published)"},
     }
     print(json.dumps(line), flush=True)
+
+
+def _rejoin_latency(comm, rank, addr, dev, bar, torch, pccl, pool):
+    """After the timed steps: a new peer connects mid-run; returns seconds from its connect() call until its first
+    all-reduce completed (admission vote + P2P establishment + IPC rendezvous + first op). Untimed for the metric."""
+    small = torch.ones(1 << 16, device=dev, dtype=torch.bfloat16)
+    out = {}
+    joiner = None
+    bar.wait()
+    if rank == 0:
+        def join():
+            c = pccl.Communicator(addr, 0, p2p_connection_pool_size=pool)
+            t0 = time.perf_counter()
+            c.connect(n_attempts=30)
+            y = torch.empty_like(small)
+            c.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=77)
+            torch.cuda.synchronize()
+            out["s"] = time.perf_counter() - t0
+            out["c"] = c
+        joiner = threading.Thread(target=join, daemon=True)
+        joiner.start()
+    deadline = time.time() + 120
+    while time.time() < deadline:
+        if comm.are_peers_pending():
+            comm.update_topology()
+            y = torch.empty_like(small)
+            comm.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=77)
+            break
+        time.sleep(0.001)
+    if joiner is not None:
+        joiner.join(timeout=120)
+        out["c"].destroy()
+    bar.wait()
+    return out.get("s")
 
 
 def bench_single_gpu(a):
@@ -96,18 +132,21 @@ def bench_single_gpu(a):
     dev = torch.device("cuda:0")
     bar = threading.Barrier(n_peers)
 
-    def fn(rank, comm):
-        torch.cuda.set_device(dev)
-        g = torch.Generator(device=dev).manual_seed(rank)
-        x = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
-        y = torch.empty_like(x)
-        return _peer_loop(comm, x, y, a.steps, a.warmup, bar.wait, torch, pccl)
-
     with local_master() as addr:
+        def fn(rank, comm):
+            torch.cuda.set_device(dev)
+            g = torch.Generator(device=dev).manual_seed(rank)
+            x = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
+            y = torch.empty_like(x)
+            r = _peer_loop(comm, x, y, a.steps, a.warmup, bar.wait, torch, pccl)
+            rejoin = _rejoin_latency(comm, rank, addr, dev, bar, torch, pccl, a.pool) if a.rejoin else None
+            return (*r, rejoin)
+
         res = run_threaded_peers(n_peers, fn, address=addr, timeout=1800,
                                  comm_kwargs={"p2p_connection_pool_size": a.pool})
     dt = max(r[0] for r in res)
-    _report(1, n_peers, a.steps, a.warmup, nbytes, dt, res[0][1], res[0][2], res[0][3], f"{n_peers} peers on 1 GPU")
+    _report(1, n_peers, a.steps, a.warmup, nbytes, dt, res[0][1], res[0][2], res[0][3], f"{n_peers} peers on 1 GPU",
+            rejoin_s=res[0][4])
 
 
 def bench_multi_gpu(a):
