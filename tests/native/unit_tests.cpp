@@ -11,9 +11,20 @@
 #include "common/numeric.hpp"
 #include "kernels/host_kernels.hpp"
 #include "master/topology.hpp"
+#include "net/event_server.hpp"
+#include "net/mux.hpp"
+#include "net/socket.hpp"
 #include "proto/packets.hpp"
 
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <thread>
+
 using namespace pccl;
+using namespace std::chrono_literals;
 
 static std::vector<std::pair<std::string, std::function<void()>>> &registry() {
     static std::vector<std::pair<std::string, std::function<void()>>> r;
@@ -154,6 +165,122 @@ TEST(simplehash_host_small) {
     const uint32_t h0 = kernels::simplehash_host(one.data(), 1);
     one[0] = 1;
     EXPECT(kernels::simplehash_host(one.data(), 1) != h0);
+}
+
+// ---------------------------------------------------------------- transport (reference tinysockets/tests)
+TEST(listen_port_bumping) {
+    uint16_t a = 0, b = 0;
+    const int fa = net::listen_tcp(inetIPv4, 0, false, a);
+    EXPECT(fa >= 0 && a != 0);
+    const int fb = net::listen_tcp(inetIPv4, a, true, b); // taken -> bumped
+    EXPECT(fb >= 0 && b > a);
+    uint16_t c = 0;
+    EXPECT(net::listen_tcp(inetIPv4, a, false, c) < 0); // taken, no bump -> fail
+    ::close(fa);
+    ::close(fb);
+}
+
+static std::pair<net::MuxConn *, net::MuxConn *> mux_pair() {
+    int sv[2];
+    EXPECT(::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+    auto *tx = new net::MuxConn(sv[0], net::MuxConn::Mode::Tx, SockAddr{});
+    auto *rx = new net::MuxConn(sv[1], net::MuxConn::Mode::Rx, SockAddr{});
+    tx->start();
+    rx->start();
+    return {tx, rx};
+}
+
+TEST(mux_sink_receives_frames_in_order) {
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> src(3 << 20), dst(3 << 20, 0);
+    for (size_t i = 0; i < src.size(); ++i) src[i] = static_cast<uint8_t>(i * 7 + 3);
+    rx->post_sink(5, 1, dst.data(), dst.size());
+    std::thread s([&] {
+        for (size_t off = 0; off < src.size(); off += 1 << 20) tx->send_frame(5, 1, src.data() + off, 1 << 20);
+    });
+    EXPECT(rx->wait_sink(5, dst.size(), 10s) == dst.size());
+    s.join();
+    EXPECT(src == dst);
+    rx->remove_sink(5);
+    delete tx;
+    delete rx;
+}
+
+TEST(mux_early_frames_queue_until_sink_posted) {
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> a(1000, 1), b(500, 2), dst(1500, 0);
+    tx->send_frame(9, 4, a.data(), a.size());
+    tx->send_frame(9, 4, b.data(), b.size());
+    std::this_thread::sleep_for(50ms); // both frames are queued by the RX thread before the sink exists
+    rx->post_sink(9, 4, dst.data(), dst.size());
+    EXPECT(rx->wait_sink(9, dst.size(), 5s) == dst.size());
+    EXPECT(dst[0] == 1 && dst[999] == 1 && dst[1000] == 2 && dst[1499] == 2);
+    rx->remove_sink(9);
+    delete tx;
+    delete rx;
+}
+
+TEST(mux_stale_ctr_frames_dropped_and_tags_independent) {
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> stale(64, 0xEE), good(64, 0x11), other(32, 0x22);
+    tx->send_frame(1, 3, stale.data(), stale.size()); // aborted earlier op with the same tag
+    tx->send_frame(2, 7, other.data(), other.size());  // another concurrent op
+    tx->send_frame(1, 4, good.data(), good.size());
+    std::this_thread::sleep_for(50ms);
+    std::vector<uint8_t> dst(64, 0);
+    rx->post_sink(1, 4, dst.data(), dst.size());
+    EXPECT(rx->wait_sink(1, 64, 5s) == 64);
+    EXPECT(dst == good);
+    auto f = rx->recv_frame(2, 7, 1s);
+    EXPECT(f.has_value() && *f == other);
+    rx->remove_sink(1);
+    delete tx;
+    delete rx;
+}
+
+TEST(mux_peer_close_is_detected) {
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> dst(128);
+    rx->post_sink(1, 1, dst.data(), dst.size());
+    delete tx; // closes the socket
+    const auto t0 = std::chrono::steady_clock::now();
+    rx->wait_sink(1, dst.size(), 5s);
+    EXPECT(!rx->is_open());
+    EXPECT(std::chrono::steady_clock::now() - t0 < 4s);
+    rx->remove_sink(1);
+    delete rx;
+}
+
+TEST(event_server_ltv_roundtrip_and_close_callbacks) {
+    SockAddr any{};
+    any.inet.protocol = inetIPv4;
+    any.port = 0;
+    net::EventServer srv(any, false);
+    std::atomic<int> got{0}, closed{0};
+    std::atomic<size_t> got_len{0};
+    srv.on_read([&](const SockAddr &a, uint16_t id, const uint8_t *p, size_t n) {
+        got_len = n;
+        got += id == 42 ? 1 : 0;
+        srv.send_raw(a, 43, std::vector<uint8_t>(p, p + n));
+    });
+    srv.on_close([&](const SockAddr &) { closed++; });
+    EXPECT(srv.listen() && srv.run_async());
+    SockAddr addr{};
+    addr.inet.protocol = inetIPv4;
+    addr.inet.ipv4.data[0] = 127;
+    addr.inet.ipv4.data[3] = 1;
+    addr.port = srv.port();
+    const int fd = net::connect_tcp(addr, 2000);
+    EXPECT(fd >= 0);
+    std::vector<uint8_t> big(8 << 20, 0x5A); // large control packet
+    EXPECT(net::send_ltv(fd, 42, big.data(), big.size()));
+    auto back = net::recv_ltv(fd);
+    EXPECT(back.has_value() && back->id == 43 && back->payload.size() == big.size());
+    ::close(fd);
+    for (int i = 0; i < 200 && closed.load() == 0; ++i) std::this_thread::sleep_for(10ms);
+    EXPECT(got.load() == 1 && got_len.load() == big.size() && closed.load() == 1);
+    srv.interrupt();
+    srv.join();
 }
 
 int main() {
