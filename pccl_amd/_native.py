@@ -6,13 +6,14 @@ runtime (SONAME libamdhip64.so.7) is the one the HIP plugin binds to — one HIP
 from __future__ import annotations
 
 import ctypes
-import importlib.util
 import os
 from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_size_t, c_uint8, c_uint16, c_uint32,
                     c_uint64, c_void_p)
 
-if importlib.util.find_spec("torch") is not None:  # share torch's HIP runtime with the plugin
+try:  # share torch's HIP runtime with the plugin
     import torch  # noqa: F401
+except ImportError:
+    pass
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 

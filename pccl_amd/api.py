@@ -8,7 +8,7 @@ HIP backend (xGMI between peers on one host, pinned-memory staging over TCP othe
 from __future__ import annotations
 
 import ctypes
-import importlib.util
+import importlib
 import logging
 import time
 from enum import Enum
@@ -29,8 +29,16 @@ class _ModuleDummy:
         raise RuntimeError(f"Module {self.name} is not available; install it to interoperate with pccl-amd.")
 
 
-torch = __import__("torch") if importlib.util.find_spec("torch") is not None else _ModuleDummy("torch")
-np = __import__("numpy") if importlib.util.find_spec("numpy") is not None else _ModuleDummy("numpy")
+def _optional(name: str):
+    """The module if importable, else a dummy (reference: numpy-only and torch-only installs both work)."""
+    try:
+        return importlib.import_module(name)
+    except ImportError:
+        return _ModuleDummy(name)
+
+
+torch = _optional("torch")
+np = _optional("numpy")
 
 
 class Result(Enum):
