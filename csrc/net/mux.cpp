@@ -1,7 +1,11 @@
 #include "mux.hpp"
 
 #include <cerrno>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -17,6 +21,52 @@ size_t multiplex_chunk_size() {
 }
 
 static constexpr size_t kMaxFrame = 1ull << 30;
+
+const WanSim &wan_sim() {
+    static const WanSim s = [] {
+        WanSim w;
+        const char *e = std::getenv("PCCL_SIM_WAN");
+        if (!e || !*e) return w;
+        double lat = 0, flow = 0, link = 0;
+        const int n = std::sscanf(e, "%lf:%lf:%lf", &lat, &flow, &link);
+        if (n >= 2 && flow > 0) {
+            w.enabled = true;
+            w.latency_s = lat / 1e3;
+            w.flow_bps = flow * 1e6 / 8;
+            w.link_bps = n >= 3 ? link * 1e6 / 8 : 0;
+            LOG(WARN) << "WAN emulation on: " << lat << " ms one-way, " << flow << " Mbit/s per flow"
+                      << (n >= 3 ? ", shared link " + std::to_string(link) + " Mbit/s" : std::string());
+        }
+        return w;
+    }();
+    return s;
+}
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// shared bottleneck link of all emulated flows of this process
+static std::mutex g_link_mtx;
+static double g_link_next_free = 0;
+
+static void wan_shape(size_t n, double &flow_next_free, double &last_send) {
+    const WanSim &w = wan_sim();
+    double start = now_s();
+    if (start - last_send > w.latency_s) start += w.latency_s; // new burst: pay the pipe latency once
+    start = std::max(start, flow_next_free);
+    double done = start + static_cast<double>(n) / w.flow_bps;
+    if (w.link_bps > 0) {
+        std::lock_guard l(g_link_mtx);
+        const double lstart = std::max(start, g_link_next_free);
+        g_link_next_free = lstart + static_cast<double>(n) / w.link_bps;
+        done = std::max(done, g_link_next_free);
+    }
+    flow_next_free = done;
+    const double wait = done - now_s();
+    if (wait > 0) std::this_thread::sleep_for(std::chrono::duration<double>(wait));
+    last_send = now_s();
+}
 
 MuxConn::MuxConn(int fd, Mode mode, const SockAddr &peer_addr) : fd_(fd), mode_(mode), peer_addr_(peer_addr) {}
 
@@ -57,6 +107,7 @@ bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n)
         for (int i = 0; i < 8; ++i) hdr[v * 8 + i] = static_cast<uint8_t>(vals[v] >> (8 * (7 - i)));
     iovec iov[2] = {{hdr, 24}, {const_cast<void *>(data), n}};
     std::lock_guard lock(tx_mtx_);
+    if (wan_sim().enabled) wan_shape(n + 24, sim_next_free_, sim_last_send_);
     if (!sendv_all(fd_, iov, n ? 2 : 1)) {
         open_.store(false, std::memory_order_release);
         return false;

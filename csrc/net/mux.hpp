@@ -94,6 +94,8 @@ private:
     std::atomic<bool> stop_{false};
     std::thread rx_thread_;
     std::mutex tx_mtx_;
+    double sim_next_free_ = 0; // WAN emulation: time (s, steady clock) at which this flow's link is free again
+    double sim_last_send_ = -1e9;
 
     std::mutex mtx_;
     std::condition_variable cv_;
@@ -103,5 +105,15 @@ private:
 };
 
 size_t multiplex_chunk_size();
+
+// Built-in WAN emulation for tests and benchmarks without root / tc-netem (reference BASELINE config "int8-quantized
+// all-reduce over tc-netem 50 ms simulated WAN"): PCCL_SIM_WAN="<one-way latency ms>:<per-flow Mbit/s>[:<link Mbit/s>]"
+// shapes every P2P data connection: each frame is serialised at the flow rate (and the shared link rate), and a burst
+// that starts after an idle gap pays the latency once (pipelined frames overlap it, as on a real long-fat pipe).
+struct WanSim {
+    bool enabled = false;
+    double latency_s = 0, flow_bps = 0, link_bps = 0;
+};
+const WanSim &wan_sim();
 
 } // namespace pccl::net
