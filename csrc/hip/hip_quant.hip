@@ -9,31 +9,35 @@ namespace pccl::hipk {
 bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                            const kernels::QuantParams &p, hipStream_t st) {
     if (count == 0) return true;
-    const int grid = grid_for(count);
     return with_float_elem(vtype, [&](auto e) {
         using E = decltype(e);
         using S = typename E::S;
+        constexpr int V = vec_width<S>();
         return with_op(op, [&](auto o) {
             using O = decltype(o);
-            if (p.algo == QuantAlgo::MinMax && qtype == DType::F8E4M3)
+            if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
+                const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src_q, 1}});
+                const int grid = grid_for(count, pl.vec ? V : 1);
+                auto *d = static_cast<S *>(dst);
+                auto *q = static_cast<const uint8_t *>(src_q);
                 return launch_ok([&] {
-                    k_dq_fp8<E, O, true><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst), static_cast<const uint8_t *>(src_q), count, p);
+                    if (qtype == DType::F8E4M3)
+                        k_dq_fp8<E, O, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
+                    else
+                        k_dq_fp8<E, O, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
                 });
-            if (p.algo == QuantAlgo::MinMax && qtype == DType::F8E5M2)
-                return launch_ok([&] {
-                    k_dq_fp8<E, O, false><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst), static_cast<const uint8_t *>(src_q), count, p);
-                });
+            }
             return with_qint(qtype, [&](auto qv) {
                 using Q = decltype(qv);
+                const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src_q, sizeof(Q)}});
+                const int grid = grid_for(count, pl.vec ? V : 1);
+                auto *d = static_cast<S *>(dst);
+                auto *q = static_cast<const Q *>(src_q);
                 if (p.algo == QuantAlgo::MinMax)
-                    return launch_ok([&] {
-                        k_dq_minmax<E, O, Q><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst), static_cast<const Q *>(src_q), count, p);
-                    });
+                    return launch_ok([&] { k_dq_minmax<E, O, Q><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec); });
                 if constexpr (sizeof(Q) <= 4) {
                     if (p.algo == QuantAlgo::ZeroPointScale)
-                        return launch_ok([&] {
-                            k_dq_zps<E, O, Q><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst), static_cast<const Q *>(src_q), count, p);
-                        });
+                        return launch_ok([&] { k_dq_zps<E, O, Q><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec); });
                 }
                 return false;
             });
@@ -44,21 +48,32 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
 bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
                      const kernels::QuantParams &p, hipStream_t st) {
     if (count == 0) return true;
-    const int grid = grid_for(count);
     return with_float_elem(vtype, [&](auto e) {
         using E = decltype(e);
         using S = typename E::S;
-        if (p.algo == QuantAlgo::MinMax && qtype == DType::F8E4M3)
-            return launch_ok([&] { k_q_fp8<E, true><<<grid, kBlock, 0, st>>>(static_cast<uint8_t *>(dst_q), static_cast<const S *>(src), count, p); });
-        if (p.algo == QuantAlgo::MinMax && qtype == DType::F8E5M2)
-            return launch_ok([&] { k_q_fp8<E, false><<<grid, kBlock, 0, st>>>(static_cast<uint8_t *>(dst_q), static_cast<const S *>(src), count, p); });
+        constexpr int V = vec_width<S>();
+        auto *s = static_cast<const S *>(src);
+        if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
+            const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, 1}});
+            const int grid = grid_for(count, pl.vec ? V : 1);
+            auto *d = static_cast<uint8_t *>(dst_q);
+            return launch_ok([&] {
+                if (qtype == DType::F8E4M3)
+                    k_q_fp8<E, true><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+                else
+                    k_q_fp8<E, false><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+            });
+        }
         return with_qint(qtype, [&](auto qv) {
             using Q = decltype(qv);
+            const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, sizeof(Q)}});
+            const int grid = grid_for(count, pl.vec ? V : 1);
+            auto *d = static_cast<Q *>(dst_q);
             if (p.algo == QuantAlgo::MinMax)
-                return launch_ok([&] { k_q_minmax<E, Q><<<grid, kBlock, 0, st>>>(static_cast<Q *>(dst_q), static_cast<const S *>(src), count, p); });
+                return launch_ok([&] { k_q_minmax<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
             if constexpr (sizeof(Q) <= 4) {
                 if (p.algo == QuantAlgo::ZeroPointScale)
-                    return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(static_cast<Q *>(dst_q), static_cast<const S *>(src), count, p); });
+                    return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
             }
             return false;
         });
@@ -66,11 +81,14 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
 }
 
 bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, double *out2, hipStream_t st) {
-    const int grid = std::min(grid_for(count), 1024);
     return with_float_elem(vtype, [&](auto e) {
         using E = decltype(e);
+        using S = typename E::S;
+        constexpr int V = vec_width<S>();
+        const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}});
+        const int grid = std::min(grid_for(count, pl.vec ? V : 1), 1024);
         return launch_ok([&] {
-            k_minmax_partial<E><<<grid, kBlock, 0, st>>>(static_cast<const typename E::S *>(src), count, partial);
+            k_minmax_partial<E><<<grid, kBlock, 0, st>>>(static_cast<const S *>(src), count, partial, pl.head, pl.vec);
             k_minmax_final<><<<1, kBlock, 0, st>>>(partial, grid, count, out2);
         });
     });

@@ -11,9 +11,12 @@ bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp o
         using E = decltype(e);
         return with_op(op, [&](auto o) {
             using O = decltype(o);
+            using S = typename E::S;
+            constexpr int V = vec_width<S>();
+            const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src, sizeof(S)}});
             return launch_ok([&] {
-                k_reduce<E, O><<<grid_for(count), kBlock, 0, st>>>(static_cast<typename E::S *>(dst),
-                                                                   static_cast<const typename E::S *>(src), count);
+                k_reduce<E, O><<<grid_for(count, pl.vec ? V : 1), kBlock, 0, st>>>(
+                    static_cast<S *>(dst), static_cast<const S *>(src), count, pl.head, pl.vec);
             });
         });
     });
@@ -23,7 +26,12 @@ bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_
     if (count == 0) return true;
     return with_elem(t, [&](auto e) {
         using E = decltype(e);
-        return launch_ok([&] { k_avg<E><<<grid_for(count), kBlock, 0, st>>>(static_cast<typename E::S *>(dst), count, ws); });
+        using S = typename E::S;
+        constexpr int V = vec_width<S>();
+        const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}});
+        return launch_ok([&] {
+            k_avg<E><<<grid_for(count, pl.vec ? V : 1), kBlock, 0, st>>>(static_cast<S *>(dst), count, ws, pl.head, pl.vec);
+        });
     });
 }
 

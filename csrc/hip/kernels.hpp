@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <initializer_list>
+#include <utility>
 
 #include "../common/numeric.hpp"
 #include "../common/types.hpp"
@@ -51,99 +53,218 @@ inline int grid_for(size_t work_items, int per_thread = 1) {
     return static_cast<int>(g);
 }
 
+// ---------------------------------------------------------------- packed elementwise access
+// Every elementwise kernel processes V = 16 / sizeof(S) elements per thread-iteration with 16-byte loads/stores of
+// the value type (and V-element packs of the quantized type) when the operands can be aligned by peeling a scalar
+// head; otherwise (ring chunks start at arbitrary element offsets) it falls back to a coalesced scalar loop. The
+// per-element math is exactly the scalar math, so results stay bit-identical to the host twins.
+template<typename T, int N>
+struct alignas(sizeof(T) * N) Pack {
+    T v[N];
+};
+template<typename S>
+constexpr int vec_width() {
+    return sizeof(S) >= 16 ? 1 : static_cast<int>(16 / sizeof(S));
+}
+template<typename T, int N>
+__device__ __forceinline__ Pack<T, N> ldp(const T *p) {
+    return *reinterpret_cast<const Pack<T, N> *>(p);
+}
+template<typename T, int N>
+__device__ __forceinline__ void stp(T *p, const Pack<T, N> &v) {
+    *reinterpret_cast<Pack<T, N> *>(p) = v;
+}
+
+struct EwPlan {
+    size_t head = 0; // scalar elements before the first aligned pack
+    int vec = 0;
+};
+// operands: (pointer, element size); the first is the anchor whose 16-byte alignment fixes the head
+template<int V>
+inline EwPlan plan_ew(size_t n, std::initializer_list<std::pair<const void *, size_t>> ops) {
+    EwPlan pl;
+    const auto &a = *ops.begin();
+    const size_t pack0 = static_cast<size_t>(V) * a.second;
+    const size_t mis = reinterpret_cast<uintptr_t>(a.first) % pack0;
+    size_t head = mis == 0 ? 0 : pack0 - mis;
+    if (head % a.second != 0) return pl;
+    head /= a.second;
+    if (head >= n || (n - head) / V == 0) return pl;
+    for (const auto &o : ops)
+        if ((reinterpret_cast<uintptr_t>(o.first) + head * o.second) % (static_cast<size_t>(V) * o.second) != 0) return pl;
+    pl.head = head;
+    pl.vec = 1;
+    return pl;
+}
+
+template<int V, typename Fs, typename Fv>
+__device__ __forceinline__ void ew_loop(size_t n, size_t head, int vec, Fs &&scalar, Fv &&vector) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (!vec) {
+        for (size_t i = tid; i < n; i += stride) scalar(i);
+        return;
+    }
+    for (size_t i = tid; i < head; i += stride) scalar(i);
+    const size_t np = (n - head) / V;
+    for (size_t k = tid; k < np; k += stride) vector(head + k * V);
+    for (size_t i = head + np * V + tid; i < n; i += stride) scalar(i);
+}
+
 // ---------------------------------------------------------------- elementwise reduce (ring path)
 template<typename E, typename Op>
 __global__ __launch_bounds__(kBlock) void k_reduce(typename E::S *__restrict__ dst, const typename E::S *__restrict__ src,
-                                                   size_t n) {
+                                                   size_t n, size_t head, int vec) {
+    using S = typename E::S;
     using C = typename E::C;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
-        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), E::ld(src[i])));
+    constexpr int V = vec_width<S>();
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), E::ld(src[i]))); },
+        [&](size_t b) {
+            auto d = ldp<S, V>(dst + b);
+            const auto s = ldp<S, V>(src + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e) d.v[e] = E::st(apply_op<Op, C>(E::ld(d.v[e]), E::ld(s.v[e])));
+            stp<S, V>(dst + b, d);
+        });
 }
 
 // ---------------------------------------------------------------- fused dequant + reduce
-template<typename Q>
-struct QInt {
-    using T = Q;
-    static __device__ __forceinline__ double deq_d(T q, const QuantParams &p) {
-        return dq_minmax_int(static_cast<double>(q), p);
-    }
-};
-
 template<typename E, typename Op, typename Q>
 __global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
-                                                      QuantParams p) {
+                                                      QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
     using C = typename E::C;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const C v = static_cast<C>(dq_minmax_int(static_cast<double>(src[i]), p));
-        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
-    }
+    constexpr int V = vec_width<S>();
+    ew_loop<V>(
+        n, head, vec,
+        [&](size_t i) {
+            const C v = static_cast<C>(dq_minmax_int(static_cast<double>(src[i]), p));
+            dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
+        },
+        [&](size_t b) {
+            auto d = ldp<S, V>(dst + b);
+            const auto q = ldp<Q, V>(src + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const C v = static_cast<C>(dq_minmax_int(static_cast<double>(q.v[e]), p));
+                d.v[e] = E::st(apply_op<Op, C>(E::ld(d.v[e]), v));
+            }
+            stp<S, V>(dst + b, d);
+        });
 }
 
 template<typename E, typename Op, bool E4M3>
 __global__ __launch_bounds__(kBlock) void k_dq_fp8(typename E::S *__restrict__ dst, const uint8_t *__restrict__ src, size_t n,
-                                                   QuantParams p) {
+                                                   QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
     using C = typename E::C;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const float f = (E4M3 ? num::fp8e4m3_to_f32(src[i]) : num::fp8e5m2_to_f32(src[i])) * p.f8_inv;
-        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
-    }
+    constexpr int V = vec_width<S>();
+    auto deq = [&](uint8_t q) { return (E4M3 ? num::fp8e4m3_to_f32(q) : num::fp8e5m2_to_f32(q)) * p.f8_inv; };
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(deq(src[i])))); },
+        [&](size_t b) {
+            auto d = ldp<S, V>(dst + b);
+            const auto q = ldp<uint8_t, V>(src + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e) d.v[e] = E::st(apply_op<Op, C>(E::ld(d.v[e]), static_cast<C>(deq(q.v[e]))));
+            stp<S, V>(dst + b, d);
+        });
 }
 
 template<typename E, typename Op, typename Q>
 __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
-                                                   QuantParams p) {
+                                                   QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
     using C = typename E::C;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const float f = dq_zps(static_cast<int64_t>(src[i]), p);
-        dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
-    }
+    constexpr int V = vec_width<S>();
+    ew_loop<V>(
+        n, head, vec,
+        [&](size_t i) {
+            dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps(static_cast<int64_t>(src[i]), p))));
+        },
+        [&](size_t b) {
+            auto d = ldp<S, V>(dst + b);
+            const auto q = ldp<Q, V>(src + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                d.v[e] = E::st(apply_op<Op, C>(E::ld(d.v[e]), static_cast<C>(dq_zps(static_cast<int64_t>(q.v[e]), p))));
+            stp<S, V>(dst + b, d);
+        });
 }
 
 // ---------------------------------------------------------------- quantize
+template<typename Q>
+__device__ __forceinline__ Q q_from_double(double q) {
+    if constexpr (sizeof(Q) == 8 && !__is_signed(Q)) {
+        return q >= 18446744073709551615.0 ? ~0ull : static_cast<uint64_t>(q);
+    } else if constexpr (sizeof(Q) == 8) {
+        return q >= 9223372036854775807.0 ? INT64_MAX : static_cast<int64_t>(q);
+    } else {
+        return static_cast<Q>(static_cast<int64_t>(q));
+    }
+}
+
 template<typename E, typename Q>
 __global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
-                                                     QuantParams p) {
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const double q = q_minmax_int(static_cast<double>(E::ld(src[i])), p);
-        if constexpr (sizeof(Q) == 8 && !__is_signed(Q)) {
-            dst[i] = q >= 18446744073709551615.0 ? ~0ull : static_cast<uint64_t>(q);
-        } else if constexpr (sizeof(Q) == 8) {
-            dst[i] = q >= 9223372036854775807.0 ? INT64_MAX : static_cast<int64_t>(q);
-        } else {
-            dst[i] = static_cast<Q>(static_cast<int64_t>(q));
-        }
-    }
+                                                     QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
+    constexpr int V = vec_width<S>();
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(src[i])), p)); },
+        [&](size_t b) {
+            const auto s = ldp<S, V>(src + b);
+            Pack<Q, V> q;
+#pragma unroll
+            for (int e = 0; e < V; ++e) q.v[e] = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(s.v[e])), p));
+            stp<Q, V>(dst + b, q);
+        });
 }
 
 template<typename E, bool E4M3>
 __global__ __launch_bounds__(kBlock) void k_q_fp8(uint8_t *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
-                                                  QuantParams p) {
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const float x = static_cast<float>(E::ld(src[i])) * p.f8_scale;
-        dst[i] = E4M3 ? num::f32_to_fp8e4m3(x) : num::f32_to_fp8e5m2(x);
-    }
+                                                  QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
+    constexpr int V = vec_width<S>();
+    auto qf = [&](S v) {
+        const float x = static_cast<float>(E::ld(v)) * p.f8_scale;
+        return E4M3 ? num::f32_to_fp8e4m3(x) : num::f32_to_fp8e5m2(x);
+    };
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = qf(src[i]); },
+        [&](size_t b) {
+            const auto s = ldp<S, V>(src + b);
+            Pack<uint8_t, V> q;
+#pragma unroll
+            for (int e = 0; e < V; ++e) q.v[e] = qf(s.v[e]);
+            stp<uint8_t, V>(dst + b, q);
+        });
 }
 
 template<typename E, typename Q>
 __global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
-                                                  QuantParams p) {
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
-        dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p));
+                                                  QuantParams p, size_t head, int vec) {
+    using S = typename E::S;
+    constexpr int V = vec_width<S>();
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p)); },
+        [&](size_t b) {
+            const auto s = ldp<S, V>(src + b);
+            Pack<Q, V> q;
+#pragma unroll
+            for (int e = 0; e < V; ++e) q.v[e] = static_cast<Q>(q_zps(static_cast<float>(E::ld(s.v[e])), p));
+            stp<Q, V>(dst + b, q);
+        });
 }
 
 // ---------------------------------------------------------------- min / max (two pass, exact)
-__device__ __forceinline__ void wave_minmax(double &lo, double &hi) {
+// Comparisons run in the codec's compute type (exact for every value of the storage type); partials are doubles.
+template<typename C>
+__device__ __forceinline__ void wave_minmax(C &lo, C &hi) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const double l2 = __shfl_xor(lo, off, 64);
-        const double h2 = __shfl_xor(hi, off, 64);
+        const C l2 = __shfl_xor(lo, off, 64);
+        const C h2 = __shfl_xor(hi, off, 64);
         lo = l2 < lo ? l2 : lo;
         hi = h2 > hi ? h2 : hi;
     }
@@ -151,15 +272,23 @@ __device__ __forceinline__ void wave_minmax(double &lo, double &hi) {
 
 template<typename E>
 __global__ __launch_bounds__(kBlock) void k_minmax_partial(const typename E::S *__restrict__ src, size_t n,
-                                                           double *__restrict__ partial) {
-    __shared__ double s_lo[kBlock / 64], s_hi[kBlock / 64];
-    double lo = __builtin_inf(), hi = -__builtin_inf();
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const double v = static_cast<double>(E::ld(src[i]));
+                                                           double *__restrict__ partial, size_t head, int vec) {
+    using S = typename E::S;
+    using C = typename E::C;
+    constexpr int V = vec_width<S>();
+    __shared__ C s_lo[kBlock / 64], s_hi[kBlock / 64];
+    C lo = static_cast<C>(__builtin_inf()), hi = static_cast<C>(-__builtin_inf());
+    auto take = [&](C v) {
         lo = v < lo ? v : lo;
         hi = v > hi ? v : hi;
-    }
+    };
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { take(E::ld(src[i])); },
+        [&](size_t b) {
+            const auto s = ldp<S, V>(src + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e) take(E::ld(s.v[e]));
+        });
     wave_minmax(lo, hi);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -172,8 +301,8 @@ __global__ __launch_bounds__(kBlock) void k_minmax_partial(const typename E::S *
             lo = s_lo[k] < lo ? s_lo[k] : lo;
             hi = s_hi[k] > hi ? s_hi[k] : hi;
         }
-        partial[2 * blockIdx.x] = lo;
-        partial[2 * blockIdx.x + 1] = hi;
+        partial[2 * blockIdx.x] = static_cast<double>(lo);
+        partial[2 * blockIdx.x + 1] = static_cast<double>(hi);
     }
 }
 
@@ -205,12 +334,19 @@ __global__ __launch_bounds__(kBlock) void k_minmax_final(const double *__restric
 
 // ---------------------------------------------------------------- AVG finalize
 template<typename E>
-__global__ __launch_bounds__(kBlock) void k_avg(typename E::S *__restrict__ dst, size_t n, size_t ws) {
+__global__ __launch_bounds__(kBlock) void k_avg(typename E::S *__restrict__ dst, size_t n, size_t ws, size_t head, int vec) {
+    using S = typename E::S;
     using C = typename E::C;
+    constexpr int V = vec_width<S>();
     const C w = static_cast<C>(ws);
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
-        dst[i] = E::st(static_cast<C>(E::ld(dst[i]) / w));
+    ew_loop<V>(
+        n, head, vec, [&](size_t i) { dst[i] = E::st(static_cast<C>(E::ld(dst[i]) / w)); },
+        [&](size_t b) {
+            auto d = ldp<S, V>(dst + b);
+#pragma unroll
+            for (int e = 0; e < V; ++e) d.v[e] = E::st(static_cast<C>(E::ld(d.v[e]) / w));
+            stp<S, V>(dst + b, d);
+        });
 }
 
 // ---------------------------------------------------------------- xGMI multi-source reduce
