@@ -176,8 +176,10 @@ pcclResult_t pcclOptimizeTopology(const pcclComm_t *comm) {
     return pcclSuccess;
 }
 
-pcclResult_t pcclAllReduceAsync(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
-                                const pcclComm_t *comm, pcclAsyncReduceOp_t *handle_out) {
+// Validates and starts one all-reduce. `inline_run` executes the op on the calling thread (blocking pcclAllReduce:
+// no hand-off to a worker thread on the latency-critical path); otherwise a collective worker thread runs it.
+static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
+                                     const pcclComm_t *comm, pcclAsyncReduceOp_t *handle_out, bool inline_run) {
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr && descriptor != nullptr && handle_out != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
@@ -202,10 +204,15 @@ pcclResult_t pcclAllReduceAsync(const void *sendbuff, void *recvbuff, const pccl
     req.qalgo = *qt == *dt ? pccl::QuantAlgo::None : *qa;
     req.op = *op;
     req.tag = descriptor->tag;
-    if (!comm->client->all_reduce_async(req)) return pcclInvalidArgument;
+    if (!comm->client->all_reduce_async(req, inline_run)) return pcclInvalidArgument;
     handle_out->comm = const_cast<pcclComm_t *>(comm);
     handle_out->tag = descriptor->tag;
     return pcclSuccess;
+}
+
+pcclResult_t pcclAllReduceAsync(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
+                                const pcclComm_t *comm, pcclAsyncReduceOp_t *handle_out) {
+    return start_all_reduce(sendbuff, recvbuff, descriptor, comm, handle_out, false);
 }
 
 pcclResult_t pcclAwaitAsyncReduce(const pcclAsyncReduceOp_t *handle, pcclReduceInfo_t *info_out) {
@@ -229,7 +236,7 @@ pcclResult_t pcclAwaitAsyncReduce(const pcclAsyncReduceOp_t *handle, pcclReduceI
 pcclResult_t pcclAllReduce(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
                            const pcclComm_t *comm, pcclReduceInfo_t *info_out) {
     pcclAsyncReduceOp_t h{};
-    const pcclResult_t r = pcclAllReduceAsync(sendbuff, recvbuff, descriptor, comm, &h);
+    const pcclResult_t r = start_all_reduce(sendbuff, recvbuff, descriptor, comm, &h, true);
     if (r != pcclSuccess) return r;
     return pcclAwaitAsyncReduce(&h, info_out);
 }

@@ -100,11 +100,11 @@ PCCLX_EXPORT int pcclxDequantReduce(void *dst, const void *src_q, size_t count, 
                : -1;
 }
 
-PCCLX_EXPORT int pcclxMultiReduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, int dtype,
+PCCLX_EXPORT int pcclxMultiReduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, int dtype,
                                   int op) {
     DeviceBackend *be = device_backend();
     if (!be) return -1;
-    return be->multi_reduce(dst0, dst1, srcs, n, count, static_cast<DType>(dtype), static_cast<ReduceOp>(op), nullptr) &&
+    return be->multi_reduce(dsts, ndst, srcs, n, count, static_cast<DType>(dtype), static_cast<ReduceOp>(op), nullptr) &&
                    be->device_sync()
                ? 0
                : -1;
@@ -134,7 +134,7 @@ PCCLX_EXPORT double pcclxBenchKernel(int which, void *dst, const void *src, size
         switch (which) {
             case 0: be->reduce(dst, src, count, static_cast<DType>(dtype), ReduceOp::Sum, st); break;
             case 1: be->simplehash(src, count * dtype_size(static_cast<DType>(dtype)), st); break;
-            case 2: be->multi_reduce(dst, nullptr, srcs.data(), n, count, static_cast<DType>(dtype), ReduceOp::Sum, st); break;
+            case 2: be->multi_reduce(&dst, 1, srcs.data(), n, count, static_cast<DType>(dtype), ReduceOp::Sum, st); break;
             case 3: be->quantize(dst, src, count, static_cast<DType>(dtype), DType::U8, qp, st); break;
             default: break;
         }

@@ -72,7 +72,42 @@ bool Client::abort_received(uint64_t tag) {
 // ------------------------------------------------------------------------------------------------------------------
 // op orchestration
 // ------------------------------------------------------------------------------------------------------------------
-bool Client::all_reduce_async(const ReduceRequest &req) {
+OpWorkers::~OpWorkers() {
+    {
+        std::lock_guard l(m_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : threads_)
+        if (t.joinable()) t.join();
+}
+
+void OpWorkers::submit(std::function<void()> fn) {
+    std::lock_guard l(m_);
+    q_.push_back(std::move(fn));
+    if (q_.size() > idle_) {
+        threads_.emplace_back([this] { loop(); });
+    } else {
+        cv_.notify_one();
+    }
+}
+
+void OpWorkers::loop() {
+    std::unique_lock l(m_);
+    while (true) {
+        ++idle_;
+        cv_.wait(l, [this] { return stop_ || !q_.empty(); });
+        --idle_;
+        if (q_.empty()) return; // stop requested and nothing left to run
+        auto fn = std::move(q_.front());
+        q_.pop_front();
+        l.unlock();
+        fn();
+        l.lock();
+    }
+}
+
+bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
     if (!accepted_) return false;
     std::shared_ptr<OpState> op;
     {
@@ -80,7 +115,6 @@ bool Client::all_reduce_async(const ReduceRequest &req) {
         auto it = ops_.find(req.tag);
         if (it != ops_.end()) {
             if (!it->second->done.load()) return false; // tag in use
-            if (it->second->thread.joinable()) it->second->thread.join();
             ops_.erase(it);
         }
         op = std::make_shared<OpState>();
@@ -88,7 +122,11 @@ bool Client::all_reduce_async(const ReduceRequest &req) {
         op->revision_at_start = conn_revision_.load();
         ops_[req.tag] = op;
     }
-    op->thread = std::thread([this, op] { run_op(op); });
+    if (inline_run) {
+        run_op(op);
+    } else {
+        workers_.submit([this, op] { run_op(op); });
+    }
     return true;
 }
 
@@ -195,7 +233,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
         current_trace() = nullptr;
     }
     op->success = ok;
-    op->done.store(true);
+    op->finish();
 }
 
 bool Client::join_async_reduce(uint64_t tag) {
@@ -206,7 +244,7 @@ bool Client::join_async_reduce(uint64_t tag) {
         if (it == ops_.end()) return false;
         op = it->second;
     }
-    if (op->thread.joinable() && op->thread.get_id() != std::this_thread::get_id()) op->thread.join();
+    op->wait();
     if (!op->success) {
         // Re-establish the ring once per connection revision: every peer sees the same failures, so every peer
         // performs exactly one establishment round (several concurrent failed ops must not cascade into more).
@@ -231,10 +269,7 @@ bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {
     out.tx_bytes = it->second->tx.load();
     out.rx_bytes = it->second->rx.load();
     it->second->info_taken = true;
-    if (it->second->done.load()) {
-        if (it->second->thread.joinable()) it->second->thread.join();
-        ops_.erase(it);
-    }
+    if (it->second->done.load()) ops_.erase(it);
     return true;
 }
 

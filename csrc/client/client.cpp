@@ -435,8 +435,7 @@ bool Client::join() {
         std::lock_guard lock(ops_mtx_);
         for (auto &[_, op] : ops_) ops.push_back(op);
     }
-    for (auto &op : ops)
-        if (op->thread.joinable()) op->thread.join();
+    for (auto &op : ops) op->wait();
     if (p2p_listener_) p2p_listener_->join();
     if (ss_listener_) ss_listener_->join();
     if (bm_listener_) bm_listener_->join();

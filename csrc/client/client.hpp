@@ -4,6 +4,8 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -69,6 +71,28 @@ struct ReduceRequest {
 
 class IpcArena; // intra-node shared-memory + IPC rendezvous (ipc.cpp)
 
+// Reusable collective worker threads (the reference runs ops on a pithreadpool of PCCL_MAX_CONCURRENT_COLLECTIVE_OPS
+// workers, ccoip_client_state.hpp:17-25,98). Grows whenever every worker is busy, so an op never queues behind
+// another one (a queued op could deadlock against peers that already run it); idle workers are reused, which keeps
+// thread creation off the latency-critical path of back-to-back ops.
+class OpWorkers {
+public:
+    OpWorkers() = default;
+    OpWorkers(const OpWorkers &) = delete;
+    OpWorkers &operator=(const OpWorkers &) = delete;
+    ~OpWorkers();
+    void submit(std::function<void()> fn);
+
+private:
+    void loop();
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> threads_;
+    size_t idle_ = 0;
+    bool stop_ = false;
+};
+
 class Client {
 public:
     explicit Client(const ClientConfig &cfg);
@@ -84,7 +108,8 @@ public:
     bool optimize_topology();
     bool sync_shared_state(SharedState &ss, SSInfo &info);
 
-    bool all_reduce_async(const ReduceRequest &req);
+    // inline_run: execute on the calling thread (blocking pcclAllReduce), else on a collective worker
+    bool all_reduce_async(const ReduceRequest &req, bool inline_run = false);
     bool join_async_reduce(uint64_t tag);           // true on success
     bool get_reduce_info(uint64_t tag, ReduceInfo &out);
     bool any_collective_running();
@@ -104,8 +129,20 @@ private:
 
     struct OpState {
         ReduceRequest req;
-        std::thread thread;
+        std::mutex m;
+        std::condition_variable cv;
         std::atomic<bool> done{false};
+        void wait() {
+            std::unique_lock l(m);
+            cv.wait(l, [this] { return done.load(); });
+        }
+        void finish() {
+            {
+                std::lock_guard l(m);
+                done.store(true);
+            }
+            cv.notify_all();
+        }
         bool success = false;
         bool info_taken = false;
         uint64_t revision_at_start = 0;
@@ -164,6 +201,7 @@ private:
 
     std::mutex ops_mtx_;
     std::map<uint64_t, std::shared_ptr<OpState>> ops_;
+    OpWorkers workers_;
 
     // shared-state distribution (server side)
     std::mutex ss_mtx_;

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -28,7 +29,7 @@ constexpr uint32_t kClosed = 0x80000000u;
 constexpr uint32_t kSlots = 256;
 constexpr uint32_t kMaxWorld = 16;
 
-constexpr uint32_t PH_VOTED = 1, PH_COPIED = 2, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
+constexpr uint32_t PH_VOTED = 1, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
 
 uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
     const auto *b = static_cast<const uint8_t *>(p);
@@ -61,7 +62,7 @@ struct alignas(64) OpPeerShm {
     uint64_t bytes;
     uint32_t dtype;
     uint32_t op;
-    uint32_t zero_copy;
+    uint32_t zero_copy; // bit 0: input is the caller's send buffer, bit 1: output is the caller's receive buffer
     uint32_t pad;
     uint64_t in_raw, out_raw;
     uint64_t in_off, out_off;
@@ -84,10 +85,12 @@ struct ArenaShm {
 };
 
 struct OpCtx {
-    bool zero_copy = false;
-    void *comm = nullptr;          // staged mode: my comm buffer (input half | output half)
-    void *my_out = nullptr;        // where my reduce writes shard `rank` (peers gather from here)
-    std::vector<const uint8_t *> peer_in, peer_out;
+    void *comm = nullptr;          // pooled comm buffer (input half | output half) if either side is staged
+    bool in_staged = false;        // peers read my input from the comm buffer's input half (copied in before the vote)
+    bool out_staged = false;       // peers write / gather my output into the comm buffer's output half (copied out)
+    uint8_t *my_out = nullptr;     // my output: the caller's receive buffer or the comm output half
+    std::vector<const uint8_t *> peer_in;
+    std::vector<uint8_t *> peer_out;
     size_t bytes = 0;
 };
 
@@ -384,6 +387,40 @@ bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
     return true;
 }
 
+bool IpcArena::push_algorithm() {
+    static const bool two_shot = [] {
+        const char *v = std::getenv("PCCL_IPC_ALGO");
+        return v && std::strcmp(v, "two_shot") == 0;
+    }();
+    return !two_shot;
+}
+
+void IpcArena::drain_peers(Client &c, uint64_t seq) {
+    // Used before restoring an in-place buffer after an abort: in the push algorithm peers write into my receive
+    // buffer, so wait until every live peer that may have passed the vote barrier is past its kernel. A peer that has
+    // not voted for `seq` yet will see my ABORTED phase in its vote barrier and never launch.
+    (void)c;
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    const auto t0 = steady_clock::now();
+    const auto timeout = milliseconds(env_size("PCCL_IPC_TIMEOUT_MS", 60000));
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        if (k == rank_) continue;
+        const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
+        while (true) {
+            const uint64_t v = p->phase.load(std::memory_order_acquire);
+            const uint64_t vs = v >> 8;
+            const uint32_t vp = static_cast<uint32_t>(v & 0xff);
+            if (vs != seq + 1 || vp == PH_GATHERED || vp == PH_RELEASED || vp == PH_ABORTED) break;
+            if (!pid_alive(pids_[k])) break;
+            if (steady_clock::now() - t0 > timeout) {
+                LOG(WARN) << "IPC: peer " << k << " did not finish op seq " << seq << " before the restore";
+                break;
+            }
+            std::this_thread::sleep_for(microseconds(20));
+        }
+    }
+}
+
 int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
                         ReduceOp op, const void *src, void *dst) {
     if (!wait_slot_free(c, seq)) {
@@ -391,33 +428,46 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         return kAborted;
     }
     OpPeerShm *mine = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    DeviceBackend *be = device_backend();
     CommBuf *buf = nullptr;
-    bool zero_copy = false;
+    bool in_direct = false, out_direct = false;
     if (device_ok) {
-        // zero-copy needs distinct send / receive buffers (in-place ops keep the staged copy as their abort backup)
-        if (src != dst && !env_flag("PCCL_IPC_NO_ZERO_COPY", false)) {
-            zero_copy = export_user(const_cast<void *>(src), device, mine->in_handle, mine->in_off) &&
-                        export_user(dst, device, mine->out_handle, mine->out_off);
-        }
-        if (zero_copy) {
-            mine->in_raw = reinterpret_cast<uint64_t>(src);
-            mine->out_raw = reinterpret_cast<uint64_t>(dst);
-        } else {
+        // Direct (zero-copy) access to the caller's buffers where HIP IPC can export them. An in-place op always
+        // stages its input: peers read the staged copy while results land in the caller's buffer, and the copy is
+        // the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
+        const bool allow_direct = !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
+        if (allow_direct && src != dst) in_direct = export_user(const_cast<void *>(src), device, mine->in_handle, mine->in_off);
+        if (allow_direct) out_direct = export_user(dst, device, mine->out_handle, mine->out_off);
+        if (in_direct) mine->in_raw = reinterpret_cast<uint64_t>(src);
+        if (out_direct) mine->out_raw = reinterpret_cast<uint64_t>(dst);
+        if (!in_direct || !out_direct) {
             buf = acquire_buffer(2 * bytes, device);
             if (!buf) {
                 device_ok = false;
             } else {
-                std::memcpy(mine->in_handle, buf->handle, kIpcHandleBytes);
-                std::memcpy(mine->out_handle, buf->handle, kIpcHandleBytes);
-                mine->in_off = 0;
-                mine->out_off = bytes;
-                mine->in_raw = reinterpret_cast<uint64_t>(buf->ptr);
-                mine->out_raw = reinterpret_cast<uint64_t>(static_cast<uint8_t *>(buf->ptr) + bytes);
+                if (!in_direct) {
+                    std::memcpy(mine->in_handle, buf->handle, kIpcHandleBytes);
+                    mine->in_off = 0;
+                    mine->in_raw = reinterpret_cast<uint64_t>(buf->ptr);
+                    // copy-in before the vote: a passed vote barrier means every peer's input is readable
+                    StreamLease stream(device);
+                    if (!stream.get() || !be->memcpy_async(buf->ptr, src, bytes, stream.get()) ||
+                        !be->stream_sync(stream.get())) {
+                        LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
+                        device_ok = false;
+                    }
+                    trace_mark("copy_in");
+                }
+                if (!out_direct) {
+                    std::memcpy(mine->out_handle, buf->handle, kIpcHandleBytes);
+                    mine->out_off = bytes;
+                    mine->out_raw = reinterpret_cast<uint64_t>(static_cast<uint8_t *>(buf->ptr) + bytes);
+                }
             }
         }
     }
     mine->vote = device_ok ? 1 : 0;
-    mine->zero_copy = zero_copy ? 1 : 0;
+    mine->zero_copy = (in_direct ? 1u : 0u) | (out_direct ? 2u : 0u);
     mine->device = device;
     mine->bytes = bytes;
     mine->dtype = static_cast<uint32_t>(dtype);
@@ -427,6 +477,12 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     if (rc != 0) {
         LOG(WARN) << "IPC: vote barrier failed (rc " << rc << ")";
         set_phase(seq, PH_ABORTED);
+        if (device_ok && buf && !in_direct && src == dst && out_direct) {
+            // peers that passed the barrier before my abort may be pushing into the caller's buffer: let them
+            // finish, then restore it from the staged copy
+            drain_peers(c, seq);
+            be->memcpy_sync(dst, buf->ptr, bytes);
+        }
         release_buffer(buf);
         return kAborted;
     }
@@ -444,23 +500,28 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     }
     OpCtx ctx;
     ctx.bytes = bytes;
-    ctx.zero_copy = zero_copy;
     ctx.comm = buf ? buf->ptr : nullptr;
-    ctx.my_out = zero_copy ? dst : static_cast<uint8_t *>(buf->ptr) + bytes;
+    ctx.in_staged = !in_direct;
+    ctx.out_staged = !out_direct;
+    ctx.my_out = out_direct ? static_cast<uint8_t *>(dst) : static_cast<uint8_t *>(buf->ptr) + bytes;
     ctx.peer_in.resize(ring_.size());
     ctx.peer_out.resize(ring_.size());
     for (size_t k = 0; k < ring_.size(); ++k) {
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
         if (k == rank_ || pids_[k] == pids_[rank_]) { // same process (threaded peers): raw pointers are usable
             ctx.peer_in[k] = reinterpret_cast<const uint8_t *>(p->in_raw);
-            ctx.peer_out[k] = reinterpret_cast<const uint8_t *>(p->out_raw);
+            ctx.peer_out[k] = reinterpret_cast<uint8_t *>(p->out_raw);
             continue;
         }
         auto *in_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->in_handle, device));
-        auto *out_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->out_handle, device));
+        auto *out_base = static_cast<uint8_t *>(peer_mapping(static_cast<int>(k), p->out_handle, device));
         if (!in_base || !out_base) {
             LOG(ERR) << "IPC: cannot map the buffers of peer " << k;
             set_phase(seq, PH_ABORTED);
+            if (buf && !in_direct && src == dst && out_direct) {
+                drain_peers(c, seq);
+                be->memcpy_sync(dst, buf->ptr, bytes);
+            }
             release_buffer(buf);
             return kAborted;
         }
@@ -501,14 +562,16 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
-    auto *my_out = static_cast<uint8_t *>(ctx.my_out);
-    bool dst_touched = false;
+    uint8_t *my_out = ctx.my_out;
+    const bool push = push_algorithm();
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
+            be->stream_sync(st); // my kernels are done: no further writes from this peer
             set_phase(seq, PH_ABORTED);
-            be->stream_sync(st);
-            if (dst_touched && src == dst && ctx.comm) { // restore the caller's buffer from the staged original
+            if (src == dst && ctx.in_staged && ctx.comm) {
+                // restore the caller's buffer from the staged original once no peer can still write into it
+                if (push && !ctx.out_staged) drain_peers(c, seq);
                 be->memcpy_async(dst, ctx.comm, bytes, st);
                 be->stream_sync(st);
             }
@@ -523,18 +586,6 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         return finish(1);
     }
 
-    // 1. staged mode: copy-in (zero-copy peers expose the caller's send buffer directly)
-    if (!ctx.zero_copy) {
-        if (!be->memcpy_async(ctx.comm, src, bytes, st) || !be->stream_sync(st)) {
-            LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
-            return finish(1);
-        }
-    }
-    trace_mark("copy_in");
-    set_phase(seq, PH_COPIED);
-    if (int rc = barrier(c, tag, seq, PH_COPIED)) return finish(rc);
-    trace_mark("copied_barrier");
-
     // shard bounds: 256-byte aligned so every peer's shard is 16-byte-vector aligned
     const size_t align_el = std::max<size_t>(1, 256 / es);
     const size_t per = ((count + W - 1) / W + align_el - 1) / align_el * align_el;
@@ -543,36 +594,53 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         lo[k] = std::min(k * per, count);
         n[k] = std::min(lo[k] + per, count) - lo[k];
     }
-
-    // 2. reduce-scatter: read shard `rank` of every peer's input over xGMI, reduce in fixed peer order; the result
-    //    lands in my output (= the caller's receive buffer in zero-copy mode, else the comm buffer + caller's buffer)
     std::vector<const void *> srcs(W);
     for (size_t k = 0; k < W; ++k) srcs[k] = ctx.peer_in[k] + lo[rank_] * es;
-    dst_touched = true;
-    void *dst1 = ctx.zero_copy ? nullptr : static_cast<uint8_t *>(dst) + lo[rank_] * es;
-    if (!be->multi_reduce(my_out + lo[rank_] * es, dst1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st) ||
-        !be->stream_sync(st)) {
-        LOG(ERR) << "IPC: multi-source reduce failed";
-        return finish(1);
-    }
-    trace_mark("reduce");
-    set_phase(seq, PH_REDUCED);
-    if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
-    trace_mark("reduced_barrier");
 
-    // 3. all-gather: pull every other peer's reduced shard straight into the receive buffer
-    std::vector<const void *> gsrc(W);
-    for (size_t k = 0; k < W; ++k) gsrc[k] = ctx.peer_out[k] + lo[k] * es;
-    if (!be->multi_gather(dst, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_), dtype,
-                          st) ||
-        !be->stream_sync(st)) {
-        LOG(ERR) << "IPC: gather failed";
-        return finish(1);
+    if (push) {
+        // one-shot: read shard `rank` of every peer's input (inbound xGMI), reduce in fixed peer order and write the
+        // result into every peer's output (outbound xGMI, posted writes) — reduce-scatter and all-gather overlap in
+        // one kernel and one barrier; every peer receives the owner's bytes, so results are bit-identical
+        std::vector<void *> dsts(W);
+        for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
+        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), srcs.data(), static_cast<int>(W), n[rank_], dtype, op,
+                              st) ||
+            !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: multi-source reduce + broadcast failed";
+            return finish(1);
+        }
+        trace_mark("reduce_bcast");
+    } else {
+        // two-shot: reduce-scatter into my output, barrier, then pull every other shard (reads only)
+        void *d0 = my_out + lo[rank_] * es;
+        if (!be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st) ||
+            !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: multi-source reduce failed";
+            return finish(1);
+        }
+        trace_mark("reduce");
+        set_phase(seq, PH_REDUCED);
+        if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
+        trace_mark("reduced_barrier");
+        std::vector<const void *> gsrc(W);
+        for (size_t k = 0; k < W; ++k) gsrc[k] = ctx.peer_out[k] + lo[k] * es;
+        if (!be->multi_gather(my_out, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_),
+                              dtype, st) ||
+            !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: gather failed";
+            return finish(1);
+        }
+        trace_mark("gather");
     }
-    trace_mark("gather");
     set_phase(seq, PH_GATHERED);
     if (int rc = barrier(c, tag, seq, PH_GATHERED)) return finish(rc);
     trace_mark("gathered_barrier");
+    if (ctx.out_staged) { // the caller's receive buffer could not be exported: copy the assembled result out
+        if (!be->memcpy_async(dst, my_out, bytes, st) || !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: copy-out failed";
+            return finish(1);
+        }
+    }
 
     const uint64_t moved = static_cast<uint64_t>(bytes) * (W - 1) / W;
     tx += 2 * moved;

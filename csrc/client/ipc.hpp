@@ -1,15 +1,16 @@
 // Intra-node xGMI fast path.
 //
 // When every peer of a ring runs on this host (loopback run), the peers rendezvous in a POSIX shared-memory arena
-// and each exports HBM communication buffers through HIP IPC. An all-reduce whose buffers are on GPUs at every peer
-// then runs as a "two-shot" direct-access collective instead of a TCP ring:
-//   1. copy-in: each peer copies its send buffer into its exported comm buffer (local HBM)
-//   2. reduce-scatter: peer r owns shard r and reduces it by reading shard r from *all* peers' comm buffers at once
-//      (one fused kernel, 16-byte loads, fixed peer order -> every peer gets bit-identical results); the result goes
-//      to its own output region and straight into the user's receive buffer
-//   3. all-gather: each peer reads the other peers' reduced shards directly into its receive buffer
-// A ring moves data over one xGMI link per GPU; this uses all W-1 links of the fully connected MI355X node
-// concurrently and needs 3 kernel launches instead of 2(W-1) dependent ring steps.
+// and exchange HIP IPC handles of their op buffers. An all-reduce whose buffers are on GPUs at every peer then runs
+// as a direct-access collective instead of a TCP ring. Each peer publishes an *input* (the caller's send buffer, or a
+// staged copy for in-place ops) and an *output* (the caller's receive buffer, or a staged comm buffer if it cannot be
+// exported). Peer r owns shard r:
+//   push (default, "one-shot"): one kernel reads shard r of every peer's input over xGMI (inbound), reduces in fixed
+//     peer order with fp32 accumulation and writes the result into every peer's output (outbound, posted writes).
+//     Reduce-scatter and all-gather overlap in one pass and use both directions of every link; one barrier.
+//   two_shot (PCCL_IPC_ALGO=two_shot): reduce shard r into my output, barrier, then pull every other peer's shard.
+// Either way every peer holds the owner's bytes for every shard (bit-identical results), all W-1 links of the fully
+// connected MI355X node are used concurrently, and an op needs 1-2 kernel launches instead of 2(W-1) ring steps.
 //
 // Synchronization is a per-op barrier in shared memory keyed by the master-assigned sequence number (so concurrent
 // ops with different tags proceed independently). Every wait is bounded and also watches the master's abort packet
@@ -77,6 +78,10 @@ private:
     int barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase);
     void set_phase(uint64_t seq, uint32_t phase);
     bool wait_slot_free(Client &c, uint64_t seq);
+    // waits until no live peer can still write into my receive buffer for `seq` (push algorithm, abort path)
+    void drain_peers(Client &c, uint64_t seq);
+    // PCCL_IPC_ALGO: "push" (default, one-shot reduce + broadcast) or "two_shot" (reduce-scatter, then gather)
+    static bool push_algorithm();
 
     std::vector<Uuid> ring_;
     size_t rank_ = 0;

@@ -67,8 +67,9 @@ public:
     virtual bool finalize_avg(void *dst, size_t count, DType t, size_t world_size, DevStream s) = 0;
 
     // Intra-node xGMI kernels. srcs[k] points to shard `count` elements in peer k's buffer (IPC-mapped);
-    // dst0/dst1 receive op(srcs[0..n)) reduced in order 0..n-1 (dst1 may be null). Avg divides by n at the end.
-    virtual bool multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t,
+    // every dsts[0..ndst) receives op(srcs[0..n)) reduced in order 0..n-1 (the own output and, in the one-shot push
+    // all-reduce, the IPC-mapped outputs of the peers). Avg divides by n at the end.
+    virtual bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
                               ReduceOp op, DevStream s) = 0;
     // dst regions gathered from n sources: dst[k*stride ...] = srcs[k] for k != skip (count elements each,
     // segment k has counts[k] elements at element offset offsets[k]).

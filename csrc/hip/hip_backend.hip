@@ -162,9 +162,9 @@ public:
     bool finalize_avg(void *dst, size_t count, DType t, size_t ws, DevStream s) override {
         return hipk::launch_finalize_avg(dst, count, t, ws, static_cast<hipStream_t>(s));
     }
-    bool multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
+    bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
                       DevStream s) override {
-        return hipk::launch_multi_reduce(dst0, dst1, srcs, n, count, t, op, static_cast<hipStream_t>(s));
+        return hipk::launch_multi_reduce(dsts, ndst, srcs, n, count, t, op, static_cast<hipStream_t>(s));
     }
     bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n, int skip,
                       DType t, DevStream s) override {

@@ -7,15 +7,21 @@
 
 namespace pccl::hipk {
 
-bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
-                         hipStream_t st) {
+bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
+                         ReduceOp op, hipStream_t st) {
     if (count == 0) return true;
-    if (n < 1 || n > kMaxSrc) return false;
+    if (n < 1 || n > kMaxSrc || ndst < 1 || ndst > kMaxSrc) return false;
     SrcList sl{};
-    uintptr_t align_or = reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(dst1);
+    DstList dl{};
+    uintptr_t align_or = 0;
     for (int k = 0; k < n; ++k) {
         sl.p[k] = srcs[k];
         align_or |= reinterpret_cast<uintptr_t>(srcs[k]);
+    }
+    for (int k = 0; k < ndst; ++k) {
+        if (!dsts[k]) return false;
+        dl.p[k] = dsts[k];
+        align_or |= reinterpret_cast<uintptr_t>(dsts[k]);
     }
     const bool avg = op == ReduceOp::Avg;
     return with_elem(t, [&](auto e) {
@@ -32,23 +38,24 @@ bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n,
                 ok = launch_ok([&] {
                     if constexpr (std::is_same_v<O, OpSum>) {
                         if (avg) {
-                            k_multi_reduce_vec<E, O, true><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst0), static_cast<S *>(dst1), sl, n, nvec);
+                            k_multi_reduce_vec<E, O, true><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
                             return;
                         }
                     }
-                    k_multi_reduce_vec<E, O, false><<<grid, kBlock, 0, st>>>(static_cast<S *>(dst0), static_cast<S *>(dst1), sl, n, nvec);
+                    k_multi_reduce_vec<E, O, false><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
                 });
             }
             const size_t begin = nvec * V;
             if (ok && begin < count) {
+                const int grid = grid_for(count - begin);
                 ok = launch_ok([&] {
                     if constexpr (std::is_same_v<O, OpSum>) {
                         if (avg) {
-                            k_multi_reduce_scalar<E, O, true><<<grid_for(count - begin), kBlock, 0, st>>>(static_cast<S *>(dst0), static_cast<S *>(dst1), sl, n, count, begin);
+                            k_multi_reduce_scalar<E, O, true><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin);
                             return;
                         }
                     }
-                    k_multi_reduce_scalar<E, O, false><<<grid_for(count - begin), kBlock, 0, st>>>(static_cast<S *>(dst0), static_cast<S *>(dst1), sl, n, count, begin);
+                    k_multi_reduce_scalar<E, O, false><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin);
                 });
             }
             return ok;

@@ -361,9 +361,17 @@ struct Vec {
     static constexpr int N = 16 / sizeof(S);
 };
 
+// Destinations of a reduced shard: the owner's own output plus (one-shot push all-reduce) every peer's output.
+struct DstList {
+    void *p[kMaxSrc];
+};
+
+// Reads VEC-element vectors i and i+stride from every source (fixed peer order, fp32 accumulation, one rounding, so
+// every peer gets bit-identical bytes) and stores the result to every destination. In the one-shot IPC all-reduce the
+// destinations are the receive buffers of all peers (remote ones over xGMI: posted writes, so the outbound direction
+// of the links carries the all-gather while the inbound direction carries the reduce-scatter reads).
 template<typename E, typename Op, bool AVG>
-__global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(typename E::S *__restrict__ dst0, typename E::S *__restrict__ dst1,
-                                                             SrcList srcs, int nsrc, size_t nvec) {
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec) {
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = Vec<E>::N;
@@ -410,18 +418,17 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(typename E::S *__re
             o0[e] = E::st(acc0[e]);
             o1[e] = E::st(acc1[e]);
         }
-        nt_store(reinterpret_cast<uint4 *>(dst0) + i, out0);
-        if (dst1) nt_store(reinterpret_cast<uint4 *>(dst1) + i, out0);
-        if (has2) {
-            nt_store(reinterpret_cast<uint4 *>(dst0) + j, out1);
-            if (dst1) nt_store(reinterpret_cast<uint4 *>(dst1) + j, out1);
+#pragma unroll 4
+        for (int k = 0; k < ndst; ++k) {
+            nt_store(static_cast<uint4 *>(dsts.p[k]) + i, out0);
+            if (has2) nt_store(static_cast<uint4 *>(dsts.p[k]) + j, out1);
         }
     }
 }
 
 template<typename E, typename Op, bool AVG>
-__global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(typename E::S *__restrict__ dst0, typename E::S *__restrict__ dst1,
-                                                                SrcList srcs, int nsrc, size_t n, size_t begin) {
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t n,
+                                                                size_t begin) {
     using S = typename E::S;
     using C = typename E::C;
     const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
@@ -430,8 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(typename E::S *_
         for (int k = 1; k < nsrc; ++k) acc = apply_op<Op, C>(acc, E::ld(static_cast<const S *>(srcs.p[k])[i]));
         if (AVG) acc = static_cast<C>(acc / static_cast<C>(nsrc));
         const S v = E::st(acc);
-        dst0[i] = v;
-        if (dst1) dst1[i] = v;
+        for (int k = 0; k < ndst; ++k) static_cast<S *>(dsts.p[k])[i] = v;
     }
 }
 

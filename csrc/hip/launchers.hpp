@@ -25,8 +25,8 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
 bool launch_minmax(const void *src, size_t count, DType vtype, double *partial_scratch, double *out2, hipStream_t s);
 
 // hip_ipc.hip
-bool launch_multi_reduce(void *dst0, void *dst1, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
-                         hipStream_t s);
+bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
+                         ReduceOp op, hipStream_t s);
 bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
                          int skip, DType t, hipStream_t s);
 

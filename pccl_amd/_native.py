@@ -141,7 +141,7 @@ def _load() -> ctypes.CDLL:
         "pcclxFinalizeAvg": ([c_void_p, c_size_t, c_int, c_size_t, c_int], c_int),
         "pcclxQuantize": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double)], c_int),
         "pcclxDequantReduce": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double), c_int], c_int),
-        "pcclxMultiReduce": ([c_void_p, c_void_p, p(c_void_p), c_int, c_size_t, c_int, c_int], c_int),
+        "pcclxMultiReduce": ([p(c_void_p), c_int, p(c_void_p), c_int, c_size_t, c_int, c_int], c_int),
         "pcclxMultiGather": ([c_void_p, p(c_void_p), p(c_size_t), p(c_size_t), c_int, c_int, c_int], c_int),
         "pcclxBenchKernel": ([c_int, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int], c_double),
         "pcclxPseudoGrad": ([c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int], c_int),

@@ -93,14 +93,20 @@ def dequant_reduce(dst: torch.Tensor, q: torch.Tensor, meta: Sequence[float], al
 
 
 def multi_reduce(srcs: Sequence[torch.Tensor], op: str = "sum", out: Optional[torch.Tensor] = None,
-                 out2: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = op(srcs[0], ..., srcs[n-1]) in fixed order (the xGMI reduce-scatter kernel; GPU only)."""
+                 out2: Optional[torch.Tensor] = None, outs: Sequence[torch.Tensor] = ()) -> torch.Tensor:
+    """out = op(srcs[0], ..., srcs[n-1]) in fixed order, also stored to out2 and every tensor of ``outs`` (the xGMI
+    one-shot reduce + broadcast kernel; GPU only)."""
     s0 = srcs[0]
     out = torch.empty_like(s0) if out is None else out
     _on_device(s0)
+    dsts = [out] + ([out2] if out2 is not None else []) + list(outs)
+    for d in dsts:
+        if d.numel() != s0.numel() or d.dtype != s0.dtype:
+            raise ValueError("multi_reduce: every output must match the sources' shape and dtype")
     arr = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
-    _check(C.pcclxMultiReduce(out.data_ptr(), out2.data_ptr() if out2 is not None else None, arr, len(srcs),
-                              s0.numel(), WIRE_DTYPE[s0.dtype], OPS[op]), "multi_reduce")
+    darr = (ctypes.c_void_p * len(dsts))(*[d.data_ptr() for d in dsts])
+    _check(C.pcclxMultiReduce(darr, len(dsts), arr, len(srcs), s0.numel(), WIRE_DTYPE[s0.dtype], OPS[op]),
+           "multi_reduce")
     return out
 
 

@@ -96,6 +96,24 @@ def test_multi_reduce(hip, dtype, nsrc, op):
     assert torch.equal(out2.cpu(), ref)
 
 
+@pytest.mark.parametrize("ndst", [1, 2, 8, 16])
+@pytest.mark.parametrize("misalign", [0, 3])
+def test_multi_reduce_broadcast(hip, ndst, misalign):
+    """One-shot push kernel: the reduced shard lands in every destination (scalar path when misaligned)."""
+    n = (1 << 17) + 5
+    srcs = [_rand(n + misalign, torch.bfloat16, 40 + k).to(hip)[misalign:] for k in range(4)]
+    acc = srcs[0].cpu().float()
+    for s in srcs[1:]:
+        acc = acc + s.cpu().float()
+    ref = acc.bfloat16()
+    outs = [torch.full((n,), 7.0, dtype=torch.bfloat16, device=hip) for _ in range(ndst - 1)]
+    got = K.multi_reduce(srcs, "sum", outs=outs)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref)
+    for o in outs:
+        assert torch.equal(o.cpu(), ref)
+
+
 def test_multi_gather(hip):
     parts = [torch.randn(n, device=hip) for n in (1000, 0, 4099, 17)]
     offs = [0, 1000, 1000, 5099]
