@@ -1,0 +1,137 @@
+"""BASELINE config 3: int8/uint8-quantized all-reduce over a simulated 50 ms WAN, 8 peers.
+
+    python benchmarks/wan_quantized.py [--peers 8] [--mib 512] [--latency-ms 50] [--flow-mbit 2500]
+                                        [--link-mbit 45000] [--device cuda:0|cpu] [--pool 8]
+
+Peer processes on one host with the built-in WAN emulation (PCCL_SIM_WAN, csrc/net/mux.hpp: one-way latency, a
+per-TCP-flow rate and a per-peer shared link rate -- tc-netem needs root, which the benchmark boxes do not grant).
+The xGMI IPC path is disabled (PCCL_DISABLE_IPC=1) so every byte crosses the emulated WAN through the TCP ring:
+device tensors are staged through pinned memory and (de)quantized by the HIP kernels.
+For each wire format (fp32 / uint8 min-max / int8 zero-point-scale / fp8 e4m3 min-max) an AVG all-reduce of --mib MiB
+of fp32 per peer, split into --concurrent slices in flight at once, is timed after a warm-up. Reported per format:
+  * seconds, effective algorithm bandwidth (fp32 bytes / time) and bus bandwidth (x 2(n-1)/n),
+  * the reference's metric: (rx + tx wire bytes) / time per peer, in Gbit/s -- comparable to its published
+    25 / 45 Gbit/s WAN figures (docs/md/01_Introduction.md:8), which were link-limited as the emulated link is here,
+  * the max abs error vs the exact fp32 average.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FORMATS = ["fp32", "uint8", "int8_zps", "fp8"]
+
+
+def peer(a):
+    import torch
+
+    import pccl_amd as pccl
+    from pccl_amd.utils import wait_for_world
+    dev = torch.device(a.device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool)
+    comm.connect(n_attempts=60)
+    wait_for_world(comm, a.peers, timeout=300)
+    D, Q = pccl.DataType, pccl.QuantizationAlgorithm
+    qopts = {"fp32": None, "uint8": pccl.QuantizationOptions(D.UINT8, Q.MIN_MAX),
+             "int8_zps": pccl.QuantizationOptions(D.INT8, Q.ZERO_POINT_SCALE),
+             "fp8": pccl.QuantizationOptions(D.FLOAT8_E4M3, Q.MIN_MAX)}
+    n = (a.mib << 20) // 4
+
+    def inputs(r, k=None):  # deterministic, size-independent synthetic data (no RNG stream to replay)
+        i = torch.arange(n if k is None else k, dtype=torch.float64)
+        return (torch.sin(0.37 * i + r) * (1.0 + 0.1 * r) + 0.05 * torch.cos(0.011 * i * (r + 1))).float()
+
+    check = min(n, 1 << 20)
+    exact = torch.stack([inputs(r, check) for r in range(a.peers)]).double().mean(0).float()
+    x = inputs(a.rank).to(dev)
+    out = {}
+    tag = 0
+    for f in a.formats.split(","):
+        y = torch.empty_like(x)
+        comm.all_reduce(x[:65536], y[:65536], op=pccl.ReduceOp.AVG, tag=tag, quantization_options=qopts[f])
+        tag += 1
+        # --concurrent all-reduces of equal slices in flight at once over the connection pool (the reference's
+        # recipe for long fat pipes: pcclAllReduceMultipleWithRetry, docs/md/01_Introduction.md:8)
+        q = qopts[f] or pccl.QuantizationOptions(D.FLOAT, Q.NONE)
+        per = (n + a.concurrent - 1) // a.concurrent
+        descs = []
+        for k in range(a.concurrent):
+            lo, hi = k * per, min(n, (k + 1) * per)
+            rd = pccl.ReduceDescriptor(hi - lo, pccl.ReduceOp.AVG, tag, pccl.ReduceOperandDescriptor(D.FLOAT), q)
+            descs.append(pccl.ReduceOpDescriptor.from_torch(x[lo:hi], y[lo:hi], rd))
+            tag += 1
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=a.concurrent)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        err = float((y[:check].cpu() - exact).abs().max())
+        out[f] = {"seconds": dt, "tx": info.tx_bytes, "rx": info.rx_bytes, "max_abs_err": err}
+    print(json.dumps({"rank": a.rank, "res": out}), flush=True)
+    comm.destroy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--mib", type=int, default=512)
+    ap.add_argument("--latency-ms", type=float, default=50)
+    ap.add_argument("--flow-mbit", type=float, default=2500)
+    ap.add_argument("--link-mbit", type=float, default=45000)
+    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--formats", default=",".join(FORMATS))
+    ap.add_argument("--rank", type=int, default=None)
+    ap.add_argument("--master", default=None)
+    a = ap.parse_args()
+    if a.rank is not None:
+        return peer(a)
+    from pccl_amd.utils import local_master, spawn_python
+    env = {"PCCL_SIM_WAN": f"{a.latency_ms}:{a.flow_mbit}:{a.link_mbit}", "PCCL_DISABLE_IPC": "1",
+           "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)}
+    args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
+            "--concurrent", str(a.concurrent),
+            "--formats", a.formats]
+    with local_master() as addr:
+        ps = [spawn_python([os.path.abspath(__file__), "--rank", str(r), "--master", addr, *args], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(a.peers)]
+        outs = [p.communicate(timeout=1500) for p in ps]
+    res = []
+    for p, (o, e) in zip(ps, outs):
+        if p.returncode != 0:
+            raise RuntimeError(e[-3000:])
+        res.append(json.loads([x for x in o.splitlines() if x.startswith("{")][-1])["res"])
+    nbytes = (a.mib << 20)
+    summary = {}
+    for f in a.formats.split(","):
+        t = max(r[f]["seconds"] for r in res)
+        wire = max((r[f]["tx"] + r[f]["rx"]) / r[f]["seconds"] for r in res)
+        alg = nbytes / t
+        summary[f] = {"seconds": round(t, 4), "alg_GBps": round(alg / 1e9, 3),
+                      "bus_GBps": round(alg * 2 * (a.peers - 1) / a.peers / 1e9, 3),
+                      "ref_metric_rx_plus_tx_Gbit_per_peer": round(wire * 8 / 1e9, 2),
+                      "effective_fp32_Gbit_per_peer": round(2 * nbytes * (a.peers - 1) / a.peers * 2 / t * 8 / 1e9, 2),
+                      "max_abs_err": max(r[f]["max_abs_err"] for r in res)}
+    print(json.dumps({"metric": "quantized all-reduce over emulated WAN",
+                      "config": "int8-quantized all-reduce over tc-netem 50 ms simulated WAN, 8 peers",
+                      "peers": a.peers, "mib_per_peer": a.mib, "device": a.device,
+                      "wan": {"one_way_latency_ms": a.latency_ms, "flow_mbit": a.flow_mbit, "link_mbit": a.link_mbit,
+                              "pool": a.pool, "concurrent_ops": a.concurrent},
+                      "reference_published_Gbit": {"transatlantic": 25, "collocated_eu": 45},
+                      "formats": summary}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

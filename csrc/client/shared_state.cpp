@@ -108,18 +108,147 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         LOG(ERR) << "Shared state sync: no response from master (kicked?)";
         return false;
     }
+    std::map<std::string, SSEntry *> by_key;
+    for (auto &e : ss.entries) by_key[e.key] = &e;
+    DeviceBackend *be = device_backend();
+
+    // receives one entry streamed as raw bytes (HBM destinations through a double-buffered pinned staging ring)
+    auto recv_stream_entry = [&](int fd, SSEntry &dst) -> bool {
+        DevPtrInfo pi{};
+        if (be) be->pointer_info(dst.data, pi);
+        if (!pi.is_device) return net::recv_all(fd, dst.data, dst.bytes);
+        be->set_device(pi.device);
+        StreamLease stream(pi.device);
+        DevStream st = stream.get();
+        Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
+        uint8_t *stage[2] = {a.data(), b.data()};
+        DevEvent evs[2] = {event_pool().get(), event_pool().get()};
+        bool ok = a.ok() && b.ok();
+        size_t off = 0, k = 0;
+        while (ok && off < dst.bytes) {
+            const size_t n = std::min(kStagePiece, dst.bytes - off);
+            if (k >= 2) be->event_sync(evs[k % 2]); // previous H2D from this staging buffer done
+            ok = net::recv_all(fd, stage[k % 2], n);
+            if (!ok) break;
+            be->memcpy_async(static_cast<uint8_t *>(dst.data) + off, stage[k % 2], n, st);
+            be->event_record(evs[k % 2], st);
+            off += n;
+            ++k;
+        }
+        be->stream_sync(st);
+        event_pool().put(evs[0]);
+        event_pool().put(evs[1]);
+        return ok;
+    };
+    auto lookup = [&](size_t i, const std::string &key, uint64_t size) -> SSEntry * {
+        auto it = by_key.find(key);
+        if (it == by_key.end() || i >= resp->outdated_keys.size() || key != resp->outdated_keys[i]) {
+            LOG(ERR) << "Shared state sync: unexpected key " << key;
+            return nullptr;
+        }
+        if (size != it->second->bytes) {
+            LOG(ERR) << "Shared state sync: size mismatch for " << key;
+            return nullptr;
+        }
+        return it->second;
+    };
+    auto verify = [&](size_t i, SSEntry &dst) -> bool {
+        if (dst.allow_content_inequality || i >= resp->expected_hashes.size()) return true;
+        uint64_t h = 0;
+        HashType t;
+        if (!hash_entry(dst, h, t)) return false;
+        if (!verify_hash(this, dst, resp->expected_hashes[i], resp->expected_hash_types[i], h)) {
+            LOG(ERR) << "Shared state sync: distributor sent corrupt content for " << dst.key;
+            return false;
+        }
+        return true;
+    };
+    struct FdGuard {
+        int fd;
+        ~FdGuard() { ::close(fd); }
+    };
+
+    // Same-host distributor: HBM entries are handed over as HIP IPC handles and copied device-to-device (over xGMI
+    // between GPUs) instead of D2H -> TCP -> H2D. `fallback` is set if the distributor does not speak the extension.
+    auto fetch_ipc = [&](const SockAddr &distributor, bool &fallback) -> bool {
+        fallback = false;
+        const int fd = net::connect_tcp(distributor, 10000);
+        if (fd < 0) return false;
+        FdGuard fdg{fd};
+        C2SRequestSharedStateIpc req;
+        req.keys = resp->outdated_keys;
+        req.host_token = net::host_token();
+        req.pid = static_cast<uint32_t>(getpid());
+        if (!net::send_packet(fd, req)) return false;
+        auto pkt = net::recv_ltv(fd);
+        if (!pkt || pkt->id != S2CSharedStateIpcResponse::kId) {
+            fallback = true;
+            return false;
+        }
+        auto sresp = decode_payload<S2CSharedStateIpcResponse>(pkt->payload.data(), pkt->payload.size());
+        if (!sresp || sresp->status != SharedStateStatus::Success ||
+            sresp->entries.size() != resp->outdated_keys.size()) {
+            LOG(WARN) << "Shared state sync: distributor refused the IPC request";
+            return false;
+        }
+        ss.revision = sresp->revision;
+        bool ok = true;
+        for (size_t i = 0; ok && i < sresp->entries.size(); ++i) {
+            const auto &se = sresp->entries[i];
+            SSEntry *dst = lookup(i, se.key, se.size_bytes);
+            if (!dst) {
+                ok = false;
+                break;
+            }
+            if (se.mode == 1 && !be) {
+                LOG(ERR) << "Shared state sync: IPC entry " << se.key << " but no HIP backend";
+                ok = false;
+            } else if (se.mode == 1) {
+                DevPtrInfo pi{};
+                be->pointer_info(dst->data, pi);
+                const int dev = pi.is_device ? pi.device : std::max(0, se.device);
+                be->set_device(dev);
+                void *mapped = nullptr;
+                const uint8_t *src = nullptr;
+                if (sresp->pid == static_cast<uint32_t>(getpid())) {
+                    src = reinterpret_cast<const uint8_t *>(se.raw_ptr); // same process: plain pointer
+                } else {
+                    mapped = be->ipc_open(se.handle);
+                    if (mapped) src = static_cast<const uint8_t *>(mapped) + se.offset;
+                }
+                ok = src && be->memcpy_sync(dst->data, src, dst->bytes);
+                if (mapped) be->ipc_close(mapped);
+                if (!ok) LOG(ERR) << "Shared state sync: IPC copy of " << se.key << " failed";
+            } else {
+                ok = recv_stream_entry(fd, *dst);
+                if (!ok) LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
+            }
+            if (ok) {
+                info.rx_bytes += dst->bytes;
+                ok = verify(i, *dst);
+            }
+        }
+        net::send_packet(fd, C2SSharedStateIpcDone{ok});
+        return ok;
+    };
+
     // Fetches the outdated entries from one distributor; false if it failed or died mid-transfer (partially written
     // entries are overwritten by the next attempt, and every entry is hash-verified at the end).
     auto fetch_from = [&](const SockAddr &distributor) -> bool {
+        // PCCL_SS_IPC_PROTOCOL=1 forces the extension even without a GPU (tests: every entry is then streamed)
+        const bool try_ipc = (be || env_flag("PCCL_SS_IPC_PROTOCOL", false)) && !env_flag("PCCL_SS_NO_IPC", false);
+        if (try_ipc && net::is_local_address(distributor)) {
+            bool fallback = false;
+            if (fetch_ipc(distributor, fallback)) return true;
+            if (!fallback) return false;
+            info.rx_bytes = 0;
+        }
         const int fd = net::connect_tcp(distributor, 10000);
         if (fd < 0) {
             LOG(WARN) << "Shared state sync: cannot reach distributor " << sockaddr_str(distributor);
             return false;
         }
-        struct FdGuard {
-            int fd;
-            ~FdGuard() { ::close(fd); }
-        } fdg{fd};
+        FdGuard fdg{fd};
         C2SRequestSharedState req;
         req.keys = resp->outdated_keys;
         if (!net::send_packet(fd, req)) return false;
@@ -130,66 +259,17 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             return false;
         }
         ss.revision = sresp->revision;
-        std::map<std::string, SSEntry *> by_key;
-        for (auto &e : ss.entries) by_key[e.key] = &e;
         if (sresp->entries.size() != resp->outdated_keys.size()) return false;
-        DeviceBackend *be = device_backend();
         for (size_t i = 0; i < sresp->entries.size(); ++i) {
             const auto &se = sresp->entries[i];
-            auto it = by_key.find(se.key);
-            if (it == by_key.end() || se.key != resp->outdated_keys[i]) {
-                LOG(ERR) << "Shared state sync: unexpected key " << se.key;
+            SSEntry *dst = lookup(i, se.key, se.size_bytes);
+            if (!dst) return false;
+            if (!recv_stream_entry(fd, *dst)) {
+                LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
                 return false;
             }
-            SSEntry &dst = *it->second;
-            if (se.size_bytes != dst.bytes) {
-                LOG(ERR) << "Shared state sync: size mismatch for " << se.key;
-                return false;
-            }
-            DevPtrInfo pi{};
-            if (be) be->pointer_info(dst.data, pi);
-            if (pi.is_device) {
-                be->set_device(pi.device);
-                StreamLease stream(pi.device);
-                DevStream st = stream.get();
-                Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
-                uint8_t *stage[2] = {a.data(), b.data()};
-                DevEvent evs[2] = {event_pool().get(), event_pool().get()};
-                bool ok = a.ok() && b.ok();
-                size_t off = 0, k = 0;
-                while (ok && off < dst.bytes) {
-                    const size_t n = std::min(kStagePiece, dst.bytes - off);
-                    if (k >= 2) be->event_sync(evs[k % 2]); // previous H2D from this staging buffer done
-                    ok = net::recv_all(fd, stage[k % 2], n);
-                    if (!ok) break;
-                    be->memcpy_async(static_cast<uint8_t *>(dst.data) + off, stage[k % 2], n, st);
-                    be->event_record(evs[k % 2], st);
-                    off += n;
-                    ++k;
-                }
-                be->stream_sync(st);
-                event_pool().put(evs[0]);
-                event_pool().put(evs[1]);
-                if (!ok) {
-                    LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
-                    return false;
-                }
-            } else {
-                if (!net::recv_all(fd, dst.data, dst.bytes)) {
-                    LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
-                    return false;
-                }
-            }
-            info.rx_bytes += dst.bytes;
-            if (!dst.allow_content_inequality && i < resp->expected_hashes.size()) {
-                uint64_t h = 0;
-                HashType t;
-                if (!hash_entry(dst, h, t)) return false;
-                if (!verify_hash(this, dst, resp->expected_hashes[i], resp->expected_hash_types[i], h)) {
-                    LOG(ERR) << "Shared state sync: distributor sent corrupt content for " << se.key;
-                    return false;
-                }
-            }
+            info.rx_bytes += dst->bytes;
+            if (!verify(i, *dst)) return false;
         }
         return true;
     };
@@ -229,75 +309,134 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
     } g{fd};
     timeval tv{30, 0};
     setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-    auto req = net::recv_packet<C2SRequestSharedState>(fd);
-    if (!req) return;
-    S2CSharedStateResponse resp;
+    auto pkt = net::recv_ltv(fd);
+    if (!pkt) return;
+    std::vector<std::string> keys;
+    bool ipc_request = false, same_host = false;
+    if (pkt->id == C2SRequestSharedState::kId) {
+        auto req = decode_payload<C2SRequestSharedState>(pkt->payload.data(), pkt->payload.size());
+        if (!req) return;
+        keys = std::move(req->keys);
+    } else if (pkt->id == C2SRequestSharedStateIpc::kId) {
+        auto req = decode_payload<C2SRequestSharedStateIpc>(pkt->payload.data(), pkt->payload.size());
+        if (!req) return;
+        keys = std::move(req->keys);
+        ipc_request = true;
+        same_host = req->host_token == net::host_token();
+    } else {
+        return;
+    }
+    SharedStateStatus status = SharedStateStatus::Success;
+    uint64_t revision = 0;
     std::vector<SSEntry> to_send;
     {
         std::lock_guard l(ss_mtx_);
         if (serving_ == nullptr) {
-            resp.status = SharedStateStatus::NotDistributed;
+            status = SharedStateStatus::NotDistributed;
         } else {
-            resp.status = SharedStateStatus::Success;
-            resp.revision = serving_->revision;
-            for (const auto &k : req->keys) {
+            revision = serving_->revision;
+            for (const auto &k : keys) {
                 auto it = std::find_if(serving_->entries.begin(), serving_->entries.end(),
                                        [&](const SSEntry &e) { return e.key == k; });
                 if (it == serving_->entries.end()) {
-                    resp.status = SharedStateStatus::UnknownKey;
-                    resp.entries.clear();
+                    status = SharedStateStatus::UnknownKey;
                     to_send.clear();
                     break;
                 }
-                resp.entries.push_back(SharedStateEntryInfo{k, it->bytes});
                 to_send.push_back(*it);
             }
         }
     }
-    if (!net::send_packet(fd, resp)) return;
     DeviceBackend *be = device_backend();
-    for (const auto &e : to_send) {
+    auto stream_entry = [&](const SSEntry &e) -> bool {
         DevPtrInfo pi{};
         if (be) be->pointer_info(e.data, pi);
-        if (pi.is_device) {
-            be->set_device(pi.device);
-            StreamLease stream(pi.device);
-            DevStream st = stream.get();
-            Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
-            uint8_t *stage[2] = {a.data(), b.data()};
-            DevEvent evs[2] = {event_pool().get(), event_pool().get()};
-            bool ok = a.ok() && b.ok();
-            const size_t npieces = (e.bytes + kStagePiece - 1) / kStagePiece;
-            auto issue = [&](size_t k) {
-                const size_t off = k * kStagePiece;
-                const size_t n = std::min(kStagePiece, e.bytes - off);
-                be->memcpy_async(stage[k % 2], static_cast<const uint8_t *>(e.data) + off, n, st);
-                be->event_record(evs[k % 2], st);
-            };
-            if (ok && npieces > 0) issue(0);
-            for (size_t k = 0; ok && k < npieces; ++k) {
-                be->event_sync(evs[k % 2]);
-                if (k + 1 < npieces) issue(k + 1); // overlap next D2H with this send
-                const size_t off = k * kStagePiece;
-                const size_t n = std::min(kStagePiece, e.bytes - off);
-                ok = net::send_all(fd, stage[k % 2], n);
-                if (ok) ss_tx_bytes_ += n;
-            }
-            be->stream_sync(st);
-            event_pool().put(evs[0]);
-            event_pool().put(evs[1]);
-            if (!ok) {
-                LOG(WARN) << "Shared state: streaming " << e.key << " to " << sockaddr_str(peer) << " failed";
-                return;
-            }
-        } else {
-            if (!net::send_all(fd, e.data, e.bytes)) {
+        if (!pi.is_device) return net::send_all(fd, e.data, e.bytes);
+        be->set_device(pi.device);
+        StreamLease stream(pi.device);
+        DevStream st = stream.get();
+        Lease a(pinned_pool(), kStagePiece), b(pinned_pool(), kStagePiece);
+        uint8_t *stage[2] = {a.data(), b.data()};
+        DevEvent evs[2] = {event_pool().get(), event_pool().get()};
+        bool ok = a.ok() && b.ok();
+        const size_t npieces = (e.bytes + kStagePiece - 1) / kStagePiece;
+        auto issue = [&](size_t k) {
+            const size_t off = k * kStagePiece;
+            const size_t n = std::min(kStagePiece, e.bytes - off);
+            be->memcpy_async(stage[k % 2], static_cast<const uint8_t *>(e.data) + off, n, st);
+            be->event_record(evs[k % 2], st);
+        };
+        if (ok && npieces > 0) issue(0);
+        for (size_t k = 0; ok && k < npieces; ++k) {
+            be->event_sync(evs[k % 2]);
+            if (k + 1 < npieces) issue(k + 1); // overlap next D2H with this send
+            const size_t off = k * kStagePiece;
+            const size_t n = std::min(kStagePiece, e.bytes - off);
+            ok = net::send_all(fd, stage[k % 2], n);
+        }
+        be->stream_sync(st);
+        event_pool().put(evs[0]);
+        event_pool().put(evs[1]);
+        return ok;
+    };
+
+    if (!ipc_request) {
+        S2CSharedStateResponse resp;
+        resp.status = status;
+        resp.revision = revision;
+        for (const auto &e : to_send) resp.entries.push_back(SharedStateEntryInfo{e.key, e.bytes});
+        if (!net::send_packet(fd, resp)) return;
+        for (const auto &e : to_send) {
+            if (!stream_entry(e)) {
                 LOG(WARN) << "Shared state: streaming " << e.key << " to " << sockaddr_str(peer) << " failed";
                 return;
             }
             ss_tx_bytes_ += e.bytes;
         }
+        return;
     }
+
+    // IPC request: export HBM entries (same host only), stream the rest, keep the exports valid until the
+    // requester reports that its copies are done
+    S2CSharedStateIpcResponse resp;
+    resp.status = status;
+    resp.revision = revision;
+    resp.pid = static_cast<uint32_t>(getpid());
+    uint64_t ipc_bytes = 0;
+    for (const auto &e : to_send) {
+        SharedStateIpcEntry ie;
+        ie.key = e.key;
+        ie.size_bytes = e.bytes;
+        DevPtrInfo pi{};
+        if (be && same_host && e.bytes > 0) be->pointer_info(e.data, pi);
+        void *base = nullptr;
+        size_t size = 0;
+        if (pi.is_device && be->address_range(e.data, &base, &size) && base) {
+            be->set_device(pi.device);
+            if (be->ipc_export(base, ie.handle)) {
+                ie.mode = 1;
+                ie.device = pi.device;
+                ie.offset = static_cast<uint64_t>(static_cast<const uint8_t *>(e.data) - static_cast<uint8_t *>(base));
+                ie.raw_ptr = reinterpret_cast<uint64_t>(e.data);
+                ipc_bytes += e.bytes;
+            }
+        }
+        resp.entries.push_back(ie);
+    }
+    if (!net::send_packet(fd, resp)) return;
+    for (size_t i = 0; i < to_send.size(); ++i) {
+        if (resp.entries[i].mode == 1) continue;
+        if (!stream_entry(to_send[i])) {
+            LOG(WARN) << "Shared state: streaming " << to_send[i].key << " to " << sockaddr_str(peer) << " failed";
+            return;
+        }
+        ss_tx_bytes_ += to_send[i].bytes;
+    }
+    if (status != SharedStateStatus::Success) return;
+    timeval tv_done{600, 0}; // the requester copies (and re-hashes) every entry before it answers
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv_done, sizeof(tv_done));
+    auto done = net::recv_packet<C2SSharedStateIpcDone>(fd);
+    if (done && done->ok) ss_tx_bytes_ += ipc_bytes;
 }
 
 } // namespace pccl::client

@@ -4,6 +4,9 @@
 #include <cerrno>
 #include <cstring>
 #include <fcntl.h>
+#include <ifaddrs.h>
+#include <fstream>
+#include <mutex>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -247,6 +250,39 @@ bool is_connected(int fd) {
     if (k == 0) return false;
     if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return false;
     return true;
+}
+
+bool is_local_address(const SockAddr &a) {
+    if (sockaddr_is_loopback(a)) return true;
+    ifaddrs *ifs = nullptr;
+    if (getifaddrs(&ifs) != 0) return false;
+    bool found = false;
+    for (ifaddrs *it = ifs; it && !found; it = it->ifa_next) {
+        if (!it->ifa_addr) continue;
+        if (it->ifa_addr->sa_family == AF_INET && a.inet.protocol == inetIPv4) {
+            const auto *s4 = reinterpret_cast<const sockaddr_in *>(it->ifa_addr);
+            found = std::memcmp(&s4->sin_addr, a.inet.ipv4.data, 4) == 0;
+        } else if (it->ifa_addr->sa_family == AF_INET6 && a.inet.protocol == inetIPv6) {
+            const auto *s6 = reinterpret_cast<const sockaddr_in6 *>(it->ifa_addr);
+            found = std::memcmp(&s6->sin6_addr, a.inet.ipv6.data, 16) == 0;
+        }
+    }
+    freeifaddrs(ifs);
+    return found;
+}
+
+const std::string &host_token() {
+    static std::once_flag once;
+    static std::string token;
+    std::call_once(once, [] {
+        std::ifstream f("/proc/sys/kernel/random/boot_id");
+        std::getline(f, token);
+        char host[256] = {};
+        gethostname(host, sizeof(host) - 1);
+        token += "|";
+        token += host;
+    });
+    return token;
 }
 
 } // namespace pccl::net

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <optional>
+#include <string>
 #include <vector>
 
 #include "../common/types.hpp"
@@ -59,6 +60,10 @@ std::optional<P> recv_packet(int fd) {
 }
 
 void close_fd(int &fd);
+// True if `a` is a loopback address or one of this host's interface addresses.
+bool is_local_address(const SockAddr &a);
+// Identifies this host (kernel boot id + hostname): equal tokens mean two processes can share HIP IPC handles.
+const std::string &host_token();
 bool is_connected(int fd); // MSG_PEEK probe (non-blocking)
 
 } // namespace pccl::net

@@ -318,4 +318,56 @@ bool S2CSharedStateResponse::decode(RBuf &r) {
     return r.ok();
 }
 
+void C2SRequestSharedStateIpc::encode(WBuf &w) const {
+    w.u64(keys.size());
+    for (const auto &k : keys) w.str(k);
+    w.str(host_token);
+    w.u32(pid);
+}
+
+bool C2SRequestSharedStateIpc::decode(RBuf &r) {
+    const uint64_t n = r.u64();
+    if (!r.plausible_count(n, 8)) return false;
+    keys.resize(n);
+    for (auto &k : keys) k = r.str();
+    host_token = r.str();
+    pid = r.u32();
+    return r.ok();
+}
+
+void S2CSharedStateIpcResponse::encode(WBuf &w) const {
+    w.u8(static_cast<uint8_t>(status));
+    w.u64(revision);
+    w.u32(pid);
+    w.u64(entries.size());
+    for (const auto &e : entries) {
+        w.str(e.key);
+        w.u64(e.size_bytes);
+        w.u8(e.mode);
+        w.u32(static_cast<uint32_t>(e.device));
+        w.u64(e.offset);
+        w.u64(e.raw_ptr);
+        w.bytes(e.handle, sizeof(e.handle));
+    }
+}
+
+bool S2CSharedStateIpcResponse::decode(RBuf &r) {
+    status = static_cast<SharedStateStatus>(r.u8());
+    revision = r.u64();
+    pid = r.u32();
+    const uint64_t n = r.u64();
+    if (!r.plausible_count(n, 8 + 8 + 1 + 4 + 8 + 8 + 64)) return false;
+    entries.resize(n);
+    for (auto &e : entries) {
+        e.key = r.str();
+        e.size_bytes = r.u64();
+        e.mode = r.u8();
+        e.device = static_cast<int32_t>(r.u32());
+        e.offset = r.u64();
+        e.raw_ptr = r.u64();
+        r.bytes(e.handle, sizeof(e.handle));
+    }
+    return r.ok();
+}
+
 } // namespace pccl::proto

@@ -48,6 +48,10 @@ constexpr PacketId P2P_DEQUANTIZATION_META = 3;
 // ---- shared state client <-> server ----
 constexpr PacketId C2S_REQUEST_SHARED_STATE = 1;
 constexpr PacketId S2C_SHARED_STATE_RESPONSE = 1;
+// extension (not in the reference protocol): same-host HBM hand-off over HIP IPC instead of a TCP byte stream
+constexpr PacketId C2S_REQUEST_SHARED_STATE_IPC = 2;
+constexpr PacketId S2C_SHARED_STATE_IPC_RESPONSE = 2;
+constexpr PacketId C2S_SHARED_STATE_IPC_DONE = 3;
 // ---- benchmark ----
 constexpr PacketId C2B_HELLO = 1;
 constexpr PacketId B2C_BENCHMARK_SERVER_IS_BUSY = 1;
@@ -364,6 +368,49 @@ struct S2CSharedStateResponse {
     std::vector<SharedStateEntryInfo> entries;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
+};
+
+// Same-host request: like C2SRequestSharedState plus the requester's host identity (boot id + hostname) and pid.
+// A distributor on the same host answers device-resident entries with HIP IPC handles (mode 1) that the requester
+// maps and copies from over xGMI / HBM; everything else (mode 0) follows as raw bytes on the stream, in order.
+struct C2SRequestSharedStateIpc {
+    static constexpr PacketId kId = C2S_REQUEST_SHARED_STATE_IPC;
+    std::vector<std::string> keys;
+    std::string host_token;
+    uint32_t pid = 0;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+struct SharedStateIpcEntry {
+    std::string key;
+    uint64_t size_bytes = 0;
+    uint8_t mode = 0; // 0: bytes follow on the stream, 1: IPC handle
+    int32_t device = -1;
+    uint64_t offset = 0;   // byte offset of the entry inside the exported allocation
+    uint64_t raw_ptr = 0;  // the distributor's pointer (usable directly when both peers share a process)
+    uint8_t handle[64]{};  // hipIpcMemHandle_t of the allocation
+};
+
+struct S2CSharedStateIpcResponse {
+    static constexpr PacketId kId = S2C_SHARED_STATE_IPC_RESPONSE;
+    SharedStateStatus status = SharedStateStatus::Success;
+    uint64_t revision = 0;
+    uint32_t pid = 0;
+    std::vector<SharedStateIpcEntry> entries;
+    void encode(WBuf &w) const;
+    bool decode(RBuf &r);
+};
+
+// Requester -> distributor after all IPC copies finished (the distributor keeps its exports alive until then).
+struct C2SSharedStateIpcDone {
+    static constexpr PacketId kId = C2S_SHARED_STATE_IPC_DONE;
+    bool ok = true;
+    void encode(WBuf &w) const { w.boolean(ok); }
+    bool decode(RBuf &r) {
+        ok = r.boolean();
+        return r.ok();
+    }
 };
 
 struct C2BHello {

@@ -1,0 +1,62 @@
+"""The BASELINE-config benchmark scripts (benchmarks/) at toy sizes: they must run end to end and report exact results.
+
+CPU variants run everywhere; the `gpu` variants exercise the HBM paths (HIP IPC shared-state hand-off between two
+processes, device ring with HIP quantization kernels under the WAN emulation, IPC all-reduce under fault injection).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(script, *args, timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", script), *args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("device,transport", [("cpu", "tcp"), ("cpu", "ipc"),
+                                              pytest.param("cuda:0", "ipc", marks=pytest.mark.gpu),
+                                              pytest.param("cuda:0", "tcp", marks=pytest.mark.gpu)])
+def test_shared_state_catch_up(device, transport):
+    r = _run("shared_state_sync.py", "--params", "3000001", "--tensors", "3", "--device", device,
+             "--transport", transport)
+    assert r["content_ok"] and r["adopted_revision"] == 3
+    assert r["joiner_rx_bytes"] == r["bytes"] == 3000001 * 4
+    assert r["trainer_tx_bytes"] == r["bytes"]
+
+
+def test_basic_reduce():
+    r = _run("basic_reduce.py", "--iters", "30", "--tensors", "4", "--numel", "65536", "--pool", "4")
+    assert r["latency_us"]["median"] > 0
+    assert r["multi_tensor"]["busbw_GBps"] > 0
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_wan_quantized(device):
+    r = _run("wan_quantized.py", "--peers", "3", "--mib", "2", "--latency-ms", "5", "--flow-mbit", "2000",
+             "--link-mbit", "8000", "--pool", "2", "--concurrent", "2", "--device", device,
+             "--formats", "fp32,uint8,int8_zps")
+    f = r["formats"]
+    assert f["fp32"]["max_abs_err"] < 1e-5
+    assert f["uint8"]["max_abs_err"] < 0.05 and f["int8_zps"]["max_abs_err"] < 0.05
+    # quantized wire formats move ~4x fewer bytes than fp32
+    assert f["uint8"]["ref_metric_rx_plus_tx_Gbit_per_peer"] * f["uint8"]["seconds"] < \
+        0.35 * f["fp32"]["ref_metric_rx_plus_tx_Gbit_per_peer"] * f["fp32"]["seconds"]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_fault_tolerance(device):
+    r = _run("fault_tolerance.py", "--peers", "3", "--mib", "1", "--device", device, "--kill-after", "0.3",
+             "--respawn-after", "0.2", "--stop-after-optimize", "5", timeout=400)
+    assert r["all_results_exact"] and not r["peer_errors"]
+    assert r["recovery_ms"] is not None and r["rejoin_ms"] is not None
+    assert r["topology_resolve_ok"]

@@ -21,7 +21,12 @@ def _state(tensors, allow=()):
                              for name, t in tensors.items()])
 
 
-def test_popular_state_wins():
+@pytest.mark.parametrize("ipc_protocol", [False, True])
+def test_popular_state_wins(ipc_protocol, monkeypatch):
+    """ipc_protocol: the same-host request extension (C2SRequestSharedStateIpc) is forced on; without a GPU the
+    distributor answers every entry in stream mode, so the byte accounting is identical."""
+    if ipc_protocol:
+        monkeypatch.setenv("PCCL_SS_IPC_PROTOCOL", "1")
     world, n = 3, 100_000
 
     def fn(rank, comm):
