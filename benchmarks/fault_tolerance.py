@@ -105,6 +105,10 @@ def main():
     ap.add_argument("--joiner", action="store_true")
     ap.add_argument("--deadline", type=float, default=0)
     ap.add_argument("--stop-after-optimize", type=int, default=20)
+    ap.add_argument("--no-ipc", action="store_true",
+                    help="device ring over TCP instead of the xGMI IPC path (see docs/PERFORMANCE.md: a peer killed "
+                         "while a kernel of another peer accesses its exported HBM)")
+    ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
     a = ap.parse_args()
     if a.rank is not None:
         return peer(a)
@@ -115,8 +119,12 @@ def main():
     common = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
               "--deadline", str(deadline), "--stop-after-optimize", str(a.stop_after_optimize)]
     env = {"PCCL_BENCHMARK_MILLIS": "300", "PCCL_NUM_BENCHMARK_CONNECTIONS": "2"}
+    if a.no_ipc:
+        env["PCCL_DISABLE_IPC"] = "1"
     lines = []
     lock = threading.Lock()
+    if a.log_dir:
+        os.makedirs(a.log_dir, exist_ok=True)
 
     def reader(p):
         for ln in p.stdout:
@@ -128,7 +136,9 @@ def main():
         procs, threads = [], []
 
         def start(rank, joiner=False):
-            err = tempfile.TemporaryFile(mode="w+")  # not a pipe: a chatty peer must never block on stderr
+            # a file, not a pipe: a chatty peer must never block on stderr
+            err = open(os.path.join(a.log_dir, f"peer{rank}.err"), "w+") if a.log_dir else \
+                tempfile.TemporaryFile(mode="w+")
             p = spawn_python([me, "--rank", str(rank), "--master", addr, *common] + (["--joiner"] if joiner else []),
                              env=env, stdout=subprocess.PIPE, stderr=err, text=True, start_new_session=True)
             p.err_file = err
@@ -146,20 +156,27 @@ def main():
                 return [x for x in lines if x["event"] == "ok" and (rank is None or x["rank"] == rank)
                         and (world is None or x["world"] == world) and x["t"] > after]
 
+        def progress(what):
+            print(json.dumps({"progress": what, "t": time.time(), "ops": len(oks())}), flush=True)
+
         while len(oks(world=a.peers)) < 3 * a.peers and time.time() < deadline:
             time.sleep(0.05)
+        progress("running")
         time.sleep(a.kill_after)
         victim = procs[a.peers - 1]
         t_kill = time.time()
         os.killpg(victim.pid, signal.SIGKILL)  # its own session: only that peer's process group
         victim.wait()
+        progress("killed")
         while not oks(world=a.peers - 1, after=t_kill) and time.time() < deadline:
             time.sleep(0.01)
+        progress("recovered")
         time.sleep(a.respawn_after)
         t_spawn = time.time()
         start(a.peers, joiner=True)
         while not oks(rank=a.peers) and time.time() < deadline:
             time.sleep(0.01)
+        progress("rejoined")
         for p in procs[:a.peers - 1] + procs[a.peers:]:
             try:
                 p.wait(timeout=max(1.0, deadline - time.time() + 30))

@@ -18,6 +18,6 @@ STEPS=${STEPS:-tests,ss_ipc,ss_tcp,wan,ft,basic}
 [[ $STEPS == *ss_ipc* ]] && { run ss_ipc 300 python benchmarks/shared_state_sync.py --params 1e9 --transport ipc || exit $?; }
 [[ $STEPS == *ss_tcp* ]] && { run ss_tcp 300 python benchmarks/shared_state_sync.py --params 1e9 --transport tcp || exit $?; }
 [[ $STEPS == *wan* ]] && { run wan 400 python benchmarks/wan_quantized.py || exit $?; }
-[[ $STEPS == *ft* ]] && { run ft 300 python benchmarks/fault_tolerance.py || exit $?; }
+[[ $STEPS == *ft* ]] && { run ft 300 python benchmarks/fault_tolerance.py --no-ipc --log-dir gpurun_out/ft_logs || exit $?; }
 [[ $STEPS == *basic* ]] && { run basic 300 python benchmarks/basic_reduce.py || exit $?; }
 exit 0

@@ -55,8 +55,11 @@ def test_wan_quantized(device):
 
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
 def test_fault_tolerance(device):
+    # GPU: device ring over TCP; killing a peer mid-kernel on the xGMI IPC path is not exercised on shared boxes
+    # (docs/PERFORMANCE.md, fault tolerance notes)
     r = _run("fault_tolerance.py", "--peers", "3", "--mib", "1", "--device", device, "--kill-after", "0.3",
-             "--respawn-after", "0.2", "--stop-after-optimize", "5", timeout=400)
+             "--respawn-after", "0.2", "--stop-after-optimize", "5", *(["--no-ipc"] if device != "cpu" else []),
+             timeout=400)
     assert r["all_results_exact"] and not r["peer_errors"]
     assert r["recovery_ms"] is not None and r["rejoin_ms"] is not None
     assert r["topology_resolve_ok"]
