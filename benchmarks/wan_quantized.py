@@ -1,7 +1,10 @@
 """BASELINE config 3: int8/uint8-quantized all-reduce over a simulated 50 ms WAN, 8 peers.
 
-    python benchmarks/wan_quantized.py [--peers 8] [--mib 512] [--latency-ms 50] [--flow-mbit 2500]
-                                        [--link-mbit 45000] [--device cuda:0|cpu] [--pool 8]
+    python benchmarks/wan_quantized.py [--peers 8] [--mib 2048] [--latency-ms 50] [--flow-mbit 1000]
+                                        [--link-mbit 25000] [--device cuda:0|cpu] [--pool 16] [--concurrent 8]
+
+Defaults model a transatlantic long fat pipe: 50 ms one way, ~1 Gbit/s per TCP flow (window-limited at 100 ms RTT),
+a 25 Gbit/s NIC per peer (the reference's transatlantic figure), 16 pooled connections per neighbour.
 
 Peer processes on one host with the built-in WAN emulation (PCCL_SIM_WAN, csrc/net/mux.hpp: one-way latency, a
 per-TCP-flow rate and a per-peer shared link rate -- tc-netem needs root, which the benchmark boxes do not grant).
@@ -46,13 +49,14 @@ def peer(a):
              "fp8": pccl.QuantizationOptions(D.FLOAT8_E4M3, Q.MIN_MAX)}
     n = (a.mib << 20) // 4
 
-    def inputs(r, k=None):  # deterministic, size-independent synthetic data (no RNG stream to replay)
-        i = torch.arange(n if k is None else k, dtype=torch.float64)
-        return (torch.sin(0.37 * i + r) * (1.0 + 0.1 * r) + 0.05 * torch.cos(0.011 * i * (r + 1))).float()
+    def inputs(r, k=None, device="cpu"):  # deterministic, size-independent synthetic data (no RNG stream to replay)
+        i = torch.arange(n if k is None else k, dtype=torch.float32, device=device)
+        return torch.sin(0.37 * i + r) * (1.0 + 0.1 * r) + 0.05 * torch.cos(0.011 * i * (r + 1))
 
     check = min(n, 1 << 20)
-    exact = torch.stack([inputs(r, check) for r in range(a.peers)]).double().mean(0).float()
-    x = inputs(a.rank).to(dev)
+    # the exact average of the first `check` elements, from every peer's inputs computed on this peer's device
+    exact = torch.stack([inputs(r, check, dev) for r in range(a.peers)]).double().mean(0).float().cpu()
+    x = inputs(a.rank, device=dev)
     out = {}
     tag = 0
     for f in a.formats.split(","):
@@ -85,11 +89,11 @@ def peer(a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--peers", type=int, default=8)
-    ap.add_argument("--mib", type=int, default=512)
+    ap.add_argument("--mib", type=int, default=2048)
     ap.add_argument("--latency-ms", type=float, default=50)
-    ap.add_argument("--flow-mbit", type=float, default=2500)
-    ap.add_argument("--link-mbit", type=float, default=45000)
-    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--flow-mbit", type=float, default=1000)
+    ap.add_argument("--link-mbit", type=float, default=25000)
+    ap.add_argument("--pool", type=int, default=16)
     ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--formats", default=",".join(FORMATS))

@@ -120,6 +120,7 @@ bool Client::connect() {
 
     C2MRequestSessionRegistration reg;
     reg.peer_group = cfg_.peer_group;
+    reg.host_token = net::host_token();
     reg.use_explicit_addresses = cfg_.explicit_addresses;
     if (cfg_.explicit_addresses) {
         reg.advertised_p2p = cfg_.adv_p2p;
@@ -270,9 +271,11 @@ Client::EstablishResult Client::establish() {
         old_arena = arena_;
     }
     // Intra-node fast path: every peer of a loopback run lives on this host (the master enforces loopback
-    // exclusivity), so the ring can rendezvous in shared memory and exchange device buffers over xGMI.
+    // exclusivity), or the master reports that every ring member registered with this host's identity; the ring can
+    // then rendezvous in shared memory and exchange device buffers over xGMI.
     std::shared_ptr<IpcArena> arena;
-    if (resp->ring_order.size() >= 2 && sockaddr_is_loopback(cfg_.master) && !env_flag("PCCL_DISABLE_IPC", false) &&
+    const bool one_host = sockaddr_is_loopback(cfg_.master) || resp->single_host;
+    if (resp->ring_order.size() >= 2 && one_host && !env_flag("PCCL_DISABLE_IPC", false) &&
         device_backend_available()) {
         if (old_arena && old_arena->matches(resp->ring_order)) {
             arena = old_arena;

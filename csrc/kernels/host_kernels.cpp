@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <limits>
 #include <thread>
 #include <vector>
@@ -374,19 +375,63 @@ uint32_t simplehash_host(const void *data, size_t n_bytes) {
 // CRC-32C
 // ------------------------------------------------------------------------------------------------------------------
 static uint32_t g_crc_table[8][256];
-static bool g_crc_init = false;
+static uint32_t g_x2n[64]; // x^(2^k) mod P
+static std::once_flag g_crc_once;
 static bool g_spoof_no_hw = false;
+static constexpr uint32_t kCrcPoly = 0x82F63B78u;
 
 static void crc_init() {
-    if (g_crc_init) return;
-    for (uint32_t i = 0; i < 256; ++i) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
-        g_crc_table[0][i] = c;
+    std::call_once(g_crc_once, [] {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : (c >> 1);
+            g_crc_table[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int t = 1; t < 8; ++t)
+                g_crc_table[t][i] = (g_crc_table[t - 1][i] >> 8) ^ g_crc_table[0][g_crc_table[t - 1][i] & 0xff];
+        g_x2n[0] = 1u << 30; // x^1
+        for (int k = 1; k < 64; ++k) g_x2n[k] = crc32c_gf_mul(g_x2n[k - 1], g_x2n[k - 1]);
+    });
+}
+
+const uint32_t (*crc32c_tables())[256] {
+    crc_init();
+    return g_crc_table;
+}
+
+uint32_t crc32c_gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 31; i >= 0; --i) { // bit 31 of a is x^0
+        p ^= (0u - ((a >> i) & 1u)) & b;
+        b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
     }
-    for (uint32_t i = 0; i < 256; ++i)
-        for (int t = 1; t < 8; ++t) g_crc_table[t][i] = (g_crc_table[t - 1][i] >> 8) ^ g_crc_table[0][g_crc_table[t - 1][i] & 0xff];
-    g_crc_init = true;
+    return p;
+}
+
+uint32_t crc32c_x8n(uint64_t n) {
+    crc_init();
+    uint32_t p = 1u << 31; // x^0
+    for (int k = 3; n; n >>= 1, ++k) // x^(8n) = prod over set bits j of n of x^(2^(j+3))
+        if (n & 1) p = crc32c_gf_mul(g_x2n[k & 63], p);
+    return p;
+}
+
+uint32_t crc32c_raw_update(uint32_t c, const void *data, size_t n) {
+    crc_init();
+    const auto *p = static_cast<const uint8_t *>(data);
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        v ^= c;
+        c = g_crc_table[7][v & 0xff] ^ g_crc_table[6][(v >> 8) & 0xff] ^ g_crc_table[5][(v >> 16) & 0xff] ^
+            g_crc_table[4][(v >> 24) & 0xff] ^ g_crc_table[3][(v >> 32) & 0xff] ^ g_crc_table[2][(v >> 40) & 0xff] ^
+            g_crc_table[1][(v >> 48) & 0xff] ^ g_crc_table[0][v >> 56];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) c = (c >> 8) ^ g_crc_table[0][(c ^ *p++) & 0xff];
+    return c;
 }
 
 uint32_t crc32c_sw(const void *data, size_t n) {

@@ -46,4 +46,15 @@ uint32_t crc32c_hw(const void *data, size_t n_bytes);
 void crc32c_spoof_no_hw(bool no_hw); // test hook: force the software path
 bool crc32c_has_hw();
 
+// CRC-32C algebra for split computation (HIP kernel partials, hip_hash.hip). A "raw" CRC has no initial value and no
+// final inversion; it is linear: raw(A || B) = shift(raw(A), |B|) ^ raw(B), and crc(M) = ~(shift(~0, |M|) ^ raw(M)).
+// Polynomials are in the reflected representation (x^0 is the most significant bit).
+uint32_t crc32c_raw_update(uint32_t state, const void *data, size_t n_bytes); // continues from `state`
+uint32_t crc32c_gf_mul(uint32_t a, uint32_t b);                                // a * b mod P
+uint32_t crc32c_x8n(uint64_t n_bytes);                                         // x^(8 n) mod P
+inline uint32_t crc32c_shift(uint32_t raw, uint64_t n_bytes) { return crc32c_gf_mul(crc32c_x8n(n_bytes), raw); }
+inline uint32_t crc32c_finish(uint32_t raw, uint64_t n_bytes) { return ~(crc32c_shift(0xffffffffu, n_bytes) ^ raw); }
+// slicing-by-8 tables: T[k][b] = raw CRC of byte b followed by k zero bytes
+const uint32_t (*crc32c_tables())[256];
+
 } // namespace pccl::kernels

@@ -300,6 +300,7 @@ void Master::handle_join(const SockAddr &addr, const C2MRequestSessionRegistrati
         c.uuid = Uuid::random();
         c.addr = addr;
         c.group = p.peer_group;
+        c.host_token = p.host_token;
         if (p.use_explicit_addresses) {
             c.p2p = p.advertised_p2p;
             c.ss = p.advertised_ss;
@@ -421,6 +422,13 @@ bool Master::check_p2p_established() {
         M2CP2PConnectionsEstablished pkt;
         pkt.success = !failure;
         pkt.ring_order = ring_of(c.group, false);
+        // every ring member on one host (same boot id + hostname): the peers may rendezvous for the xGMI IPC path
+        // even if the master itself is remote
+        pkt.single_host = !pkt.ring_order.empty();
+        for (const auto &ru : pkt.ring_order) {
+            const ClientInfo *rc = client_by_uuid(ru);
+            pkt.single_host = pkt.single_host && rc && !rc->host_token.empty() && rc->host_token == c.host_token;
+        }
         server_.send_packet(c.addr, pkt);
     }
     if (failure) {

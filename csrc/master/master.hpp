@@ -65,6 +65,7 @@ struct ClientInfo {
     uint32_t group = 0;
     SockAddr p2p{}, ss{}, bm{};
     uint64_t ss_revision = 0; // revision announced in the current shared-state round
+    std::string host_token;   // registration extension; empty for reference clients
 };
 
 struct GroupState {

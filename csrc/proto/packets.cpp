@@ -16,6 +16,7 @@ void C2MRequestSessionRegistration::encode(WBuf &w) const {
         w.u16(ss_port);
         w.u16(bm_port);
     }
+    if (!host_token.empty()) w.str(host_token);
 }
 
 bool C2MRequestSessionRegistration::decode(RBuf &r) {
@@ -33,6 +34,7 @@ bool C2MRequestSessionRegistration::decode(RBuf &r) {
         ss_port = r.u16();
         bm_port = r.u16();
     }
+    if (r.ok() && r.remaining() > 0) host_token = r.str(); // absent when the peer is a reference implementation
     return r.ok();
 }
 
@@ -128,8 +130,15 @@ static bool decode_uuid_list(RBuf &r, bool &success, std::vector<Uuid> &v) {
     return r.ok();
 }
 
-void M2CP2PConnectionsEstablished::encode(WBuf &w) const { encode_uuid_list(w, success, ring_order); }
-bool M2CP2PConnectionsEstablished::decode(RBuf &r) { return decode_uuid_list(r, success, ring_order); }
+void M2CP2PConnectionsEstablished::encode(WBuf &w) const {
+    encode_uuid_list(w, success, ring_order);
+    w.boolean(single_host);
+}
+bool M2CP2PConnectionsEstablished::decode(RBuf &r) {
+    if (!decode_uuid_list(r, success, ring_order)) return false;
+    single_host = r.remaining() > 0 && r.boolean();
+    return r.ok();
+}
 void M2COptimizeTopologyComplete::encode(WBuf &w) const { encode_uuid_list(w, success, ring_order); }
 bool M2COptimizeTopologyComplete::decode(RBuf &r) { return decode_uuid_list(r, success, ring_order); }
 

@@ -67,6 +67,9 @@ struct C2MRequestSessionRegistration {
     bool use_explicit_addresses = false;
     SockAddr advertised_p2p{}, advertised_ss{}, advertised_bm{};
     uint16_t p2p_port = 0, ss_port = 0, bm_port = 0;
+    // extension (appended, optional on decode): host identity (boot id + hostname) so the master can tell peers
+    // that share a host -- and may use the xGMI IPC path -- even when the master is not on loopback
+    std::string host_token;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };
@@ -212,6 +215,7 @@ struct M2CP2PConnectionsEstablished {
     static constexpr PacketId kId = M2C_P2P_CONNECTIONS_ESTABLISHED;
     bool success = false;
     std::vector<Uuid> ring_order;
+    bool single_host = false; // extension (appended, optional): every ring member reported the same host token
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };

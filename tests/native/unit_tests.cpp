@@ -92,6 +92,80 @@ TEST(packet_complete) {
     EXPECT(q.tag == 9 && q.was_aborted);
 }
 
+// Appended extension fields (host token, single_host, shared-state IPC) are optional on decode, so packets from a
+// reference implementation (without them) still parse.
+TEST(packet_extensions_backward_compatible) {
+    proto::C2MRequestSessionRegistration r;
+    r.peer_group = 3;
+    r.p2p_port = 1;
+    r.ss_port = 2;
+    r.bm_port = 4;
+    r.host_token = "boot-id|host";
+    auto bytes = proto::encode_with_id(r);
+    auto full = proto::decode_payload<proto::C2MRequestSessionRegistration>(bytes.data() + 2, bytes.size() - 2);
+    EXPECT(full && full->host_token == "boot-id|host" && full->bm_port == 4);
+    const size_t legacy = 2 + 4 + 1 + 6; // id + group + bool + 3 ports: the reference layout
+    auto old = proto::decode_payload<proto::C2MRequestSessionRegistration>(bytes.data() + 2, legacy - 2);
+    EXPECT(old && old->host_token.empty() && old->peer_group == 3 && old->bm_port == 4);
+
+    proto::M2CP2PConnectionsEstablished e;
+    e.success = true;
+    e.ring_order = {Uuid::random(), Uuid::random()};
+    e.single_host = true;
+    bytes = proto::encode_with_id(e);
+    auto fe = proto::decode_payload<proto::M2CP2PConnectionsEstablished>(bytes.data() + 2, bytes.size() - 2);
+    EXPECT(fe && fe->single_host && fe->ring_order == e.ring_order);
+    auto oe = proto::decode_payload<proto::M2CP2PConnectionsEstablished>(bytes.data() + 2, bytes.size() - 3);
+    EXPECT(oe && !oe->single_host && oe->ring_order == e.ring_order);
+
+    proto::S2CSharedStateIpcResponse s;
+    s.revision = 9;
+    s.pid = 1234;
+    proto::SharedStateIpcEntry ie;
+    ie.key = "w";
+    ie.size_bytes = 4096;
+    ie.mode = 1;
+    ie.device = 2;
+    ie.offset = 512;
+    ie.raw_ptr = 0xdeadbeef;
+    ie.handle[0] = 7;
+    ie.handle[63] = 9;
+    s.entries.push_back(ie);
+    auto q = roundtrip(s);
+    EXPECT(q.revision == 9 && q.pid == 1234 && q.entries.size() == 1 && q.entries[0].key == "w" &&
+           q.entries[0].mode == 1 && q.entries[0].device == 2 && q.entries[0].offset == 512 &&
+           q.entries[0].raw_ptr == 0xdeadbeef && q.entries[0].handle[0] == 7 && q.entries[0].handle[63] == 9);
+    proto::C2SRequestSharedStateIpc rq;
+    rq.keys = {"a", "b"};
+    rq.host_token = "t";
+    rq.pid = 5;
+    auto rq2 = roundtrip(rq);
+    EXPECT(rq2.keys == rq.keys && rq2.host_token == "t" && rq2.pid == 5);
+}
+
+// CRC-32C split algebra used by the HIP kernel: raw(A || B) = shift(raw(A), |B|) ^ raw(B)
+TEST(crc32c_split_combine) {
+    std::vector<uint8_t> m(100003);
+    uint64_t x = 88172645463325252ull;
+    for (auto &b : m) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        b = static_cast<uint8_t>(x);
+    }
+    const uint32_t ref = kernels::crc32c_sw(m.data(), m.size());
+    EXPECT(kernels::crc32c_finish(kernels::crc32c_raw_update(0, m.data(), m.size()), m.size()) == ref);
+    for (size_t cut : {size_t(0), size_t(1), size_t(7), size_t(4096), size_t(65536), m.size() - 3, m.size()}) {
+        const uint32_t ra = kernels::crc32c_raw_update(0, m.data(), cut);
+        const uint32_t rb = kernels::crc32c_raw_update(0, m.data() + cut, m.size() - cut);
+        EXPECT(kernels::crc32c_finish(kernels::crc32c_shift(ra, m.size() - cut) ^ rb, m.size()) == ref);
+        // continuing from a state equals the split form
+        EXPECT(kernels::crc32c_raw_update(ra, m.data() + cut, m.size() - cut) ==
+               (kernels::crc32c_shift(ra, m.size() - cut) ^ rb));
+    }
+    EXPECT(kernels::crc32c_gf_mul(1u << 31, 0x12345678u) == 0x12345678u); // 1 * b = b
+}
+
 static double brute_force_tour(const std::vector<std::vector<double>> &c) {
     const int n = static_cast<int>(c.size());
     std::vector<int> perm(n - 1);
