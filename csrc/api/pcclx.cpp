@@ -27,7 +27,15 @@ PCCLX_EXPORT uint32_t pcclxSimpleHash(const void *p, size_t n, int on_device) {
     return be->simplehash(p, n, nullptr);
 }
 
+// CRC-32C of host or device memory (device: HIP kernel, device_crc32c). force_sw selects the host table path.
 PCCLX_EXPORT uint32_t pcclxCrc32c(const void *p, size_t n, int force_sw) {
+    DeviceBackend *be = device_backend();
+    DevPtrInfo pi{};
+    if (be && n > 0) be->pointer_info(p, pi);
+    if (pi.is_device) {
+        be->set_device(pi.device);
+        return device_crc32c(be, p, n, nullptr);
+    }
     return force_sw ? kernels::crc32c_sw(p, n) : kernels::crc32c(p, n);
 }
 
@@ -120,7 +128,7 @@ PCCLX_EXPORT int pcclxMultiGather(void *dst, const void *const *srcs, const size
 }
 
 // Event-timed device kernel micro-benchmark: returns average microseconds per call of `which`
-// (0 = reduce, 1 = simplehash, 2 = multi_reduce with `n` aliases of src, 3 = quantize u8 min-max).
+// (0 = reduce, 1 = simplehash, 2 = multi_reduce with `n` aliases of src, 3 = quantize u8 min-max, 4 = crc32c).
 PCCLX_EXPORT double pcclxBenchKernel(int which, void *dst, const void *src, size_t count, int dtype, int n, int iters) {
     DeviceBackend *be = device_backend();
     if (!be) return -1;
@@ -136,6 +144,7 @@ PCCLX_EXPORT double pcclxBenchKernel(int which, void *dst, const void *src, size
             case 1: be->simplehash(src, count * dtype_size(static_cast<DType>(dtype)), st); break;
             case 2: be->multi_reduce(&dst, 1, srcs.data(), n, count, static_cast<DType>(dtype), ReduceOp::Sum, st); break;
             case 3: be->quantize(dst, src, count, static_cast<DType>(dtype), DType::U8, qp, st); break;
+            case 4: device_crc32c(be, src, count * dtype_size(static_cast<DType>(dtype)), st); break;
             default: break;
         }
     };

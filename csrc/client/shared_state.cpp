@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
@@ -24,8 +25,18 @@ using namespace proto;
 
 static constexpr size_t kStagePiece = 32ull << 20;
 
+// PCCL_SHARED_STATE_HASH=crc32c makes this peer announce CRC-32C content hashes (HIP kernel for HBM tensors, SSE4.2
+// on the host) instead of simplehash. Every peer of a group must use the same setting: the master compares values.
+static HashType announced_hash_type() {
+    static const HashType t = [] {
+        const char *v = std::getenv("PCCL_SHARED_STATE_HASH");
+        return v && (std::strcmp(v, "crc32c") == 0 || std::strcmp(v, "crc32") == 0) ? HashType::Crc32 : HashType::Simple;
+    }();
+    return t;
+}
+
 bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
-    type = HashType::Simple;
+    type = announced_hash_type();
     if (e.bytes == 0) {
         hash = 0;
         return true;
@@ -33,6 +44,20 @@ bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
     DeviceBackend *be = device_backend();
     DevPtrInfo pi{};
     if (be) be->pointer_info(e.data, pi);
+    if (type == HashType::Crc32) {
+        if (pi.is_device) {
+            be->set_device(pi.device);
+            bool ok = true;
+            hash = device_crc32c(be, e.data, e.bytes, nullptr, &ok);
+            return ok;
+        }
+        if (e.device == DeviceType::Gpu) {
+            LOG(ERR) << "Shared state entry '" << e.key << "' declared as GPU tensor but pointer is not device memory";
+            return false;
+        }
+        hash = kernels::crc32c(e.data, e.bytes);
+        return true;
+    }
     if (pi.is_device) {
         be->set_device(pi.device);
         if (reinterpret_cast<uintptr_t>(e.data) % 16 != 0) {
@@ -58,16 +83,34 @@ bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
     return true;
 }
 
-static bool verify_hash(Client *, const SSEntry &e, uint64_t expected, HashType type, uint64_t actual_simple) {
-    if (type == HashType::Simple) return actual_simple == expected;
-    // CRC32 (accepted for compatibility; never produced by this implementation)
-    std::vector<uint8_t> host(e.bytes);
+// `actual` was computed with announced_hash_type(); recompute if the distributor's entry uses the other type
+static bool verify_hash(Client *, const SSEntry &e, uint64_t expected, HashType type, uint64_t actual,
+                        HashType actual_type) {
+    if (type == actual_type) return actual == expected;
     DeviceBackend *be = device_backend();
     DevPtrInfo pi{};
-    if (be) be->pointer_info(e.data, pi);
-    if (pi.is_device) be->memcpy_sync(host.data(), e.data, e.bytes);
-    else std::memcpy(host.data(), e.data, e.bytes);
-    return kernels::crc32c(host.data(), host.size()) == expected;
+    if (be && e.bytes > 0) be->pointer_info(e.data, pi);
+    if (type == HashType::Crc32) {
+        if (pi.is_device) {
+            be->set_device(pi.device);
+            bool ok = true;
+            const uint32_t c = device_crc32c(be, e.data, e.bytes, nullptr, &ok);
+            return ok && c == expected;
+        }
+        return kernels::crc32c(e.data, e.bytes) == expected;
+    }
+    if (pi.is_device) {
+        be->set_device(pi.device);
+        if (reinterpret_cast<uintptr_t>(e.data) % 16 != 0) {
+            Lease tmp(device_pool(), e.bytes, pi.device);
+            be->memcpy_sync(tmp.data(), e.data, e.bytes);
+            return be->simplehash(tmp.data(), e.bytes, nullptr) == expected;
+        }
+        return be->simplehash(e.data, e.bytes, nullptr) == expected;
+    }
+    Lease tmp(host_pool(), e.bytes);
+    std::memcpy(tmp.data(), e.data, e.bytes);
+    return kernels::simplehash_host(tmp.data(), e.bytes) == expected;
 }
 
 bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
@@ -157,7 +200,7 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         uint64_t h = 0;
         HashType t;
         if (!hash_entry(dst, h, t)) return false;
-        if (!verify_hash(this, dst, resp->expected_hashes[i], resp->expected_hash_types[i], h)) {
+        if (!verify_hash(this, dst, resp->expected_hashes[i], resp->expected_hash_types[i], h, t)) {
             LOG(ERR) << "Shared state sync: distributor sent corrupt content for " << dst.key;
             return false;
         }
@@ -218,10 +261,14 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 }
                 ok = src && be->memcpy_sync(dst->data, src, dst->bytes);
                 if (mapped) be->ipc_close(mapped);
-                if (!ok) LOG(ERR) << "Shared state sync: IPC copy of " << se.key << " failed";
+                if (!ok) {
+                    LOG(ERR) << "Shared state sync: IPC copy of " << se.key << " failed";
+                }
             } else {
                 ok = recv_stream_entry(fd, *dst);
-                if (!ok) LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
+                if (!ok) {
+                    LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
+                }
             }
             if (ok) {
                 info.rx_bytes += dst->bytes;
@@ -278,7 +325,9 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         std::vector<SockAddr> sources;
         if (!sockaddr_is_zero(resp->distributor)) sources.push_back(resp->distributor);
         for (const auto &f : resp->fallback_distributors) sources.push_back(f);
-        if (sources.empty()) LOG(ERR) << "Shared state sync: master assigned no distributor";
+        if (sources.empty()) {
+            LOG(ERR) << "Shared state sync: master assigned no distributor";
+        }
         for (const auto &src : sources) {
             info.rx_bytes = 0;
             if ((fetched = fetch_from(src))) break;

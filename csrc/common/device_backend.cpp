@@ -2,10 +2,13 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <vector>
 
+#include "../kernels/host_kernels.hpp"
 #include "log.hpp"
 
 namespace pccl {
@@ -53,5 +56,52 @@ DeviceBackend *device_backend() {
 }
 
 bool device_backend_available() { return device_backend() != nullptr; }
+
+uint32_t device_crc32c(DeviceBackend *be, const void *dev_ptr, size_t n, DevStream s, bool *ok) {
+    constexpr size_t kChunk = 64, kTile = 256 * kChunk, kMaxPartials = 1024;
+    static const std::vector<uint32_t> tables = [] { // 8 slicing tables + tile-shift table, 12 x 256 words
+        std::vector<uint32_t> t(12 * 256);
+        const uint32_t(*sl)[256] = kernels::crc32c_tables();
+        for (int k = 0; k < 8; ++k)
+            for (int b = 0; b < 256; ++b) t[k * 256 + b] = sl[k][b];
+        const uint32_t m = kernels::crc32c_x8n(kTile);
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b) t[(8 + k) * 256 + b] = kernels::crc32c_gf_mul(m, b << (8 * k));
+        return t;
+    }();
+    static const std::vector<uint32_t> levels = [] {
+        std::vector<uint32_t> l(8);
+        for (int k = 0; k < 8; ++k) l[k] = kernels::crc32c_x8n(kChunk << k);
+        return l;
+    }();
+    if (ok) *ok = true;
+    if (n == 0) return 0;
+    const auto *p = static_cast<const uint8_t *>(dev_ptr);
+    const size_t head = std::min(n, (16 - reinterpret_cast<uintptr_t>(p) % 16) % 16);
+    const size_t n_tiles = (n - head) / kTile;
+    const size_t main = n_tiles * kTile;
+    const size_t tail = n - head - main;
+    std::vector<uint8_t> edge(head + tail);
+    bool good = true;
+    if (head) good = be->memcpy_sync(edge.data(), p, head);
+    if (good && tail) good = be->memcpy_sync(edge.data() + head, p + head + main, tail);
+    uint32_t raw = kernels::crc32c_raw_update(0, edge.data(), head);
+    if (good && n_tiles) {
+        std::vector<uint32_t> part(kMaxPartials);
+        size_t np = 0, tpw = 0;
+        good = be->crc32c_tiles(p + head, n_tiles, tables.data(), levels.data(), part.data(), part.size(), np, tpw, s);
+        uint32_t main_raw = 0;
+        const uint32_t full = kernels::crc32c_x8n(tpw * kTile);
+        for (size_t g = 0; good && g < np; ++g) {
+            const size_t tiles = std::min(tpw, n_tiles - g * tpw);
+            const uint32_t m = tiles == tpw ? full : kernels::crc32c_x8n(tiles * kTile);
+            main_raw = kernels::crc32c_gf_mul(m, main_raw) ^ part[g];
+        }
+        raw = kernels::crc32c_shift(raw, main) ^ main_raw;
+    }
+    raw = kernels::crc32c_raw_update(raw, edge.data() + head, tail);
+    if (!good && ok) *ok = false;
+    return kernels::crc32c_finish(raw, n);
+}
 
 } // namespace pccl

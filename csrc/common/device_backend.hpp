@@ -78,6 +78,12 @@ public:
 
     // Simple hash of device memory (bit-identical to kernels::simplehash_host). Synchronous.
     virtual uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) = 0;
+    // CRC-32C kernel pass over n_tiles 16 KiB tiles at a 16-byte aligned device pointer. Returns one raw CRC partial
+    // per workgroup (each covers tiles_per_wg tiles, the last one the remainder). `tables` = 12 x 256 words (8 slicing
+    // tables + the 16 KiB tile-shift table), `levels` = the 8 tree multipliers. Synchronous. Use device_crc32c().
+    virtual bool crc32c_tiles(const void *dev_ptr, size_t n_tiles, const uint32_t *tables, const uint32_t *levels,
+                              uint32_t *partials, size_t max_partials, size_t &n_partials, size_t &tiles_per_wg,
+                              DevStream s) = 0;
     // Fills device memory with the reference test pattern (random_init_kernel of the reference tests).
     virtual bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) = 0;
 
@@ -91,6 +97,10 @@ public:
 // Returns the process-wide backend (nullptr if HIP is unavailable). Loaded lazily and thread-safely.
 DeviceBackend *device_backend();
 bool device_backend_available();
+
+// Standard CRC-32C of device memory: HIP kernel over the 16-byte aligned 16 KiB tiles, host-side fold of the
+// workgroup partials plus the unaligned head and the tail (bit-identical to kernels::crc32c). `ok` reports failure.
+uint32_t device_crc32c(DeviceBackend *be, const void *dev_ptr, size_t n_bytes, DevStream s, bool *ok = nullptr);
 
 } // namespace pccl
 

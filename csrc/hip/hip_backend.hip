@@ -2,6 +2,7 @@
 // Kernel families live in hip_reduce.hip / hip_quant.hip / hip_ipc.hip / hip_hash.hip (see kernels.hpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -183,6 +184,37 @@ public:
         }
         return out[0];
     }
+    bool crc32c_tiles(const void *dev_ptr, size_t n_tiles, const uint32_t *tables, const uint32_t *levels,
+                      uint32_t *partials, size_t max_partials, size_t &n_partials, size_t &tiles_per_wg,
+                      DevStream s) override {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return false;
+        void *tab = nullptr;
+        {
+            std::lock_guard l(scratch_mtx_);
+            auto it = crc_tables_.find(dev);
+            if (it == crc_tables_.end()) {
+                if (!HIP_OK(hipMalloc(&tab, 12 * 256 * sizeof(uint32_t))) ||
+                    !HIP_OK(hipMemcpy(tab, tables, 12 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice)))
+                    return false;
+                crc_tables_[dev] = tab;
+            } else {
+                tab = it->second;
+            }
+        }
+        Scratch &sc = scratch_for(s);
+        std::lock_guard l(*sc.mtx);
+        auto *part = reinterpret_cast<uint32_t *>(sc.dev); // 16 KiB of scratch: up to 4096 partials
+        size_t grid = 0;
+        const auto st = static_cast<hipStream_t>(s);
+        if (!hipk::launch_crc32c(dev_ptr, n_tiles, tab, levels, part, std::min<size_t>(max_partials, 4096), grid,
+                                 tiles_per_wg, st) ||
+            !HIP_OK(hipMemcpyAsync(partials, part, grid * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
+            !HIP_OK(hipStreamSynchronize(st)))
+            return false;
+        n_partials = grid;
+        return true;
+    }
     bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) override {
         return hipk::launch_test_pattern(dev_ptr, n_u64, static_cast<hipStream_t>(s));
     }
@@ -213,6 +245,7 @@ private:
     int n_devices_ = 0;
     std::mutex scratch_mtx_;
     std::map<DevStream, Scratch> scratch_;
+    std::map<int, void *> crc_tables_; // per device, uploaded on first use
 };
 
 } // namespace

@@ -565,6 +565,84 @@ __global__ __launch_bounds__(kBlock) void k_hash_final(const uint32_t *__restric
     }
 }
 
+// ---------------------------------------------------------------- CRC-32C
+// Split CRC (csrc/kernels/host_kernels.hpp): thread t of a workgroup owns the 64-byte chunk t of every 16 KiB tile of
+// the workgroup's contiguous range (a wave reads 4 KiB contiguously). Per tile it computes the chunk's raw CRC with
+// slicing-by-8 LDS tables and folds it into its accumulator, which is first moved 16 KiB further down the message
+// (multiplication by the constant x^(8*16384) as 4 LDS table lookups). The 256 accumulators are then combined in an
+// 8-level LDS tree (shift by 64 * 2^k bytes = one GF(2) multiply by a host-computed constant). The host folds the
+// per-workgroup partials and the unaligned head / tail bytes, then applies the standard init / final inversion.
+constexpr int kCrcChunk = 64;
+constexpr int kCrcTile = kBlock * kCrcChunk; // 16 KiB
+struct CrcTables {
+    uint32_t slice[8][256]; // slice[k][b]: raw CRC of byte b followed by k zero bytes
+    uint32_t tile[4][256];  // tile[k][b]: (b << 8k) * x^(8 * kCrcTile) mod P
+};
+struct CrcLevels {
+    uint32_t m[8]; // x^(8 * kCrcChunk * 2^k) mod P
+};
+
+__device__ __forceinline__ uint32_t crc_gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+        p ^= (0u - ((a >> i) & 1u)) & b;
+        b = (b >> 1) ^ (0x82F63B78u & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+template<int Unused = 0>
+__global__ __launch_bounds__(kBlock) void k_crc32c(const uint8_t *__restrict__ data, size_t n_tiles,
+                                                   size_t tiles_per_wg, const CrcTables *__restrict__ tabs,
+                                                   CrcLevels lv, uint32_t *__restrict__ partial) {
+    __shared__ uint32_t sl[8][256];
+    __shared__ uint32_t st[4][256];
+    __shared__ uint32_t red[kBlock];
+    const int t = threadIdx.x;
+    for (int i = t; i < 8 * 256; i += kBlock) (&sl[0][0])[i] = (&tabs->slice[0][0])[i];
+    for (int i = t; i < 4 * 256; i += kBlock) (&st[0][0])[i] = (&tabs->tile[0][0])[i];
+    __syncthreads();
+    const size_t t0 = static_cast<size_t>(blockIdx.x) * tiles_per_wg;
+    const size_t t1 = t0 + tiles_per_wg < n_tiles ? t0 + tiles_per_wg : n_tiles;
+    uint32_t acc = 0;
+    uint4 cur[4], nxt[4];
+    auto load = [&](size_t tile, uint4 *v) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(data + tile * kCrcTile + static_cast<size_t>(t) * kCrcChunk);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = nt_load(p + k);
+    };
+    if (t0 < t1) load(t0, cur);
+    for (size_t tile = t0; tile < t1; ++tile) {
+        if (tile + 1 < t1) load(tile + 1, nxt); // next tile's loads in flight during this tile's table work
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t w[2] = {static_cast<uint64_t>(cur[k].x) | (static_cast<uint64_t>(cur[k].y) << 32),
+                                   static_cast<uint64_t>(cur[k].z) | (static_cast<uint64_t>(cur[k].w) << 32)};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint64_t v = w[h] ^ c;
+                c = sl[7][v & 0xff] ^ sl[6][(v >> 8) & 0xff] ^ sl[5][(v >> 16) & 0xff] ^ sl[4][(v >> 24) & 0xff] ^
+                    sl[3][(v >> 32) & 0xff] ^ sl[2][(v >> 40) & 0xff] ^ sl[1][(v >> 48) & 0xff] ^ sl[0][v >> 56];
+            }
+        }
+        acc = st[0][acc & 0xff] ^ st[1][(acc >> 8) & 0xff] ^ st[2][(acc >> 16) & 0xff] ^ st[3][acc >> 24];
+        acc ^= c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    }
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int s = 1 << k;
+        if ((t & (2 * s - 1)) == 0) red[t] = crc_gf_mul(red[t], lv.m[k]) ^ red[t + s];
+        __syncthreads();
+    }
+    if (t == 0) partial[blockIdx.x] = red[0];
+}
+
 // reference test pattern (ccoip/tests/unit_tests/simple_hash/simplehash_cpu_test.cu:17-23), launched <<<8, 256>>>
 template<int Unused = 0>
 __global__ void k_test_pattern(uint64_t *data, size_t N) {

@@ -38,5 +38,8 @@ bool launch_outer_sgd(float *outer, float *mom, const float *pg, void *local, si
 // hip_hash.hip
 bool launch_simplehash(const void *dev_ptr, size_t n_bytes, uint32_t *partial_scratch, uint32_t *out, hipStream_t s);
 bool launch_test_pattern(void *dev_ptr, size_t n_u64, hipStream_t s);
+// tables: 12 x 256 words in device memory (CrcTables layout); returns the grid size / tiles per workgroup used
+bool launch_crc32c(const void *dev_ptr, size_t n_tiles, const void *tables_dev, const uint32_t *levels,
+                   uint32_t *partial_dev, size_t max_partials, size_t &grid, size_t &tiles_per_wg, hipStream_t s);
 
 } // namespace pccl::hipk

@@ -47,7 +47,10 @@ def simplehash(t: torch.Tensor) -> int:
 
 
 def crc32c(t: torch.Tensor, force_software: bool = False) -> int:
-    assert t.device.type == "cpu" and t.is_contiguous()
+    """CRC-32C (Castagnoli) of a contiguous tensor: host SSE4.2 / table path, or the HIP kernel for GPU tensors."""
+    assert t.is_contiguous()
+    if t.device.type != "cpu":
+        _on_device(t)
     return int(C.pcclxCrc32c(t.data_ptr(), t.numel() * t.element_size(), int(force_software)))
 
 
@@ -122,8 +125,8 @@ def multi_gather(dst: torch.Tensor, srcs: Sequence[torch.Tensor], offsets: Seque
 
 
 def bench_kernel(which: str, dst: torch.Tensor, src: torch.Tensor, n: int = 1, iters: int = 20) -> float:
-    """Average microseconds per launch of a device kernel ('reduce', 'hash', 'multi_reduce', 'quantize')."""
-    w = {"reduce": 0, "hash": 1, "multi_reduce": 2, "quantize": 3}[which]
+    """Average microseconds per launch of a device kernel ('reduce', 'hash', 'multi_reduce', 'quantize', 'crc32c')."""
+    w = {"reduce": 0, "hash": 1, "multi_reduce": 2, "quantize": 3, "crc32c": 4}[which]
     _on_device(src)
     return float(C.pcclxBenchKernel(w, dst.data_ptr(), src.data_ptr(), src.numel(), WIRE_DTYPE[src.dtype], n, iters))
 

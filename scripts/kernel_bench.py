@@ -53,7 +53,11 @@ def main():
         row("dequant_reduce fp8->bf16 sum (pccl)",
             timeit(lambda: K.dequant_reduce(x, q8, m8, "min_max", "sum"), a.iters), n + 2 * n * 2)
     u8 = y.view(torch.uint8)
+    dst2 = [torch.empty_like(x), torch.empty_like(x)]
     row("simplehash (pccl)", timeit(lambda: K.simplehash(u8), a.iters), n * 2)
+    row("crc32c (pccl, tiled kernel + host fold)", timeit(lambda: K.crc32c(u8), a.iters), n * 2)
+    row("multi_reduce 2 srcs -> 2 dsts bf16 (pccl push kernel)",
+        timeit(lambda: K.multi_reduce([x, y], "sum", out=dst2[0], outs=[dst2[1]]), a.iters), 4 * n * 2)
     srcs = [bf() for _ in range(8)]
     m = n // 8
     shards = [s[:m] for s in srcs]

@@ -13,8 +13,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(script, *args, timeout=300):
+def _run(script, *args, timeout=300, extra_env=None):
     env = dict(os.environ)
+    env.update(extra_env or {})
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", script), *args], env=env,
@@ -32,6 +33,14 @@ def test_shared_state_catch_up(device, transport):
     assert r["content_ok"] and r["adopted_revision"] == 3
     assert r["joiner_rx_bytes"] == r["bytes"] == 3000001 * 4
     assert r["trainer_tx_bytes"] == r["bytes"]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_shared_state_catch_up_crc32c(device):
+    """PCCL_SHARED_STATE_HASH=crc32c: peers announce CRC-32C content hashes (HIP kernel for HBM tensors)."""
+    r = _run("shared_state_sync.py", "--params", "1000003", "--tensors", "2", "--device", device,
+             extra_env={"PCCL_SHARED_STATE_HASH": "crc32c"})
+    assert r["content_ok"] and r["joiner_rx_bytes"] == r["bytes"]
 
 
 def test_basic_reduce():

@@ -36,6 +36,15 @@ def test_device_hash_equals_host(hip, n):
     assert K.simplehash(x.to(hip)) == K.simplehash(x)
 
 
+@pytest.mark.parametrize("n", [1, 15, 16, 16384, 16384 * 5 + 3, (1 << 22) + 77, 154533888])
+@pytest.mark.parametrize("offset", [0, 5])
+def test_device_crc32c_equals_host(hip, n, offset):
+    """HIP CRC-32C (tiled kernel + host fold) == the host SSE4.2 / table implementation, any length and alignment."""
+    x = torch.from_numpy(lcg_bytes(n + offset, seed=n % 1000))
+    expect = K.crc32c(x[offset:].clone())
+    assert K.crc32c(x.to(hip)[offset:]) == expect
+
+
 @pytest.mark.parametrize("dtype", FLOATS + INTS)
 @pytest.mark.parametrize("op", ["sum", "prod", "max", "min", "set"])
 @pytest.mark.parametrize("n", [1, 4099, (1 << 20) + 3])
