@@ -114,7 +114,7 @@ bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
         std::lock_guard lock(ops_mtx_);
         auto it = ops_.find(req.tag);
         if (it != ops_.end()) {
-            if (!it->second->done.load()) return false; // tag in use
+            if (!it->second->joined.load()) return false; // tag in use until its op has been awaited
             ops_.erase(it);
         }
         op = std::make_shared<OpState>();
@@ -245,6 +245,7 @@ bool Client::join_async_reduce(uint64_t tag) {
         op = it->second;
     }
     op->wait();
+    op->joined.store(true);
     if (!op->success) {
         // Re-establish the ring once per connection revision: every peer sees the same failures, so every peer
         // performs exactly one establishment round (several concurrent failed ops must not cascade into more).

@@ -410,7 +410,7 @@ bool Client::optimize_topology() {
 bool Client::any_collective_running() {
     std::lock_guard lock(ops_mtx_);
     for (auto &[_, op] : ops_)
-        if (!op->done.load()) return true;
+        if (!op->joined.load()) return true; // started and not yet awaited (reference semantics)
     return false;
 }
 

@@ -132,6 +132,9 @@ private:
         std::mutex m;
         std::condition_variable cv;
         std::atomic<bool> done{false};
+        // awaited by the application; until then the op counts as running (reference ccoip_client_state.cpp:
+        // a tag stays in running_collective_coms_ops_tags until joinAsyncCollectiveOp)
+        std::atomic<bool> joined{false};
         void wait() {
             std::unique_lock l(m);
             cv.wait(l, [this] { return done.load(); });
