@@ -42,7 +42,8 @@ bool host_outer_sgd(float *outer, float *mom, const float *pg, void *local, size
 // CRC-32C (Castagnoli). Uses SSE4.2 when available (and not spoofed off), otherwise slicing-by-8 tables.
 uint32_t crc32c(const void *data, size_t n_bytes);
 uint32_t crc32c_sw(const void *data, size_t n_bytes);
-uint32_t crc32c_hw(const void *data, size_t n_bytes);
+uint32_t crc32c_hw(const void *data, size_t n_bytes);  // one crc32q chain
+uint32_t crc32c_hw3(const void *data, size_t n_bytes); // three interleaved chains + table-driven combine (default)
 void crc32c_spoof_no_hw(bool no_hw); // test hook: force the software path
 bool crc32c_has_hw();
 

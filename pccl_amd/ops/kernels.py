@@ -46,12 +46,14 @@ def simplehash(t: torch.Tensor) -> int:
     return int(C.pcclxSimpleHash(t.data_ptr(), t.numel() * t.element_size(), _on_device(t)))
 
 
-def crc32c(t: torch.Tensor, force_software: bool = False) -> int:
-    """CRC-32C (Castagnoli) of a contiguous tensor: host SSE4.2 / table path, or the HIP kernel for GPU tensors."""
+def crc32c(t: torch.Tensor, force_software: bool = False, single_chain: bool = False) -> int:
+    """CRC-32C (Castagnoli) of a contiguous tensor: host SSE4.2 (3 interleaved chains; ``single_chain`` selects the
+    one-chain variant) or table path (``force_software``), or the HIP kernel for GPU tensors."""
     assert t.is_contiguous()
     if t.device.type != "cpu":
         _on_device(t)
-    return int(C.pcclxCrc32c(t.data_ptr(), t.numel() * t.element_size(), int(force_software)))
+    mode = 1 if force_software else (2 if single_chain else 0)
+    return int(C.pcclxCrc32c(t.data_ptr(), t.numel() * t.element_size(), mode))
 
 
 def crc32c_has_hw() -> bool:

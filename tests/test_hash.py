@@ -47,12 +47,13 @@ def test_crc32c_check_value():
     assert K.crc32c(t, force_software=True) == 0xE3069283
 
 
-@pytest.mark.parametrize("n", [1, 7, 8, 63, 64, 65, 1000, 4097, 100003])
+@pytest.mark.parametrize("n", [1, 7, 8, 63, 64, 65, 1000, 4097, 100003, 3 * 8192, 3 * 8192 + 5, 1000003])
 def test_crc32c_hw_vs_sw_vs_bytewise(n):
     data = lcg_bytes(n, seed=n)
     t = torch.from_numpy(data)
     sw = K.crc32c(t, force_software=True)
     assert sw == K.crc32c(t)
+    assert sw == K.crc32c(t, single_chain=True)
     if n <= 4097:
         assert sw == _crc32c_bytewise(data.tobytes())
     assert sw != zlib.crc32(data.tobytes()) or n == 0  # Castagnoli, not IEEE
