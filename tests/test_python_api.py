@@ -1,0 +1,105 @@
+"""Python API lifecycle tests (reference python/tests/unit_tests/pccl_test.py), using a free port per test instead of
+the fixed 48148 so that tests can run side by side, plus the `import pccl` alias the reference's users write."""
+import gc
+
+import numpy as np
+import pytest
+
+from pccl_amd.utils import free_port
+
+
+def test_import_lib():
+    import pccl  # noqa: F401  (alias package: the reference's import name)
+    import pccl_amd  # noqa: F401
+
+
+def test_alias_exports_reference_names():
+    import pccl
+    for name in ("Communicator", "MasterNode", "SharedState", "TensorInfo", "ReduceOp", "Attribute", "DataType",
+                 "DeviceType", "QuantizationAlgorithm", "QuantizationOptions", "ReduceDescriptor",
+                 "ReduceOperandDescriptor", "ReduceOpDescriptor", "SharedStateSyncStrategy", "DistributionHint",
+                 "PCCLError", "Result", "ReduceInfo", "AsyncReduceHandle", "SharedStateSyncInfo"):
+        assert hasattr(pccl, name), name
+
+
+def _master():
+    import pccl
+    addr = f"127.0.0.1:{free_port()}"
+    m = pccl.MasterNode(listen_address=addr)
+    m.run()
+    return m, addr
+
+
+def test_master_node_run():
+    m, _ = _master()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_communicator():
+    import pccl
+    m, addr = _master()
+    c = pccl.Communicator(addr, 0)
+    c.connect()
+    assert c.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE) == 1
+    c.destroy()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_communicator_destructor_with_connect():
+    import pccl
+    m, addr = _master()
+
+    def connect():
+        c = pccl.Communicator(addr, 0)
+        c.connect()
+
+    connect()
+    gc.collect()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_communicator_destructor_without_connect():
+    import pccl
+    m, addr = _master()
+
+    def create():
+        pccl.Communicator(addr, 0)
+
+    create()
+    gc.collect()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_communicator_update_topology_without_connect():
+    import pccl
+    m, addr = _master()
+    c = pccl.Communicator(addr, 0)
+    with pytest.raises(pccl.PCCLError):
+        c.update_topology()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_all_reduce_single_peer_too_few_peers():
+    """numpy_only_test.py / pytorch_only_test.py: a lone peer's all-reduce raises PCCLError(TooFewPeers)."""
+    import pccl
+    m, addr = _master()
+    c = pccl.Communicator(addr, 0)
+    c.connect()
+    x = np.ones(8, dtype=np.float32)
+    with pytest.raises(pccl.PCCLError) as e:
+        c.all_reduce(x, np.empty_like(x), op=pccl.ReduceOp.SUM)
+    assert e.value.result == pccl.Result.TOO_FEW_PEERS
+    c.destroy()
+    m.interrupt()
+    m.await_termination()
+
+
+def test_build_info():
+    import pccl
+    info = pccl.build_info()
+    assert "has_hip_support" in info and "has_cuda_support" in info
