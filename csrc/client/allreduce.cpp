@@ -137,37 +137,46 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     bool success = false, abort_seen = false;
     uint64_t seq = 0;
     bool commenced = false;
+    uint8_t agreed = 0;
+    // the ring cannot change while this op runs (re-establishment waits for running ops), so the view taken here
+    // is the one the op executes on
+    auto rv = ring_view(0);
+    DevPtrInfo si{}, di{};
+    DeviceBackend *be = device_backend();
+    if (be) {
+        be->pointer_info(op->req.src, si);
+        be->pointer_info(op->req.dst, di);
+    }
+    const bool device = si.is_device && di.is_device && si.device == di.device;
     {
         C2MCollectiveCommsInitiate init;
         init.tag = tag;
         init.count = op->req.count;
         init.data_type = op->req.dtype;
         init.op = op->req.op;
+        if (rv && rv->hier && device) init.flags |= kCollFlagHierarchical;
         if (master_.send(init)) {
             auto c = master_.receive<M2CCollectiveCommsCommence>(
                 [tag](const M2CCollectiveCommsCommence &p) { return p.tag == tag; });
             if (c) {
                 seq = c->seq_nr;
+                agreed = c->flags;
                 commenced = true;
                 trace_mark("commence");
             }
         }
     }
     if (commenced) {
-        auto rv = ring_view(seq);
         if (rv && rv->ring.size() >= 2) {
             op->world = static_cast<uint32_t>(rv->ring.size());
-            // classify buffers
-            DevPtrInfo si{}, di{};
-            DeviceBackend *be = device_backend();
-            if (be) {
-                be->pointer_info(op->req.src, si);
-                be->pointer_info(op->req.dst, di);
-            }
-            const bool device = si.is_device && di.is_device && si.device == di.device;
             std::pair<bool, bool> r{false, false};
             bool done = false;
-            if (rv->arena) {
+            if ((agreed & kCollFlagHierarchical) && rv->hier) {
+                // every participant announced the capability (master AND): IPC inside hosts, TCP ring across them
+                r = hier_reduce(*op, *rv, seq, di.device);
+                done = true;
+                if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::Hierarchical);
+            } else if (rv->arena) {
                 // every peer of an intra-node ring votes; the xGMI path runs only if all buffers are on GPUs
                 const int decision = rv->arena->vote(*this, *op, seq, device, device ? di.device : -1);
                 trace_mark("vote");
@@ -225,10 +234,10 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     }
     if (current_trace()) {
         trace.mark("complete");
-        static const char *names[] = {"none", "host_ring", "device_ring", "ipc"};
+        static const char *names[] = {"none", "host_ring", "device_ring", "ipc", "hier", "?", "?", "?"};
         std::fprintf(stderr, "[pccl-trace] tag %llu seq %llu bytes %zu world %u path %s %s%s\n",
                      static_cast<unsigned long long>(tag), static_cast<unsigned long long>(seq),
-                     op->req.count * dtype_size(op->req.dtype), op->world, names[last_path_.load() & 3],
+                     op->req.count * dtype_size(op->req.dtype), op->world, names[last_path_.load() & 7],
                      ok ? "ok" : "FAILED", trace.str().c_str());
         current_trace() = nullptr;
     }
@@ -567,16 +576,16 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     auto aborted = [&] { return abort_received(q.tag); };
 
     Lease backup;
-    if (q.src == q.dst) {
+    if (q.src == q.dst && !q.scratch) {
         backup = Lease(device_pool(), bytes, device);
         if (!backup.ok()) return {false, false};
         be->memcpy_async(backup.data(), q.src, bytes, st);
-    } else {
+    } else if (q.src != q.dst) {
         be->memcpy_async(dst, q.src, bytes, st);
     }
     auto restore = [&] {
         be->stream_sync(st);
-        if (q.src == q.dst) {
+        if (q.src == q.dst && !q.scratch) {
             be->memcpy_async(dst, backup.data(), bytes, st);
             be->stream_sync(st);
         }

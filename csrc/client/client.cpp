@@ -197,14 +197,44 @@ Client::EstablishResult Client::establish() {
     n_groups_ = info->num_distinct_peer_groups;
     largest_group_ = info->largest_peer_group_world_size;
 
-    std::vector<PeerInfo> neighbors;
+    std::vector<PeerInfo> neighbors, tx_targets;
+    std::vector<ExtraPeer> extras;
     {
         std::lock_guard lock(p2p_mtx_);
         if (!info->unchanged) neighbors_ = info->all_peers;
+        extras_ = info->extra_peers;
         neighbors = neighbors_;
+        extras = extras_;
+    }
+    tx_targets = neighbors;
+    std::vector<PeerInfo> extra_tx; // inter-host ring partners: connection failures only disable the hierarchy
+    for (const auto &e : extras) {
+        const bool dup = std::any_of(neighbors.begin(), neighbors.end(),
+                                     [&](const PeerInfo &p) { return p.peer_uuid == e.peer.peer_uuid; });
+        if ((e.role & kExtraTx) && !dup) extra_tx.push_back(e.peer);
     }
     bool ok = true;
     std::vector<Uuid> failed;
+    for (const auto &n : extra_tx) {
+        bool healthy = false;
+        {
+            std::lock_guard lock(p2p_mtx_);
+            auto it = tx_.find(n.peer_uuid);
+            if (it != tx_.end() && it->second.size() == cfg_.pool_size)
+                healthy = std::all_of(it->second.begin(), it->second.end(), [](auto &c) { return c && c->is_open(); });
+        }
+        if (healthy) continue;
+        std::vector<std::shared_ptr<net::MuxConn>> pool;
+        if (!connect_pool(n, pool)) {
+            LOG(WARN) << "P2P: inter-host ring partner " << n.peer_uuid.str() << " unreachable (hierarchy disabled)";
+            continue;
+        }
+        std::lock_guard lock(p2p_mtx_);
+        auto &slot = tx_[n.peer_uuid];
+        for (auto &c : slot)
+            if (c) c->interrupt();
+        slot = std::move(pool);
+    }
     for (const auto &n : neighbors) {
         bool healthy = false;
         {
@@ -232,8 +262,12 @@ Client::EstablishResult Client::establish() {
         auto is_nb = [&](const Uuid &u) {
             return std::any_of(neighbors.begin(), neighbors.end(), [&](const PeerInfo &p) { return p.peer_uuid == u; });
         };
+        auto is_extra = [&](const Uuid &u, uint8_t role) {
+            return std::any_of(extras.begin(), extras.end(),
+                               [&](const ExtraPeer &e) { return e.peer.peer_uuid == u && (e.role & role); });
+        };
         for (auto it = tx_.begin(); it != tx_.end();) {
-            if (!is_nb(it->first)) {
+            if (!is_nb(it->first) && !is_extra(it->first, kExtraTx)) {
                 for (auto &c : it->second)
                     if (c) c->interrupt();
                 it = tx_.erase(it);
@@ -242,7 +276,7 @@ Client::EstablishResult Client::establish() {
             }
         }
         for (auto it = rx_.begin(); it != rx_.end();) {
-            if (!is_nb(it->first)) {
+            if (!is_nb(it->first) && !is_extra(it->first, kExtraRx)) {
                 for (auto &c : it->second)
                     if (c) c->interrupt();
                 it = rx_.erase(it);
@@ -274,7 +308,8 @@ Client::EstablishResult Client::establish() {
     // exclusivity), or the master reports that every ring member registered with this host's identity; the ring can
     // then rendezvous in shared memory and exchange device buffers over xGMI.
     std::shared_ptr<IpcArena> arena;
-    const bool one_host = sockaddr_is_loopback(cfg_.master) || resp->single_host;
+    // (a master that predates the host extension: a loopback master implies one host)
+    const bool one_host = resp->has_host_info ? resp->single_host : sockaddr_is_loopback(cfg_.master);
     if (resp->ring_order.size() >= 2 && one_host && !env_flag("PCCL_DISABLE_IPC", false) &&
         device_backend_available()) {
         if (old_arena && old_arena->matches(resp->ring_order)) {
@@ -283,9 +318,48 @@ Client::EstablishResult Client::establish() {
             arena = IpcArena::create(*this, resp->ring_order, cfg_.master.port, cfg_.peer_group);
         }
     }
+    // Hierarchical layout across hosts: IPC arena over my host's members + the inter-host ring of my local rank
+    std::shared_ptr<HierState> hier;
+    const auto &host_of = resp->host_of;
+    if (host_of.size() == resp->ring_order.size() && host_of.size() >= 4 && !env_flag("PCCL_DISABLE_IPC", false) &&
+        env_flag("PCCL_HIERARCHICAL", true) && device_backend_available()) {
+        const auto &ring = resp->ring_order;
+        const size_t me = static_cast<size_t>(std::find(ring.begin(), ring.end(), uuid_) - ring.begin());
+        if (me < ring.size()) {
+            auto h = std::make_shared<HierState>();
+            h->hosts = *std::max_element(host_of.begin(), host_of.end()) + 1;
+            h->host = host_of[me];
+            std::vector<Uuid> local;
+            for (size_t k = 0; k < ring.size(); ++k) {
+                if (host_of[k] != h->host) continue;
+                if (k == me) h->local_rank = local.size();
+                local.push_back(ring[k]);
+            }
+            h->local = local.size();
+            std::vector<std::vector<Uuid>> per_host(h->hosts);
+            for (size_t k = 0; k < ring.size(); ++k) per_host[host_of[k]].push_back(ring[k]);
+            bool valid = h->local >= 2 && h->hosts >= 2;
+            for (const auto &ph : per_host) valid = valid && ph.size() == h->local;
+            if (valid) {
+                for (const auto &ph : per_host) h->host_ring.push_back(ph[h->local_rank]);
+                std::shared_ptr<HierState> prev;
+                {
+                    std::lock_guard lock(p2p_mtx_);
+                    prev = hier_;
+                }
+                if (prev && prev->arena && prev->arena->matches(local)) {
+                    h->arena = prev->arena;
+                } else {
+                    h->arena = IpcArena::create(*this, local, cfg_.master.port, cfg_.peer_group);
+                }
+                if (h->arena) hier = h;
+            }
+        }
+    }
     {
         std::lock_guard lock(p2p_mtx_);
         arena_ = arena;
+        hier_ = hier;
     }
     return EstablishResult::Success;
 }
@@ -350,6 +424,18 @@ std::optional<Client::RingView> Client::ring_view(uint64_t seq) {
     if (t == tx_.end() || r == rx_.end() || t->second.empty() || r->second.empty()) return std::nullopt;
     rv.tx = t->second;
     rv.rx = r->second;
+    if (hier_) {
+        const auto &hr = hier_->host_ring;
+        const Uuid hnext = hr[(hier_->host + 1) % hr.size()];
+        const Uuid hprev = hr[(hier_->host + hr.size() - 1) % hr.size()];
+        auto ht = tx_.find(hnext);
+        auto hrx = rx_.find(hprev);
+        if (ht != tx_.end() && hrx != rx_.end() && !ht->second.empty() && !hrx->second.empty()) {
+            rv.hier = hier_;
+            rv.htx = ht->second;
+            rv.hrx = hrx->second;
+        }
+    }
     (void)seq;
     return rv;
 }

@@ -67,6 +67,7 @@ struct ReduceRequest {
     QuantAlgo qalgo = QuantAlgo::None;
     ReduceOp op = ReduceOp::Sum;
     uint64_t tag = 0;
+    bool scratch = false; // internal: dst is library scratch, no abort backup needed (hierarchical inner ring)
 };
 
 class IpcArena; // intra-node shared-memory + IPC rendezvous (ipc.cpp)
@@ -153,12 +154,22 @@ private:
         uint32_t world = 0;
     };
 
+    // Hierarchical layout (master's host_of extension): hosts x local ranks. The host-local peers share an IPC arena;
+    // the peers with my local rank on every host form the inter-host ring (extra TX / RX pools).
+    struct HierState {
+        size_t hosts = 0, local = 0;   // H, L
+        size_t host = 0, local_rank = 0;
+        std::vector<Uuid> host_ring;   // the member with my local rank on host 0 .. H-1
+        std::shared_ptr<IpcArena> arena; // over my host's members, in ring order
+    };
     struct RingView { // immutable snapshot used by an op thread
         std::vector<Uuid> ring;
         size_t rank = 0;
         std::vector<std::shared_ptr<net::MuxConn>> tx; // pool to next
         std::vector<std::shared_ptr<net::MuxConn>> rx; // pool from prev
         std::shared_ptr<IpcArena> arena;
+        std::shared_ptr<HierState> hier;                    // null unless the layout qualifies
+        std::vector<std::shared_ptr<net::MuxConn>> htx, hrx; // inter-host ring pools (to next / from previous host)
     };
 
     // connection management
@@ -177,6 +188,7 @@ private:
     std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);
     std::pair<bool, bool> ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
+    std::pair<bool, bool> hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     bool abort_received(uint64_t tag);
 
     // shared state
@@ -194,8 +206,10 @@ private:
     std::map<Uuid, std::vector<std::shared_ptr<net::MuxConn>>> tx_;
     std::map<Uuid, std::vector<std::shared_ptr<net::MuxConn>>> rx_;
     std::vector<proto::PeerInfo> neighbors_;
+    std::vector<proto::ExtraPeer> extras_;
     std::vector<Uuid> ring_;
     std::shared_ptr<IpcArena> arena_;
+    std::shared_ptr<HierState> hier_;
     std::mutex establish_mtx_; // serializes concurrent re-establishment attempts
 
     std::atomic<uint64_t> conn_revision_{0};

@@ -537,7 +537,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
 
 std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
                                     DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
-                                    std::atomic<uint64_t> &rx) {
+                                    std::atomic<uint64_t> &rx, const InterHost *inter, size_t world) {
     OpCtx ctx;
     {
         std::lock_guard l(g_ctx_mtx);
@@ -563,7 +563,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
     uint8_t *my_out = ctx.my_out;
-    const bool push = push_algorithm();
+    const bool push = inter != nullptr || push_algorithm();
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
@@ -597,7 +597,31 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     std::vector<const void *> srcs(W);
     for (size_t k = 0; k < W; ++k) srcs[k] = ctx.peer_in[k] + lo[rank_] * es;
 
-    if (push) {
+    if (inter) {
+        // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push
+        Lease part(device_pool(), std::max<size_t>(n[rank_] * es, 256), device);
+        if (!part.ok()) return finish(1);
+        void *p = part.data();
+        const ReduceOp local_op = op == ReduceOp::Avg ? ReduceOp::Sum : op;
+        if (!be->multi_reduce(&p, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, local_op, st) ||
+            !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: host-local reduce failed";
+            return finish(1);
+        }
+        trace_mark("local_reduce");
+        if (int rc = (*inter)(p, n[rank_])) return finish(rc);
+        trace_mark("inter_host");
+        if (op == ReduceOp::Avg && n[rank_] > 0) be->finalize_avg(p, n[rank_], dtype, world, st);
+        std::vector<void *> dsts(W);
+        for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
+        const void *one = p;
+        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, n[rank_], dtype, ReduceOp::Sum, st) ||
+            !be->stream_sync(st)) {
+            LOG(ERR) << "IPC: host-local broadcast failed";
+            return finish(1);
+        }
+        trace_mark("local_bcast");
+    } else if (push) {
         // one-shot: read shard `rank` of every peer's input (inbound xGMI), reduce in fixed peer order and write the
         // result into every peer's output (outbound xGMI, posted writes) — reduce-scatter and all-gather overlap in
         // one kernel and one barrier; every peer receives the owner's bytes, so results are bit-identical
@@ -651,6 +675,39 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
 std::pair<bool, bool> Client::ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device) {
     return rv.arena->run(*this, op.req.tag, seq, op.req.src, op.req.dst, op.req.count, op.req.dtype, op.req.op, device,
                          op.tx, op.rx);
+}
+
+// Hierarchical all-reduce (ring spans several hosts with L peers each): reduce-scatter inside each host over xGMI,
+// one TCP device ring per local rank across hosts on the 1/L shard, all-gather inside the host over xGMI. Every byte
+// crosses the network once per host instead of once per GPU.
+std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    const HierState &h = *rv.hier;
+    const int decision = h.arena->vote(*this, op, seq, true, device);
+    if (decision != IpcArena::kUseIpc) {
+        // every participant announced the capability, so a local refusal means inconsistent buffers: fail the op
+        LOG(ERR) << "hierarchical all-reduce: host-local vote failed (decision " << decision << ")";
+        return {false, abort_received(op.req.tag)};
+    }
+    RingView sub;
+    sub.ring = h.host_ring;
+    sub.rank = h.host;
+    sub.tx = rv.htx;
+    sub.rx = rv.hrx;
+    IpcArena::InterHost inter = [&](void *part, size_t count) -> int {
+        OpState inner;
+        inner.req = op.req;
+        inner.req.src = part;
+        inner.req.dst = part;
+        inner.req.count = count;
+        inner.req.scratch = true;
+        if (inner.req.op == ReduceOp::Avg) inner.req.op = ReduceOp::Sum; // divided by the whole world afterwards
+        const auto r = ring_reduce_device(inner, sub, seq, device);
+        op.tx += inner.tx.load();
+        op.rx += inner.rx.load();
+        return r.first && !r.second ? 0 : (r.second ? 2 : 1);
+    };
+    return h.arena->run(*this, op.req.tag, seq, op.req.src, op.req.dst, op.req.count, op.req.dtype, op.req.op, device,
+                        op.tx, op.rx, &inter, rv.ring.size());
 }
 
 } // namespace pccl::client

@@ -21,6 +21,7 @@
 #include <array>
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -50,10 +51,16 @@ public:
     template<typename Op>
     int vote(Client &c, Op &op, uint64_t seq, bool device_ok, int device);
 
+    // Inter-host stage of the hierarchical all-reduce: all-reduces (SUM / MIN / MAX / PROD, never AVG) `count`
+    // elements of device scratch in place across hosts. Returns 0 ok, 1 failure, 2 master abort.
+    using InterHost = std::function<int(void *part, size_t count)>;
+
     // Runs the IPC all-reduce for a voted op. Returns {success, aborted}.
+    // With `inter` (hierarchical mode, this arena spans one host): reduce my local shard into scratch, all-reduce it
+    // across hosts with `inter`, divide by `world` for AVG, then push it into every local peer's output.
     std::pair<bool, bool> run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
                               DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
-                              std::atomic<uint64_t> &rx);
+                              std::atomic<uint64_t> &rx, const InterHost *inter = nullptr, size_t world = 0);
 
     // internal (exposed for the vote template)
     int vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,

@@ -44,7 +44,7 @@ enum class SyncStrategy : uint8_t { EnforcePopular = 0, RxOnly = 1, TxOnly = 2 }
 enum class DeviceType : uint8_t { Cpu = 0, Gpu = 1 };
 
 // Which data path executed an all-reduce (exposed through PCCL_ATTRIBUTE_LAST_REDUCE_PATH).
-enum class ReducePath : int { None = 0, HostRing = 1, DeviceRing = 2, DeviceIpc = 3 };
+enum class ReducePath : int { None = 0, HostRing = 1, DeviceRing = 2, DeviceIpc = 3, Hierarchical = 4 };
 
 struct Uuid {
     std::array<uint8_t, 16> data{};

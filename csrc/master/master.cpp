@@ -92,6 +92,30 @@ uint64_t Master::largest_group(bool include_registered) const {
 
 // The ring of a group: members are accepted peers plus newcomers currently connecting. Existing members keep their
 // relative order (so optimized rings survive churn); new members are appended in UUID order.
+std::vector<uint32_t> Master::host_layout(const std::vector<Uuid> &ring) {
+    if (ring.size() < 4 || !env_flag("PCCL_HIERARCHICAL", true)) return {};
+    std::vector<std::string> hosts;
+    std::vector<uint32_t> host_of;
+    std::vector<size_t> members;
+    for (const auto &u : ring) {
+        const ClientInfo *c = client_by_uuid(u);
+        if (!c || c->host_token.empty()) return {};
+        auto it = std::find(hosts.begin(), hosts.end(), c->host_token);
+        if (it == hosts.end()) {
+            hosts.push_back(c->host_token);
+            members.push_back(0);
+            it = hosts.end() - 1;
+        }
+        const auto h = static_cast<uint32_t>(it - hosts.begin());
+        host_of.push_back(h);
+        ++members[h];
+    }
+    if (hosts.size() < 2 || members[0] < 2) return {};
+    for (size_t m : members)
+        if (m != members[0]) return {};
+    return host_of;
+}
+
 std::vector<Uuid> Master::ring_of(uint32_t group, bool /*include_registered*/) {
     auto &gs = groups_[group];
     std::set<Uuid> members;
@@ -181,6 +205,25 @@ void Master::send_connection_info(bool include_registered) {
                 const Uuid next = ring[(pos + 1) % ring.size()];
                 neighbors.push_back(prev);
                 if (next != prev) neighbors.push_back(next);
+            }
+        }
+        // hierarchical layout: TX pool to the member with my local rank on the next host, RX pool from the previous
+        const auto layout = host_layout(ring);
+        const size_t me = std::find(ring.begin(), ring.end(), u) - ring.begin();
+        if (!layout.empty() && me < ring.size()) {
+            const uint32_t hosts = *std::max_element(layout.begin(), layout.end()) + 1;
+            auto local_rank = [&](size_t k) {
+                return static_cast<size_t>(std::count(layout.begin(), layout.begin() + static_cast<long>(k), layout[k]));
+            };
+            const size_t j = local_rank(me);
+            for (size_t k = 0; k < ring.size(); ++k) {
+                if (k == me || local_rank(k) != j) continue;
+                // with two hosts the partner is both the next and the previous host
+                const uint8_t role = (layout[k] == (layout[me] + 1) % hosts ? kExtraTx : 0) |
+                                     (layout[k] == (layout[me] + hosts - 1) % hosts ? kExtraRx : 0);
+                if (!role) continue;
+                const ClientInfo *nc = client_by_uuid(ring[k]);
+                if (nc) info.extra_peers.push_back(ExtraPeer{PeerInfo{nc->p2p, ring[k]}, role});
             }
         }
         auto &prev = prev_neighbors_[u];
@@ -429,6 +472,7 @@ bool Master::check_p2p_established() {
             const ClientInfo *rc = client_by_uuid(ru);
             pkt.single_host = pkt.single_host && rc && !rc->host_token.empty() && rc->host_token == c.host_token;
         }
+        pkt.host_of = host_layout(pkt.ring_order);
         server_.send_packet(c.addr, pkt);
     }
     if (failure) {
@@ -841,6 +885,7 @@ void Master::handle_coll_initiate(const SockAddr &addr, const C2MCollectiveComms
     }
     c->state = State::CollectiveCommsRunning;
     c->colls[p.tag] = CollState::VoteInitiate;
+    c->coll_flags[p.tag] = p.flags;
     check_coll_initiate_consensus(c->group, p.tag);
 }
 
@@ -857,6 +902,12 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
     M2CCollectiveCommsCommence pkt;
     pkt.tag = tag;
     pkt.seq_nr = seq;
+    pkt.flags = 0xff; // a capability holds for the op only if every participant announced it
+    for (auto &[_, c] : clients_) {
+        if (c.group != group || c.phase != Phase::Accepted) continue;
+        auto f = c.coll_flags.find(tag);
+        pkt.flags &= f == c.coll_flags.end() ? 0 : f->second;
+    }
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         c.colls[tag] = CollState::Perform;
@@ -916,6 +967,7 @@ void Master::check_coll_complete_consensus(uint32_t group, uint64_t tag) {
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         c.colls.erase(tag);
+        c.coll_flags.erase(tag);
         if (c.colls.empty()) c.state = State::Idle;
         server_.send_packet(c.addr, pkt);
     }

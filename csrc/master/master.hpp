@@ -62,6 +62,7 @@ struct ClientInfo {
     State state = State::Idle;
     bool voted_pending_query = false;
     std::map<uint64_t, CollState> colls;
+    std::map<uint64_t, uint8_t> coll_flags; // initiate capability bits per running tag
     uint32_t group = 0;
     SockAddr p2p{}, ss{}, bm{};
     uint64_t ss_revision = 0; // revision announced in the current shared-state round
@@ -139,6 +140,9 @@ private:
     ClientInfo *client_by_uuid(const Uuid &u);
     void on_peer_accepted(ClientInfo &c);
     std::vector<Uuid> ring_of(uint32_t group, bool include_registered);
+    // Host index of every ring member (hosts numbered by first appearance) if the ring qualifies for the hierarchical
+    // all-reduce: >= 2 hosts, every host with the same number (>= 2) of members, every member with a host token.
+    std::vector<uint32_t> host_layout(const std::vector<Uuid> &ring);
     std::optional<std::vector<Uuid>> reachable_ring(uint32_t group);
     uint64_t local_world_size(uint32_t group, bool include_registered) const;
     uint64_t num_groups(bool include_registered) const;

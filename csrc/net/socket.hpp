@@ -63,6 +63,7 @@ void close_fd(int &fd);
 // True if `a` is a loopback address or one of this host's interface addresses.
 bool is_local_address(const SockAddr &a);
 // Identifies this host (kernel boot id + hostname): equal tokens mean two processes can share HIP IPC handles.
+// PCCL_HOST_TOKEN overrides it (tests simulate several hosts on one machine).
 const std::string &host_token();
 bool is_connected(int fd); // MSG_PEEK probe (non-blocking)
 

@@ -90,11 +90,20 @@ void M2CP2PConnectionInfo::encode(WBuf &w) const {
     w.u64(local_world_size);
     w.u64(num_distinct_peer_groups);
     w.u64(largest_peer_group_world_size);
-    if (unchanged) return;
-    w.u64(all_peers.size());
-    for (const auto &p : all_peers) {
-        w.sockaddr(p.p2p_listen_addr);
-        w.uuid(p.peer_uuid);
+    if (!unchanged) {
+        w.u64(all_peers.size());
+        for (const auto &p : all_peers) {
+            w.sockaddr(p.p2p_listen_addr);
+            w.uuid(p.peer_uuid);
+        }
+    }
+    if (!extra_peers.empty()) {
+        w.u64(extra_peers.size());
+        for (const auto &e : extra_peers) {
+            w.sockaddr(e.peer.p2p_listen_addr);
+            w.uuid(e.peer.peer_uuid);
+            w.u8(e.role);
+        }
     }
 }
 
@@ -104,13 +113,24 @@ bool M2CP2PConnectionInfo::decode(RBuf &r) {
     local_world_size = r.u64();
     num_distinct_peer_groups = r.u64();
     largest_peer_group_world_size = r.u64();
-    if (unchanged) return r.ok();
-    const uint64_t n = r.u64();
-    if (!r.plausible_count(n, 23)) return false;
-    all_peers.resize(n);
-    for (auto &p : all_peers) {
-        p.p2p_listen_addr = r.sockaddr();
-        p.peer_uuid = r.uuid();
+    if (!unchanged) {
+        const uint64_t n = r.u64();
+        if (!r.plausible_count(n, 23)) return false;
+        all_peers.resize(n);
+        for (auto &p : all_peers) {
+            p.p2p_listen_addr = r.sockaddr();
+            p.peer_uuid = r.uuid();
+        }
+    }
+    if (r.ok() && r.remaining() > 0) {
+        const uint64_t m = r.u64();
+        if (!r.plausible_count(m, 24)) return false;
+        extra_peers.resize(m);
+        for (auto &e : extra_peers) {
+            e.peer.p2p_listen_addr = r.sockaddr();
+            e.peer.peer_uuid = r.uuid();
+            e.role = r.u8();
+        }
     }
     return r.ok();
 }
@@ -133,10 +153,21 @@ static bool decode_uuid_list(RBuf &r, bool &success, std::vector<Uuid> &v) {
 void M2CP2PConnectionsEstablished::encode(WBuf &w) const {
     encode_uuid_list(w, success, ring_order);
     w.boolean(single_host);
+    if (!host_of.empty()) {
+        w.u64(host_of.size());
+        for (uint32_t h : host_of) w.u32(h);
+    }
 }
 bool M2CP2PConnectionsEstablished::decode(RBuf &r) {
     if (!decode_uuid_list(r, success, ring_order)) return false;
-    single_host = r.remaining() > 0 && r.boolean();
+    has_host_info = r.remaining() > 0;
+    single_host = has_host_info && r.boolean();
+    if (r.ok() && r.remaining() > 0) {
+        const uint64_t n = r.u64();
+        if (!r.plausible_count(n, 4)) return false;
+        host_of.resize(n);
+        for (auto &h : host_of) h = r.u32();
+    }
     return r.ok();
 }
 void M2COptimizeTopologyComplete::encode(WBuf &w) const { encode_uuid_list(w, success, ring_order); }

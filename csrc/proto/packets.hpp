@@ -149,20 +149,27 @@ struct C2MCollectiveCommsInitiate {
     uint64_t count = 0;
     DType data_type = DType::F32;
     ReduceOp op = ReduceOp::Sum;
+    // extension (appended, optional): capability bits of this peer for this op (kCollFlagHierarchical)
+    uint8_t flags = 0;
     void encode(WBuf &w) const {
         w.u64(tag);
         w.u64(count);
         w.u8(static_cast<uint8_t>(data_type));
         w.u8(static_cast<uint8_t>(op));
+        if (flags) w.u8(flags);
     }
     bool decode(RBuf &r) {
         tag = r.u64();
         count = r.u64();
         data_type = static_cast<DType>(r.u8());
         op = static_cast<ReduceOp>(r.u8());
+        flags = r.ok() && r.remaining() > 0 ? r.u8() : 0;
         return r.ok();
     }
 };
+
+// the peer can run this op hierarchically (device buffers, host-local IPC arena, inter-host ring connections)
+constexpr uint8_t kCollFlagHierarchical = 1;
 
 struct C2MCollectiveCommsComplete {
     static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_COMPLETE;
@@ -199,6 +206,13 @@ struct PeerInfo {
     Uuid peer_uuid;
 };
 
+// Extension: inter-host ring partners of the hierarchical all-reduce (same local rank on the next / previous host).
+struct ExtraPeer {
+    PeerInfo peer;
+    uint8_t role = 0; // kExtraTx: open a TX pool to it; kExtraRx: keep the RX pool it opens to us
+};
+constexpr uint8_t kExtraTx = 1, kExtraRx = 2;
+
 struct M2CP2PConnectionInfo {
     static constexpr PacketId kId = M2C_P2P_CONNECTION_INFO;
     bool unchanged = false;
@@ -207,6 +221,7 @@ struct M2CP2PConnectionInfo {
     uint64_t num_distinct_peer_groups = 0;
     uint64_t largest_peer_group_world_size = 0;
     std::vector<PeerInfo> all_peers;
+    std::vector<ExtraPeer> extra_peers; // extension (appended, optional; sent even when `unchanged`)
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };
@@ -216,6 +231,8 @@ struct M2CP2PConnectionsEstablished {
     bool success = false;
     std::vector<Uuid> ring_order;
     bool single_host = false; // extension (appended, optional): every ring member reported the same host token
+    bool has_host_info = false; // decode only: the master sent the extension (so single_host is authoritative)
+    std::vector<uint32_t> host_of; // extension (appended, optional): host index of every ring member (ring order)
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };
@@ -273,13 +290,16 @@ struct M2CCollectiveCommsCommence {
     static constexpr PacketId kId = M2C_COLLECTIVE_COMMS_COMMENCE;
     uint64_t tag = 0;
     uint64_t seq_nr = 0;
+    uint8_t flags = 0; // extension (appended, optional): AND of every participant's initiate flags
     void encode(WBuf &w) const {
         w.u64(tag);
         w.u64(seq_nr);
+        if (flags) w.u8(flags);
     }
     bool decode(RBuf &r) {
         tag = r.u64();
         seq_nr = r.u64();
+        flags = r.ok() && r.remaining() > 0 ? r.u8() : 0;
         return r.ok();
     }
 };

@@ -90,7 +90,8 @@ typedef enum pcclAttribute_t {
     /** [pccl-amd extension] position of this peer in the current ring order (-1 if unknown) */
     PCCL_ATTRIBUTE_RING_RANK = 65,
     /** [pccl-amd extension] data path of the last completed all-reduce: 0 none, 1 host ring/TCP,
-     *  2 device ring/TCP via pinned staging, 3 device xGMI/IPC (same host) */
+     *  2 device ring/TCP via pinned staging, 3 device xGMI/IPC (same host), 4 hierarchical (xGMI/IPC inside each
+     *  host + one TCP ring per local rank across hosts) */
     PCCL_ATTRIBUTE_LAST_REDUCE_PATH = 66
 } pcclAttribute_t;
 

@@ -102,6 +102,7 @@ class ReducePath(Enum):
     HOST_RING = 1
     DEVICE_RING = 2
     DEVICE_IPC = 3
+    HIERARCHICAL = 4
 
 
 class SharedStateSyncStrategy(Enum):

@@ -1,7 +1,7 @@
 """Standalone peer process used by the multi-process tests (CPU and GPU).
 
 usage: allreduce_peer.py MASTER WORLD RANK [--n N] [--dtype f32|bf16|f16|i32] [--device cpu|cuda:0] [--steps K]
-                         [--die-at STEP] [--const] [--no-wait]
+                         [--die-at STEP] [--const] [--no-wait] [--inplace] [--op sum|avg|max] [--quant none|u8]
 Each step all-reduces a tensor and checks the result; prints one JSON line per attempt.
   default: x = rank + 1 + step, tag = step (all peers start together)
   --const: x = 1, tag 0, result must equal the op's world size (membership may change between steps)
@@ -36,7 +36,12 @@ def main():
     ap.add_argument("--no-wait", action="store_true", help="do not wait for WORLD peers (late joiner)")
     ap.add_argument("--step-sleep", type=float, default=0.0)
     ap.add_argument("--inplace", action="store_true")
+    ap.add_argument("--op", default="sum", choices=["sum", "avg", "max"])
+    ap.add_argument("--quant", default="none", choices=["none", "u8"])
     a = ap.parse_args()
+    op = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[a.op]
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant == "u8" \
+        else None
     dev = torch.device(a.device)
     t_start = time.perf_counter()
     comm = pccl.Communicator(a.master, 0)
@@ -60,7 +65,7 @@ def main():
             os._exit(17)  # simulated crash (no clean disconnect)
         t0 = time.perf_counter()
         try:
-            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0 if a.const else step)
+            info = comm.all_reduce(x, y, op=op, tag=0 if a.const else step, quantization_options=qopt)
         except pccl.PCCLError as e:
             print(json.dumps({"rank": a.rank, "step": step, "error": e.result.name}), flush=True)
             failures += 1
