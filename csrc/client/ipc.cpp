@@ -64,6 +64,7 @@ struct alignas(64) OpPeerShm {
     uint32_t op;
     uint32_t zero_copy; // bit 0: input is the caller's send buffer, bit 1: output is the caller's receive buffer
     uint32_t pad;
+    uint64_t gpu_uid;   // physical GPU of this op's buffers (peers sharing a GPU split its CUs)
     uint64_t in_raw, out_raw;
     uint64_t in_off, out_off;
     uint8_t in_handle[kIpcHandleBytes];
@@ -466,6 +467,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
             }
         }
     }
+    mine->gpu_uid = device_ok ? be->device_uid(device) : 0;
     mine->vote = device_ok ? 1 : 0;
     mine->zero_copy = (in_direct ? 1u : 0u) | (out_direct ? 2u : 0u);
     mine->device = device;
@@ -596,6 +598,15 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     }
     std::vector<const void *> srcs(W);
     for (size_t k = 0; k < W; ++k) srcs[k] = ctx.peer_in[k] + lo[rank_] * es;
+    // workgroup budget: 512 per GPU (2 per CU, the measured optimum for these streaming kernels), split between the
+    // peers whose kernels run concurrently on this GPU, but not below 256 per kernel (fewer cannot saturate HBM)
+    int sharing = 0;
+    {
+        const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+        const uint64_t me = shm_->op(slot, static_cast<uint32_t>(rank_))->gpu_uid;
+        for (size_t k = 0; k < W; ++k) sharing += shm_->op(slot, static_cast<uint32_t>(k))->gpu_uid == me ? 1 : 0;
+    }
+    const int grid = std::max(256, 512 / std::max(1, sharing));
 
     if (inter) {
         // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push
@@ -603,7 +614,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         if (!part.ok()) return finish(1);
         void *p = part.data();
         const ReduceOp local_op = op == ReduceOp::Avg ? ReduceOp::Sum : op;
-        if (!be->multi_reduce(&p, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, local_op, st) ||
+        if (!be->multi_reduce(&p, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, local_op, st, grid) ||
             !be->stream_sync(st)) {
             LOG(ERR) << "IPC: host-local reduce failed";
             return finish(1);
@@ -615,7 +626,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         std::vector<void *> dsts(W);
         for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
         const void *one = p;
-        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, n[rank_], dtype, ReduceOp::Sum, st) ||
+        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, n[rank_], dtype, ReduceOp::Sum, st, grid) ||
             !be->stream_sync(st)) {
             LOG(ERR) << "IPC: host-local broadcast failed";
             return finish(1);
@@ -628,7 +639,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         std::vector<void *> dsts(W);
         for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
         if (!be->multi_reduce(dsts.data(), static_cast<int>(W), srcs.data(), static_cast<int>(W), n[rank_], dtype, op,
-                              st) ||
+                              st, grid) ||
             !be->stream_sync(st)) {
             LOG(ERR) << "IPC: multi-source reduce + broadcast failed";
             return finish(1);
@@ -637,7 +648,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     } else {
         // two-shot: reduce-scatter into my output, barrier, then pull every other shard (reads only)
         void *d0 = my_out + lo[rank_] * es;
-        if (!be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st) ||
+        if (!be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st, grid) ||
             !be->stream_sync(st)) {
             LOG(ERR) << "IPC: multi-source reduce failed";
             return finish(1);

@@ -31,6 +31,8 @@ public:
     virtual bool pointer_info(const void *p, DevPtrInfo &out) = 0;
     virtual bool set_device(int dev) = 0;
     virtual int current_device() = 0;
+    // process-independent identity of a device (hash of its PCI bus id): peers compare it to find GPU sharing
+    virtual uint64_t device_uid(int dev) = 0;
 
     // memory
     virtual void *alloc_device(size_t n) = 0;
@@ -69,8 +71,9 @@ public:
     // Intra-node xGMI kernels. srcs[k] points to shard `count` elements in peer k's buffer (IPC-mapped);
     // every dsts[0..ndst) receives op(srcs[0..n)) reduced in order 0..n-1 (the own output and, in the one-shot push
     // all-reduce, the IPC-mapped outputs of the peers). Avg divides by n at the end.
+    // max_grid: workgroup budget of this launch (0 = default); peers sharing one GPU split the chip between them
     virtual bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
-                              ReduceOp op, DevStream s) = 0;
+                              ReduceOp op, DevStream s, int max_grid = 0) = 0;
     // dst regions gathered from n sources: dst[k*stride ...] = srcs[k] for k != skip (count elements each,
     // segment k has counts[k] elements at element offset offsets[k]).
     virtual bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,

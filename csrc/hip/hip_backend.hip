@@ -39,6 +39,16 @@ public:
     }
 
     bool set_device(int dev) override { return HIP_OK(hipSetDevice(dev)); }
+    uint64_t device_uid(int dev) override {
+        char bus[64] = {};
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return static_cast<uint64_t>(dev) + 1;
+        }
+        uint64_t h = 1469598103934665603ull; // FNV-1a
+        for (const char *c = bus; *c; ++c) h = (h ^ static_cast<uint8_t>(*c)) * 1099511628211ull;
+        return h;
+    }
     int current_device() override {
         int d = -1;
         (void)hipGetDevice(&d);
@@ -164,8 +174,8 @@ public:
         return hipk::launch_finalize_avg(dst, count, t, ws, static_cast<hipStream_t>(s));
     }
     bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
-                      DevStream s) override {
-        return hipk::launch_multi_reduce(dsts, ndst, srcs, n, count, t, op, static_cast<hipStream_t>(s));
+                      DevStream s, int max_grid) override {
+        return hipk::launch_multi_reduce(dsts, ndst, srcs, n, count, t, op, static_cast<hipStream_t>(s), max_grid);
     }
     bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n, int skip,
                       DType t, DevStream s) override {

@@ -1,5 +1,6 @@
 // Intra-node xGMI kernels: multi-source reduce (reduce-scatter) and multi-source gather (all-gather) launchers.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "dispatch.hpp"
@@ -7,8 +8,13 @@
 
 namespace pccl::hipk {
 
+static int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
-                         ReduceOp op, hipStream_t st) {
+                         ReduceOp op, hipStream_t st, int max_grid_hint) {
     if (count == 0) return true;
     if (n < 1 || n > kMaxSrc || ndst < 1 || ndst > kMaxSrc) return false;
     SrcList sl{};
@@ -34,15 +40,29 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
             using O = decltype(o);
             bool ok = true;
             if (nvec > 0) {
-                const int grid = std::min(grid_for(nvec, 2), 1024); // 4 WGs / CU measured best (kbench)
+                // 512 workgroups (2 per CU) and 2 vectors per thread measured best on MI355X for one kernel per GPU
+                // (profiles/r1_ipc_grid_sweep.md); concurrent peers on one GPU pass a smaller budget. PCCL_IPC_GRID /
+                // PCCL_IPC_UNROLL (2 or 4) override both for tuning sweeps.
+                static const int env_grid = env_int("PCCL_IPC_GRID", 0);
+                static const int unroll = env_int("PCCL_IPC_UNROLL", 2) == 4 ? 4 : 2;
+                const int max_grid = env_grid > 0 ? env_grid : (max_grid_hint > 0 ? max_grid_hint : 512);
+                const int grid = std::max(1, std::min(grid_for(nvec, unroll), max_grid));
                 ok = launch_ok([&] {
+                    auto go = [&](auto avg_c, auto u_c) {
+                        k_multi_reduce_vec<E, O, decltype(avg_c)::value, decltype(u_c)::value>
+                            <<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
+                    };
+                    using T2 = std::integral_constant<int, 2>;
+                    using T4 = std::integral_constant<int, 4>;
                     if constexpr (std::is_same_v<O, OpSum>) {
                         if (avg) {
-                            k_multi_reduce_vec<E, O, true><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
+                            if (unroll == 4) go(std::true_type{}, T4{});
+                            else go(std::true_type{}, T2{});
                             return;
                         }
                     }
-                    k_multi_reduce_vec<E, O, false><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
+                    if (unroll == 4) go(std::false_type{}, T4{});
+                    else go(std::false_type{}, T2{});
                 });
             }
             const size_t begin = nvec * V;

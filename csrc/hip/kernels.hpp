@@ -370,58 +370,59 @@ struct DstList {
 // every peer gets bit-identical bytes) and stores the result to every destination. In the one-shot IPC all-reduce the
 // destinations are the receive buffers of all peers (remote ones over xGMI: posted writes, so the outbound direction
 // of the links carries the all-gather while the inbound direction carries the reduce-scatter reads).
-template<typename E, typename Op, bool AVG>
+template<typename E, typename Op, bool AVG, int U = 2>
 __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec) {
+    // U vectors (i, i + stride, ...) per thread and iteration: U x nsrc 16-byte loads in flight
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = Vec<E>::N;
     const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
     const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-    for (size_t i = tid; i < nvec; i += 2 * stride) {
-        const size_t j = i + stride;
-        const bool has2 = j < nvec;
-        const size_t j2 = has2 ? j : i; // keep the second load in bounds; its result is discarded
-        C acc0[V], acc1[V];
-        {
-            const uint4 a = reinterpret_cast<const uint4 *>(srcs.p[0])[i];
-            const uint4 b = reinterpret_cast<const uint4 *>(srcs.p[0])[j2];
-            const S *s0 = reinterpret_cast<const S *>(&a);
-            const S *s1 = reinterpret_cast<const S *>(&b);
+    for (size_t i = tid; i < nvec; i += U * stride) {
+        size_t idx[U];
+        bool has[U];
 #pragma unroll
-            for (int e = 0; e < V; ++e) {
-                acc0[e] = E::ld(s0[e]);
-                acc1[e] = E::ld(s1[e]);
-            }
+        for (int u = 0; u < U; ++u) {
+            const size_t j = i + static_cast<size_t>(u) * stride;
+            has[u] = j < nvec;
+            idx[u] = has[u] ? j : i; // keep every load in bounds; results of the clamped ones are discarded
         }
-        // sources are read in fixed peer order (bit-identical on every peer); 4 sources x 2 vectors in flight
+        C acc[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint4 a = reinterpret_cast<const uint4 *>(srcs.p[0])[idx[u]];
+            const S *s0 = reinterpret_cast<const S *>(&a);
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc[u][e] = E::ld(s0[e]);
+        }
+        // sources are read in fixed peer order (bit-identical on every peer)
 #pragma unroll 4
         for (int k = 1; k < nsrc; ++k) {
-            const uint4 a = reinterpret_cast<const uint4 *>(srcs.p[k])[i];
-            const uint4 b = reinterpret_cast<const uint4 *>(srcs.p[k])[j2];
-            const S *s0 = reinterpret_cast<const S *>(&a);
-            const S *s1 = reinterpret_cast<const S *>(&b);
+            uint4 a[U];
 #pragma unroll
-            for (int e = 0; e < V; ++e) {
-                acc0[e] = apply_op<Op, C>(acc0[e], E::ld(s0[e]));
-                acc1[e] = apply_op<Op, C>(acc1[e], E::ld(s1[e]));
+            for (int u = 0; u < U; ++u) a[u] = reinterpret_cast<const uint4 *>(srcs.p[k])[idx[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const S *s1 = reinterpret_cast<const S *>(&a[u]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc[u][e] = apply_op<Op, C>(acc[u][e], E::ld(s1[e]));
             }
         }
-        uint4 out0, out1;
-        S *o0 = reinterpret_cast<S *>(&out0);
-        S *o1 = reinterpret_cast<S *>(&out1);
+        uint4 out[U];
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-            if (AVG) {
-                acc0[e] = static_cast<C>(acc0[e] / static_cast<C>(nsrc));
-                acc1[e] = static_cast<C>(acc1[e] / static_cast<C>(nsrc));
+        for (int u = 0; u < U; ++u) {
+            S *o = reinterpret_cast<S *>(&out[u]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (AVG) acc[u][e] = static_cast<C>(acc[u][e] / static_cast<C>(nsrc));
+                o[e] = E::st(acc[u][e]);
             }
-            o0[e] = E::st(acc0[e]);
-            o1[e] = E::st(acc1[e]);
         }
 #pragma unroll 4
         for (int k = 0; k < ndst; ++k) {
-            nt_store(static_cast<uint4 *>(dsts.p[k]) + i, out0);
-            if (has2) nt_store(static_cast<uint4 *>(dsts.p[k]) + j, out1);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
         }
     }
 }

@@ -82,3 +82,29 @@ def test_hierarchical_quantized_inter_host(hip):
             e = _expect(4, ln["step"], "sum")
             assert abs(ln["lo"] - e) < 0.05 and abs(ln["hi"] - e) < 0.05
             assert ln["path"] == pccl.ReducePath.HIERARCHICAL.value
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_peer_crash_with_host_layout(device, request):
+    """A peer of a 2 x 2 layout crashes between ops: the hosts become unequal, the master drops the layout (flat ring
+    from then on) and the survivors keep reducing with exact results."""
+    if device != "cpu":
+        request.getfixturevalue("hip")
+    world = 4
+    with local_master() as addr:
+        procs = []
+        for r in range(world):
+            args = [WORKER, addr, str(world), str(r), "--n", str(1 << 16), "--dtype", "f32", "--device", device,
+                    "--steps", "12", "--const", *(["--die-at", "4"] if r == 3 else [])]
+            procs.append(spawn_python(args, env={"PCCL_HOST_TOKEN": f"simhost{r // 2}"},
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=300) for p in procs]
+    assert procs[3].returncode == 17
+    for r in range(3):
+        assert procs[r].returncode == 0, outs[r][1][-3000:]
+        lines = [json.loads(x) for x in outs[r][0].splitlines() if x.startswith("{")]
+        oks = [ln for ln in lines if "error" not in ln]
+        assert len(oks) == 12 and not any(ln.get("bad") for ln in oks)
+        assert oks[-1]["world"] == 3
+        if device != "cpu":
+            assert oks[0]["path"] == pccl.ReducePath.HIERARCHICAL.value
