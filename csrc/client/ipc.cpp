@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
@@ -323,7 +324,23 @@ void IpcArena::set_phase(uint64_t seq, uint32_t phase) {
         ->phase.store(((seq + 1) << 8) | phase, std::memory_order_release);
 }
 
-static bool pid_alive(int pid) { return kill(pid, 0) == 0 || errno == EPERM; }
+// A crashed peer stays a zombie until its parent reaps it, and kill(pid, 0) succeeds on zombies: also check the
+// process state in /proc so that survivors abort promptly instead of waiting for the barrier timeout.
+static bool pid_alive(int pid) {
+    if (kill(pid, 0) != 0 && errno != EPERM) return false;
+    char path[64];
+    std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+    FILE *f = std::fopen(path, "r");
+    if (!f) return true; // no procfs view of it (other namespace): trust kill()
+    char buf[512];
+    const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    const char *rp = std::strrchr(buf, ')'); // "pid (comm) state ..."; comm may contain spaces or parentheses
+    if (!rp || rp[1] == 0 || rp[2] == 0) return true;
+    const char state = rp[2];
+    return state != 'Z' && state != 'X' && state != 'x';
+}
 
 int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
     const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
