@@ -184,8 +184,8 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
                     r = ipc_reduce(*op, *rv, seq, di.device);
                     done = true;
                     if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceIpc);
-                } else if (decision == IpcArena::kAborted) {
-                    r = {false, abort_received(tag)};
+                } else if (decision == IpcArena::kAborted || decision == IpcArena::kAbortedByMaster) {
+                    r = {false, decision == IpcArena::kAbortedByMaster || abort_received(tag)};
                     done = true;
                 }
             }

@@ -503,7 +503,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
             be->memcpy_sync(dst, buf->ptr, bytes);
         }
         release_buffer(buf);
-        return kAborted;
+        return rc == 2 ? kAbortedByMaster : kAborted;
     }
     bool all = true;
     const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
@@ -714,7 +714,7 @@ std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint6
     if (decision != IpcArena::kUseIpc) {
         // every participant announced the capability, so a local refusal means inconsistent buffers: fail the op
         LOG(ERR) << "hierarchical all-reduce: host-local vote failed (decision " << decision << ")";
-        return {false, abort_received(op.req.tag)};
+        return {false, decision == IpcArena::kAbortedByMaster || abort_received(op.req.tag)};
     }
     RingView sub;
     sub.ring = h.host_ring;

@@ -38,7 +38,9 @@ struct ArenaShm;
 
 class IpcArena {
 public:
-    static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1;
+    // kAbortedByMaster: the vote barrier consumed the master's abort packet for this op (exactly one is sent per op,
+    // so the caller must not wait for it again)
+    static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1, kAbortedByMaster = -2;
 
     static std::shared_ptr<IpcArena> create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
                                             uint32_t group);
