@@ -297,15 +297,22 @@ struct StepIo {
 
 constexpr size_t kMetaFrameOverhead = 24;
 
-// Exchanges dequantization metadata for one step. Returns 0 ok, 1 io failure, 2 abort.
-int exchange_meta(Client *self, const StepIo &io, const QuantMeta &mine, QuantMeta &theirs, std::atomic<uint64_t> &tx,
-                  std::atomic<uint64_t> &rx, const std::function<bool()> &aborted) {
+// Dequantization metadata of one quantized step (reference reduce.cpp:154-192 sends its own and then waits for the
+// peer's before any data moves, which costs one extra network latency per ring step). Here the sender sends its meta
+// and immediately its data; the receiver waits for the peer's meta before posting its data sink (data frames that
+// arrive first are queued by the connection), so meta and data share one latency. Returns 0 ok, 1 io failure.
+int send_meta(const StepIo &io, const QuantMeta &mine, std::atomic<uint64_t> &tx) {
     P2PDequantizationMeta pkt;
     pkt.tag = io.tag;
     pkt.meta = mine;
     auto bytes = encode_with_id(pkt);
     if (!io.tx->send_frame(io.tag, io.seq, bytes.data(), bytes.size())) return 1;
     tx += bytes.size() + kMetaFrameOverhead;
+    return 0;
+}
+
+// Waits for the peer's metadata of this step. Returns 0 ok, 1 io failure, 2 abort.
+int recv_meta(const StepIo &io, QuantMeta &theirs, std::atomic<uint64_t> &rx, const std::function<bool()> &aborted) {
     while (true) {
         auto m = io.rx->recv_packet<P2PDequantizationMeta>(io.tag, io.seq, 20ms);
         if (m) {
@@ -316,7 +323,6 @@ int exchange_meta(Client *self, const StepIo &io, const QuantMeta &mine, QuantMe
         if (!io.rx->is_open()) return 1;
         if (aborted()) return 2;
     }
-    (void)self;
 }
 
 // Striping: a large ring-step payload is split into up to PCCL_RING_STRIPES contiguous stripes, each sent on its own
@@ -348,18 +354,21 @@ StripePlan plan_stripes(size_t bytes, size_t conns) {
 
 // One full-duplex ring step over the striped connections. `tx_ready(end)` blocks until payload bytes [0, end) may be
 // sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any order across
-// stripes, in order within a stripe). Returns 0 ok, 1 io failure, 2 abort.
+// stripes, in order within a stripe). `before_rx` (optional) runs after the senders started and before the receive
+// sinks are posted (the quantized steps receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
 int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
                  const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
                  size_t rx_bytes, size_t elem, size_t frame, const std::function<void(size_t, size_t)> &consume,
-                 const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr) {
+                 const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr,
+                 const std::function<int()> &before_rx = {}) {
     const StripePlan tp = plan_stripes(tx_bytes, txs.size());
     const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
     auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
     auto tx_conn = [&](size_t k) { return txs[(seq + k) % txs.size()].get(); };
-    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    bool sinks_posted = false;
     auto remove_sinks = [&] {
+        if (!sinks_posted) return;
         for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->remove_sink(tag);
     };
 
@@ -381,6 +390,15 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
     senders.reserve(tp.off.size());
     for (size_t k = 0; k < tp.off.size(); ++k)
         if (tp.len[k] > 0) senders.emplace_back(send_stripe, k);
+    if (before_rx) {
+        if (const int brc = before_rx()) {
+            send_rc.store(brc);
+            for (auto &t : senders) t.join();
+            return brc;
+        }
+    }
+    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    sinks_posted = true;
 
     std::vector<size_t> done(rp.off.size(), 0); // elements consumed per stripe
     size_t remaining = rp.off.size();
@@ -473,10 +491,12 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     // One full-duplex (striped) step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)`
     // for newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
-                        const std::function<void(size_t, size_t)> &consume) -> int {
+                        const std::function<void(size_t, size_t)> &consume,
+                        const std::function<int()> &before_rx = {}) -> int {
         return striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes,
-                            qs, chunk, consume, aborted, op.tx, op.rx);
+                            qs, chunk, consume, aborted, op.tx, op.rx, before_rx);
     };
+    auto await_meta = [&](QuantMeta &theirs) { return [&, pt = &theirs] { return recv_meta(io, *pt, op.rx, aborted); }; };
     auto fail = [&](int code) -> std::pair<bool, bool> {
         restore();
         return {code == 2, code == 2};
@@ -493,7 +513,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
             if (te > ts) mine = kernels::host_quantize(qbuf.data(), dst + ts * es, te - ts, q.dtype, q.qtype, q.qalgo);
             else mine = kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
             payload = qbuf.data();
-            if (int rc = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(rc);
+            if (int rc = send_meta(io, mine, op.tx)) return fail(rc);
         }
         uint8_t *rx_region = dst + rs * es;
         const int rc = run_step(payload, (te - ts) * qs, rbuf.data(), (re - rs) * qs, [&](size_t a, size_t b) {
@@ -501,7 +521,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
                 kernels::host_dequant_reduce(rx_region + a * es, rbuf.data() + a * qs, b - a, q.dtype, q.qtype, q.op, theirs);
             else
                 kernels::host_reduce(rx_region + a * es, rbuf.data() + a * es, b - a, q.dtype, q.op);
-        });
+        }, quant ? std::function<int()>(await_meta(theirs)) : std::function<int()>());
         if (rc) return fail(rc);
     }
 
@@ -536,11 +556,11 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
                 mine = prev_meta;
                 payload = ag[(step - 1) % 2].data();
             }
-            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
+            if (int m = send_meta(io, mine, op.tx)) return fail(m);
             uint8_t *sink = ag[step % 2].data();
             rc = run_step(payload, (te - ts) * qs, sink, (re - rs) * qs, [&](size_t a, size_t b) {
                 kernels::host_dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, theirs);
-            });
+            }, await_meta(theirs));
             prev_meta = theirs;
         } else {
             rc = run_step(dst + ts * es, (te - ts) * es, rx_region, (re - rs) * es, [](size_t, size_t) {});
@@ -629,9 +649,10 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
 
     // one full-duplex (striped) step. `tx_ready(end)` blocks until payload bytes [0, end) may be sent.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
-                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume) -> int {
+                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
+                        const std::function<int()> &before_rx = {}) -> int {
         const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs, piece,
-                                    consume, aborted, op.tx, op.rx);
+                                    consume, aborted, op.tx, op.rx, before_rx);
         if (rc == 0) be->stream_sync(st); // everything consumed from `sink` has landed in HBM
         return rc;
     };
@@ -660,11 +681,15 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         int rc;
         if (quant) {
             QuantMeta theirs;
+            kernels::QuantParams params{};
             const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts);
-            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
-            const auto params = kernels::make_params(theirs, q.qtype);
+            if (int m = send_meta(io, mine, op.tx)) return fail(m);
             rc = run_step(txbuf.data(), (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
                 be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, q.op, params, st);
+            }, [&] {
+                const int m = recv_meta(io, theirs, op.rx, aborted);
+                if (m == 0) params = kernels::make_params(theirs, q.qtype);
+                return m;
             });
         } else {
             stage_d2h(dst + ts * es, (te - ts) * es);
@@ -700,10 +725,14 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
                 mine = prev_meta;
                 payload = rxbuf[(step - 1) % 2];
             }
-            if (int m = exchange_meta(this, io, mine, theirs, op.tx, op.rx, aborted)) return fail(m);
-            const auto params = kernels::make_params(theirs, q.qtype);
+            if (int m = send_meta(io, mine, op.tx)) return fail(m);
+            kernels::QuantParams params{};
             rc = run_step(payload, (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
                 be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, params, st);
+            }, [&] {
+                const int m = recv_meta(io, theirs, op.rx, aborted);
+                if (m == 0) params = kernels::make_params(theirs, q.qtype);
+                return m;
             });
             prev_meta = theirs;
         } else {
