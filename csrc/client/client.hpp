@@ -223,6 +223,8 @@ private:
     // shared-state distribution (server side)
     std::mutex ss_mtx_;
     SharedState *serving_ = nullptr;
+    int ss_active_serves_ = 0;       // serve threads still reading serving_'s memory (guarded by ss_mtx_)
+    std::condition_variable ss_cv_;  // signalled when a serve ends
     std::atomic<uint64_t> ss_tx_bytes_{0};
     std::vector<std::thread> ss_threads_;
 

@@ -139,9 +139,17 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             std::lock_guard l(c->ss_mtx_);
             c->serving_ = s;
         }
-        ~PhaseGuard() {
-            std::lock_guard l(c->ss_mtx_);
+        bool released = false;
+        ~PhaseGuard() { release(); }
+        void release() {
+            if (released) return;
+            released = true;
+            std::unique_lock l(c->ss_mtx_);
             c->serving_ = nullptr;
+            // a requester reports completion once it holds the bytes, possibly before our sender thread returned
+            // from its last send: wait for the serves so the caller may modify its tensors and tx_bytes is final
+            if (!c->ss_cv_.wait_for(l, std::chrono::seconds(30), [&] { return c->ss_active_serves_ == 0; }))
+                LOG(WARN) << "Shared state sync: a serve to a peer is still running after 30 s";
         }
     } guard(this, &ss); // serve requests from the moment we vote (peers may be faster than our master packet)
 
@@ -344,6 +352,7 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         LOG(ERR) << "Shared state sync: no distributor could deliver the shared state";
         return false;
     }
+    guard.release();
     info.tx_bytes = ss_tx_bytes_.exchange(0);
     return true;
 }
@@ -378,11 +387,25 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
     SharedStateStatus status = SharedStateStatus::Success;
     uint64_t revision = 0;
     std::vector<SSEntry> to_send;
+    // the sync that owns serving_ waits for this serve (its tensors stay untouched and its tx count is final)
+    bool counted = false;
+    struct ServeGuard {
+        Client *c;
+        bool &counted;
+        ~ServeGuard() {
+            if (!counted) return;
+            std::lock_guard l(c->ss_mtx_);
+            --c->ss_active_serves_;
+            c->ss_cv_.notify_all();
+        }
+    } serve_guard{this, counted};
     {
         std::lock_guard l(ss_mtx_);
         if (serving_ == nullptr) {
             status = SharedStateStatus::NotDistributed;
         } else {
+            ++ss_active_serves_;
+            counted = true;
             revision = serving_->revision;
             for (const auto &k : keys) {
                 auto it = std::find_if(serving_->entries.begin(), serving_->entries.end(),

@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include "../common/log.hpp"
+#include "../common/spin.hpp"
 #include "socket.hpp"
 
 namespace pccl::net {
@@ -60,6 +61,7 @@ void MasterConnection::rx_loop() {
         {
             std::lock_guard lock(q_mtx_);
             queue_.push_back(Item{pkt->id, std::move(pkt->payload)});
+            gen_.fetch_add(1, std::memory_order_release);
         }
         q_cv_.notify_all();
     }
@@ -72,6 +74,7 @@ bool MasterConnection::take(const std::function<bool(uint16_t, const std::vector
                             std::chrono::milliseconds timeout) {
     std::unique_lock lock(q_mtx_);
     const auto deadline = std::chrono::steady_clock::now() + timeout;
+    bool spun = false;
     while (true) {
         for (auto it = queue_.begin(); it != queue_.end(); ++it) {
             if (match(it->id, it->payload)) {
@@ -81,6 +84,14 @@ bool MasterConnection::take(const std::function<bool(uint16_t, const std::vector
         }
         if (!open_) return false;
         if (timeout.count() == 0) return false;
+        if (!spun) { // gen_ only changes under q_mtx_, so re-checking it after relocking cannot miss a notify
+            spun = true;
+            const uint64_t g = gen_.load(std::memory_order_acquire);
+            lock.unlock();
+            spin_until([&] { return gen_.load(std::memory_order_acquire) != g || !open_; });
+            lock.lock();
+            if (gen_.load(std::memory_order_acquire) != g || !open_) continue;
+        }
         if (timeout.count() < 0) {
             q_cv_.wait(lock);
         } else if (q_cv_.wait_until(lock, deadline) == std::cv_status::timeout) {

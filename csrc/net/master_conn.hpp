@@ -73,6 +73,7 @@ private:
         std::vector<uint8_t> payload;
     };
     std::deque<Item> queue_;
+    std::atomic<uint64_t> gen_{0}; // bumped per queued packet (spinning waiters watch it without the lock)
 };
 
 } // namespace pccl::net

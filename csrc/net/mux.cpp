@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include "../common/log.hpp"
+#include "../common/spin.hpp"
 #include "socket.hpp"
 
 namespace pccl::net {
@@ -268,11 +269,20 @@ size_t MuxConn::sink_progress(uint64_t tag) {
 size_t MuxConn::wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout) {
     std::unique_lock l(mtx_);
     const auto deadline = std::chrono::steady_clock::now() + timeout;
+    bool spun = false;
     while (true) {
         auto it = sinks_.find(tag);
         if (it == sinks_.end()) return 0;
         const size_t have = it->second->received.load(std::memory_order_acquire);
         if (have >= want || !is_open()) return have;
+        if (!spun) { // spin once without the lock, then re-check under it before sleeping (no lost notify)
+            spun = true;
+            Sink *sink = it->second.get(); // only the waiter's own op removes its sink
+            l.unlock();
+            spin_until([&] { return sink->received.load(std::memory_order_acquire) >= want || !is_open(); });
+            l.lock();
+            continue;
+        }
         if (cv_.wait_until(l, deadline) == std::cv_status::timeout)
             return it->second->received.load(std::memory_order_acquire);
     }
