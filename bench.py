@@ -47,7 +47,13 @@ def _args():
 def _peer_loop(comm, x, y, steps, warmup, sync_all, torch, pccl):
     """Runs warmup + timed steps; sync_all() is the cross-peer barrier. Returns (seconds, tx, rx, path)."""
     for s in range(warmup):
-        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=s)
+        for attempt in range(3):  # an aborted warmup op (e.g. the xGMI path fell back to TCP) is retried by all peers
+            try:
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=s)
+                break
+            except pccl.PCCLError:
+                if attempt == 2:
+                    raise
     torch.cuda.synchronize()
     sync_all()
     t0 = time.perf_counter()

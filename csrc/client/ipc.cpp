@@ -449,6 +449,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     DeviceBackend *be = device_backend();
     CommBuf *buf = nullptr;
     bool in_direct = false, out_direct = false;
+    if (map_failed_.load(std::memory_order_relaxed)) device_ok = false; // vote for the TCP ring from now on
     if (device_ok) {
         // Direct (zero-copy) access to the caller's buffers where HIP IPC can export them. An in-place op always
         // stages its input: peers read the staged copy while results land in the caller's buffer, and the copy is
@@ -535,7 +536,10 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         auto *in_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->in_handle, device));
         auto *out_base = static_cast<uint8_t *>(peer_mapping(static_cast<int>(k), p->out_handle, device));
         if (!in_base || !out_base) {
-            LOG(ERR) << "IPC: cannot map the buffers of peer " << k;
+            // e.g. no peer access between these GPUs: this op aborts (every peer sees ABORTED), and this peer
+            // votes against the xGMI path from now on, so the ring falls back to TCP instead of failing every op
+            LOG(ERR) << "IPC: cannot map the buffers of peer " << k << "; using the TCP ring for later ops";
+            map_failed_.store(true, std::memory_order_relaxed);
             set_phase(seq, PH_ABORTED);
             if (buf && !in_direct && src == dst && out_direct) {
                 drain_peers(c, seq);

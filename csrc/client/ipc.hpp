@@ -41,6 +41,7 @@ public:
     // kAbortedByMaster: the vote barrier consumed the master's abort packet for this op (exactly one is sent per op,
     // so the caller must not wait for it again)
     static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1, kAbortedByMaster = -2;
+    std::atomic<bool> map_failed_{false}; // a peer's IPC handle could not be opened: stop voting for xGMI
 
     static std::shared_ptr<IpcArena> create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
                                             uint32_t group);
