@@ -356,6 +356,8 @@ StripePlan plan_stripes(size_t bytes, size_t conns) {
 // sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any order across
 // stripes, in order within a stripe). `before_rx` (optional) runs after the senders started and before the receive
 // sinks are posted (the quantized steps receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
+constexpr size_t kInlineSendBytes = 256 << 10;
+
 int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
                  const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
@@ -386,10 +388,15 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
             tx_ctr += n;
         }
     };
+    // Small steps send on this thread after posting the sinks (a thread start costs more than the transfer; the
+    // peer's bytes land in the posted sinks meanwhile, so the blocking send cannot deadlock against the peer's).
+    const bool inline_send = tx_bytes <= kInlineSendBytes;
     std::vector<std::thread> senders;
-    senders.reserve(tp.off.size());
-    for (size_t k = 0; k < tp.off.size(); ++k)
-        if (tp.len[k] > 0) senders.emplace_back(send_stripe, k);
+    if (!inline_send) {
+        senders.reserve(tp.off.size());
+        for (size_t k = 0; k < tp.off.size(); ++k)
+            if (tp.len[k] > 0) senders.emplace_back(send_stripe, k);
+    }
     if (before_rx) {
         if (const int brc = before_rx()) {
             send_rc.store(brc);
@@ -399,6 +406,9 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
     }
     for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
     sinks_posted = true;
+    if (inline_send)
+        for (size_t k = 0; k < tp.off.size(); ++k)
+            if (tp.len[k] > 0) send_stripe(k);
 
     std::vector<size_t> done(rp.off.size(), 0); // elements consumed per stripe
     size_t remaining = rp.off.size();

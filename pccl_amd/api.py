@@ -8,6 +8,7 @@ HIP backend (xGMI between peers on one host, pinned-memory staging over TCP othe
 from __future__ import annotations
 
 import ctypes
+import functools
 import importlib
 import logging
 import time
@@ -165,6 +166,7 @@ class DataType(Enum):
         return m[dt]
 
 
+@functools.lru_cache(maxsize=None)
 def _torch_map():
     m = {torch.uint8: DataType.UINT8, torch.int8: DataType.INT8, torch.int16: DataType.INT16,
          torch.int32: DataType.INT32, torch.int64: DataType.INT64, torch.float16: DataType.FLOAT16,

@@ -43,8 +43,10 @@ def test_shared_state_catch_up_crc32c(device):
     assert r["content_ok"] and r["joiner_rx_bytes"] == r["bytes"]
 
 
-def test_basic_reduce():
-    r = _run("basic_reduce.py", "--iters", "30", "--tensors", "4", "--numel", "65536", "--pool", "4")
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_basic_reduce(device):
+    r = _run("basic_reduce.py", "--iters", "30", "--tensors", "4", "--numel", "65536", "--pool", "4",
+             "--device", device)
     assert r["latency_us"]["median"] > 0
     assert r["multi_tensor"]["busbw_GBps"] > 0
 
