@@ -134,6 +134,10 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     const uint64_t tag = op->req.tag;
     OpTrace trace;
     current_trace() = trace_ops_enabled() ? &trace : nullptr;
+    char range_name[96];
+    std::snprintf(range_name, sizeof(range_name), "pccl all_reduce tag %llu bytes %zu",
+                  static_cast<unsigned long long>(tag), op->req.count * dtype_size(op->req.dtype));
+    RoctxRange range(range_name);
     bool success = false, abort_seen = false;
     uint64_t seq = 0;
     bool commenced = false;

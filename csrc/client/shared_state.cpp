@@ -14,6 +14,7 @@
 #include <map>
 
 #include "../common/log.hpp"
+#include "../common/trace.hpp"
 #include "../kernels/host_kernels.hpp"
 #include "../net/socket.hpp"
 #include "client.hpp"
@@ -114,6 +115,7 @@ static bool verify_hash(Client *, const SSEntry &e, uint64_t expected, HashType 
 }
 
 bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
+    RoctxRange range("pccl sync_shared_state");
     info = SSInfo{};
     if (!accepted_ || !master_.is_open()) return false;
     if (any_collective_running()) return false;

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <dlfcn.h>
 #include <mutex>
 #include <unistd.h>
 
@@ -72,6 +73,28 @@ bool trace_ops_enabled() {
         return e != nullptr && e[0] != '\0' && e[0] != '0';
     }();
     return v;
+}
+const Roctx &roctx() {
+    static const Roctx r = [] {
+        Roctx x;
+        const char *e = std::getenv("PCCL_ROCTX");
+        if (e != nullptr && e[0] == '0') return x;
+        void *h = nullptr;
+        for (const char *lib : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                                "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"})
+            if ((h = dlopen(lib, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        if (h == nullptr) return x;
+        auto push = reinterpret_cast<int (*)(const char *)>(dlsym(h, "roctxRangePushA"));
+        auto pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        auto mark = reinterpret_cast<void (*)(const char *)>(dlsym(h, "roctxMarkA"));
+        if (push && pop && mark) {
+            x.push = push;
+            x.pop = pop;
+            x.mark = mark;
+        }
+        return x;
+    }();
+    return r;
 }
 OpTrace *&current_trace() {
     thread_local OpTrace *t = nullptr;

@@ -32,8 +32,32 @@ struct OpTrace {
 };
 
 OpTrace *&current_trace();
+
+// roctx ranges / markers for rocprofv3 (`--marker-trace`): the roctx library is dlopen'ed on first use (absent on
+// CPU-only hosts: every call is then a no-op); PCCL_ROCTX=0 disables. Collectives and shared-state syncs are ranges,
+// their protocol phases (the trace_mark points) are markers, so they line up with the kernels in a timeline.
+struct Roctx {
+    int (*push)(const char *) = nullptr;
+    int (*pop)() = nullptr;
+    void (*mark)(const char *) = nullptr;
+};
+const Roctx &roctx();
+
+struct RoctxRange {
+    bool on;
+    explicit RoctxRange(const char *name) : on(roctx().push != nullptr) {
+        if (on) roctx().push(name);
+    }
+    ~RoctxRange() {
+        if (on) roctx().pop();
+    }
+    RoctxRange(const RoctxRange &) = delete;
+    RoctxRange &operator=(const RoctxRange &) = delete;
+};
+
 inline void trace_mark(const char *what) {
     if (OpTrace *t = current_trace()) t->mark(what);
+    if (const Roctx &r = roctx(); r.mark) r.mark(what);
 }
 
 } // namespace pccl
