@@ -5,6 +5,7 @@ Hybrid (RCCL in node x PCCL across nodes, peer group per local rank):
                                   torchrun --nproc-per-node 8 train_pccl.py --master <master ip:port>
 Gradients stay on the GPU (flat device buckets, device all-reduce). Shared state = params + AdamW state + iter.
 """
+import contextlib
 import json
 import os
 import sys
@@ -23,7 +24,10 @@ from pccl_amd.utils.profiler import Profiler  # noqa: E402
 
 
 def main():
-    a = parser(__doc__).parse_args()
+    ap = parser(__doc__)
+    ap.add_argument("--overlap", action="store_true",
+                    help="start each gradient bucket's all-reduce during backward (DataParallel(overlap=True))")
+    a = ap.parse_args()
     hybrid = int(os.environ.get("WORLD_SIZE", "1")) > 1
     device = device_of(a)
     if device.type == "cuda":
@@ -37,7 +41,7 @@ def main():
 
     comm = pccl.Communicator(a.master, peer_group=local_peer_group() if hybrid else 0)
     comm.connect(n_attempts=30)
-    sync = HierarchicalGradSync(model, comm) if hybrid else DataParallel(model, comm)
+    sync = HierarchicalGradSync(model, comm) if hybrid else DataParallel(model, comm, overlap=a.overlap)
     state = shared_state_for(model, opt, extra={"iter_num": iter_num})
     state.revision = start_iter
     tokens_per_iter = a.batch_size * cfg.block_size * a.grad_accum
@@ -63,11 +67,13 @@ def main():
         with prof.session("forward_backward"):
             opt.zero_grad(set_to_none=False)
             loss_acc = 0.0
-            for _ in range(a.grad_accum):
+            for micro in range(a.grad_accum):
                 x, y = data.batch(a.batch_size, cfg.block_size, device)
                 with ctx:
                     _, loss = model(x, y)
-                (loss / a.grad_accum).backward()
+                last = micro == a.grad_accum - 1
+                with sync.no_sync() if (a.overlap and not hybrid and not last) else contextlib.nullcontext():
+                    (loss / a.grad_accum).backward()
                 loss_acc += loss.item() / a.grad_accum
         with prof.session("all_reduce"):
             res = sync.sync_gradients()

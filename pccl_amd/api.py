@@ -479,10 +479,11 @@ class Communicator:
         return SharedStateSyncInfo(info.tx_bytes, info.rx_bytes)
 
     # --- all-reduce -------------------------------------------------------------------------------------------
-    def _descriptor(self, send, recv, op, tag, operand_descriptor, quantization_options):
+    def _descriptor(self, send, recv, op, tag, operand_descriptor, quantization_options, sync=True):
         if not isinstance(torch, _ModuleDummy) and isinstance(send, torch.Tensor) and isinstance(recv, torch.Tensor):
             _check_pair_torch(send, recv)
-            _sync_device(send)
+            if sync:
+                _sync_device(send)
             dtype = DataType.from_torch_dtype(send.dtype)
             sptr, rptr, n = send.data_ptr(), recv.data_ptr(), recv.numel()
         elif not isinstance(np, _ModuleDummy) and isinstance(send, np.ndarray) and isinstance(recv, np.ndarray):
@@ -510,6 +511,17 @@ class Communicator:
                          operand_descriptor: Optional[ReduceOperandDescriptor] = None,
                          quantization_options: Optional[QuantizationOptions] = None) -> AsyncReduceHandle:
         sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options)
+        handle = _native.AsyncReduceOpC()
+        PCCLError.check(C.pcclAllReduceAsync(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(handle)),
+                        "pcclAllReduceAsync")
+        return AsyncReduceHandle(handle, keepalive=(send, recv))
+
+    def _all_reduce_async_ready(self, send, recv, *, op: ReduceOp, tag: int,
+                                operand_descriptor: Optional[ReduceOperandDescriptor] = None,
+                                quantization_options: Optional[QuantizationOptions] = None) -> AsyncReduceHandle:
+        """all_reduce_async for device tensors whose producers the caller already waited for (e.g. on an event):
+        skips the current-stream synchronisation, so a comm thread does not wait for unrelated queued kernels."""
+        sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options, sync=False)
         handle = _native.AsyncReduceOpC()
         PCCLError.check(C.pcclAllReduceAsync(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(handle)),
                         "pcclAllReduceAsync")

@@ -6,16 +6,28 @@ parameter's ``.grad`` is a view into one flat buffer per (device, dtype), so a b
 communication buffer and the all-reduce runs on the device path (xGMI IPC between local peers, pinned-staged TCP ring
 otherwise) with no gather/scatter copies. Large buckets (default 1 GiB) suit 288 GB of HBM and keep per-op protocol
 overhead negligible; they are reduced concurrently (one tag each) with retry on peer churn.
+
+``overlap=True`` starts each bucket's all-reduce during the backward pass, as soon as every gradient in it has been
+accumulated (post-accumulate-grad hooks; a comm thread waits on a HIP event recorded on the producing stream, so the
+autograd thread never blocks). Gradients arrive roughly in reverse parameter order, so buckets are cut from the end
+of the flat buffer; with buckets smaller than the model, the reduction of late layers runs while the early layers are
+still back-propagating. ``sync_gradients`` launches buckets whose hooks did not all fire (unused parameters), waits
+for every op and re-reduces failed buckets through the retry path (the library restores an aborted in-place buffer,
+and the master's per-tag abort decision is the same on every peer, so all peers retry the same buckets).
 """
 from __future__ import annotations
 
+import contextlib
+import queue
+import threading
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from ..api import Communicator, QuantizationOptions, ReduceOp
-from .elastic import RetryResult, all_reduce_multiple_with_retry
+from ..api import (Communicator, DataType, DistributionHint, PCCLError, QuantizationAlgorithm, QuantizationOptions,
+                   ReduceOp, ReduceOperandDescriptor)
+from .elastic import RetryResult, all_reduce_multiple_with_retry, world_size
 
 
 class GradBuckets:
@@ -64,30 +76,42 @@ class GradBuckets:
         return out
 
 
+_FLUSH = -1  # comm-thread queue marker: everything queued before it has been launched
+
+
 class DataParallel:
     """Gradient all-reduce for a model replicated across PCCL peers.
 
     usage::
 
-        dp = DataParallel(model, comm)
+        dp = DataParallel(model, comm)             # overlap=True: buckets are reduced during backward
         loss.backward()
         res = dp.sync_gradients()        # AVG over the current world; retries on churn
         optimizer.step()
     """
 
-    def __init__(self, model: torch.nn.Module, comm: Communicator, *, bucket_bytes: int = 1 << 30,
+    def __init__(self, model: torch.nn.Module, comm: Communicator, *, bucket_bytes: Optional[int] = None,
                  op: ReduceOp = ReduceOp.AVG, max_in_flight: int = 8, tag_base: int = 1 << 20,
-                 quantization: Optional[QuantizationOptions] = None):
+                 quantization: Optional[QuantizationOptions] = None, overlap: bool = False):
         self.model = model
         self.comm = comm
-        self.bucket_bytes = bucket_bytes
+        # overlap needs several buckets per model to have anything to overlap with
+        self.bucket_bytes = bucket_bytes or ((128 << 20) if overlap else (1 << 30))
         self.op = op
         self.max_in_flight = max_in_flight
         self.tag_base = tag_base
         self.quantization = quantization
         self.buckets = GradBuckets(list(model.parameters()))
+        self.overlap = overlap
+        self._sync_enabled = True
+        self._hooks = []
+        if overlap:
+            self._setup_overlap()
 
+    # -- synchronous path ------------------------------------------------------------------------------------------
     def sync_gradients(self) -> RetryResult:
+        if self.overlap:
+            return self._finish_overlapped()
         self.buckets.rebind()
         slices = self.buckets.slices(self.bucket_bytes)
         return all_reduce_multiple_with_retry(self.comm, slices, self.op, max_in_flight=self.max_in_flight,
@@ -95,3 +119,147 @@ class DataParallel:
 
     def zero_grad(self) -> None:
         self.buckets.zero_()
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: backward passes inside do not start all-reduces (overlap mode)."""
+        prev, self._sync_enabled = self._sync_enabled, False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
+    # -- overlapped path -------------------------------------------------------------------------------------------
+    def _setup_overlap(self) -> None:
+        # buckets cut from the END of each flat buffer (reverse parameter order = backward order)
+        self._bucket_views: List[torch.Tensor] = []
+        members: List[List[torch.nn.Parameter]] = []
+        for (dev, dt), buf in self.buckets.flat.items():
+            per = max(1, self.bucket_bytes // buf.element_size())
+            ps = [p for p in self.buckets.params if (p.device, p.dtype) == (dev, dt)]
+            spans, off = [], 0
+            for p in ps:
+                spans.append((off, off + p.numel(), p))
+                off += p.numel()
+            end = buf.numel()
+            while end > 0:
+                start = max(0, end - per)
+                self._bucket_views.append(buf[start:end])
+                members.append([p for a, b, p in spans if a < end and b > start])
+                end = start
+        self._bucket_of: Dict[torch.nn.Parameter, List[int]] = {}
+        for i, ps in enumerate(members):
+            for p in ps:
+                self._bucket_of.setdefault(p, []).append(i)
+        self._need = [len(ps) for ps in members]
+        self._pending = list(self._need)
+        self._launched = [False] * len(self._bucket_views)
+        self._handles: List[Optional[object]] = [None] * len(self._bucket_views)
+        self._errors: List[BaseException] = []
+        self._q: "queue.Queue" = queue.Queue()
+        self._lock = threading.Lock()
+        self._thread = threading.Thread(target=self._comm_loop, name="pccl-ddp-comm", daemon=True)
+        self._thread.start()
+        for p in self._bucket_of:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p: torch.nn.Parameter) -> None:
+        v = self.buckets.views.get(p)
+        if v is not None and (p.grad is None or p.grad.data_ptr() != v.data_ptr()):
+            # .grad was reset to None (zero_grad(set_to_none=True)): autograd allocated a fresh tensor
+            if p.grad is not None:
+                v.copy_(p.grad)
+            p.grad = v
+        if not self._sync_enabled:
+            return
+        ready = []
+        with self._lock:
+            for i in self._bucket_of.get(p, ()):
+                self._pending[i] -= 1
+                if self._pending[i] == 0 and not self._launched[i]:
+                    self._launched[i] = True
+                    ready.append(i)
+        for i in ready:
+            ev = None
+            if self._bucket_views[i].is_cuda:  # the gradient kernels are queued, not done: hand over an event
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self._bucket_views[i].device))
+            self._q.put((i, ev, None))
+
+    def _launch(self, i: int):
+        t = self._bucket_views[i]
+        dt = DataType.from_torch_dtype(t.dtype)
+        q = self.quantization or QuantizationOptions(dt, QuantizationAlgorithm.NONE)
+        return self.comm._all_reduce_async_ready(t, t, op=self.op, tag=self.tag_base + i,
+                                                 operand_descriptor=ReduceOperandDescriptor(dt, DistributionHint.NONE),
+                                                 quantization_options=q)
+
+    def _comm_loop(self) -> None:
+        while True:
+            item = self._q.get()
+            if item is None:
+                return
+            i, ev, done = item
+            if i == _FLUSH:
+                done.set()
+                continue
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                self._handles[i] = self._launch(i)
+            except BaseException as e:  # surfaced by sync_gradients
+                self._errors.append(e)
+                self._handles[i] = None
+
+    def _finish_overlapped(self) -> RetryResult:
+        # buckets whose hooks did not all fire (unused parameters, or no_sync ended mid-step) start now; unused
+        # parameters get zero gradients like on the synchronous path
+        self.buckets.rebind()
+        with self._lock:
+            rest = [i for i, l in enumerate(self._launched) if not l]
+            for i in rest:
+                self._launched[i] = True
+        if rest and self._bucket_views[0].is_cuda:
+            torch.cuda.current_stream(self._bucket_views[0].device).synchronize()
+        for i in rest:
+            self._q.put((i, None, None))
+        # wait until the comm thread has launched everything queued so far
+        flushed = threading.Event()
+        self._q.put((_FLUSH, None, flushed))
+        flushed.wait()
+        tx = rx = 0
+        failed = []
+        for i, h in enumerate(self._handles):
+            if h is None:
+                failed.append(i)
+                continue
+            ok, _, info = h.wait()
+            if ok:
+                tx += info.tx_bytes
+                rx += info.rx_bytes
+            else:
+                failed.append(i)
+        self._handles = [None] * len(self._bucket_views)
+        with self._lock:
+            self._pending = list(self._need)
+            self._launched = [False] * len(self._bucket_views)
+        errors, self._errors = self._errors, []
+        for e in errors:
+            if not isinstance(e, PCCLError):
+                raise e
+        retries = 0
+        if failed:
+            # same buckets on every peer (per-tag abort consensus); aborted in-place buffers were restored
+            res = all_reduce_multiple_with_retry(self.comm, [self._bucket_views[i] for i in failed], self.op,
+                                                 max_in_flight=self.max_in_flight, tag_base=self.tag_base,
+                                                 quantization=self.quantization)
+            return RetryResult(res.ok, tx + res.tx_bytes, rx + res.rx_bytes, res.retries + 1, res.world_size)
+        return RetryResult(True, tx, rx, retries, world_size(self.comm))
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self.overlap and self._thread.is_alive():
+            self._q.put(None)
+            self._thread.join(timeout=10)

@@ -34,8 +34,9 @@ def _run(script, extra, device="cpu", world=2, timeout=300):
     return done
 
 
-def test_train_pccl_ddp():
-    res = _run("train_pccl.py", ["--max-iters", "6"])
+@pytest.mark.parametrize("extra", [[], ["--overlap", "--grad-accum", "2"]])
+def test_train_pccl_ddp(extra):
+    res = _run("train_pccl.py", ["--max-iters", "6", *extra])
     assert all(r["done"] and r["iter"] == 6 for r in res)
     assert res[0]["param_sum"] == res[1]["param_sum"]
 
@@ -49,8 +50,9 @@ def test_diloco(extra):
 
 
 @pytest.mark.gpu
-def test_train_pccl_ddp_gpu(hip):
-    res = _run("train_pccl.py", ["--max-iters", "6"], device="cuda")
+@pytest.mark.parametrize("extra", [[], ["--overlap"]])
+def test_train_pccl_ddp_gpu(hip, extra):
+    res = _run("train_pccl.py", ["--max-iters", "6", *extra], device="cuda")
     assert res[0]["param_sum"] == res[1]["param_sum"]
 
 
