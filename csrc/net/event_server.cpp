@@ -47,7 +47,7 @@ bool EventServer::run_async() {
     if (listen_fd_ < 0 || running_) return false;
     running_ = true;
     thread_ = std::thread([this] { loop(); });
-    loop_tid_ = thread_.get_id();
+    loop_tid_.store(thread_.get_id(), std::memory_order_release);
     return true;
 }
 
@@ -64,7 +64,7 @@ void EventServer::join() {
 }
 
 void EventServer::loop() {
-    loop_tid_ = std::this_thread::get_id();
+    loop_tid_.store(std::this_thread::get_id(), std::memory_order_release);
     std::vector<epoll_event> events(256);
     while (!stop_) {
         const int n = epoll_wait(epoll_fd_, events.data(), static_cast<int>(events.size()), 500);

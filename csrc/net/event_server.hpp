@@ -37,7 +37,7 @@ public:
     void interrupt();
     void join();
     bool running() const { return running_.load(); }
-    std::thread::id loop_thread_id() const { return loop_tid_; }
+    std::thread::id loop_thread_id() const { return loop_tid_.load(std::memory_order_acquire); }
 
     // Loop-thread only.
     bool send_raw(const SockAddr &client, uint16_t id, std::vector<uint8_t> payload);
@@ -75,7 +75,7 @@ private:
     int event_fd_ = -1;
     uint16_t port_ = 0;
     std::thread thread_;
-    std::thread::id loop_tid_;
+    std::atomic<std::thread::id> loop_tid_{};
     std::atomic<bool> running_{false};
     std::atomic<bool> stop_{false};
     std::unordered_map<int, std::unique_ptr<Client>> clients_by_fd_;

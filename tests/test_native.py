@@ -87,3 +87,39 @@ def test_sanitizer_build_unit_and_peers():
     finally:
         m.terminate()
         m.wait(timeout=60)
+
+
+@pytest.mark.skipif(os.environ.get("PCCL_TEST_SANITIZE") != "1", reason="set PCCL_TEST_SANITIZE=1 (slow build)")
+def test_tsan_build_unit_and_peers(tmp_path):
+    """ThreadSanitizer build (-DPCCL_SANITIZE_THREAD=ON, ROCm's clang: GCC 11's libtsan does not intercept
+    pthread_cond_clockwait, so every condition-variable wait looks like a lost unlock): the unit tests and a 3-peer
+    C-API run with concurrent ops (master, RX threads, striped senders, collective workers) must report no races."""
+    bdir = os.path.join(ROOT, "build-tsan")
+    out = os.path.join(bdir, "lib")
+    clang = "/opt/rocm/llvm/bin/clang"
+    env_cc = dict(os.environ, CC=clang, CXX=clang + "++")
+    subprocess.run(["cmake", "-S", ROOT, "-B", bdir, "-G", "Ninja", "-DPCCL_SANITIZE_THREAD=ON",
+                    "-DPCCL_BUILD_HIP_SUPPORT=OFF", f"-DPCCL_OUTPUT_DIR={out}", "-DCMAKE_BUILD_TYPE=RelWithDebInfo"],
+                   check=True, capture_output=True, env=env_cc)
+    subprocess.run(["ninja", "-C", bdir, "-j", "8"], check=True, capture_output=True)
+    logs = tmp_path / "tsan"
+    env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=0 report_signal_unsafe=0 log_path={logs}")
+    r = subprocess.run([os.path.join(bdir, "tests", "pccl_unit_tests")], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    port = free_port()
+    m = subprocess.Popen([os.path.join(out, "ccoip_master"), "--port", str(port)], stdout=subprocess.PIPE, text=True,
+                         env=env)
+    try:
+        m.stdout.readline()
+        peers = [subprocess.Popen([os.path.join(bdir, "tests", "pccl_reduce_peer"), str(port), "3", "6", "4",
+                                   "200003", "3"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                 for _ in range(3)]
+        for p in peers:
+            o, e = p.communicate(timeout=600)
+            assert p.returncode == 0, e[-3000:]
+    finally:
+        m.terminate()
+        m.wait(timeout=60)
+    reports = [f.read_text() for f in tmp_path.glob("tsan*")]
+    assert not any("WARNING: ThreadSanitizer" in t for t in reports), "\n".join(reports)[:5000]
