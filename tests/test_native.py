@@ -4,6 +4,7 @@ import json
 import os
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -121,5 +122,16 @@ def test_tsan_build_unit_and_peers(tmp_path):
     finally:
         m.terminate()
         m.wait(timeout=60)
+    # the Python-level scenarios (threaded peers in one process: all-reduce matrix, shared-state protocol) against
+    # the TSan library, with the clang TSan runtime preloaded into the (uninstrumented) interpreter
+    import glob
+    rt = sorted(glob.glob("/opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.tsan-x86_64.so"))[-1]
+    py_env = dict(env, PCCL_DISABLE_HIP="1", PCCL_LIBRARY=os.path.join(out, "libpccl.so"), LD_PRELOAD=rt,
+                  TSAN_OPTIONS=env["TSAN_OPTIONS"] + " ignore_noninstrumented_modules=1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
+                        os.path.join(ROOT, "tests", "test_allreduce.py"),
+                        os.path.join(ROOT, "tests", "test_shared_state_scenarios.py")],
+                       capture_output=True, text=True, env=py_env, timeout=900, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reports = [f.read_text() for f in tmp_path.glob("tsan*")]
     assert not any("WARNING: ThreadSanitizer" in t for t in reports), "\n".join(reports)[:5000]
