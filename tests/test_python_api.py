@@ -103,3 +103,32 @@ def test_build_info():
     import pccl
     info = pccl.build_info()
     assert "has_hip_support" in info and "has_cuda_support" in info
+
+
+def test_profiler_nested_sessions_report_and_trace(tmp_path):
+    """pccl_amd.utils.profiler (reference nanogptddp/profiler.py): nested sessions, totals, text report, Chrome
+    trace export, and averages over a ProfilerCollection."""
+    import json
+    import time
+
+    from pccl_amd.utils.profiler import Profiler, ProfilerCollection
+    col = ProfilerCollection()
+    for _ in range(2):
+        p = Profiler()
+        with p.session("step"):
+            with p.session("forward"):
+                time.sleep(0.002)
+            with p.session("all_reduce"):
+                time.sleep(0.001)
+        col.add(p)
+    t = col.profilers[0].totals()
+    assert set(t) == {"step", "step/forward", "step/all_reduce"}
+    assert t["step"] >= t["step/forward"] + t["step/all_reduce"] > 0
+    rep = col.profilers[0].report()
+    assert "forward" in rep and "all_reduce" in rep and "ms" in rep
+    avg = col.averages()
+    assert avg["step/forward"] >= 0.002
+    path = tmp_path / "trace.json"
+    col.chrome_trace(str(path))
+    ev = json.loads(path.read_text())["traceEvents"]
+    assert len(ev) == 6 and all(e["ph"] == "X" and e["dur"] > 0 for e in ev)
