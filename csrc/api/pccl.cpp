@@ -5,6 +5,7 @@
 #include <atomic>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <vector>
@@ -17,7 +18,18 @@
 struct pcclComm_t {
     pcclCommCreateParams_t params{};
     std::unique_ptr<pccl::client::Client> client;
+    // Control-plane calls (connect, topology update / optimisation, shared-state sync) drive one master dialogue at
+    // a time. The reference asserts they stay on the creating thread (THREAD_GUARD); here a second concurrent call
+    // is refused with pcclInvalidUsage instead of interleaving two dialogues.
+    mutable std::mutex control;
 };
+
+#define PCCL_CONTROL_GUARD(comm)                                                                                       \
+    std::unique_lock<std::mutex> control_guard((comm)->control, std::try_to_lock);                                     \
+    if (!control_guard.owns_lock()) {                                                                                  \
+        LOG(ERR) << __func__ << ": another control-plane call of this communicator is running on another thread";     \
+        return pcclInvalidUsage;                                                                                       \
+    }
 
 struct pcclMasterInstanceState_t {
     std::unique_ptr<pccl::master::Master> master;
@@ -125,6 +137,7 @@ pcclResult_t pcclConnect(pcclComm_t *comm) {
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client == nullptr, pcclInvalidUsage);
+    PCCL_CONTROL_GUARD(comm);
     const auto &p = comm->params;
     pccl::client::ClientConfig cfg;
     cfg.master = p.master_address;
@@ -151,6 +164,7 @@ pcclResult_t pcclUpdateTopology(pcclComm_t *comm) {
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
+    PCCL_CONTROL_GUARD(comm);
     if (comm->client->any_collective_running()) return pcclPendingAsyncOps;
     if (!comm->client->update_topology()) return pcclUpdateTopologyFailed;
     return pcclSuccess;
@@ -170,6 +184,7 @@ pcclResult_t pcclOptimizeTopology(const pcclComm_t *comm) {
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
+    PCCL_CONTROL_GUARD(comm);
     if (comm->client->global_world_size() <= 1) return pcclInvalidUsage;
     if (comm->client->any_collective_running()) return pcclPendingAsyncOps;
     if (!comm->client->optimize_topology()) return pcclTopologyOptimizationFailed;
@@ -303,6 +318,7 @@ pcclResult_t pcclSynchronizeSharedState(const pcclComm_t *comm, pcclSharedState_
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr && shared_state != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
+    PCCL_CONTROL_GUARD(comm);
     if (comm->client->any_collective_running()) return pcclPendingAsyncOps;
     pccl::client::SharedState ss;
     switch (strategy) {

@@ -187,3 +187,35 @@ def test_late_joiner_catches_up():
     assert rev == out[0][0] - 1
     assert torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][1], w_join + 1.0)
+
+
+def test_concurrent_control_plane_call_is_refused():
+    """A control-plane call (update_topology) while another thread of the same communicator is inside one
+    (a shared-state sync waiting for its peer) fails with INVALID_USAGE instead of interleaving two master dialogues.
+    The reference asserts such calls stay on one thread (THREAD_GUARD, ccoip_client_state.cpp:56,85,93)."""
+    go = threading.Event()
+
+    def fn(rank, comm):
+        x = np.full(1000, float(rank), dtype=np.float32)
+        st = pccl.SharedState([pccl.TensorInfo.from_numpy(x, "x")])
+        if rank == 1:
+            go.wait(30)
+            comm.sync_shared_state(st)
+            return None
+        out = {}
+        t = threading.Thread(target=lambda: out.setdefault("info", comm.sync_shared_state(st)))
+        t.start()
+        time.sleep(0.5)  # the sync is now waiting on the master for peer 1
+        try:
+            comm.update_topology()
+            refused = None
+        except pccl.PCCLError as e:
+            refused = e.result
+        finally:
+            go.set()
+        t.join(30)
+        return refused, "info" in out
+
+    with local_master() as addr:
+        res = run_threaded_peers(2, fn, address=addr)
+    assert res[0] == (pccl.Result.INVALID_USAGE, True)
