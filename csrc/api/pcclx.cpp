@@ -2,6 +2,7 @@
 // dtype arguments use the CCoIP wire encoding (pccl::DType), op uses pccl::ReduceOp, algo uses pccl::QuantAlgo.
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../common/device_backend.hpp"
@@ -74,11 +75,14 @@ PCCLX_EXPORT int pcclxQuantize(void *dst_q, const void *src, size_t count, int v
     } else {
         DeviceBackend *be = device_backend();
         if (!be) return -1;
-        double *mm = static_cast<double *>(be->alloc_pinned(16));
+        // one process-wide pinned min/max slot: a hipHostMalloc/hipHostFree pair per call cost more than the kernels
+        static std::mutex mm_mutex;
+        static double *mm = nullptr;
+        std::lock_guard<std::mutex> lk(mm_mutex);
+        if (mm == nullptr && (mm = static_cast<double *>(be->alloc_pinned(16))) == nullptr) return -1;
         be->minmax(src, count, vt, mm, nullptr);
-        be->device_sync();
+        if (!be->device_sync()) return -1;
         m = kernels::make_meta(al, vt, qt, mm[0], mm[1]);
-        be->free_pinned(mm);
         if (!be->quantize(dst_q, src, count, vt, qt, kernels::make_params(m, qt), nullptr) || !be->device_sync()) return -1;
     }
     if (meta_out) {

@@ -17,7 +17,7 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
             using O = decltype(o);
             if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
                 const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src_q, 1}});
-                const int grid = grid_for(count, pl.vec ? V : 1);
+                const int grid = grid_ew(count, pl, V);
                 auto *d = static_cast<S *>(dst);
                 auto *q = static_cast<const uint8_t *>(src_q);
                 return launch_ok([&] {
@@ -34,7 +34,9 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
                 auto *d = static_cast<S *>(dst);
                 auto *q = static_cast<const Q *>(src_q);
                 if (p.algo == QuantAlgo::MinMax)
-                    return launch_ok([&] { k_dq_minmax<E, O, Q><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec); });
+                    return launch_ok([&] {
+                        k_dq_minmax<E, O, Q><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
+                    });
                 if constexpr (sizeof(Q) <= 4) {
                     if (p.algo == QuantAlgo::ZeroPointScale)
                         return launch_ok([&] { k_dq_zps<E, O, Q><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec); });
@@ -55,7 +57,7 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
         auto *s = static_cast<const S *>(src);
         if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
             const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, 1}});
-            const int grid = grid_for(count, pl.vec ? V : 1);
+            const int grid = grid_ew(count, pl, V);
             auto *d = static_cast<uint8_t *>(dst_q);
             return launch_ok([&] {
                 if (qtype == DType::F8E4M3)
@@ -70,7 +72,8 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
             const int grid = grid_for(count, pl.vec ? V : 1);
             auto *d = static_cast<Q *>(dst_q);
             if (p.algo == QuantAlgo::MinMax)
-                return launch_ok([&] { k_q_minmax<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
+                return launch_ok(
+                    [&] { k_q_minmax<E, Q><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
             if constexpr (sizeof(Q) <= 4) {
                 if (p.algo == QuantAlgo::ZeroPointScale)
                     return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });

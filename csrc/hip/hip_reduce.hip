@@ -15,7 +15,7 @@ bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp o
             constexpr int V = vec_width<S>();
             const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src, sizeof(S)}});
             return launch_ok([&] {
-                k_reduce<E, O><<<grid_for(count, pl.vec ? V : 1), kBlock, 0, st>>>(
+                k_reduce<E, O><<<grid_ew(count, pl, V), kBlock, 0, st>>>(
                     static_cast<S *>(dst), static_cast<const S *>(src), count, pl.head, pl.vec);
             });
         });
@@ -30,7 +30,7 @@ bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_
         constexpr int V = vec_width<S>();
         const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}});
         return launch_ok([&] {
-            k_avg<E><<<grid_for(count, pl.vec ? V : 1), kBlock, 0, st>>>(static_cast<S *>(dst), count, ws, pl.head, pl.vec);
+            k_avg<E><<<grid_ew(count, pl, V), kBlock, 0, st>>>(static_cast<S *>(dst), count, ws, pl.head, pl.vec);
         });
     });
 }
