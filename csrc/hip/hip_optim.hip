@@ -1,8 +1,8 @@
 // Fused DiLoCo outer-step kernels (math in csrc/kernels/optim_common.hpp, shared with the host twin).
 //
 // Memory-bound elementwise work over the whole model: one pass reading outer/mom/pg (fp32) and writing
-// outer/mom/local instead of the ~5 passes of the unfused torch update. 4 elements per thread per iteration with
-// 16-byte fp32 vector accesses (local: 16 B for fp32, 8 B for 16-bit types); scalar tail for the remainder.
+// outer/mom/local instead of the ~5 passes of the unfused torch update. 4 elements per pack with 16-byte fp32 vector
+// accesses (local: 16 B for fp32, 8 B for 16-bit types); scalar tail for the remainder.
 #include "dispatch.hpp"
 #include "launchers.hpp"
 #include "../kernels/optim_common.hpp"
@@ -24,60 +24,74 @@ struct Local4<EF16> {
     using V = uint2;
 };
 
+__device__ __forceinline__ float4 ld4_nt(const float *p) {
+    return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p)));
+}
+__device__ __forceinline__ void st4_nt(float *p, const float4 &v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(v4u32, v), reinterpret_cast<v4u32 *>(p));
+}
+
+// Both kernels run on the tiled ew_loop_ls (kernels.hpp): kEwUnroll independent 16-byte streaming loads per operand
+// per thread, one tile per workgroup.
 template<typename E>
 __global__ __launch_bounds__(kBlock) void k_pseudo_grad(float *__restrict__ pg, const float *__restrict__ outer,
-                                                        const typename E::S *__restrict__ local, size_t n4, size_t n) {
+                                                        const typename E::S *__restrict__ local, size_t n, int vec) {
     using S = typename E::S;
     using V = typename Local4<E>::V;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-    for (size_t i = tid; i < n4; i += stride) {
-        const float4 o = reinterpret_cast<const float4 *>(outer)[i];
-        const V lv = reinterpret_cast<const V *>(local)[i];
-        const S *l = reinterpret_cast<const S *>(&lv);
-        float4 r;
-        r.x = o.x - static_cast<float>(E::ld(l[0]));
-        r.y = o.y - static_cast<float>(E::ld(l[1]));
-        r.z = o.z - static_cast<float>(E::ld(l[2]));
-        r.w = o.w - static_cast<float>(E::ld(l[3]));
-        reinterpret_cast<float4 *>(pg)[i] = r;
-    }
-    for (size_t i = n4 * 4 + tid; i < n; i += stride) pg[i] = outer[i] - static_cast<float>(E::ld(local[i]));
+    struct In {
+        float4 o;
+        V l;
+    };
+    ew_loop_ls<4, kEwUnroll>(
+        n, 0, vec, [&](size_t i) { pg[i] = outer[i] - static_cast<float>(E::ld(local[i])); },
+        [&](size_t b) { return In{ld4_nt(outer + b), *reinterpret_cast<const V *>(local + b)}; },
+        [&](size_t b, const In &x) {
+            const S *l = reinterpret_cast<const S *>(&x.l);
+            float4 r;
+            r.x = x.o.x - static_cast<float>(E::ld(l[0]));
+            r.y = x.o.y - static_cast<float>(E::ld(l[1]));
+            r.z = x.o.z - static_cast<float>(E::ld(l[2]));
+            r.w = x.o.w - static_cast<float>(E::ld(l[3]));
+            st4_nt(pg + b, r);
+        });
 }
 
 template<typename E>
 __global__ __launch_bounds__(kBlock) void k_outer_sgd(float *__restrict__ outer, float *__restrict__ mom,
                                                       const float *__restrict__ pg, typename E::S *__restrict__ local,
-                                                      size_t n4, size_t n, OuterSgdParams p) {
+                                                      size_t n, int vec, OuterSgdParams p) {
     using S = typename E::S;
     using V = typename Local4<E>::V;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-    const size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-    for (size_t i = tid; i < n4; i += stride) {
-        float4 o = reinterpret_cast<const float4 *>(outer)[i];
-        float4 m = p.first ? make_float4(0.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4 *>(mom)[i];
-        const float4 g = reinterpret_cast<const float4 *>(pg)[i];
-        outer_sgd_elem(o.x, m.x, g.x, p);
-        outer_sgd_elem(o.y, m.y, g.y, p);
-        outer_sgd_elem(o.z, m.z, g.z, p);
-        outer_sgd_elem(o.w, m.w, g.w, p);
-        reinterpret_cast<float4 *>(outer)[i] = o;
-        reinterpret_cast<float4 *>(mom)[i] = m;
-        V lv;
-        S *l = reinterpret_cast<S *>(&lv);
-        l[0] = E::st(o.x);
-        l[1] = E::st(o.y);
-        l[2] = E::st(o.z);
-        l[3] = E::st(o.w);
-        reinterpret_cast<V *>(local)[i] = lv;
-    }
-    for (size_t i = n4 * 4 + tid; i < n; i += stride) {
-        float o = outer[i], m = p.first ? 0.f : mom[i];
-        outer_sgd_elem(o, m, pg[i], p);
-        outer[i] = o;
-        mom[i] = m;
-        local[i] = E::st(o);
-    }
+    struct In {
+        float4 o, m, g;
+    };
+    ew_loop_ls<4, kEwUnroll>(
+        n, 0, vec,
+        [&](size_t i) {
+            float o = outer[i], m = p.first ? 0.f : mom[i];
+            outer_sgd_elem(o, m, pg[i], p);
+            outer[i] = o;
+            mom[i] = m;
+            local[i] = E::st(o);
+        },
+        [&](size_t b) {
+            return In{ld4_nt(outer + b), p.first ? make_float4(0.f, 0.f, 0.f, 0.f) : ld4_nt(mom + b), ld4_nt(pg + b)};
+        },
+        [&](size_t b, In x) {
+            outer_sgd_elem(x.o.x, x.m.x, x.g.x, p);
+            outer_sgd_elem(x.o.y, x.m.y, x.g.y, p);
+            outer_sgd_elem(x.o.z, x.m.z, x.g.z, p);
+            outer_sgd_elem(x.o.w, x.m.w, x.g.w, p);
+            st4_nt(outer + b, x.o);
+            st4_nt(mom + b, x.m);
+            V lv;
+            S *l = reinterpret_cast<S *>(&lv);
+            l[0] = E::st(x.o.x);
+            l[1] = E::st(x.o.y);
+            l[2] = E::st(x.o.z);
+            l[3] = E::st(x.o.w);
+            *reinterpret_cast<V *>(local + b) = lv;
+        });
 }
 
 template<typename F>
@@ -97,10 +111,10 @@ bool launch_pseudo_grad(float *pg, const float *outer, const void *local, size_t
     return with_local(lt, [&](auto e) {
         using E = decltype(e);
         const bool vec = aligned(pg, 16) && aligned(outer, 16) && aligned(local, 4 * sizeof(typename E::S));
-        const size_t n4 = vec ? count / 4 : 0;
+        const EwPlan pl{0, vec && count >= 4 ? 1 : 0};
         return launch_ok([&] {
-            k_pseudo_grad<E><<<grid_for(n4 ? n4 : count), kBlock, 0, st>>>(
-                pg, outer, static_cast<const typename E::S *>(local), n4, count);
+            k_pseudo_grad<E><<<grid_ew(count, pl, 4), kBlock, 0, st>>>(
+                pg, outer, static_cast<const typename E::S *>(local), count, pl.vec);
         });
     });
 }
@@ -112,10 +126,10 @@ bool launch_outer_sgd(float *outer, float *mom, const float *pg, void *local, si
         using E = decltype(e);
         const bool vec = aligned(outer, 16) && aligned(mom, 16) && aligned(pg, 16) &&
                          aligned(local, 4 * sizeof(typename E::S));
-        const size_t n4 = vec ? count / 4 : 0;
+        const EwPlan pl{0, vec && count >= 4 ? 1 : 0};
         return launch_ok([&] {
-            k_outer_sgd<E><<<grid_for(n4 ? n4 : count), kBlock, 0, st>>>(
-                outer, mom, pg, static_cast<typename E::S *>(local), n4, count, p);
+            k_outer_sgd<E><<<grid_ew(count, pl, 4), kBlock, 0, st>>>(
+                outer, mom, pg, static_cast<typename E::S *>(local), count, pl.vec, p);
         });
     });
 }
