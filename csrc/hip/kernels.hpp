@@ -485,6 +485,71 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int n
     }
 }
 
+// Tiled variant of k_multi_reduce_vec: workgroup t owns the contiguous tile [t*kBlock*U, (t+1)*kBlock*U) of vectors
+// (walking tiles blockIdx.x, blockIdx.x + gridDim.x, ...), every source read with non-temporal 16-byte loads so the
+// streamed operands do not evict each other from L2; U x nsrc loads in flight per thread. Same fixed peer order and
+// single rounding as k_multi_reduce_vec (bit-identical results).
+template<typename E, typename Op, bool AVG, int U = 4>
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_tile(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec) {
+    using S = typename E::S;
+    using C = typename E::C;
+    constexpr int V = Vec<E>::N;
+    constexpr size_t T = static_cast<size_t>(kBlock) * U;
+    const size_t ntiles = (nvec + T - 1) / T;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t base = t * T + threadIdx.x;
+        size_t idx[U];
+        bool has[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t j = base + static_cast<size_t>(u) * kBlock;
+            has[u] = j < nvec;
+            idx[u] = has[u] ? j : base; // base < nvec for every thread that has u = 0 work; clamped loads are discarded
+        }
+        if (!has[0]) continue;
+        C acc[U][V];
+        {
+            uint4 a[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) a[u] = nt_load(static_cast<const uint4 *>(srcs.p[0]) + idx[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const S *s0 = reinterpret_cast<const S *>(&a[u]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc[u][e] = E::ld(s0[e]);
+            }
+        }
+#pragma unroll 4
+        for (int k = 1; k < nsrc; ++k) {
+            uint4 a[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) a[u] = nt_load(static_cast<const uint4 *>(srcs.p[k]) + idx[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const S *s1 = reinterpret_cast<const S *>(&a[u]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc[u][e] = apply_op<Op, C>(acc[u][e], E::ld(s1[e]));
+            }
+        }
+        uint4 out[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            S *o = reinterpret_cast<S *>(&out[u]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (AVG) acc[u][e] = static_cast<C>(acc[u][e] / static_cast<C>(nsrc));
+                o[e] = E::st(acc[u][e]);
+            }
+        }
+#pragma unroll 4
+        for (int k = 0; k < ndst; ++k) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
+        }
+    }
+}
+
 template<typename E, typename Op, bool AVG>
 __global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t n,
                                                                 size_t begin) {

@@ -105,6 +105,19 @@ def test_multi_reduce(hip, dtype, nsrc, op):
     assert torch.equal(out2.cpu(), ref)
 
 
+def test_multi_reduce_more_tiles_than_workgroups(hip):
+    """Large shard: more vector tiles than the 512-workgroup budget, so each workgroup walks several tiles (plus a
+    partial last tile and a scalar tail)."""
+    n = 5_000_000 + 3
+    srcs = [_rand(n, torch.bfloat16, 60 + k) for k in range(3)]
+    ref = (srcs[0].float() + srcs[1].float() + srcs[2].float()).bfloat16()
+    outs = [torch.empty(n, dtype=torch.bfloat16, device=hip)]
+    got = K.multi_reduce([s.to(hip) for s in srcs], "sum", outs=outs)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref)
+    assert torch.equal(outs[0].cpu(), ref)
+
+
 @pytest.mark.parametrize("ndst", [1, 2, 8, 16])
 @pytest.mark.parametrize("misalign", [0, 3])
 def test_multi_reduce_broadcast(hip, ndst, misalign):
