@@ -13,7 +13,7 @@ def short(name: str) -> str:
 
 
 def main(path: str) -> None:
-    c = sqlite3.connect(path)
+    c = sqlite3.connect(f"file:{path}?mode=ro", uri=True)  # never creates a database
     rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     print(f"# rocprofv3 kernel summary: `{path.split('/')[-1]}`\n")
     print("| kernel | calls | total (us) | avg (us) | % |")
@@ -23,7 +23,7 @@ def main(path: str) -> None:
     try:
         q = ("select name, count(*), sum(end-start), avg(end-start), max(grid_x), max(workgroup_x), max(vgpr_count), "
              "max(sgpr_count), max(lds_size) from kernels group by name order by sum(end-start) desc limit 12")
-        print("\n| kernel | calls | total (us) | avg (us) | grid_x | wg | VGPR | SGPR | LDS |")
+        print("\n| kernel | calls | total (us) | avg (us) | grid (threads) | wg | VGPR | SGPR | LDS |")
         print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
         for name, n, tot, avg, gx, wg, vg, sg, lds in c.execute(q):
             print(f"| `{short(name)}` | {n} | {tot / 1e3:.1f} | {avg / 1e3:.1f} | {gx} | {wg} | {vg} | {sg} | {lds} |")
@@ -39,4 +39,6 @@ def main(path: str) -> None:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) != 2 or sys.argv[1].startswith("-"):
+        sys.exit(__doc__)
     main(sys.argv[1])
