@@ -1,25 +1,35 @@
-"""Flagship benchmark: ring all-reduce of a 1 GiB bf16 HIP device buffer per peer (BASELINE.json config 2).
+"""Flagship benchmark — BASELINE.json config 2: ring all-reduce (SUM) of a 1 GiB bf16 HIP device buffer per peer,
+8 peers, over the loopback-TCP device ring.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--peers 8] [--mib 1024] [--quick]
 
-N == 1 : two peers (threads of this process) share cuda:0 — an all-reduce needs >= 2 peers.
-N  > 1 : launched by torch.distributed.run, one peer per GPU (LOCAL_RANK); rank 0 also hosts the CCoIP master.
-         torch.distributed (gloo) is used only for the bench's own barriers / max-over-ranks and to share the port.
+Layout: the job always has ``--peers`` peers (default 8, the config's peer count), spread evenly over the N GPUs:
+  N == 1 : all 8 peers are threads of this process on cuda:0 (as literally as one GPU allows).
+  N  > 1 : launched by torch.distributed.run, one process per GPU (LOCAL_RANK), 8/N peer threads per process;
+           rank 0 also hosts the CCoIP master. torch.distributed (gloo) only carries the bench's own barriers,
+           the master port and the max-over-ranks of the timings.
+The total work (8 x 1 GiB) is fixed as N grows, so ``scaling`` is "strong".
 
-Each timed step is one pcclAllReduce(SUM) of the whole buffer on every peer. Peers on one host rendezvous in shared
-memory and reduce over xGMI (DEVICE_IPC path); the ring over loopback TCP is the fallback (PCCL_DISABLE_IPC=1).
+Headline (``value``): the TCP device ring (PCCL_DISABLE_IPC=1 — peers do not short-circuit to xGMI): every ring step
+stages HBM -> pinned host (hipMemcpyAsync), sends over loopback TCP and reduces the received bytes into HBM with the
+HIP reduce kernel. ``value`` is the whole-job aggregate bus bandwidth = sum over the peers of the nccl-tests busBW,
+busBW = (bytes / t) * 2 (n - 1) / n; ``extra.bus_bw_per_peer_GBps`` is the per-peer busBW and
+``extra.ref_metric_rx_plus_tx_per_peer_GBps`` the reference's own metric ((rx + tx) / t per peer,
+reference tests/basic_reduce_test/main.cpp:141-143).
 
-Reported: ``value`` = whole-job aggregate bus bandwidth = n_peers x busBW, with the nccl-tests convention
-busBW = (bytes / t) x 2 (n - 1) / n. ``extra`` carries per-peer busBW/algBW and the reference's own metric,
-(rx_bytes + tx_bytes) / t per peer (reference tests/basic_reduce_test/main.cpp:141-143).
-vs_baseline = value / 5.625 GB/s (the reference's best published all-reduce throughput, 45 Gbit/s,
-docs/md/01_Introduction.md:8).
+``extra`` also carries, measured in the same run: the xGMI/IPC path at the same peers (the library's default for
+same-host peers), 2 peers over IPC (N == 1), a busBW-vs-size sweep for both paths, small-message latencies
+(2-peer 4-element CPU all-reduce = BASELINE config 1; 1 MiB over IPC) and the peer-rejoin latency.
+
+vs_baseline is null: the reference publishes only WAN throughputs (25 / 45 Gbit/s), which are not
+comparable with a single-host loopback/HBM measurement.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import threading
 import time
@@ -27,7 +37,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BASELINE_GBPS = 45e9 / 8 / 1e9  # 45 Gbit/s
+METRIC = "all-reduce bus BW (GB/s) vs tensor bytes, 2/4/8 peers; peer-rejoin latency"
 
 
 def _args():
@@ -35,175 +45,328 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mib", type=int, default=1024, help="buffer size per peer in MiB (flagship: 1024)")
-    ap.add_argument("--peers-per-gpu", type=int, default=0, help="N==1 only: peers sharing cuda:0 (default 2)")
-    ap.add_argument("--path", default="auto", choices=["auto", "ring"],
-                    help="auto: xGMI IPC between same-host peers; ring: force the pipelined TCP ring")
-    ap.add_argument("--pool", type=int, default=4, help="P2P connections per neighbour (ring stripes)")
-    ap.add_argument("--rejoin", type=int, default=1, help="N==1: also measure peer-rejoin latency after the timed steps")
+    ap.add_argument("--peers", type=int, default=8, help="total peers of the job (config: 8)")
+    ap.add_argument("--mib", type=int, default=1024, help="buffer per peer in MiB (config: 1024)")
+    ap.add_argument("--pool", type=int, default=4, help="P2P connections per ring neighbour (ring stripes)")
+    ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
+    ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     return ap.parse_args()
 
 
-def _peer_loop(comm, x, y, steps, warmup, sync_all, torch, pccl):
-    """Runs warmup + timed steps; sync_all() is the cross-peer barrier. Returns (seconds, tx, rx, path)."""
-    for s in range(warmup):
-        for attempt in range(3):  # an aborted warmup op (e.g. the xGMI path fell back to TCP) is retried by all peers
+class Job:
+    """This process's share of the job: `local` peer threads on `dev`, `first` = global index of the first one."""
+
+    def __init__(self, a):
+        import torch
+        self.torch = torch
+        self.a = a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.dist = None
+        local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
+        same_gpu = os.environ.get("PCCL_BENCH_SAME_GPU") == "1"  # rehearsal of the N>1 path on a 1-GPU box
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+        self.gpu = 0 if same_gpu else local_rank
+        torch.cuda.set_device(self.gpu)
+        self.dev = torch.device("cuda", self.gpu)
+        self.total = max(a.peers, self.world)
+        self.total += (-self.total) % self.world  # equal peers per process
+        self.local = self.total // self.world
+        self.first = self.rank * self.local
+        self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
+        self.bar = threading.Barrier(self.local)
+
+    # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
+    def sync(self, i: int):
+        self.bar.wait()
+        if self.dist is not None and i == 0:
+            self.dist.barrier()
+        self.bar.wait()
+
+    def max_over_job(self, vals):
+        v = max(vals)
+        if self.dist is not None:
+            t = self.torch.tensor([v], dtype=self.torch.float64)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            v = float(t.item())
+        return v
+
+    def broadcast(self, obj):
+        if self.dist is None:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    # -- one phase: fresh master + communicators, `fn(i, comm)` on every local peer thread ------------------------
+    def phase(self, fn, *, ipc: bool, peers: int = 0, timeout: float = 900.0):
+        import pccl_amd as pccl
+        from pccl_amd.utils import free_port, peer_ports, wait_for_world
+        total = peers or self.total
+        local = total // self.world
+        if ipc:
+            os.environ.pop("PCCL_DISABLE_IPC", None)
+        else:
+            os.environ["PCCL_DISABLE_IPC"] = "1"
+        master = None
+        port = free_port() if self.rank == 0 else 0
+        if self.rank == 0:
+            master = pccl.MasterNode(f"127.0.0.1:{port}")
+            master.run()
+        port = self.broadcast(port)
+        addr = f"127.0.0.1:{port}"
+        self.addr = addr
+        ports = peer_ports(local)
+        out = [None] * local
+        errs = [None] * local
+        comms = [None] * local
+        bar = threading.Barrier(local)
+        self.bar = bar
+
+        def body(i):
             try:
-                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=s)
+                self.torch.cuda.set_device(self.dev)
+                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.a.pool, **ports[i])
+                comms[i] = c
+                c.connect(n_attempts=30)
+                wait_for_world(c, total, timeout=300)
+                out[i] = fn(i, c)
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                errs[i] = e
+                try:
+                    bar.abort()
+                except Exception:  # noqa: BLE001
+                    pass
+
+        ths = [threading.Thread(target=body, args=(i,), daemon=True) for i in range(local)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=timeout)
+        if any(t.is_alive() for t in ths):
+            raise TimeoutError("bench phase did not finish")
+        for e in errs:
+            if e is not None:
+                raise e
+        for c in comms:
+            if c is not None:
+                c.destroy()
+        if self.dist is not None:
+            self.dist.barrier()
+        if master is not None:
+            master.interrupt()
+            master.await_termination()
+        return out
+
+
+def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
+    """warmup + `steps` timed all-reduces between job-wide barriers; returns (seconds, tx, rx, path)."""
+    import pccl_amd as pccl
+    torch = job.torch
+    for s in range(warmup):
+        for attempt in range(3):  # an aborted warmup op (e.g. xGMI vote fell back) is retried by all peers
+            try:
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + s)
                 break
             except pccl.PCCLError:
                 if attempt == 2:
                     raise
     torch.cuda.synchronize()
-    sync_all()
+    job.sync(i)
     t0 = time.perf_counter()
     tx = rx = 0
     for s in range(steps):
-        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=warmup + s)
+        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + warmup + s)
         tx += info.tx_bytes
         rx += info.rx_bytes
     torch.cuda.synchronize()
-    sync_all()
-    dt = time.perf_counter() - t0
-    return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+    job.sync(i)
+    return time.perf_counter() - t0, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
 
 
-def _report(n_gpus, n_peers, steps, warmup, nbytes, dt, tx, rx, path, parallelism, rejoin_s=None):
+def _check(job, i, comm, x, y, peers):
+    """Exactness: every peer contributes (global index + 1); the bf16 sum of small integers is exact."""
     import pccl_amd as pccl
-    t = dt / steps
+    x.fill_(float(job.first + i + 1))
+    comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=999_999)
+    job.torch.cuda.synchronize()
+    want = peers * (peers + 1) / 2
+    lo, hi = float(y.min()), float(y.max())
+    return lo == hi == want
+
+
+def _bw(nbytes, t, n):
     alg = nbytes / t / 1e9
-    bus = alg * 2 * (n_peers - 1) / n_peers
-    value = bus * n_peers
-    line = {
-        "metric": "all-reduce bus BW (GB/s) vs tensor bytes, 2/4/8 peers; peer-rejoin latency",
-        "value": round(value, 3), "unit": "GB/s", "n_gpus": n_gpus, "steps": steps, "warmup": warmup,
-        "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_GBPS, 3), "dtype": "bf16",
-        "data": "synthetic (torch.randn bf16 on device)",
-        "config": {"model": "8-peer ring all-reduce, 1 GiB bf16 HIP device buffer per MI355X, loopback TCP",
-                   "global_batch": n_peers, "seq_len": nbytes // 2, "parallelism": parallelism,
-                   "tensor_bytes": nbytes, "n_peers": n_peers},
-        "extra": {"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
-                  "ref_metric_rx_plus_tx_per_peer_GBps": round((tx + rx) / steps / t / 1e9, 3),
-                  "reduce_path": pccl.ReducePath(path).name,
-                  "peer_rejoin_latency_ms": round(rejoin_s * 1e3, 1) if rejoin_s else None,
-                  "baseline_note": "vs_baseline divides the aggregate value by the reference's 45 Gbit/s "
-                                   "per-run WAN figure (no like-for-like MI355X number is published)"},
-    }
-    print(json.dumps(line), flush=True)
+    return alg, alg * 2 * (n - 1) / n
 
 
-def _rejoin_latency(comm, rank, addr, dev, bar, torch, pccl, pool):
-    """After the timed steps: a new peer connects mid-run; returns seconds from its connect() call until its first
-    all-reduce completed (admission vote + P2P establishment + IPC rendezvous + first op). Untimed for the metric."""
-    small = torch.ones(1 << 16, device=dev, dtype=torch.bfloat16)
-    out = {}
-    joiner = None
-    bar.wait()
-    if rank == 0:
-        def join():
-            c = pccl.Communicator(addr, 0, p2p_connection_pool_size=pool)
+def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
+    """Runs one phase; returns {"t": s/op (max over the job), "tx", "rx", "path", "sweep": {bytes: s/op}, "ok"}."""
+    torch = job.torch
+    total = peers or job.total
+
+    def fn(i, comm):
+        g = torch.Generator(device=job.dev).manual_seed(job.first + i)
+        n = nbytes // 2
+        x = torch.randn(n, device=job.dev, dtype=torch.bfloat16, generator=g)
+        y = torch.empty_like(x)
+        r = {"main": _timed(job, i, comm, x, y, steps, warmup)}
+        tag = 10_000
+        for b in sweep:
+            m = b // 2
+            reps = max(3, min(50, int(2e9 // max(b, 1) // 8)))
+            r[b] = _timed(job, i, comm, x[:m], y[:m], reps, 2, tag0=tag)[0] / reps
+            tag += reps + 10
+        if check:
+            r["ok"] = _check(job, i, comm, x, y, total)
+        return r
+
+    res = job.phase(fn, ipc=ipc, peers=peers)
+    dt = job.max_over_job([r["main"][0] for r in res])
+    out = {"t": dt / steps, "tx": res[0]["main"][1] / steps, "rx": res[0]["main"][2] / steps,
+           "path": res[0]["main"][3], "sweep": {}}
+    for b in sweep:
+        out["sweep"][b] = job.max_over_job([r[b] for r in res])
+    if check:
+        ok = all(r["ok"] for r in res)
+        if job.dist is not None:
+            t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+            job.dist.all_reduce(t, op=job.dist.ReduceOp.MAX)
+            ok = t.item() == 0.0
+        out["ok"] = ok
+    return out
+
+
+def latency_cpu(job, n_ops=300):
+    """BASELINE config 1: 2 peers, 4 fp32 elements, host memory; median / p99 microseconds per all-reduce."""
+    import numpy as np
+
+    import pccl_amd as pccl
+
+    def fn(i, comm):
+        x = np.arange(4, dtype=np.float32) + i
+        y = np.empty_like(x)
+        ts = []
+        for s in range(n_ops):
+            job.bar.wait()
             t0 = time.perf_counter()
-            c.connect(n_attempts=30)
-            y = torch.empty_like(small)
-            c.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=77)
-            torch.cuda.synchronize()
-            out["s"] = time.perf_counter() - t0
-            out["c"] = c
-        joiner = threading.Thread(target=join, daemon=True)
-        joiner.start()
-    deadline = time.time() + 120
-    while time.time() < deadline:
-        if comm.are_peers_pending():
-            comm.update_topology()
-            y = torch.empty_like(small)
-            comm.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=77)
-            break
-        time.sleep(0.001)
-    if joiner is not None:
-        joiner.join(timeout=120)
-        out["c"].destroy()
-    bar.wait()
+            comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=s)
+            ts.append(time.perf_counter() - t0)
+        return ts
+
+    res = job.phase(fn, ipc=False, peers=2)
+    ts = sorted(max(r[k] for r in res) for k in range(n_ops))[10:]
+    return {"median_us": round(statistics.median(ts) * 1e6, 1), "p99_us": round(ts[int(0.99 * (len(ts) - 1))] * 1e6, 1)}
+
+
+def rejoin_latency(job):
+    """A new peer connects mid-run; seconds from its connect() until its first all-reduce completed (admission vote +
+    P2P establishment + IPC rendezvous + first op). N == 1 only."""
+    import pccl_amd as pccl
+    torch = job.torch
+    out = {}
+
+    def fn(i, comm):
+        small = torch.ones(1 << 16, device=job.dev, dtype=torch.bfloat16)
+        y = torch.empty_like(small)
+        comm.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=1)
+        joiner = None
+        if i == 0:
+            def join():
+                c = pccl.Communicator(job.addr, 0, p2p_connection_pool_size=job.a.pool)
+                t0 = time.perf_counter()
+                c.connect(n_attempts=30)
+                yy = torch.empty_like(small)
+                c.all_reduce(small, yy, op=pccl.ReduceOp.SUM, tag=77)
+                torch.cuda.synchronize()
+                out["s"] = time.perf_counter() - t0
+                out["c"] = c
+            joiner = threading.Thread(target=join, daemon=True)
+            joiner.start()
+        deadline = time.time() + 120
+        while time.time() < deadline:
+            if comm.are_peers_pending():
+                comm.update_topology()
+                comm.all_reduce(small, y, op=pccl.ReduceOp.SUM, tag=77)
+                break
+            time.sleep(0.001)
+        if joiner is not None:
+            joiner.join(timeout=120)
+            if "c" in out:
+                out["c"].destroy()
+
+    job.phase(fn, ipc=True, peers=2)
     return out.get("s")
-
-
-def bench_single_gpu(a):
-    import torch
-
-    import pccl_amd as pccl
-    from pccl_amd.utils import local_master, run_threaded_peers
-    n_peers = a.peers_per_gpu or 2
-    nbytes = a.mib << 20
-    n = nbytes // 2
-    dev = torch.device("cuda:0")
-    bar = threading.Barrier(n_peers)
-
-    with local_master() as addr:
-        def fn(rank, comm):
-            torch.cuda.set_device(dev)
-            g = torch.Generator(device=dev).manual_seed(rank)
-            x = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
-            y = torch.empty_like(x)
-            r = _peer_loop(comm, x, y, a.steps, a.warmup, bar.wait, torch, pccl)
-            rejoin = _rejoin_latency(comm, rank, addr, dev, bar, torch, pccl, a.pool) if a.rejoin else None
-            return (*r, rejoin)
-
-        res = run_threaded_peers(n_peers, fn, address=addr, timeout=1800,
-                                 comm_kwargs={"p2p_connection_pool_size": a.pool})
-    dt = max(r[0] for r in res)
-    _report(1, n_peers, a.steps, a.warmup, nbytes, dt, res[0][1], res[0][2], res[0][3], f"{n_peers} peers on 1 GPU",
-            rejoin_s=res[0][4])
-
-
-def bench_multi_gpu(a):
-    import torch
-    import torch.distributed as dist
-
-    import pccl_amd as pccl
-    from pccl_amd.utils import free_port, wait_for_world
-    rank = int(os.environ["RANK"])
-    world = int(os.environ["WORLD_SIZE"])
-    local_rank = int(os.environ.get("LOCAL_RANK", rank))
-    # rehearsal on a 1-GPU box: PCCL_BENCH_SAME_GPU=1 puts every rank on cuda:0 (the real run uses one GPU per rank)
-    if os.environ.get("PCCL_BENCH_SAME_GPU") == "1":
-        local_rank = 0
-    dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    master = None
-    port = [free_port() if rank == 0 else 0]
-    if rank == 0:
-        master = pccl.MasterNode(f"127.0.0.1:{port[0]}")
-        master.run()
-    dist.broadcast_object_list(port, src=0)
-    comm = pccl.Communicator(f"127.0.0.1:{port[0]}", 0, p2p_connection_pool_size=a.pool)
-    comm.connect(n_attempts=30)
-    wait_for_world(comm, world, timeout=300)
-    nbytes = a.mib << 20
-    g = torch.Generator(device=dev).manual_seed(rank)
-    x = torch.randn(nbytes // 2, device=dev, dtype=torch.bfloat16, generator=g)
-    y = torch.empty_like(x)
-    dt, tx, rx, path = _peer_loop(comm, x, y, a.steps, a.warmup, dist.barrier, torch, pccl)
-    t = torch.tensor([dt], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    if rank == 0:
-        _report(world, world, a.steps, a.warmup, nbytes, float(t.item()), tx, rx, path, f"dp{world} (1 peer/GPU)")
-    dist.barrier()
-    comm.destroy()
-    if master is not None:
-        master.interrupt()
-        master.await_termination()
-    dist.destroy_process_group()
 
 
 def main():
     a = _args()
-    if a.path == "ring":
-        os.environ["PCCL_DISABLE_IPC"] = "1"
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        bench_multi_gpu(a)
-    else:
-        bench_single_gpu(a)
+    job = Job(a)
+    nbytes = a.mib << 20
+    P = job.total
+    extra = {}
+
+    # ---- headline: TCP device ring, P peers x 1 GiB bf16
+    ring = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=not a.quick,
+                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20))
+    import pccl_amd as pccl
+    alg, bus = _bw(nbytes, ring["t"], P)
+    path_name = pccl.ReducePath(ring["path"]).name
+    extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
+                  "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
+                  "reduce_path": path_name, "peers_per_gpu": job.local,
+                  "result_exact": ring.get("ok")})
+    sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
+                                                    "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
+                             for b, t in ring["sweep"].items()}}
+    sweep["DEVICE_RING"][f"{a.mib}MiB"] = {"ms": round(ring["t"] * 1e3, 3), "bus_bw_per_peer_GBps": round(bus, 3)}
+
+    if not a.quick and not a.no_ipc_extra:
+        # ---- same job over the xGMI/IPC path (default for same-host GPU peers)
+        ipc = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
+                      sweep=(1 << 20, 16 << 20, 256 << 20))
+        ialg, ibus = _bw(nbytes, ipc["t"], P)
+        extra["ipc_same_peers"] = {"ms_per_op": round(ipc["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(ibus, 3),
+                                   "aggregate_bus_bw_GBps": round(ibus * P, 3),
+                                   "reduce_path": pccl.ReducePath(ipc["path"]).name, "result_exact": ipc.get("ok")}
+        sweep["DEVICE_IPC"] = {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 4),
+                                                      "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
+                               for b, t in ipc["sweep"].items()}
+        sweep["DEVICE_IPC"][f"{a.mib}MiB"] = {"ms": round(ipc["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(ibus, 3)}
+        extra["latency_1MiB_ipc_us"] = round(ipc["sweep"][1 << 20] * 1e6, 1)
+        if job.world == 1:
+            two = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=2)
+            talg, tbus = _bw(nbytes, two["t"], 2)
+            extra["ipc_2_peers_1gpu"] = {"ms_per_op": round(two["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(tbus, 3),
+                                         "reduce_path": pccl.ReducePath(two["path"]).name}
+    if not a.quick and job.world == 1:
+        extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
+        r = rejoin_latency(job)
+        extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
+    extra["sweep"] = sweep
+
+    cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "
+                 f"{'loopback TCP device ring' if path_name == 'DEVICE_RING' else path_name}")
+    line = {
+        "metric": METRIC, "value": round(bus * P, 3),
+        "unit": "GB/s (job aggregate: sum over peers of per-peer busBW)",
+        "n_gpus": job.n_gpus, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ring["t"] * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (torch.randn bf16 on device)",
+        "config": {"model": cfg_model, "global_batch": P, "seq_len": nbytes // 2,
+                   "parallelism": f"{P} peers on {job.n_gpus} GPU{'s' if job.n_gpus > 1 else ''} "
+                                  f"({job.local} per GPU), reduce path {path_name}",
+                   "tensor_bytes": nbytes, "n_peers": P, "reduce_path": path_name},
+        "extra": extra,
+    }
+    if job.rank == 0:
+        print(json.dumps(line), flush=True)
+    if job.dist is not None:
+        job.dist.barrier()
+        job.dist.destroy_process_group()
 
 
 if __name__ == "__main__":
