@@ -47,7 +47,9 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--peers", type=int, default=8, help="total peers of the job (config: 8)")
     ap.add_argument("--mib", type=int, default=1024, help="buffer per peer in MiB (config: 1024)")
-    ap.add_argument("--pool", type=int, default=4, help="P2P connections per ring neighbour (ring stripes)")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="P2P connections per ring neighbour (ring stripes); 0 = 16 / peers on the host, in [1, 8]: "
+                         "8 peers x 2 stripes measured fastest on one MI355X box (profiles/r2/ring_sweep.md)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     return ap.parse_args()
@@ -78,6 +80,8 @@ class Job:
         self.first = self.rank * self.local
         self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
         self.bar = threading.Barrier(self.local)
+        if a.pool <= 0:
+            a.pool = max(1, min(8, 16 // self.total))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
@@ -317,7 +321,7 @@ def main():
     path_name = pccl.ReducePath(ring["path"]).name
     extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
                   "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
-                  "reduce_path": path_name, "peers_per_gpu": job.local,
+                  "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": a.pool,
                   "result_exact": ring.get("ok")})
     sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
                                                     "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}

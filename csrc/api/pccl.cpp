@@ -1,5 +1,6 @@
 // Public C API (include/pccl.h). Same validation / result semantics as the reference src/pccl.cpp, implemented over
 // pccl::client::Client and pccl::master::Master.
+#include <cstddef>
 #include "pccl.h"
 
 #include <atomic>
@@ -396,8 +397,17 @@ pcclResult_t pcclDestroyMaster(pcclMasterInstance_t *m) {
 pcclResult_t pcclGetBuildInfo(pcclBuildInfo_t *info) {
     PCCL_REQUIRE(info != nullptr, pcclInvalidArgument);
     pccl::DeviceBackend *be = pccl::device_backend();
-    info->has_hip_support = be != nullptr;
+    info->has_cuda_support = be != nullptr; // reference layout: exactly one bool is written
+    return pcclSuccess;
+}
+
+pcclResult_t pcclGetBuildInfoEx(pcclBuildInfoEx_t *info) {
+    PCCL_REQUIRE(info != nullptr, pcclInvalidArgument);
+    PCCL_REQUIRE(info->struct_size >= offsetof(pcclBuildInfoEx_t, hip_device_count) + sizeof(int),
+                 pcclInvalidArgument);
+    pccl::DeviceBackend *be = pccl::device_backend();
     info->has_cuda_support = be != nullptr;
+    info->has_hip_support = be != nullptr;
     info->hip_device_count = be ? be->device_count() : 0;
     return pcclSuccess;
 }

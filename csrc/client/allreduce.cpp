@@ -12,7 +12,10 @@
 //    each piece is sent as soon as its event completes; received bytes land in pinned memory and HIP kernels reduce /
 //    de-quantize them straight from pinned memory into HBM (zero-copy over PCIe), overlapped with the socket.
 #include <algorithm>
+#include <map>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <thread>
 #include <chrono>
 #include <cstring>
@@ -356,18 +359,35 @@ StripePlan plan_stripes(size_t bytes, size_t conns) {
     return s;
 }
 
-// One full-duplex ring step over the striped connections. `tx_ready(end)` blocks until payload bytes [0, end) may be
-// sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any order across
-// stripes, in order within a stripe). `before_rx` (optional) runs after the senders started and before the receive
-// sinks are posted (the quantized steps receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
+// One full-duplex ring step over the striped connections. `tx_ready(end)` blocks until payload bytes [0, end) of the
+// calling stripe may be sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any
+// order across stripes, in order within a stripe, in batches of at least `gran` bytes unless a stripe ends).
+// `before_rx` (optional) runs after the senders started and before the receive sinks are posted (the quantized steps
+// receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
+// Stripes are sent by each connection's persistent sender thread (MuxConn::post_send_job); steps of at most
+// kInlineSendBytes are sent on the calling thread after the sinks are posted.
 constexpr size_t kInlineSendBytes = 256 << 10;
+
+struct CountDown {
+    std::mutex m;
+    std::condition_variable cv;
+    size_t n = 0;
+    void done() {
+        std::lock_guard l(m);
+        if (--n == 0) cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock l(m);
+        cv.wait(l, [&] { return n == 0; });
+    }
+};
 
 int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
                  const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
                  size_t rx_bytes, size_t elem, size_t frame, const std::function<void(size_t, size_t)> &consume,
                  const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr,
-                 const std::function<int()> &before_rx = {}) {
+                 const std::function<int()> &before_rx = {}, size_t gran = 0) {
     const StripePlan tp = plan_stripes(tx_bytes, txs.size());
     const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
     auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
@@ -392,19 +412,22 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
             tx_ctr += n;
         }
     };
-    // Small steps send on this thread after posting the sinks (a thread start costs more than the transfer; the
-    // peer's bytes land in the posted sinks meanwhile, so the blocking send cannot deadlock against the peer's).
     const bool inline_send = tx_bytes <= kInlineSendBytes;
-    std::vector<std::thread> senders;
+    CountDown senders;
     if (!inline_send) {
-        senders.reserve(tp.off.size());
         for (size_t k = 0; k < tp.off.size(); ++k)
-            if (tp.len[k] > 0) senders.emplace_back(send_stripe, k);
+            if (tp.len[k] > 0) ++senders.n;
+        for (size_t k = 0; k < tp.off.size(); ++k)
+            if (tp.len[k] > 0)
+                tx_conn(k)->post_send_job([&, k] {
+                    send_stripe(k);
+                    senders.done();
+                });
     }
     if (before_rx) {
         if (const int brc = before_rx()) {
             send_rc.store(brc);
-            for (auto &t : senders) t.join();
+            senders.wait();
             return brc;
         }
     }
@@ -414,6 +437,7 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
         for (size_t k = 0; k < tp.off.size(); ++k)
             if (tp.len[k] > 0) send_stripe(k);
 
+    const size_t gran_el = std::max<size_t>(1, gran / elem);
     std::vector<size_t> done(rp.off.size(), 0); // elements consumed per stripe
     size_t remaining = rp.off.size();
     for (size_t k = 0; k < rp.off.size(); ++k)
@@ -426,7 +450,7 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
             const size_t want = rp.len[k] / elem;
             if (done[k] >= want) continue;
             const size_t have = rx_conn(k)->sink_progress(tag) / elem;
-            if (have > done[k]) {
+            if (have > done[k] && (have - done[k] >= gran_el || have >= want)) {
                 const size_t e0 = rp.off[k] / elem;
                 consume(e0 + done[k], e0 + have);
                 done[k] = have;
@@ -438,11 +462,11 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
             idle = 0;
             continue;
         }
-        // block on one unfinished stripe (round robin) for a short while
+        // block on one unfinished stripe (round robin) until its next batch is complete or a short timeout
         size_t k = rr++ % rp.off.size();
         while (done[k] >= rp.len[k] / elem) k = rr++ % rp.off.size();
         net::MuxConn *c = rx_conn(k);
-        c->wait_sink(tag, rp.len[k], 5ms);
+        c->wait_sink(tag, std::min(rp.len[k], (done[k] + gran_el) * elem), 5ms);
         if (!c->is_open() || send_rc.load() != 0) {
             rc = 1;
             break;
@@ -454,12 +478,12 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
     }
     if (rc != 0) {
         send_rc.store(rc);
-        // unblock senders stuck in send() on a dead peer: the connection is being torn down anyway
-        for (auto &t : senders) t.join();
+        // senders stuck in send() on a dead peer return once the connection is torn down
+        senders.wait();
         remove_sinks();
         return rc;
     }
-    for (auto &t : senders) t.join();
+    senders.wait();
     remove_sinks();
     if (send_rc.load() != 0) return 1;
     rx_ctr += rx_bytes;
@@ -589,17 +613,250 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
 // ------------------------------------------------------------------------------------------------------------------
 // device ring (HBM buffers, pinned staging, HIP kernels)
 // ------------------------------------------------------------------------------------------------------------------
+//
+// PCIe is the device ring's second bottleneck after the network (8 peers on one GPU share one x16 link). Measured on
+// MI355X (profiles/r2/pcie_probe.md): one copy-engine queue per direction reaches ~55 GB/s one way and ~94 GB/s full
+// duplex with >= 4 MiB copies, while 4-8 queues per direction fall to ~60 GB/s duplex, kernels reading pinned host
+// memory run at <= 57 GB/s and drop to ~60 GB/s duplex next to copy traffic, and a copy issued behind a kernel on
+// the same stream becomes a blit kernel. Hence:
+//   * every staging copy of the process goes to ONE host->device and ONE device->host stream per GPU (shared by all
+//     ops and all peers of the process); nothing is queued behind a cross-stream wait there, so ROCclr keeps them on
+//     the copy engines;
+//   * received bytes are copied into HBM staging by the copy engine and reduced HBM->HBM on the op's compute stream
+//     (cross-stream event wait, no host round trip) by k_reduce_copy, which also streams the result into pinned
+//     memory as the NEXT step's payload: a ring step's sends start the moment the previous step's last piece lands,
+//     and the only device->host copies left are the step-0 pieces of the input.
+// PCIe bytes per peer and 1 GiB: D2H 1 GiB (step-0 payload + reduced pieces), H2D 1.75 GiB (received pieces).
+
+namespace {
+
+struct PcieQueues {
+    DevStream h2d = nullptr, d2h = nullptr;
+};
+
+// process-wide copy queues of `device` (never destroyed: they may outlive static destruction order)
+PcieQueues shared_pcie_queues(DeviceBackend *be, int device) {
+    static std::mutex m;
+    static auto *q = new std::map<int, PcieQueues>();
+    std::lock_guard l(m);
+    PcieQueues &e = (*q)[device];
+    if (!e.h2d) {
+        const int cur = be->current_device();
+        be->set_device(device);
+        e.h2d = be->create_stream();
+        e.d2h = be->create_stream();
+        if (cur >= 0) be->set_device(cur);
+    }
+    return e;
+}
+
+// per-step phase marks for PCCL_TRACE_OPS (first 16 steps of each phase)
+void step_mark(bool reduce_scatter, size_t step) {
+    static const char *rs[] = {"rs0", "rs1", "rs2", "rs3", "rs4", "rs5", "rs6", "rs7",
+                               "rs8", "rs9", "rs10", "rs11", "rs12", "rs13", "rs14", "rs15"};
+    static const char *ag[] = {"ag0", "ag1", "ag2", "ag3", "ag4", "ag5", "ag6", "ag7",
+                               "ag8", "ag9", "ag10", "ag11", "ag12", "ag13", "ag14", "ag15"};
+    if (step < 16) trace_mark(reduce_scatter ? rs[step] : ag[step]);
+}
+
+// payload bytes [a, b) of a pinned staging buffer become valid once `e` has completed
+struct Staged {
+    size_t a, b;
+    DevEvent e;
+};
+
+} // namespace
+
 std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    const ReduceRequest &q = op.req;
+    if (q.qalgo != QuantAlgo::None && q.qtype != q.dtype) return ring_reduce_device_quant(op, rv, seq, device);
+    DeviceBackend *be = device_backend();
+    const size_t ws = rv.ring.size(), rank = rv.rank;
+    const size_t es = dtype_size(q.dtype);
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    // copy granularity: >= 4 MiB keeps the copy engines near their peak (1 MiB copies: ~37 GB/s)
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20)) / es * es;
+
+    be->set_device(device);
+    StreamLease stream(device);
+    DevStream st = stream.get();
+    if (!st) return {false, false};
+    PcieQueues pq;
+    StreamLease own_h2d(device), own_d2h(device);
+    if (env_size("PCCL_SHARED_COPY_QUEUES", 1) != 0) {
+        pq = shared_pcie_queues(be, device);
+    } else { // A/B switch: per-op copy streams
+        pq.h2d = own_h2d.get();
+        pq.d2h = own_d2h.get();
+    }
+    if (!pq.h2d || !pq.d2h) return {false, false};
+
+    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
+    (void) io;
+    auto aborted = [&] { return abort_received(q.tag); };
+
+    // events of this op (returned to the pool once everything they guard has completed)
+    std::vector<DevEvent> owned;
+    DevEvent last_h2d = nullptr, last_d2h = nullptr;
+    auto record = [&](DevStream s) {
+        DevEvent e = event_pool().get();
+        owned.push_back(e);
+        be->event_record(e, s);
+        return e;
+    };
+    struct Drain { // runs on every exit: nothing of this op may still touch its staging buffers / dst afterwards
+        DeviceBackend *be;
+        DevStream st;
+        DevEvent *h2d, *d2h;
+        std::vector<DevEvent> *ev;
+        ~Drain() {
+            if (*h2d) be->event_sync(*h2d);
+            if (*d2h) be->event_sync(*d2h);
+            be->stream_sync(st);
+            for (auto e : *ev) event_pool().put(e);
+        }
+    } drain{be, st, &last_h2d, &last_d2h, &owned};
+
+    Lease backup;
+    if (q.src == q.dst && !q.scratch) {
+        backup = Lease(device_pool(), bytes, device);
+        if (!backup.ok()) return {false, false};
+        be->memcpy_async(backup.data(), q.src, bytes, st);
+    } else if (q.src != q.dst) {
+        be->memcpy_async(dst, q.src, bytes, st);
+    }
+    auto restore = [&] {
+        if (last_h2d) be->event_sync(last_h2d);
+        if (last_d2h) be->event_sync(last_d2h);
+        be->stream_sync(st);
+        if (q.src == q.dst && !q.scratch) {
+            be->memcpy_async(dst, backup.data(), bytes, st);
+            be->stream_sync(st);
+        }
+    };
+    auto fail = [&](int code) -> std::pair<bool, bool> {
+        restore();
+        return {code == 2, code == 2};
+    };
+
+    const auto bounds = chunk_bounds(q.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t stage_bytes = max_chunk * es + 64;
+    Lease txa(pinned_pool(), stage_bytes), txb(pinned_pool(), stage_bytes);
+    Lease rxa(pinned_pool(), stage_bytes), rxb(pinned_pool(), stage_bytes);
+    Lease da(device_pool(), stage_bytes, device), db(device_pool(), stage_bytes, device);
+    if (!txa.ok() || !txb.ok() || !rxa.ok() || !rxb.ok() || !da.ok() || !db.ok()) return {false, false};
+    uint8_t *txbuf[2] = {txa.data(), txb.data()};
+    uint8_t *rxbuf[2] = {rxa.data(), rxb.data()};
+    uint8_t *rxdev[2] = {da.data(), db.data()};
+    std::vector<Staged> ready[2]; // staged payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    size_t txshift[2] = {0, 0};   // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
+    DevEvent sink_free[2] = {nullptr, nullptr}; // last H2D copy reading rxbuf[i]
+
+    // tx_ready over a staged payload: the sender of a stripe asks for [.., end); the range holding byte end-1 was
+    // queued after every earlier range of that stripe on the (in-order) D2H queue, so its event covers them all
+    auto ready_fn = [&](std::vector<Staged> &lst) {
+        std::sort(lst.begin(), lst.end(), [](const Staged &x, const Staged &y) { return x.a < y.a; });
+        return [&lst, be](size_t end) {
+            if (end == 0) return true;
+            auto it = std::upper_bound(lst.begin(), lst.end(), end - 1,
+                                       [](size_t v, const Staged &x) { return v < x.a; });
+            if (it == lst.begin()) return false;
+            --it;
+            return end <= it->b && be->event_sync(it->e);
+        };
+    };
+    auto always_ready = [](size_t) { return true; };
+    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
+                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume) {
+        return striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, es, piece, consume,
+                            aborted, op.tx, op.rx, {}, piece);
+    };
+
+    size_t g = 0; // global step (reduce-scatter and all-gather): alternates the double buffers
+    // ---- reduce-scatter
+    for (size_t step = 0; step + 1 < ws; ++step, ++g) {
+        const size_t cur = g % 2, nxt = cur ^ 1;
+        const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
+        const auto [ts, te] = bounds[tx_idx];
+        const auto [rs, re] = bounds[rx_idx];
+        if (sink_free[cur]) be->event_sync(sink_free[cur]);
+        if (step == 0) { // own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+            ready[cur].clear();
+            txshift[cur] = 0;
+            for (size_t off = 0; off < (te - ts) * es; off += piece) {
+                const size_t n = std::min(piece, (te - ts) * es - off);
+                be->memcpy_async(txbuf[cur] + off, static_cast<const uint8_t *>(q.src) + ts * es + off, n, pq.d2h);
+                last_d2h = record(pq.d2h);
+                ready[cur].push_back({off, off + n, last_d2h});
+            }
+        }
+        ready[nxt].clear();
+        uint8_t *region = dst + rs * es;
+        // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
+        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
+        txshift[nxt] = shift;
+        uint8_t *sink = rxbuf[cur], *stage = rxdev[cur] + shift, *out = txbuf[nxt] + shift;
+        const int rc = run_step(txbuf[cur] + txshift[cur], (te - ts) * es, ready_fn(ready[cur]), sink,
+                                (re - rs) * es, [&](size_t a, size_t b) {
+            const size_t off = a * es, n = (b - a) * es;
+            be->memcpy_async(stage + off, sink + off, n, pq.h2d);
+            last_h2d = record(pq.h2d);
+            be->stream_wait_event(st, last_h2d);
+            be->reduce_copy(region + off, stage + off, out + off, b - a, q.dtype, q.op, st);
+            ready[nxt].push_back({off, off + n, record(st)});
+        });
+        sink_free[cur] = last_h2d;
+        if (rc) return fail(rc);
+        step_mark(true, step);
+    }
+
+    trace_mark("reduce_scatter");
+    // ---- all-gather: step 0 sends the owned chunk (staged by the last reduce-scatter step), later steps forward the
+    // previous step's received bytes verbatim from pinned memory; received bytes go to HBM on the H2D queue
+    size_t cur_chunk = (rank + 1) % ws;
+    for (size_t step = 0; step + 1 < ws; ++step, ++g) {
+        const size_t cur = g % 2, prev = cur ^ 1;
+        const size_t inc = (cur_chunk + ws - 1) % ws;
+        const auto [ts, te] = bounds[cur_chunk];
+        const auto [rs, re] = bounds[inc];
+        if (sink_free[cur]) be->event_sync(sink_free[cur]);
+        uint8_t *sink = rxbuf[cur], *region = dst + rs * es;
+        auto consume = [&](size_t a, size_t b) {
+            be->memcpy_async(region + a * es, sink + a * es, (b - a) * es, pq.h2d);
+            last_h2d = record(pq.h2d);
+        };
+        const int rc = step == 0
+                           ? run_step(txbuf[cur] + txshift[cur], (te - ts) * es, ready_fn(ready[cur]), sink,
+                                      (re - rs) * es, consume)
+                           : run_step(rxbuf[prev], (te - ts) * es, always_ready, sink, (re - rs) * es, consume);
+        sink_free[cur] = last_h2d;
+        if (rc) return fail(rc);
+        step_mark(false, step);
+        cur_chunk = inc;
+    }
+    if (last_h2d) be->stream_wait_event(st, last_h2d);
+    if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
+    if (!be->stream_sync(st)) return {false, false};
+    return {true, false};
+}
+
+// Quantized device ring: per ring step the owner reduces min/max of its outgoing chunk on the GPU (the metadata
+// packet needs them on the host), then quantizes the chunk piece by piece straight into pinned memory; each piece
+// is sent as soon as its quantize kernel has finished. The receiver de-quantizes + reduces from pinned memory (the
+// wire bytes are 2-4x smaller than the values, so PCIe is not the bound here; the network is).
+std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device) {
     DeviceBackend *be = device_backend();
     const ReduceRequest &q = op.req;
     const size_t ws = rv.ring.size(), rank = rv.rank;
     const size_t es = dtype_size(q.dtype);
-    const bool quant = q.qalgo != QuantAlgo::None && q.qtype != q.dtype;
-    const size_t qs = quant ? dtype_size(q.qtype) : es;
+    const size_t qs = dtype_size(q.qtype);
     auto *dst = static_cast<uint8_t *>(q.dst);
     const size_t bytes = q.count * es;
-    const size_t chunk = net::multiplex_chunk_size();
-    const size_t piece = std::max<size_t>(1 << 20, std::min(chunk, env_size("PCCL_DEVICE_PIECE_BYTES", 4u << 20)));
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20)) / es * es;
+    const size_t piece_el = piece / es; // quantized pieces hold the same elements
 
     be->set_device(device);
     StreamLease stream(device);
@@ -628,7 +885,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     const auto bounds = chunk_bounds(q.count, ws);
     size_t max_chunk = 0;
     for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
-    const size_t stage_bytes = max_chunk * std::max(qs, es) + 64;
+    const size_t stage_bytes = max_chunk * qs + 64;
     Lease txbuf(pinned_pool(), stage_bytes), rxa(pinned_pool(), stage_bytes), rxb(pinned_pool(), stage_bytes);
     Lease mm(pinned_pool(), 64);
     if (!txbuf.ok() || !rxa.ok() || !rxb.ok() || !mm.ok()) return {false, false};
@@ -650,39 +907,43 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         }
     } eg{be, st, &events};
 
-    // quantize `n` elements at device `src` into pinned txbuf; returns meta
+    // min/max of `n` elements at device `src` (one host round trip: the meta packet carries them), then the quantize
+    // kernels of every piece into pinned txbuf, each followed by an event that releases the piece to the senders
     auto quantize_to_pinned = [&](const uint8_t *src, size_t n) -> QuantMeta {
         if (n == 0) return kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
         be->minmax(src, n, q.dtype, minmax_out, st);
         be->stream_sync(st);
         QuantMeta m = kernels::make_meta(q.qalgo, q.dtype, q.qtype, minmax_out[0], minmax_out[1]);
-        be->quantize(txbuf.data(), src, n, q.dtype, q.qtype, kernels::make_params(m, q.qtype), st);
-        be->stream_sync(st);
+        const auto params = kernels::make_params(m, q.qtype);
+        size_t k = 0;
+        for (size_t off = 0; off < n; off += piece_el, ++k) {
+            be->quantize(txbuf.data() + off * qs, src + off * es, std::min(piece_el, n - off), q.dtype, q.qtype, params,
+                         st);
+            be->event_record(ev(k), st);
+        }
         return m;
     };
+    auto quant_ready = [&](size_t end) { return end == 0 || be->event_sync(ev((end - 1) / (piece_el * qs))); };
+    auto always_ready = [](size_t) { return true; };
 
-    // one full-duplex (striped) step. `tx_ready(end)` blocks until payload bytes [0, end) may be sent.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
                         uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
-                        const std::function<int()> &before_rx = {}) -> int {
-        const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs, piece,
-                                    consume, aborted, op.tx, op.rx, before_rx);
+                        const std::function<int()> &before_rx) -> int {
+        const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs,
+                                    piece_el * qs, consume, aborted, op.tx, op.rx, before_rx, piece_el * qs);
         if (rc == 0) be->stream_sync(st); // everything consumed from `sink` has landed in HBM
         return rc;
     };
-    auto always_ready = [](size_t) { return true; };
-    // stage device bytes to pinned txbuf in pieces; tx_ready waits for the piece's event
-    auto stage_d2h = [&](const uint8_t *src, size_t n) {
-        size_t k = 0;
-        for (size_t off = 0; off < n; off += piece, ++k) {
-            be->memcpy_async(txbuf.data() + off, src + off, std::min(piece, n - off), st);
-            be->event_record(ev(k), st);
-        }
-    };
-    auto d2h_ready = [&](size_t end) { return end == 0 || be->event_sync(ev((end - 1) / piece)); };
     auto fail = [&](int code) -> std::pair<bool, bool> {
         restore();
         return {code == 2, code == 2};
+    };
+    auto meta_then = [&](QuantMeta &theirs, kernels::QuantParams &params) {
+        return [&, pt = &theirs, pp = &params] {
+            const int m = recv_meta(io, *pt, op.rx, aborted);
+            if (m == 0) *pp = kernels::make_params(*pt, q.qtype);
+            return m;
+        };
     };
 
     // ---- reduce-scatter
@@ -692,30 +953,19 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         const auto [rs, re] = bounds[rx_idx];
         uint8_t *rx_region = dst + rs * es;
         uint8_t *sink = rxbuf[step % 2];
-        int rc;
-        if (quant) {
-            QuantMeta theirs;
-            kernels::QuantParams params{};
-            const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts);
-            if (int m = send_meta(io, mine, op.tx)) return fail(m);
-            rc = run_step(txbuf.data(), (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-                be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, q.op, params, st);
-            }, [&] {
-                const int m = recv_meta(io, theirs, op.rx, aborted);
-                if (m == 0) params = kernels::make_params(theirs, q.qtype);
-                return m;
-            });
-        } else {
-            stage_d2h(dst + ts * es, (te - ts) * es);
-            rc = run_step(txbuf.data(), (te - ts) * es, d2h_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
-                be->reduce(rx_region + a * es, sink + a * es, b - a, q.dtype, q.op, st);
-            });
-        }
+        QuantMeta theirs;
+        kernels::QuantParams params{};
+        const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts);
+        if (int m = send_meta(io, mine, op.tx)) return fail(m);
+        const int rc = run_step(txbuf.data(), (te - ts) * qs, quant_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+            be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, q.op, params, st);
+        }, meta_then(theirs, params));
         if (rc) return fail(rc);
     }
 
     trace_mark("reduce_scatter");
-    // ---- all-gather
+    // ---- all-gather: the owner quantizes its finished chunk once and overwrites its own copy with D(Q(x)) (every
+    // peer ends bit-identical); received quantized chunks are forwarded verbatim
     QuantMeta prev_meta;
     size_t cur = (rank + 1) % ws;
     for (size_t step = 0; step + 1 < ws; ++step) {
@@ -725,44 +975,25 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         uint8_t *rx_region = dst + rs * es;
         uint8_t *sink = rxbuf[step % 2];
         const uint8_t *payload;
-        int rc;
-        if (quant) {
-            QuantMeta mine, theirs;
-            if (step == 0) {
-                mine = quantize_to_pinned(dst + ts * es, te - ts);
-                if (te > ts) { // parity: own chunk := D(Q(x))
-                    be->dequant_reduce(dst + ts * es, txbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set,
-                                       kernels::make_params(mine, q.qtype), st);
-                }
-                payload = txbuf.data();
-            } else {
-                mine = prev_meta;
-                payload = rxbuf[(step - 1) % 2];
-            }
-            if (int m = send_meta(io, mine, op.tx)) return fail(m);
-            kernels::QuantParams params{};
-            rc = run_step(payload, (te - ts) * qs, always_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-                be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, params, st);
-            }, [&] {
-                const int m = recv_meta(io, theirs, op.rx, aborted);
-                if (m == 0) params = kernels::make_params(theirs, q.qtype);
-                return m;
-            });
-            prev_meta = theirs;
+        QuantMeta mine, theirs;
+        std::function<bool(size_t)> ready = always_ready;
+        if (step == 0) {
+            mine = quantize_to_pinned(dst + ts * es, te - ts);
+            if (te > ts) // parity: own chunk := D(Q(x))
+                be->dequant_reduce(dst + ts * es, txbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set,
+                                   kernels::make_params(mine, q.qtype), st);
+            payload = txbuf.data();
+            ready = quant_ready;
         } else {
-            if (step == 0) {
-                stage_d2h(dst + ts * es, (te - ts) * es);
-                payload = txbuf.data();
-                rc = run_step(payload, (te - ts) * es, d2h_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
-                    be->memcpy_async(rx_region + a * es, sink + a * es, (b - a) * es, st);
-                });
-            } else {
-                payload = rxbuf[(step - 1) % 2]; // forward what we received last step, verbatim from pinned memory
-                rc = run_step(payload, (te - ts) * es, always_ready, sink, (re - rs) * es, [&](size_t a, size_t b) {
-                    be->memcpy_async(rx_region + a * es, sink + a * es, (b - a) * es, st);
-                });
-            }
+            mine = prev_meta;
+            payload = rxbuf[(step - 1) % 2];
         }
+        if (int m = send_meta(io, mine, op.tx)) return fail(m);
+        kernels::QuantParams params{};
+        const int rc = run_step(payload, (te - ts) * qs, ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+            be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, params, st);
+        }, meta_then(theirs, params));
+        prev_meta = theirs;
         if (rc) return fail(rc);
         cur = inc;
     }

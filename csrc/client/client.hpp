@@ -187,6 +187,7 @@ private:
     // returns {success, abort_received}
     std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);
     std::pair<bool, bool> ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device);
+    std::pair<bool, bool> ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     bool abort_received(uint64_t tag);

@@ -54,12 +54,17 @@ public:
     virtual bool event_record(DevEvent e, DevStream s) = 0;
     virtual int event_query(DevEvent e) = 0; // 1 complete, 0 pending, -1 error
     virtual bool event_sync(DevEvent e) = 0;
+    // work submitted to `s` after this call waits for `e` (recorded on any stream of the same device)
+    virtual bool stream_wait_event(DevStream s, DevEvent e) = 0;
     virtual bool memcpy_async(void *dst, const void *src, size_t n, DevStream s) = 0; // any direction
     virtual bool memcpy_sync(void *dst, const void *src, size_t n) = 0;
     virtual bool device_sync() = 0;
 
     // kernels
     virtual bool reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, DevStream s) = 0;
+    // dst = op(dst, src) and out = the result (out: pinned host memory, the next ring step's payload)
+    virtual bool reduce_copy(void *dst, const void *src, void *out, size_t count, DType t, ReduceOp op,
+                             DevStream s) = 0;
     virtual bool dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                                 const kernels::QuantParams &p, DevStream s) = 0;
     virtual bool quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,

@@ -141,6 +141,9 @@ public:
         return -1;
     }
     bool event_sync(DevEvent e) override { return HIP_OK(hipEventSynchronize(static_cast<hipEvent_t>(e))); }
+    bool stream_wait_event(DevStream s, DevEvent e) override {
+        return HIP_OK(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0));
+    }
     bool memcpy_async(void *dst, const void *src, size_t n, DevStream s) override {
         if (n == 0) return true;
         return HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, static_cast<hipStream_t>(s)));
@@ -153,6 +156,9 @@ public:
 
     bool reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, DevStream s) override {
         return hipk::launch_reduce(dst, src, count, t, op, static_cast<hipStream_t>(s));
+    }
+    bool reduce_copy(void *dst, const void *src, void *out, size_t count, DType t, ReduceOp op, DevStream s) override {
+        return hipk::launch_reduce_copy(dst, src, out, count, t, op, static_cast<hipStream_t>(s));
     }
     bool dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                         const kernels::QuantParams &p, DevStream s) override {

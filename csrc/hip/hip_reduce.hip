@@ -22,6 +22,27 @@ bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp o
     });
 }
 
+bool launch_reduce_copy(void *dst, const void *src, void *out, size_t count, DType t, ReduceOp op, hipStream_t st) {
+    if (count == 0) return true;
+    if (op == ReduceOp::Set) {
+        return hipMemcpyAsync(dst, src, count * dtype_size(t), hipMemcpyDefault, st) == hipSuccess &&
+               hipMemcpyAsync(out, src, count * dtype_size(t), hipMemcpyDefault, st) == hipSuccess;
+    }
+    return with_elem(t, [&](auto e) {
+        using E = decltype(e);
+        return with_op(op, [&](auto o) {
+            using O = decltype(o);
+            using S = typename E::S;
+            constexpr int V = vec_width<S>();
+            const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src, sizeof(S)}, {out, sizeof(S)}});
+            return launch_ok([&] {
+                k_reduce_copy<E, O><<<grid_ew(count, pl, V), kBlock, 0, st>>>(
+                    static_cast<S *>(dst), static_cast<const S *>(src), static_cast<S *>(out), count, pl.head, pl.vec);
+            });
+        });
+    });
+}
+
 bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_t st) {
     if (count == 0) return true;
     return with_elem(t, [&](auto e) {

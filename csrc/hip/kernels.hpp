@@ -181,6 +181,37 @@ __global__ __launch_bounds__(kBlock) void k_reduce(typename E::S *__restrict__ d
         });
 }
 
+// Device-ring reduce-scatter step, fused with the next step's staging: dst op= src (both HBM) and the result is also
+// streamed to `out` in pinned host memory (posted PCIe writes from the kernel), which is the next ring step's payload.
+// A separate device->host copy would have to wait on this kernel on another stream - and ROCclr turns copies queued
+// behind a cross-stream wait into blit kernels (measured: profiles/r2/ring_*.md) - so the producer writes it itself.
+template<typename E, typename Op>
+__global__ __launch_bounds__(kBlock) void k_reduce_copy(typename E::S *__restrict__ dst,
+                                                        const typename E::S *__restrict__ src,
+                                                        typename E::S *__restrict__ out, size_t n, size_t head,
+                                                        int vec) {
+    using S = typename E::S;
+    using C = typename E::C;
+    constexpr int V = vec_width<S>();
+    struct DS {
+        Pack<S, V> d, s;
+    };
+    ew_loop_ls<V, kEwUnroll>(
+        n, head, vec,
+        [&](size_t i) {
+            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), E::ld(src[i])));
+            dst[i] = r;
+            out[i] = r;
+        },
+        [&](size_t b) { return DS{ldp_nt<S, V>(dst + b), ldp_nt<S, V>(src + b)}; },
+        [&](size_t b, DS x) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), E::ld(x.s.v[e])));
+            stp_nt<S, V>(dst + b, x.d);
+            stp_nt<S, V>(out + b, x.d);
+        });
+}
+
 // ---------------------------------------------------------------- fused dequant + reduce
 template<typename E, typename Op, typename Q>
 __global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,

@@ -15,6 +15,7 @@ namespace pccl::hipk {
 
 // hip_reduce.hip
 bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, hipStream_t s);
+bool launch_reduce_copy(void *dst, const void *src, void *out, size_t count, DType t, ReduceOp op, hipStream_t s);
 bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_t s);
 
 // hip_quant.hip

@@ -98,6 +98,32 @@ void MuxConn::interrupt() {
 
 void MuxConn::join() {
     if (rx_thread_.joinable()) rx_thread_.join();
+    {
+        std::lock_guard l(job_mtx_);
+        jobs_stop_ = true;
+    }
+    job_cv_.notify_all();
+    if (tx_job_thread_.joinable()) tx_job_thread_.join();
+}
+
+void MuxConn::post_send_job(std::function<void()> job) {
+    std::lock_guard l(job_mtx_);
+    jobs_.push_back(std::move(job));
+    if (!tx_job_thread_.joinable() && !jobs_stop_) tx_job_thread_ = std::thread([this] { tx_job_loop(); });
+    job_cv_.notify_one();
+}
+
+void MuxConn::tx_job_loop() {
+    std::unique_lock l(job_mtx_);
+    while (true) {
+        job_cv_.wait(l, [this] { return jobs_stop_ || !jobs_.empty(); });
+        if (jobs_.empty()) return; // stopped and drained
+        auto job = std::move(jobs_.front());
+        jobs_.pop_front();
+        l.unlock();
+        job();
+        l.lock();
+    }
 }
 
 bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n) {

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <optional>
 #include <thread>
@@ -43,6 +44,10 @@ public:
 
     // ---- TX side ----
     bool send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n);
+    // Runs `job` on this connection's persistent sender thread (started on first use, FIFO). Ring steps post one
+    // job per stripe instead of starting a thread per stripe per step. A job must not wait on another job of the
+    // same connection; it may block on the socket or on device events (both finish on their own).
+    void post_send_job(std::function<void()> job);
     template<typename P>
     bool send_packet(uint64_t tag, uint64_t ctr, const P &p) {
         auto bytes = proto::encode_with_id(p);
@@ -94,6 +99,12 @@ private:
     std::atomic<bool> stop_{false};
     std::thread rx_thread_;
     std::mutex tx_mtx_;
+    void tx_job_loop();
+    std::mutex job_mtx_;
+    std::condition_variable job_cv_;
+    std::deque<std::function<void()>> jobs_;
+    std::thread tx_job_thread_;
+    bool jobs_stop_ = false;
     double sim_next_free_ = 0; // WAN emulation: time (s, steady clock) at which this flow's link is free again
     double sim_last_send_ = -1e9;
 

@@ -9,7 +9,8 @@
  *     through pinned-host staging over TCP with reduction/quantization done by CDNA4 HIP kernels.
  *   - fp16/bf16 reduction and OCP fp8 (e4m3 / e5m2) as quantized wire types.
  *   - extra communicator attributes (connection revision, ring rank, data path of the last all-reduce).
- *   - pcclGetBuildInfo reports HIP support.
+ *   - pcclGetBuildInfoEx reports HIP support and the visible HIP device count (pcclBuildInfo_t itself keeps the
+ *     reference's one-field layout: a caller built against the reference header allocates exactly that).
  */
 #ifndef PCCL_AMD_PCCL_H
 #define PCCL_AMD_PCCL_H
@@ -203,11 +204,19 @@ typedef struct pcclMasterInstanceState_t pcclMasterInstance_t;
 typedef struct pcclBuildInfo_t {
     /** True if this build can operate on GPU device memory (name kept from the reference ABI). */
     bool has_cuda_support;
-    /** [pccl-amd extension] True if the HIP (ROCm) backend is compiled in and loadable. */
-    bool has_hip_support;
-    /** [pccl-amd extension] Number of HIP devices visible (0 if none / HIP unavailable). */
-    int hip_device_count;
 } pcclBuildInfo_t;
+
+/** [pccl-amd extension] Extended build information (pcclGetBuildInfoEx). `struct_size` must be set by the caller to
+ *  sizeof(pcclBuildInfoEx_t); fields beyond it are not written, so the struct can grow without breaking callers. */
+typedef struct pcclBuildInfoEx_t {
+    size_t struct_size;
+    /** True if this build can operate on GPU device memory. */
+    bool has_cuda_support;
+    /** True if the HIP (ROCm) backend is compiled in and loadable. */
+    bool has_hip_support;
+    /** Number of HIP devices visible (0 if none / HIP unavailable). */
+    int hip_device_count;
+} pcclBuildInfoEx_t;
 
 #define PCCL_NULLABLE /* nothing */
 
@@ -283,8 +292,11 @@ PCCL_EXPORT pcclResult_t pcclMasterAwaitTermination(pcclMasterInstance_t *master
 /** Frees a master instance (after pcclMasterAwaitTermination). */
 PCCL_EXPORT pcclResult_t pcclDestroyMaster(pcclMasterInstance_t *master_instance);
 
-/** Reports build / backend information. */
+/** Reports build / backend information (reference layout: one bool). */
 PCCL_EXPORT pcclResult_t pcclGetBuildInfo(pcclBuildInfo_t *info);
+
+/** [pccl-amd extension] Extended build information; info->struct_size must be initialised by the caller. */
+PCCL_EXPORT pcclResult_t pcclGetBuildInfoEx(pcclBuildInfoEx_t *info);
 
 /** [pccl-amd extension] Size in bytes of a pcclDataType_t (0 for unknown). Fixes reference bug returning 0 for
  *  fp16/bf16/int16. */

@@ -99,7 +99,12 @@ class SharedStateSyncInfoC(Structure):
 
 
 class BuildInfoC(Structure):
-    _fields_ = [("has_cuda_support", c_bool), ("has_hip_support", c_bool), ("hip_device_count", c_int)]
+    _fields_ = [("has_cuda_support", c_bool)]  # reference layout (one bool)
+
+
+class BuildInfoExC(Structure):
+    _fields_ = [("struct_size", c_size_t), ("has_cuda_support", c_bool), ("has_hip_support", c_bool),
+                ("hip_device_count", c_int)]
 
 
 def _load() -> ctypes.CDLL:
@@ -130,6 +135,7 @@ def _load() -> ctypes.CDLL:
         "pcclMasterAwaitTermination": ([c_void_p], c_int),
         "pcclDestroyMaster": ([c_void_p], c_int),
         "pcclGetBuildInfo": ([p(BuildInfoC)], c_int),
+        "pcclGetBuildInfoEx": ([p(BuildInfoExC)], c_int),
         "pcclDataTypeSize": ([c_int], c_size_t),
         # kernel-level extension API (tests / micro-benchmarks)
         "pcclxHipDeviceCount": ([], c_int),

@@ -73,8 +73,9 @@ PCCLError.check(C.pcclInit(), "pcclInit")
 
 
 def build_info() -> Dict[str, object]:
-    bi = _native.BuildInfoC()
-    PCCLError.check(C.pcclGetBuildInfo(ctypes.byref(bi)), "pcclGetBuildInfo")
+    bi = _native.BuildInfoExC()
+    bi.struct_size = ctypes.sizeof(bi)
+    PCCLError.check(C.pcclGetBuildInfoEx(ctypes.byref(bi)), "pcclGetBuildInfoEx")
     return {"has_cuda_support": bool(bi.has_cuda_support), "has_hip_support": bool(bi.has_hip_support),
             "hip_device_count": int(bi.hip_device_count)}
 

@@ -80,6 +80,45 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
             assert torch.all(y == float(1 + 2 * j))
 
 
+@pytest.mark.parametrize("shared_queues", ["1", "0"])
+@pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
+def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, monkeypatch):
+    """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
+    chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_SHARED_COPY_QUEUES", shared_queues)
+    n = 9_000_011
+    base = (torch.arange(n, dtype=torch.int64) % 31).float()  # every partial sum < 256: exact in bf16
+    inputs = [(base + 7 * r).to(torch.bfloat16) for r in range(world)]
+    stack = torch.stack([x.float() for x in inputs])
+    if op == "sum":
+        expect = stack.sum(0)
+    elif op == "avg":
+        expect = stack.sum(0) / world
+    else:
+        expect = stack.max(0).values
+    expect = expect.to(torch.bfloat16)
+    rop = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[op]
+
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        y = x if inplace else torch.empty_like(x)
+        for tag in range(2):  # second op reuses pooled staging buffers and events
+            if tag:
+                x.copy_(inputs[rank].to(hip))
+            comm.all_reduce(x, y, op=rop, tag=tag)
+        torch.cuda.synchronize()
+        return y.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, timeout=180, comm_kwargs={"p2p_connection_pool_size": 4})
+    for y, path in res:
+        assert path == pccl.ReducePath.DEVICE_RING.value
+        assert torch.equal(y, expect)
+
+
 @pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
 def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
