@@ -87,6 +87,7 @@ static std::optional<pccl::QuantAlgo> to_qalgo(pcclQuantizationAlgorithm_t a) {
 extern "C" {
 
 pcclResult_t pcclInit(void) {
+    pccl::install_debug_backtrace_signal();
     g_initialized.store(true);
     return pcclSuccess;
 }

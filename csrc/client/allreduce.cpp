@@ -811,6 +811,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         sink_free[cur] = last_h2d;
         if (rc) return fail(rc);
         step_mark(true, step);
+        if (step == 0) fault_point("ring_step", seq);
     }
 
     trace_mark("reduce_scatter");

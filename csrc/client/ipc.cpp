@@ -27,7 +27,7 @@ using namespace std::chrono;
 namespace {
 constexpr uint64_t kMagic = 0x5043434c49504331ull; // "PCCLIPC1"
 constexpr uint32_t kClosed = 0x80000000u;
-constexpr uint32_t kSlots = 256;
+constexpr uint32_t kSlots = 128; // ops in flight per ring (slot = seq % kSlots)
 constexpr uint32_t kMaxWorld = 16;
 
 constexpr uint32_t PH_VOTED = 1, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
@@ -53,8 +53,9 @@ struct alignas(64) PeerSlotShm {
 
 // Per (op slot, peer) record. Every peer publishes where its op *input* (read by the reduce-scatter) and *output*
 // (written by its own reduce, read by the all-gather) live:
-//   zero-copy (out-of-place device buffers): input = the caller's send buffer, output = the caller's receive buffer
-//   staged (in-place or export failure):     input / output = the two halves of a pooled, exported comm buffer
+//   zero-copy (out-of-place device buffers in allocations of <= kIpcMaxExport bytes): the caller's send / receive
+//     buffer, one exported allocation + offset (n_segs = 1)
+//   staged (in-place, large allocations, export failure): a pooled comm buffer of n_segs kIpcSegBytes segments
 // Peers may mix the two modes. *_raw are usable directly by peers in the same process (threaded peers).
 struct alignas(64) OpPeerShm {
     std::atomic<uint64_t> phase; // (seq + 1) << 8 | phase
@@ -66,10 +67,11 @@ struct alignas(64) OpPeerShm {
     uint32_t zero_copy; // bit 0: input is the caller's send buffer, bit 1: output is the caller's receive buffer
     uint32_t pad;
     uint64_t gpu_uid;   // physical GPU of this op's buffers (peers sharing a GPU split its CUs)
-    uint64_t in_raw, out_raw;
-    uint64_t in_off, out_off;
-    uint8_t in_handle[kIpcHandleBytes];
-    uint8_t out_handle[kIpcHandleBytes];
+    uint32_t in_segs, out_segs;
+    uint64_t in_off, out_off; // offset into the (single) exported allocation
+    uint64_t in_raw[kIpcMaxSegs], out_raw[kIpcMaxSegs];
+    uint8_t in_handle[kIpcMaxSegs][kIpcHandleBytes];
+    uint8_t out_handle[kIpcMaxSegs][kIpcHandleBytes];
 };
 
 struct ArenaShm {
@@ -86,13 +88,19 @@ struct ArenaShm {
     static size_t bytes() { return 64 + sizeof(PeerSlotShm) * kMaxWorld + sizeof(OpPeerShm) * kSlots * kMaxWorld; }
 };
 
+// One peer's input or output as seen from this process: one contiguous mapping (offset applied) or the segments of
+// a staged comm buffer. Kernels only ever touch [x, y) ranges that do not cross a multiple of kIpcSegBytes.
+struct PeerView {
+    std::vector<uint8_t *> seg;
+    uint8_t *at(size_t x) const { return seg.size() == 1 ? seg[0] + x : seg[x / kIpcSegBytes] + x % kIpcSegBytes; }
+};
+
 struct OpCtx {
-    void *comm = nullptr;          // pooled comm buffer (input half | output half) if either side is staged
-    bool in_staged = false;        // peers read my input from the comm buffer's input half (copied in before the vote)
-    bool out_staged = false;       // peers write / gather my output into the comm buffer's output half (copied out)
-    uint8_t *my_out = nullptr;     // my output: the caller's receive buffer or the comm output half
-    std::vector<const uint8_t *> peer_in;
-    std::vector<uint8_t *> peer_out;
+    void *in_buf = nullptr, *out_buf = nullptr; // my staged comm buffers (IpcArena::CommBuf *), if any
+    bool in_staged = false;  // peers read my input from my staged input buffer (copied in before the vote)
+    bool out_staged = false; // peers write / gather my output into my staged output buffer (copied out)
+    std::vector<PeerView> in, out;
+    std::vector<IpcArena::MapKey> pins; // mappings this op holds
     size_t bytes = 0;
 };
 
@@ -226,13 +234,13 @@ IpcArena::~IpcArena() {
     DeviceBackend *be = device_backend();
     if (be) {
         const int cur = be->current_device();
-        for (auto &[key, p] : mappings_) {
+        for (auto &[key, m] : mappings_) {
             be->set_device(std::get<2>(key));
-            be->ipc_close(p);
+            be->ipc_close(m.ptr);
         }
         for (auto &b : bufs_) {
             be->set_device(b->device);
-            be->free_device(b->ptr);
+            for (void *p : b->segs) be->free_device(p);
         }
         if (cur >= 0) be->set_device(cur);
     }
@@ -248,18 +256,29 @@ IpcArena::CommBuf *IpcArena::acquire_buffer(size_t bytes, int device) {
         best->busy = true;
         return best;
     }
+    if (bytes > kIpcSegBytes * kIpcMaxSegs) return nullptr;
     DeviceBackend *be = device_backend();
     auto b = std::make_unique<CommBuf>();
-    b->cap = std::max<size_t>(bytes, 1 << 20);
     b->device = device;
     be->set_device(device);
-    b->ptr = be->alloc_device(b->cap);
-    if (!b->ptr || !be->ipc_export(b->ptr, b->handle)) {
-        if (b->ptr) be->free_device(b->ptr);
-        LOG(ERR) << "IPC arena: failed to allocate/export " << b->cap << " bytes";
-        return nullptr;
+    const size_t nseg = bytes <= kIpcSegBytes ? 1 : (bytes + kIpcSegBytes - 1) / kIpcSegBytes;
+    const size_t seg_cap = nseg == 1 ? std::max<size_t>(bytes, 1 << 20) : kIpcSegBytes;
+    auto undo = [&] {
+        for (void *p : b->segs) be->free_device(p);
+    };
+    for (size_t k = 0; k < nseg; ++k) {
+        void *p = be->alloc_device(seg_cap);
+        std::array<uint8_t, kIpcHandleBytes> h{};
+        if (!p || !be->ipc_export(p, h.data())) {
+            if (p) be->free_device(p);
+            undo();
+            LOG(ERR) << "IPC arena: failed to allocate/export a " << seg_cap << "-byte comm buffer segment";
+            return nullptr;
+        }
+        b->segs.push_back(p);
+        b->handles.push_back(h);
     }
-    b->id = next_buf_id_++;
+    b->cap = nseg * seg_cap;
     b->busy = true;
     bufs_.push_back(std::move(b));
     return bufs_.back().get();
@@ -271,41 +290,44 @@ void IpcArena::release_buffer(CommBuf *b) {
     b->busy = false;
 }
 
-void *IpcArena::peer_mapping(int peer, const uint8_t *handle, int my_device) {
+void *IpcArena::pin_mapping(int peer, const uint8_t *handle, int my_device, MapKey &key) {
     std::lock_guard l(mtx_);
     std::array<uint8_t, kIpcHandleBytes> hb;
     std::memcpy(hb.data(), handle, kIpcHandleBytes);
-    const auto key = std::make_tuple(peer, hb, my_device);
+    key = std::make_tuple(peer, hb, my_device);
     auto it = mappings_.find(key);
     if (it != mappings_.end()) {
-        auto pos = std::find(mapping_lru_.begin(), mapping_lru_.end(), key); // touch (most recently used last)
-        if (pos != mapping_lru_.end() && pos + 1 != mapping_lru_.end()) {
-            mapping_lru_.erase(pos);
-            mapping_lru_.push_back(key);
-        }
-        return it->second;
+        ++it->second.refs;
+        it->second.used = ++map_clock_;
+        return it->second.ptr;
     }
     DeviceBackend *be = device_backend();
     be->set_device(my_device);
     void *p = be->ipc_open(handle);
     if (!p) return nullptr;
-    mappings_[key] = p;
-    mapping_lru_.push_back(key);
-    // bound the number of open mappings (user allocations come and go); never evict entries of in-flight ops:
-    // those were (re)inserted at the back by this call or by the vote of the op that uses them
+    mappings_[key] = Mapping{p, 1, ++map_clock_};
+    // bound the number of open mappings (user allocations come and go): close the least recently used ones that no
+    // op holds (an op's kernels may be reading / writing through every mapping it pinned)
     constexpr size_t kMaxMappings = 256;
-    while (mapping_lru_.size() > kMaxMappings) {
-        auto old = mapping_lru_.front();
-        mapping_lru_.erase(mapping_lru_.begin());
-        auto mit = mappings_.find(old);
-        if (mit != mappings_.end()) {
-            be->set_device(std::get<2>(old));
-            be->ipc_close(mit->second);
-            mappings_.erase(mit);
-        }
+    while (mappings_.size() > kMaxMappings) {
+        auto victim = mappings_.end();
+        for (auto m = mappings_.begin(); m != mappings_.end(); ++m)
+            if (m->second.refs == 0 && (victim == mappings_.end() || m->second.used < victim->second.used)) victim = m;
+        if (victim == mappings_.end()) break; // everything is pinned by in-flight ops
+        be->set_device(std::get<2>(victim->first));
+        be->ipc_close(victim->second.ptr);
+        mappings_.erase(victim);
     }
     be->set_device(my_device);
     return p;
+}
+
+void IpcArena::unpin_mappings(const std::vector<MapKey> &keys) {
+    std::lock_guard l(mtx_);
+    for (const auto &k : keys) {
+        auto it = mappings_.find(k);
+        if (it != mappings_.end() && it->second.refs > 0) --it->second.refs;
+    }
 }
 
 bool IpcArena::export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset) {
@@ -313,6 +335,7 @@ bool IpcArena::export_user(void *p, int device, uint8_t handle[kIpcHandleBytes],
     void *base = nullptr;
     size_t size = 0;
     if (!be->address_range(p, &base, &size) || base == nullptr) return false;
+    if (size > kIpcMaxExport) return false; // see kIpcMaxExport: staged instead
     be->set_device(device);
     if (!be->ipc_export(base, handle)) return false; // e.g. VMM / expandable-segment memory: use the staged mode
     offset = static_cast<uint64_t>(static_cast<uint8_t *>(p) - static_cast<uint8_t *>(base));
@@ -439,50 +462,80 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
     }
 }
 
+namespace {
+// staged comm buffer segments <-> a contiguous device buffer (copies on `st`, not synchronised)
+bool copy_staged(DeviceBackend *be, const std::vector<void *> &segs, uint8_t *user, size_t bytes, bool to_user,
+                 DevStream st) {
+    for (size_t k = 0, off = 0; off < bytes; ++k, off += kIpcSegBytes) {
+        const size_t n = std::min(kIpcSegBytes, bytes - off);
+        uint8_t *seg = static_cast<uint8_t *>(segs[k]);
+        if (!(to_user ? be->memcpy_async(user + off, seg, n, st) : be->memcpy_async(seg, user + off, n, st)))
+            return false;
+    }
+    return true;
+}
+} // namespace
+
 int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,
                         ReduceOp op, const void *src, void *dst) {
     if (!wait_slot_free(c, seq)) {
         LOG(WARN) << "IPC: slot of op seq " << seq << " not released by a peer";
         return kAborted;
     }
-    OpPeerShm *mine = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    OpPeerShm *mine = shm_->op(slot, static_cast<uint32_t>(rank_));
     DeviceBackend *be = device_backend();
-    CommBuf *buf = nullptr;
+    CommBuf *inb = nullptr, *outb = nullptr;
     bool in_direct = false, out_direct = false;
     if (map_failed_.load(std::memory_order_relaxed)) device_ok = false; // vote for the TCP ring from now on
+    if (bytes > kIpcSegBytes * kIpcMaxSegs) device_ok = false;          // beyond the staged segments: TCP ring
+    auto publish = [](const CommBuf *b, uint32_t &nsegs, uint64_t &off, uint64_t *raw,
+                      uint8_t (*handles)[kIpcHandleBytes]) {
+        nsegs = static_cast<uint32_t>(b->segs.size());
+        off = 0;
+        for (size_t k = 0; k < b->segs.size(); ++k) {
+            raw[k] = reinterpret_cast<uint64_t>(b->segs[k]);
+            std::memcpy(handles[k], b->handles[k].data(), kIpcHandleBytes);
+        }
+    };
     if (device_ok) {
         // Direct (zero-copy) access to the caller's buffers where HIP IPC can export them. An in-place op always
         // stages its input: peers read the staged copy while results land in the caller's buffer, and the copy is
         // the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
         const bool allow_direct = !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
-        if (allow_direct && src != dst) in_direct = export_user(const_cast<void *>(src), device, mine->in_handle, mine->in_off);
-        if (allow_direct) out_direct = export_user(dst, device, mine->out_handle, mine->out_off);
-        if (in_direct) mine->in_raw = reinterpret_cast<uint64_t>(src);
-        if (out_direct) mine->out_raw = reinterpret_cast<uint64_t>(dst);
-        if (!in_direct || !out_direct) {
-            buf = acquire_buffer(2 * bytes, device);
-            if (!buf) {
+        if (allow_direct && src != dst)
+            in_direct = export_user(const_cast<void *>(src), device, mine->in_handle[0], mine->in_off);
+        if (allow_direct) out_direct = export_user(dst, device, mine->out_handle[0], mine->out_off);
+        if (in_direct) {
+            mine->in_segs = 1;
+            mine->in_raw[0] = reinterpret_cast<uint64_t>(src);
+        }
+        if (out_direct) {
+            mine->out_segs = 1;
+            mine->out_raw[0] = reinterpret_cast<uint64_t>(dst);
+        }
+        if (!in_direct) {
+            inb = acquire_buffer(bytes, device);
+            if (!inb) {
                 device_ok = false;
             } else {
-                if (!in_direct) {
-                    std::memcpy(mine->in_handle, buf->handle, kIpcHandleBytes);
-                    mine->in_off = 0;
-                    mine->in_raw = reinterpret_cast<uint64_t>(buf->ptr);
-                    // copy-in before the vote: a passed vote barrier means every peer's input is readable
-                    StreamLease stream(device);
-                    if (!stream.get() || !be->memcpy_async(buf->ptr, src, bytes, stream.get()) ||
-                        !be->stream_sync(stream.get())) {
-                        LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
-                        device_ok = false;
-                    }
-                    trace_mark("copy_in");
+                publish(inb, mine->in_segs, mine->in_off, mine->in_raw, mine->in_handle);
+                // copy-in before the vote: a passed vote barrier means every peer's input is readable
+                StreamLease stream(device);
+                if (!stream.get() ||
+                    !copy_staged(be, inb->segs, static_cast<uint8_t *>(const_cast<void *>(src)), bytes, false,
+                                 stream.get()) ||
+                    !be->stream_sync(stream.get())) {
+                    LOG(ERR) << "IPC: copy-in of " << bytes << " bytes failed";
+                    device_ok = false;
                 }
-                if (!out_direct) {
-                    std::memcpy(mine->out_handle, buf->handle, kIpcHandleBytes);
-                    mine->out_off = bytes;
-                    mine->out_raw = reinterpret_cast<uint64_t>(static_cast<uint8_t *>(buf->ptr) + bytes);
-                }
+                trace_mark("copy_in");
             }
+        }
+        if (device_ok && !out_direct) {
+            outb = acquire_buffer(bytes, device);
+            if (!outb) device_ok = false;
+            else publish(outb, mine->out_segs, mine->out_off, mine->out_raw, mine->out_handle);
         }
     }
     mine->gpu_uid = device_ok ? be->device_uid(device) : 0;
@@ -493,64 +546,83 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     mine->dtype = static_cast<uint32_t>(dtype);
     mine->op = static_cast<uint32_t>(op);
     set_phase(seq, PH_VOTED);
+    fault_point("ipc_vote", seq);
+
+    std::vector<MapKey> pins;
+    // abort after my vote was published: peers that passed the barrier may be reading my input / pushing into my
+    // output; once none can, restore an in-place caller buffer from the staged original and recycle everything
+    auto abort_voted = [&](int code) {
+        set_phase(seq, PH_ABORTED);
+        drain_peers(c, seq);
+        if (device_ok && inb && src == dst && out_direct) {
+            StreamLease stream(device);
+            if (stream.get() && copy_staged(be, inb->segs, static_cast<uint8_t *>(dst), bytes, true, stream.get()))
+                be->stream_sync(stream.get());
+        }
+        unpin_mappings(pins);
+        release_buffer(inb);
+        release_buffer(outb);
+        return code;
+    };
     const int rc = barrier(c, tag, seq, PH_VOTED);
     if (rc != 0) {
         LOG(WARN) << "IPC: vote barrier failed (rc " << rc << ")";
-        set_phase(seq, PH_ABORTED);
-        if (device_ok && buf && !in_direct && src == dst && out_direct) {
-            // peers that passed the barrier before my abort may be pushing into the caller's buffer: let them
-            // finish, then restore it from the staged copy
-            drain_peers(c, seq);
-            be->memcpy_sync(dst, buf->ptr, bytes);
-        }
-        release_buffer(buf);
-        return rc == 2 ? kAbortedByMaster : kAborted;
+        return abort_voted(rc == 2 ? kAbortedByMaster : kAborted);
     }
     bool all = true;
-    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
     for (size_t k = 0; k < ring_.size(); ++k) {
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
         all = all && p->vote == 1 && p->bytes == bytes && p->dtype == static_cast<uint32_t>(dtype) &&
-              p->op == static_cast<uint32_t>(op);
+              p->op == static_cast<uint32_t>(op) && p->in_segs >= 1 && p->in_segs <= kIpcMaxSegs &&
+              p->out_segs >= 1 && p->out_segs <= kIpcMaxSegs;
     }
     if (!all) {
         set_phase(seq, PH_RELEASED);
-        release_buffer(buf);
+        release_buffer(inb);
+        release_buffer(outb);
         return kUseRing;
     }
     OpCtx ctx;
     ctx.bytes = bytes;
-    ctx.comm = buf ? buf->ptr : nullptr;
+    ctx.in_buf = inb;
+    ctx.out_buf = outb;
     ctx.in_staged = !in_direct;
     ctx.out_staged = !out_direct;
-    ctx.my_out = out_direct ? static_cast<uint8_t *>(dst) : static_cast<uint8_t *>(buf->ptr) + bytes;
-    ctx.peer_in.resize(ring_.size());
-    ctx.peer_out.resize(ring_.size());
+    ctx.in.resize(ring_.size());
+    ctx.out.resize(ring_.size());
     for (size_t k = 0; k < ring_.size(); ++k) {
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
-        if (k == rank_ || pids_[k] == pids_[rank_]) { // same process (threaded peers): raw pointers are usable
-            ctx.peer_in[k] = reinterpret_cast<const uint8_t *>(p->in_raw);
-            ctx.peer_out[k] = reinterpret_cast<uint8_t *>(p->out_raw);
-            continue;
-        }
-        auto *in_base = static_cast<const uint8_t *>(peer_mapping(static_cast<int>(k), p->in_handle, device));
-        auto *out_base = static_cast<uint8_t *>(peer_mapping(static_cast<int>(k), p->out_handle, device));
-        if (!in_base || !out_base) {
+        const bool local = k == rank_ || pids_[k] == pids_[rank_]; // same process (threaded peers): raw pointers
+        auto view = [&](uint32_t nsegs, uint64_t off, const uint64_t *raw, const uint8_t (*handles)[kIpcHandleBytes],
+                        PeerView &v) {
+            for (uint32_t j = 0; j < nsegs; ++j) {
+                if (local) {
+                    v.seg.push_back(reinterpret_cast<uint8_t *>(raw[j]));
+                    continue;
+                }
+                MapKey key;
+                auto *base = static_cast<uint8_t *>(pin_mapping(static_cast<int>(k), handles[j], device, key));
+                if (!base) return false;
+                pins.push_back(key);
+                v.seg.push_back(base + (nsegs == 1 ? off : 0));
+            }
+            return true;
+        };
+        if (!view(p->in_segs, p->in_off, p->in_raw, p->in_handle, ctx.in[k]) ||
+            !view(p->out_segs, p->out_off, p->out_raw, p->out_handle, ctx.out[k])) {
             // e.g. no peer access between these GPUs: this op aborts (every peer sees ABORTED), and this peer
             // votes against the xGMI path from now on, so the ring falls back to TCP instead of failing every op
             LOG(ERR) << "IPC: cannot map the buffers of peer " << k << "; using the TCP ring for later ops";
             map_failed_.store(true, std::memory_order_relaxed);
-            set_phase(seq, PH_ABORTED);
-            if (buf && !in_direct && src == dst && out_direct) {
-                drain_peers(c, seq);
-                be->memcpy_sync(dst, buf->ptr, bytes);
-            }
-            release_buffer(buf);
-            return kAborted;
+            return abort_voted(kAborted);
         }
-        ctx.peer_in[k] = in_base + p->in_off;
-        ctx.peer_out[k] = out_base + p->out_off;
+        if (PCCL_LOG_ENABLED(DEBUG))
+            LOG(DEBUG) << "IPC seq " << seq << " peer " << k << " pid " << pids_[k] << " in "
+                       << static_cast<const void *>(ctx.in[k].seg[0]) << " (" << ctx.in[k].seg.size() << " segs) out "
+                       << static_cast<const void *>(ctx.out[k].seg[0]) << " (" << ctx.out[k].seg.size()
+                       << " segs) bytes " << bytes;
     }
+    ctx.pins = std::move(pins);
     {
         std::lock_guard l(g_ctx_mtx);
         g_ctx[{this, seq}] = std::move(ctx);
@@ -572,12 +644,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         ctx = std::move(it->second);
         g_ctx.erase(it);
     }
-    CommBuf *mybuf = nullptr;
-    if (ctx.comm) {
-        std::lock_guard l(mtx_);
-        for (auto &b : bufs_)
-            if (b->ptr == ctx.comm) mybuf = b.get();
-    }
+    auto *inb = static_cast<CommBuf *>(ctx.in_buf);
+    auto *outb = static_cast<CommBuf *>(ctx.out_buf);
     DeviceBackend *be = device_backend();
     be->set_device(device);
     StreamLease stream(device);
@@ -585,23 +653,25 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
-    uint8_t *my_out = ctx.my_out;
     const bool push = inter != nullptr || push_algorithm();
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
-            be->stream_sync(st); // my kernels are done: no further writes from this peer
+            if (st) be->stream_sync(st); // my kernels are done: no further accesses from this peer
             set_phase(seq, PH_ABORTED);
-            if (src == dst && ctx.in_staged && ctx.comm) {
-                // restore the caller's buffer from the staged original once no peer can still write into it
-                if (push && !ctx.out_staged) drain_peers(c, seq);
-                be->memcpy_async(dst, ctx.comm, bytes, st);
+            // peers may still be running kernels that read my input / write my output for this op: nothing is
+            // restored, recycled or handed back to the caller before every live peer is past them
+            drain_peers(c, seq);
+            if (src == dst && ctx.in_staged && inb && st) { // restore the caller's buffer from the staged original
+                copy_staged(be, inb->segs, static_cast<uint8_t *>(dst), bytes, true, st);
                 be->stream_sync(st);
             }
         } else {
             set_phase(seq, PH_RELEASED);
         }
-        release_buffer(mybuf);
+        unpin_mappings(ctx.pins);
+        release_buffer(inb);
+        release_buffer(outb);
         return {rc == 0, rc == 2};
     };
     if (!st) {
@@ -617,8 +687,17 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         lo[k] = std::min(k * per, count);
         n[k] = std::min(lo[k] + per, count) - lo[k];
     }
+    // kernels run per piece of a byte range that does not cross a staged segment boundary (same for every peer)
+    auto for_pieces = [&](size_t a_el, size_t n_el, const std::function<bool(size_t, size_t)> &fn) {
+        for (size_t a = a_el * es, b = (a_el + n_el) * es; a < b;) {
+            const size_t e = std::min(b, (a / kIpcSegBytes + 1) * kIpcSegBytes);
+            if (!fn(a, e)) return false;
+            a = e;
+        }
+        return true;
+    };
     std::vector<const void *> srcs(W);
-    for (size_t k = 0; k < W; ++k) srcs[k] = ctx.peer_in[k] + lo[rank_] * es;
+    std::vector<void *> dsts(W);
     // workgroup budget: 512 per GPU (2 per CU, the measured optimum for these streaming kernels), split between the
     // peers whose kernels run concurrently on this GPU, but not below 256 per kernel (fewer cannot saturate HBM)
     int sharing = 0;
@@ -633,22 +712,29 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push
         Lease part(device_pool(), std::max<size_t>(n[rank_] * es, 256), device);
         if (!part.ok()) return finish(1);
-        void *p = part.data();
+        uint8_t *pbase = part.data();
+        const size_t b0 = lo[rank_] * es;
         const ReduceOp local_op = op == ReduceOp::Avg ? ReduceOp::Sum : op;
-        if (!be->multi_reduce(&p, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, local_op, st, grid) ||
-            !be->stream_sync(st)) {
+        const bool reduced = for_pieces(lo[rank_], n[rank_], [&](size_t a, size_t b) {
+            for (size_t k = 0; k < W; ++k) srcs[k] = ctx.in[k].at(a);
+            void *p = pbase + (a - b0);
+            return be->multi_reduce(&p, 1, srcs.data(), static_cast<int>(W), (b - a) / es, dtype, local_op, st, grid);
+        });
+        if (!reduced || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: host-local reduce failed";
             return finish(1);
         }
         trace_mark("local_reduce");
-        if (int rc = (*inter)(p, n[rank_])) return finish(rc);
+        if (int rc = (*inter)(pbase, n[rank_])) return finish(rc);
         trace_mark("inter_host");
-        if (op == ReduceOp::Avg && n[rank_] > 0) be->finalize_avg(p, n[rank_], dtype, world, st);
-        std::vector<void *> dsts(W);
-        for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
-        const void *one = p;
-        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, n[rank_], dtype, ReduceOp::Sum, st, grid) ||
-            !be->stream_sync(st)) {
+        if (op == ReduceOp::Avg && n[rank_] > 0) be->finalize_avg(pbase, n[rank_], dtype, world, st);
+        const bool bcast = for_pieces(lo[rank_], n[rank_], [&](size_t a, size_t b) {
+            for (size_t k = 0; k < W; ++k) dsts[k] = ctx.out[k].at(a);
+            const void *one = pbase + (a - b0);
+            return be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, (b - a) / es, dtype, ReduceOp::Sum, st,
+                                    grid);
+        });
+        if (!bcast || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: host-local broadcast failed";
             return finish(1);
         }
@@ -657,20 +743,28 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         // one-shot: read shard `rank` of every peer's input (inbound xGMI), reduce in fixed peer order and write the
         // result into every peer's output (outbound xGMI, posted writes) — reduce-scatter and all-gather overlap in
         // one kernel and one barrier; every peer receives the owner's bytes, so results are bit-identical
-        std::vector<void *> dsts(W);
-        for (size_t k = 0; k < W; ++k) dsts[k] = ctx.peer_out[k] + lo[rank_] * es;
-        if (!be->multi_reduce(dsts.data(), static_cast<int>(W), srcs.data(), static_cast<int>(W), n[rank_], dtype, op,
-                              st, grid) ||
-            !be->stream_sync(st)) {
+        const bool launched = for_pieces(lo[rank_], n[rank_], [&](size_t a, size_t b) {
+            for (size_t k = 0; k < W; ++k) {
+                srcs[k] = ctx.in[k].at(a);
+                dsts[k] = ctx.out[k].at(a);
+            }
+            return be->multi_reduce(dsts.data(), static_cast<int>(W), srcs.data(), static_cast<int>(W), (b - a) / es,
+                                    dtype, op, st, grid);
+        });
+        fault_point("ipc_kernel", seq); // the kernels of every peer are in flight here
+        if (!launched || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: multi-source reduce + broadcast failed";
             return finish(1);
         }
         trace_mark("reduce_bcast");
     } else {
         // two-shot: reduce-scatter into my output, barrier, then pull every other shard (reads only)
-        void *d0 = my_out + lo[rank_] * es;
-        if (!be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), n[rank_], dtype, op, st, grid) ||
-            !be->stream_sync(st)) {
+        const bool reduced = for_pieces(lo[rank_], n[rank_], [&](size_t a, size_t b) {
+            for (size_t k = 0; k < W; ++k) srcs[k] = ctx.in[k].at(a);
+            void *d0 = ctx.out[rank_].at(a);
+            return be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), (b - a) / es, dtype, op, st, grid);
+        });
+        if (!reduced || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: multi-source reduce failed";
             return finish(1);
         }
@@ -678,11 +772,16 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         set_phase(seq, PH_REDUCED);
         if (int rc = barrier(c, tag, seq, PH_REDUCED)) return finish(rc);
         trace_mark("reduced_barrier");
-        std::vector<const void *> gsrc(W);
-        for (size_t k = 0; k < W; ++k) gsrc[k] = ctx.peer_out[k] + lo[k] * es;
-        if (!be->multi_gather(my_out, gsrc.data(), lo.data(), n.data(), static_cast<int>(W), static_cast<int>(rank_),
-                              dtype, st) ||
-            !be->stream_sync(st)) {
+        bool gathered = true;
+        for (size_t k = 0; k < W && gathered; ++k) {
+            if (k == rank_) continue;
+            gathered = for_pieces(lo[k], n[k], [&](size_t a, size_t b) {
+                const void *s = ctx.out[k].at(a);
+                const size_t off = 0, cnt = (b - a) / es;
+                return be->multi_gather(ctx.out[rank_].at(a), &s, &off, &cnt, 1, -1, dtype, st);
+            });
+        }
+        if (!gathered || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: gather failed";
             return finish(1);
         }
@@ -692,7 +791,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     if (int rc = barrier(c, tag, seq, PH_GATHERED)) return finish(rc);
     trace_mark("gathered_barrier");
     if (ctx.out_staged) { // the caller's receive buffer could not be exported: copy the assembled result out
-        if (!be->memcpy_async(dst, my_out, bytes, st) || !be->stream_sync(st)) {
+        if (!copy_staged(be, outb->segs, static_cast<uint8_t *>(dst), bytes, true, st) || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: copy-out failed";
             return finish(1);
         }

@@ -16,6 +16,16 @@
 // ops with different tags proceed independently). Every wait is bounded and also watches the master's abort packet
 // and the liveness of the peer processes, so a peer dying mid-collective aborts the op on all survivors
 // (fault tolerance is preserved); a vote at the start of each op lets all peers agree on the data path.
+//
+// Exported allocations are at most kIpcMaxExport bytes: PyTorch's bundled ROCm 7.0 HIP runtime (the one every
+// Python peer process runs on) never returns from hipIpcOpenMemHandle for an allocation of >= 2 GiB (ROCm 7.2 does;
+// profiles/r2/ipc/). Staged comm buffers are therefore built from kIpcSegBytes segments, each exported separately,
+// and kernels run in pieces that never cross a segment boundary (boundaries are multiples of kIpcSegBytes in op
+// byte space, the same for every peer). User buffers in larger allocations are staged.
+//
+// Buffer lifetime under faults: a mapping is pinned (reference-counted) by every op that uses it and is only closed
+// when unpinned; after an abort a peer waits until every live peer is past its kernels for that op before it
+// restores / releases buffers or returns (a dead peer's queues are gone once its process is).
 #pragma once
 
 #include <array>
@@ -26,12 +36,17 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../common/device_backend.hpp"
 #include "../common/types.hpp"
 
 namespace pccl::client {
+
+constexpr size_t kIpcSegBytes = size_t{1} << 30;                 // staged comm buffer segment
+constexpr size_t kIpcMaxExport = (size_t{2} << 30) - (size_t{2} << 20); // largest user allocation exported as is
+constexpr uint32_t kIpcMaxSegs = 16;                              // => ops of up to 16 GiB take the xGMI path
 
 class Client;
 struct ArenaShm;
@@ -41,6 +56,7 @@ public:
     // kAbortedByMaster: the vote barrier consumed the master's abort packet for this op (exactly one is sent per op,
     // so the caller must not wait for it again)
     static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1, kAbortedByMaster = -2;
+    using MapKey = std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>; // (peer, handle, my device)
     std::atomic<bool> map_failed_{false}; // a peer's IPC handle could not be opened: stop voting for xGMI
 
     static std::shared_ptr<IpcArena> create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
@@ -71,17 +87,24 @@ public:
 
 private:
     IpcArena() = default;
+    // a staged comm buffer: `segs` allocations of kIpcSegBytes (one smaller allocation for small buffers)
     struct CommBuf {
-        uint64_t id = 0;
-        void *ptr = nullptr;
+        std::vector<void *> segs;
+        std::vector<std::array<uint8_t, kIpcHandleBytes>> handles;
         size_t cap = 0;
         int device = -1;
-        uint8_t handle[kIpcHandleBytes]{};
         bool busy = false;
     };
     CommBuf *acquire_buffer(size_t bytes, int device);
     void release_buffer(CommBuf *b);
-    void *peer_mapping(int peer, const uint8_t *handle, int my_device);
+    struct Mapping {
+        void *ptr = nullptr;
+        int refs = 0;      // ops that hold this mapping (never closed while > 0)
+        uint64_t used = 0; // LRU stamp
+    };
+    // opens (or reuses) peer `peer`'s allocation `handle` on `my_device` and pins it; nullptr on failure
+    void *pin_mapping(int peer, const uint8_t *handle, int my_device, MapKey &key);
+    void unpin_mappings(const std::vector<MapKey> &keys);
     // exports the allocation holding a user device buffer (zero-copy path); cached per allocation base
     bool export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset);
     // waits until every peer reached `phase` for `seq`; 0 ok, 1 failure (peer dead/aborted/timeout), 2 master abort
@@ -105,8 +128,8 @@ private:
     uint64_t next_buf_id_ = 1;
     // (peer, handle bytes, my device) -> mapped allocation base; handles identify allocations uniquely (a freed and
     // re-allocated block at the same address gets a new handle), so stale entries are merely unused
-    std::map<std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>, void *> mappings_;
-    std::vector<std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>> mapping_lru_;
+    std::map<MapKey, Mapping> mappings_;
+    uint64_t map_clock_ = 0;
 };
 
 template<typename Op>

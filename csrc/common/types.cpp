@@ -1,11 +1,18 @@
 #include "types.hpp"
 
 #include <arpa/inet.h>
+#include <atomic>
+#include <csignal>
+#include <dirent.h>
+#include <execinfo.h>
+#include <mutex>
+#include <sys/syscall.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
 #include <random>
+#include <string>
 #include <unistd.h>
 
 namespace pccl {
@@ -109,6 +116,56 @@ SockAddrKey SockAddrKey::of(const SockAddr &a) {
         std::memcpy(k.ip.data(), a.inet.ipv6.data, 16);
     k.port = a.port;
     return k;
+}
+
+void fault_point(const char *point, uint64_t seq) {
+    static const std::string spec = [] {
+        const char *e = std::getenv("PCCL_FAULT_INJECT");
+        return std::string(e ? e : "");
+    }();
+    if (spec.empty()) return;
+    const size_t colon = spec.rfind(':');
+    if (colon == std::string::npos || spec.compare(0, colon, point) != 0) return;
+    if (std::strtoull(spec.c_str() + colon + 1, nullptr, 10) != seq) return;
+    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu\n", point, static_cast<unsigned long long>(seq));
+    std::fflush(stderr);
+    ::kill(::getpid(), SIGKILL);
+}
+
+namespace {
+std::atomic<int> g_bt_pending{0};
+void bt_handler(int) {
+    void *frames[64];
+    const int n = ::backtrace(frames, 64);
+    char hdr[64];
+    const int k = std::snprintf(hdr, sizeof(hdr), "[pccl] backtrace tid %ld:\n", static_cast<long>(::syscall(SYS_gettid)));
+    if (k > 0) (void)!::write(2, hdr, static_cast<size_t>(k));
+    ::backtrace_symbols_fd(frames, n, 2);
+    if (g_bt_pending.fetch_add(1) == 0) { // the first thread to get the signal forwards it to every other thread
+        DIR *d = ::opendir("/proc/self/task");
+        if (d) {
+            const long me = static_cast<long>(::syscall(SYS_gettid));
+            while (dirent *e = ::readdir(d)) {
+                const long tid = std::atol(e->d_name);
+                if (tid > 0 && tid != me) ::syscall(SYS_tgkill, ::getpid(), tid, SIGUSR2);
+            }
+            ::closedir(d);
+        }
+    }
+}
+} // namespace
+
+void install_debug_backtrace_signal() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (!env_flag("PCCL_DEBUG_BACKTRACE_SIGNAL", false)) return;
+        void *warm[2];
+        (void)::backtrace(warm, 2); // loads the unwinder outside of signal context
+        struct sigaction sa{};
+        sa.sa_handler = bt_handler;
+        sa.sa_flags = SA_RESTART;
+        ::sigaction(SIGUSR2, &sa, nullptr);
+    });
 }
 
 size_t env_size(const char *name, size_t dflt) {

@@ -92,4 +92,13 @@ struct SockAddrKeyHash {
 size_t env_size(const char *name, size_t dflt);
 bool env_flag(const char *name, bool dflt);
 
+// Fault injection for the crash tests: PCCL_FAULT_INJECT="<point>:<seq>" makes this process SIGKILL itself when it
+// reaches `point` in the op with master sequence number `seq` (points: ipc_vote, ipc_kernel, ring_step). Lets a test
+// kill a peer at an exact protocol position, e.g. while its xGMI push kernel and its peers' kernels are running.
+void fault_point(const char *point, uint64_t seq);
+
+// PCCL_DEBUG_BACKTRACE_SIGNAL=1 (debugging hangs on the GPU box, where debuggers may not attach): SIGUSR2 prints the
+// native backtrace of every thread of the process to stderr (each thread is signalled in turn).
+void install_debug_backtrace_signal();
+
 } // namespace pccl

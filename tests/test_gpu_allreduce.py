@@ -187,6 +187,27 @@ def test_two_process_ipc(hip, mode):
             assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value
 
 
+@pytest.mark.parametrize("gib", [1.25, 2.5])
+def test_two_process_ipc_large(hip, gib):
+    """Ops whose staged comm buffers / user allocations exceed 1-2 GiB: staged buffers are built from 1 GiB segments
+    and kernels run per segment piece; user allocations above kIpcMaxExport are staged (PyTorch's ROCm 7.0 runtime
+    never returns from hipIpcOpenMemHandle for >= 2 GiB allocations). Rank 1 runs in place (staged input)."""
+    n = int(gib * (1 << 30)) // 2 + 3
+    with local_master() as addr:
+        procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, "2", str(r), "--n", str(n),
+                               "--dtype", "bf16", "--device", "cuda:0", "--steps", "2",
+                               *(["--inplace"] if r == 1 else [])],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+        outs = [p.communicate(timeout=200) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
+        assert len(lines) == 2
+        for ln in lines:
+            assert ln["lo"] == ln["hi"] == float(1 + 2 + 2 * ln["step"])
+            assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value
+
+
 @pytest.mark.parametrize("inplace", [(False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("no_zc", [False, True])
 def test_device_ipc_modes(hip, inplace, no_zc, monkeypatch):

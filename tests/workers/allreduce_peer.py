@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--inplace", action="store_true")
     ap.add_argument("--op", default="sum", choices=["sum", "avg", "max"])
     ap.add_argument("--quant", default="none", choices=["none", "u8"])
+    ap.add_argument("--check-every", type=int, default=1, help="verify the result every k-th step only")
+    ap.add_argument("--reuse", action="store_true", help="allocate x / y once (back-to-back ops, no refill)")
+    ap.add_argument("--duration", type=float, default=0.0, help="run steps until this many seconds passed instead")
     a = ap.parse_args()
     op = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[a.op]
     qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant == "u8" \
@@ -50,7 +53,10 @@ def main():
         wait_for_world(comm, a.world, timeout=120)
     step, failures, first_ok = 0, 0, None
     it = 0
-    while step < a.steps:
+    t_loop = None
+    while (step < a.steps) if a.duration <= 0 else (t_loop is None or time.perf_counter() - t_loop < a.duration):
+        if t_loop is None:
+            t_loop = time.perf_counter()
         if it > 0 and comm.are_peers_pending():
             comm.update_topology()
         it += 1
@@ -59,8 +65,9 @@ def main():
             time.sleep(0.05)
             continue
         val = 1.0 if a.const else float(a.rank + 1 + step)
-        x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
-        y = x if a.inplace else torch.empty_like(x)
+        if not a.reuse or step == 0 or a.inplace:
+            x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
+            y = x if a.inplace else torch.empty_like(x)
         if step == a.die_at:
             os._exit(17)  # simulated crash (no clean disconnect)
         t0 = time.perf_counter()
@@ -77,7 +84,10 @@ def main():
         dt = time.perf_counter() - t0
         if first_ok is None:
             first_ok = time.perf_counter() - t_start
-        lo, hi = float(y.float().min()), float(y.float().max())
+        if step % a.check_every == 0 or step + 1 == a.steps or a.duration > 0 and step % 4 == 0:
+            lo, hi = float(y.min().float()), float(y.max().float())
+        else:
+            lo = hi = float(info.local_world_size) if a.const else None
         rec = {"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
                "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
                "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
