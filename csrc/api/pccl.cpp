@@ -4,6 +4,8 @@
 #include "pccl.h"
 
 #include <atomic>
+#include <chrono>
+#include <deque>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -119,6 +121,7 @@ pcclResult_t pcclGetAttribute(const pcclComm_t *comm, pcclAttribute_t attribute,
         case PCCL_ATTRIBUTE_CONNECTION_REVISION: *out = static_cast<int>(c.connection_revision()); break;
         case PCCL_ATTRIBUTE_RING_RANK: *out = c.ring_rank(); break;
         case PCCL_ATTRIBUTE_LAST_REDUCE_PATH: *out = c.last_reduce_path(); break;
+        case PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS: *out = static_cast<int>(c.collective_worker_threads()); break;
         default: return pcclInvalidArgument;
     }
     return pcclSuccess;
@@ -266,45 +269,64 @@ pcclResult_t pcclAllReduceMultipleWithRetry(const pcclReduceOpDescriptor_t *desc
     auto &c = *comm->client;
     if (c.local_world_size() < 2) return pcclTooFewPeers;
 
+    // Sliding window (reference src/pccl.cpp:345-523): keep up to max_in_flight ops running, launch the next pending
+    // op (in index order, so every peer issues the same tag sequence) as soon as ANY in-flight op completes (the
+    // reference awaits the oldest one, so one slow op holds back every launch behind it);
+    // on a failure drain every in-flight op (their successes count), then relaunch everything still pending on the
+    // re-formed ring.
     uint64_t total_tx = 0, total_rx = 0;
     std::vector<bool> completed(count, false);
     size_t n_completed = 0;
-    while (n_completed < count) {
-        if (c.local_world_size() < 2) break;
-        // launch a window of pending ops, await them in order; on any failure await the rest, then retry
-        std::vector<size_t> window;
-        for (size_t i = 0; i < count && window.size() < static_cast<size_t>(max_in_flight); ++i) {
-            if (completed[i]) continue;
-            pcclAsyncReduceOp_t h{};
+    std::deque<size_t> pending, in_flight;
+    for (size_t i = 0; i < count; ++i) pending.push_back(i);
+    auto handle_of = [&](size_t i) {
+        return pcclAsyncReduceOp_t{const_cast<pcclComm_t *>(comm), descriptors[i].descriptor.tag};
+    };
+    auto await_one = [&](size_t i) {
+        pcclAsyncReduceOp_t h = handle_of(i);
+        pcclReduceInfo_t info{};
+        if (pcclAwaitAsyncReduce(&h, &info) != pcclSuccess) return false;
+        completed[i] = true;
+        ++n_completed;
+        total_tx += info.tx_bytes;
+        total_rx += info.rx_bytes;
+        return true;
+    };
+    while (n_completed < count && c.local_world_size() >= 2) {
+        while (in_flight.size() < static_cast<size_t>(max_in_flight) && !pending.empty()) {
+            const size_t i = pending.front();
             const auto &d = descriptors[i];
+            pcclAsyncReduceOp_t h{};
             const pcclResult_t r = pcclAllReduceAsync(d.sendbuf, d.recvbuf, &d.descriptor, comm, &h);
             if (r == pcclTooFewPeers) break;
             if (r != pcclSuccess) {
-                for (size_t j : window) {
-                    pcclAsyncReduceOp_t hj{const_cast<pcclComm_t *>(comm), descriptors[j].descriptor.tag};
-                    pcclAwaitAsyncReduce(&hj, nullptr);
-                }
+                for (size_t j : in_flight) await_one(j);
                 return r;
             }
-            window.push_back(i);
+            pending.pop_front();
+            in_flight.push_back(i);
         }
-        if (window.empty()) break;
-        bool any_failed = false;
-        for (size_t i : window) {
-            pcclAsyncReduceOp_t h{const_cast<pcclComm_t *>(comm), descriptors[i].descriptor.tag};
-            pcclReduceInfo_t info{};
-            if (pcclAwaitAsyncReduce(&h, &info) == pcclSuccess) {
-                completed[i] = true;
-                ++n_completed;
-                total_tx += info.tx_bytes;
-                total_rx += info.rx_bytes;
-            } else {
-                any_failed = true;
-            }
+        if (in_flight.empty()) break;
+        // the first in-flight op to complete (not the oldest: a slow op must not stall the launches behind it)
+        std::vector<uint64_t> tags;
+        for (size_t j : in_flight) tags.push_back(descriptors[j].descriptor.tag);
+        std::optional<uint64_t> done;
+        while (!(done = c.wait_any(tags, std::chrono::milliseconds(1000))) && c.local_world_size() >= 2) {
         }
-        if (any_failed) {
-            LOG(WARN) << "pcclAllReduceMultipleWithRetry: retrying failed all-reduces";
-        }
+        auto pos = in_flight.begin();
+        if (done)
+            while (pos != in_flight.end() && descriptors[*pos].descriptor.tag != *done) ++pos;
+        if (pos == in_flight.end()) pos = in_flight.begin();
+        const size_t i = *pos;
+        in_flight.erase(pos);
+        if (await_one(i)) continue;
+        LOG(WARN) << "pcclAllReduceMultipleWithRetry: all-reduce tag " << descriptors[i].descriptor.tag
+                  << " failed; draining " << in_flight.size() << " in-flight ops and retrying";
+        for (size_t j : in_flight) await_one(j);
+        in_flight.clear();
+        pending.clear();
+        for (size_t j = 0; j < count; ++j)
+            if (!completed[j]) pending.push_back(j);
     }
     if (info_out != nullptr) {
         info_out->local_world_size = static_cast<uint32_t>(c.local_world_size());

@@ -85,14 +85,28 @@ OpWorkers::~OpWorkers() {
         if (t.joinable()) t.join();
 }
 
+// Bounded like the reference's collective thread pool (PCCL_MAX_CONCURRENT_COLLECTIVE_OPS, default 16; reference
+// ccoip_client_state.hpp:17-25): a new worker starts only while fewer than the bound exist; otherwise the op waits
+// in the FIFO queue. Ops start in submission order, so peers that issue the same tag sequence dequeue it in the same
+// order (a worker blocked in the commence of tag X never starves the peers' tag X).
+size_t OpWorkers::max_workers() {
+    static const size_t v = std::max<size_t>(1, env_size("PCCL_MAX_CONCURRENT_COLLECTIVE_OPS", 16));
+    return v;
+}
+
 void OpWorkers::submit(std::function<void()> fn) {
     std::lock_guard l(m_);
     q_.push_back(std::move(fn));
-    if (q_.size() > idle_) {
+    if (q_.size() > idle_ && threads_.size() < max_workers()) {
         threads_.emplace_back([this] { loop(); });
     } else {
         cv_.notify_one();
     }
+}
+
+size_t OpWorkers::thread_count() {
+    std::lock_guard l(m_);
+    return threads_.size();
 }
 
 void OpWorkers::loop() {
@@ -135,6 +149,7 @@ bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
 
 void Client::run_op(const std::shared_ptr<OpState> &op) {
     const uint64_t tag = op->req.tag;
+    fault_delay(tag);
     OpTrace trace;
     current_trace() = trace_ops_enabled() ? &trace : nullptr;
     char range_name[96];
@@ -250,6 +265,33 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     }
     op->success = ok;
     op->finish();
+    {
+        std::lock_guard l(done_mtx_);
+    }
+    done_cv_.notify_all();
+}
+
+std::optional<uint64_t> Client::wait_any(const std::vector<uint64_t> &tags, std::chrono::milliseconds timeout) {
+    std::vector<std::shared_ptr<OpState>> ops;
+    {
+        std::lock_guard lock(ops_mtx_);
+        for (uint64_t t : tags) {
+            auto it = ops_.find(t);
+            ops.push_back(it == ops_.end() ? nullptr : it->second);
+        }
+    }
+    const auto deadline = std::chrono::steady_clock::now() + timeout;
+    std::unique_lock l(done_mtx_);
+    while (true) {
+        bool any_known = false;
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (!ops[i]) continue;
+            any_known = true;
+            if (ops[i]->done.load()) return tags[i];
+        }
+        if (!any_known) return std::nullopt;
+        if (done_cv_.wait_until(l, deadline) == std::cv_status::timeout) return std::nullopt;
+    }
 }
 
 bool Client::join_async_reduce(uint64_t tag) {

@@ -83,6 +83,8 @@ public:
     OpWorkers &operator=(const OpWorkers &) = delete;
     ~OpWorkers();
     void submit(std::function<void()> fn);
+    size_t thread_count();
+    static size_t max_workers();
 
 private:
     void loop();
@@ -114,6 +116,9 @@ public:
     bool join_async_reduce(uint64_t tag);           // true on success
     bool get_reduce_info(uint64_t tag, ReduceInfo &out);
     bool any_collective_running();
+    // Blocks until one of the given async ops (tags) has completed (or `timeout` passed); returns its tag, or
+    // nullopt on timeout / if none of the tags is known. Used by the sliding-window retry scheduler.
+    std::optional<uint64_t> wait_any(const std::vector<uint64_t> &tags, std::chrono::milliseconds timeout);
 
     size_t global_world_size() const { return global_ws_.load(); }
     size_t local_world_size() const { return local_ws_.load(); }
@@ -122,6 +127,7 @@ public:
     uint64_t connection_revision() const { return conn_revision_.load(); }
     int ring_rank();
     int last_reduce_path() const { return last_path_.load(); }
+    size_t collective_worker_threads() { return workers_.thread_count(); }
     const Uuid &uuid() const { return uuid_; }
 
 private:
@@ -218,6 +224,8 @@ private:
     std::atomic<int> last_path_{0};
 
     std::mutex ops_mtx_;
+    std::mutex done_mtx_;           // signalled whenever an op finishes (wait_any)
+    std::condition_variable done_cv_;
     std::map<uint64_t, std::shared_ptr<OpState>> ops_;
     OpWorkers workers_;
 

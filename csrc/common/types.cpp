@@ -132,6 +132,29 @@ void fault_point(const char *point, uint64_t seq) {
     ::kill(::getpid(), SIGKILL);
 }
 
+void fault_delay(uint64_t tag) {
+    static const std::string spec = [] {
+        const char *e = std::getenv("PCCL_FAULT_DELAY");
+        return std::string(e ? e : "");
+    }();
+    if (spec.empty()) return;
+    long ms = -1, any_ms = -1;
+    size_t pos = 0;
+    while (pos < spec.size()) {
+        const size_t end = std::min(spec.find(',', pos), spec.size());
+        const std::string item = spec.substr(pos, end - pos);
+        const size_t colon = item.find(':');
+        if (colon != std::string::npos) {
+            const long v = std::atol(item.c_str() + colon + 1);
+            if (item.compare(0, colon, "*") == 0) any_ms = v;
+            else if (std::strtoull(item.c_str(), nullptr, 10) == tag) ms = v;
+        }
+        pos = end + 1;
+    }
+    if (ms < 0) ms = any_ms;
+    if (ms > 0) ::usleep(static_cast<useconds_t>(ms) * 1000);
+}
+
 namespace {
 std::atomic<int> g_bt_pending{0};
 void bt_handler(int) {

@@ -96,6 +96,9 @@ bool env_flag(const char *name, bool dflt);
 // reaches `point` in the op with master sequence number `seq` (points: ipc_vote, ipc_kernel, ring_step). Lets a test
 // kill a peer at an exact protocol position, e.g. while its xGMI push kernel and its peers' kernels are running.
 void fault_point(const char *point, uint64_t seq);
+// PCCL_FAULT_DELAY="<tag>:<ms>[,*:<ms>]": an op with that tag (or any tag, "*") sleeps before it initiates
+// (scheduler tests: a slow op among fast ones).
+void fault_delay(uint64_t tag);
 
 // PCCL_DEBUG_BACKTRACE_SIGNAL=1 (debugging hangs on the GPU box, where debuggers may not attach): SIGUSR2 prints the
 // native backtrace of every thread of the process to stderr (each thread is signalled in turn).

@@ -93,7 +93,10 @@ typedef enum pcclAttribute_t {
     /** [pccl-amd extension] data path of the last completed all-reduce: 0 none, 1 host ring/TCP,
      *  2 device ring/TCP via pinned staging, 3 device xGMI/IPC (same host), 4 hierarchical (xGMI/IPC inside each
      *  host + one TCP ring per local rank across hosts) */
-    PCCL_ATTRIBUTE_LAST_REDUCE_PATH = 66
+    PCCL_ATTRIBUTE_LAST_REDUCE_PATH = 66,
+    /** [pccl-amd extension] worker threads of the async collective pool so far (bounded by
+     *  PCCL_MAX_CONCURRENT_COLLECTIVE_OPS, default 16) */
+    PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS = 67
 } pcclAttribute_t;
 
 typedef enum pcclSharedStateSyncStrategy_t {

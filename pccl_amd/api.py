@@ -97,6 +97,7 @@ class Attribute(Enum):
     CONNECTION_REVISION = 64
     RING_RANK = 65
     LAST_REDUCE_PATH = 66
+    COLLECTIVE_WORKER_THREADS = 67
 
 
 class ReducePath(Enum):

@@ -154,6 +154,71 @@ def test_all_reduce_multiple_with_retry():
             assert torch.all(o == float(1 + 2 * k))
 
 
+def test_bounded_collective_worker_pool():
+    """64 concurrent async ops per peer run on at most PCCL_MAX_CONCURRENT_COLLECTIVE_OPS (16) worker threads
+    (reference ccoip_client_state.hpp:17-25); the queued ones start as workers free up, in submission order."""
+    world, n, n_ops = 2, 2048, 64
+
+    def fn(rank, comm):
+        xs = [torch.full((n,), float(rank + k)) for k in range(n_ops)]
+        outs = [torch.empty(n) for _ in range(n_ops)]
+        hs = [comm.all_reduce_async(xs[k], outs[k], op=pccl.ReduceOp.SUM, tag=k) for k in range(n_ops)]
+        for h in hs:
+            ok, status, _ = h.wait()
+            assert ok, status
+        return outs, comm.get_attribute(pccl.Attribute.COLLECTIVE_WORKER_THREADS)
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr)
+    for outs, workers in res:
+        assert 1 <= workers <= 16, workers
+        for k, o in enumerate(outs):
+            assert torch.all(o == float(1 + 2 * k)), k
+
+
+_SLIDING = r"""
+import json, sys, time, torch
+sys.path.insert(0, sys.argv[1])
+import pccl_amd as pccl
+from pccl_amd.utils import local_master, run_threaded_peers
+n_ops, n = 256, 1024
+def fn(rank, comm):
+    xs = [torch.full((n,), float(rank + k)) for k in range(n_ops)]
+    outs = [torch.empty(n) for _ in range(n_ops)]
+    descs = []
+    for k in range(n_ops):
+        rd = pccl.ReduceDescriptor(n, pccl.ReduceOp.SUM, k,
+                                   pccl.ReduceOperandDescriptor(pccl.DataType.FLOAT, pccl.DistributionHint.NONE),
+                                   pccl.QuantizationOptions(pccl.DataType.FLOAT, pccl.QuantizationAlgorithm.NONE))
+        descs.append(pccl.ReduceOpDescriptor.from_torch(xs[k], outs[k], rd))
+    t0 = time.perf_counter()
+    comm.all_reduce_multiple_with_retry(descs, max_in_flight=8)
+    dt = time.perf_counter() - t0
+    ok = all(bool(torch.all(outs[k] == float(1 + 2 * k))) for k in range(n_ops))
+    return dt, ok
+with local_master() as addr:
+    res = run_threaded_peers(2, fn, address=addr, timeout=120)
+print(json.dumps({"t": max(r[0] for r in res), "ok": all(r[1] for r in res)}))
+"""
+
+
+def test_all_reduce_multiple_sliding_window():
+    """256 ops, max_in_flight 8, op 0 is slow (800 ms before it starts), every other op takes >= 20 ms: a batch
+    window (or awaiting the oldest op first, as the reference does) stalls all launches behind op 0 (>= 0.8 s +
+    31 x 20 ms); the sliding window keeps 7 slots busy meanwhile (~0.8 s + ~0.1 s)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PCCL_FAULT_DELAY="0:800,*:20")
+    r = subprocess.run([sys.executable, "-c", _SLIDING, root], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"]
+    assert out["t"] < 1.25, out  # stalled scheduling: >= 1.42 s
+
+
 @pytest.mark.parametrize("qdtype,algo", [(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX),
                                          (pccl.DataType.INT8, pccl.QuantizationAlgorithm.MIN_MAX),
                                          (pccl.DataType.UINT16, pccl.QuantizationAlgorithm.MIN_MAX),
