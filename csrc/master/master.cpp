@@ -467,6 +467,7 @@ bool Master::check_p2p_established() {
         pkt.ring_order = ring_of(c.group, false);
         // every ring member on one host (same boot id + hostname): the peers may rendezvous for the xGMI IPC path
         // even if the master itself is remote
+        pkt.has_host_info = true; // our clients read single_host / host_of (reference clients ignore trailing bytes)
         pkt.single_host = !pkt.ring_order.empty();
         for (const auto &ru : pkt.ring_order) {
             const ClientInfo *rc = client_by_uuid(ru);

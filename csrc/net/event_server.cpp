@@ -59,6 +59,17 @@ void EventServer::interrupt() {
     }
 }
 
+void EventServer::post(std::function<void()> fn) {
+    {
+        std::lock_guard l(posted_mtx_);
+        posted_.push_back(std::move(fn));
+    }
+    if (event_fd_ >= 0) {
+        const uint64_t one = 1;
+        [[maybe_unused]] auto r = ::write(event_fd_, &one, 8);
+    }
+}
+
 void EventServer::join() {
     if (thread_.joinable() && std::this_thread::get_id() != thread_.get_id()) thread_.join();
 }
@@ -91,6 +102,14 @@ void EventServer::loop() {
             if (!c.closing && (events[i].events & EPOLLOUT)) flush(c);
         }
         process_pending_closes();
+        std::vector<std::function<void()>> posted;
+        {
+            std::lock_guard l(posted_mtx_);
+            posted.swap(posted_);
+        }
+        for (auto &f : posted)
+            if (!stop_) f();
+        if (!posted.empty()) process_pending_closes();
         if (tick_cb_ && !stop_) tick_cb_();
     }
     // shutdown: close all clients (no callbacks on interrupt)

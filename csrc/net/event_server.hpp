@@ -7,6 +7,7 @@
 #include <deque>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -48,6 +49,8 @@ public:
         return send_raw(client, P::kId, std::move(w.data));
     }
     bool close_client(const SockAddr &client); // deferred: close callback fires after the current handler
+    // Any thread: runs `fn` on the loop thread soon (after the current batch of events).
+    void post(std::function<void()> fn);
 
 private:
     struct Client {
@@ -81,6 +84,8 @@ private:
     std::unordered_map<int, std::unique_ptr<Client>> clients_by_fd_;
     std::unordered_map<SockAddrKey, int, SockAddrKeyHash> fd_by_addr_;
     std::vector<int> pending_close_;
+    std::mutex posted_mtx_;
+    std::vector<std::function<void()>> posted_;
     ReadCb read_cb_;
     CloseCb close_cb_;
     std::function<void()> tick_cb_;

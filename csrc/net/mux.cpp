@@ -21,7 +21,22 @@ size_t multiplex_chunk_size() {
     return v == 0 ? (16ull << 20) : v;
 }
 
-static constexpr size_t kMaxFrame = 1ull << 30;
+void mux_frame_header(uint8_t out[kMuxHeaderBytes], uint64_t payload, uint64_t tag, uint64_t ctr) {
+    const uint64_t vals[3] = {payload + 16, tag, ctr};
+    for (int v = 0; v < 3; ++v)
+        for (int i = 0; i < 8; ++i) out[v * 8 + i] = static_cast<uint8_t>(vals[v] >> (8 * (7 - i)));
+}
+
+bool mux_parse_header(const uint8_t in[kMuxHeaderBytes], uint64_t &payload, uint64_t &tag, uint64_t &ctr) {
+    uint64_t vals[3] = {0, 0, 0};
+    for (int v = 0; v < 3; ++v)
+        for (int i = 0; i < 8; ++i) vals[v] = (vals[v] << 8) | in[v * 8 + i];
+    tag = vals[1];
+    ctr = vals[2];
+    if (vals[0] < 16 || vals[0] - 16 > kMuxMaxFrame) return false;
+    payload = vals[0] - 16;
+    return true;
+}
 
 const WanSim &wan_sim() {
     static const WanSim s = [] {
@@ -128,10 +143,8 @@ void MuxConn::tx_job_loop() {
 
 bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n) {
     if (!is_open()) return false;
-    uint8_t hdr[24];
-    const uint64_t vals[3] = {n + 16, tag, ctr};
-    for (int v = 0; v < 3; ++v)
-        for (int i = 0; i < 8; ++i) hdr[v * 8 + i] = static_cast<uint8_t>(vals[v] >> (8 * (7 - i)));
+    uint8_t hdr[kMuxHeaderBytes];
+    mux_frame_header(hdr, n, tag, ctr);
     iovec iov[2] = {{hdr, 24}, {const_cast<void *>(data), n}};
     std::lock_guard lock(tx_mtx_);
     if (wan_sim().enabled) wan_shape(n + 24, sim_next_free_, sim_last_send_);
@@ -168,17 +181,16 @@ bool MuxConn::read_into(uint8_t *dst, size_t n, Sink *progress_sink) {
 
 void MuxConn::rx_loop() {
     while (!stop_) {
-        uint8_t hdr[24];
-        if (!recv_all(fd_, hdr, 24)) break;
-        uint64_t vals[3] = {0, 0, 0};
-        for (int v = 0; v < 3; ++v)
-            for (int i = 0; i < 8; ++i) vals[v] = (vals[v] << 8) | hdr[v * 8 + i];
-        const uint64_t len = vals[0], tag = vals[1], ctr = vals[2];
-        if (len < 16 || len - 16 > kMaxFrame) {
-            LOG(WARN) << "MuxConn: invalid frame length " << len << " from " << sockaddr_str(peer_addr_);
+        uint8_t hdr[kMuxHeaderBytes];
+        if (!recv_all(fd_, hdr, kMuxHeaderBytes)) break;
+        uint64_t len = 0, tag = 0, ctr = 0;
+        if (!mux_parse_header(hdr, len, tag, ctr)) {
+            // malformed / oversized frame: the stream cannot be re-synchronised, so the connection is closed (the
+            // reference pops and silently drops a frame larger than the receive buffer, Appendix C #8)
+            LOG(WARN) << "MuxConn: invalid frame header from " << sockaddr_str(peer_addr_) << "; closing";
             break;
         }
-        const size_t n = len - 16;
+        const size_t n = len;
         Sink *sink = nullptr;
         size_t offset = 0;
         {

@@ -117,6 +117,14 @@ private:
 
 size_t multiplex_chunk_size();
 
+// 24-byte multiplexed frame header (reference tinysockets multiplexed_socket.cpp:406-411):
+// u64 BE (payload + 16) | u64 BE tag | u64 BE stream_ctr.
+constexpr size_t kMuxHeaderBytes = 24;
+constexpr uint64_t kMuxMaxFrame = 1ull << 30; // largest accepted payload (1 GiB)
+void mux_frame_header(uint8_t out[kMuxHeaderBytes], uint64_t payload, uint64_t tag, uint64_t ctr);
+// false if the length field is malformed (< 16) or the payload exceeds kMuxMaxFrame
+bool mux_parse_header(const uint8_t in[kMuxHeaderBytes], uint64_t &payload, uint64_t &tag, uint64_t &ctr);
+
 // Built-in WAN emulation for tests and benchmarks without root / tc-netem (reference BASELINE config "int8-quantized
 // all-reduce over tc-netem 50 ms simulated WAN"): PCCL_SIM_WAN="<one-way latency ms>:<per-flow Mbit/s>[:<link Mbit/s>]"
 // shapes every P2P data connection: each frame is serialised at the flow rate (and the shared link rate), and a burst

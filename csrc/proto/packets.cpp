@@ -152,6 +152,7 @@ static bool decode_uuid_list(RBuf &r, bool &success, std::vector<Uuid> &v) {
 
 void M2CP2PConnectionsEstablished::encode(WBuf &w) const {
     encode_uuid_list(w, success, ring_order);
+    if (!has_host_info && !single_host && host_of.empty()) return; // reference layout
     w.boolean(single_host);
     if (!host_of.empty()) {
         w.u64(host_of.size());
@@ -202,6 +203,7 @@ void M2CSyncSharedState::encode(WBuf &w) const {
     for (size_t i = 0; i < outdated_keys.size(); ++i) w.u64(i < expected_hashes.size() ? expected_hashes[i] : 0);
     for (size_t i = 0; i < outdated_keys.size(); ++i)
         w.u8(static_cast<uint8_t>(i < expected_hash_types.size() ? expected_hash_types[i] : HashType::Simple));
+    if (fallback_distributors.empty()) return; // reference layout
     w.u64(fallback_distributors.size());
     for (const auto &a : fallback_distributors) w.sockaddr(a);
 }

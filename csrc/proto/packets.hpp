@@ -231,7 +231,7 @@ struct M2CP2PConnectionsEstablished {
     bool success = false;
     std::vector<Uuid> ring_order;
     bool single_host = false; // extension (appended, optional): every ring member reported the same host token
-    bool has_host_info = false; // decode only: the master sent the extension (so single_host is authoritative)
+    bool has_host_info = false; // the extension is present (decode) / to be sent (encode): single_host is authoritative
     std::vector<uint32_t> host_of; // extension (appended, optional): host index of every ring member (ring order)
     void encode(WBuf &w) const;
     bool decode(RBuf &r);

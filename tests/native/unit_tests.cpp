@@ -26,22 +26,7 @@
 using namespace pccl;
 using namespace std::chrono_literals;
 
-static std::vector<std::pair<std::string, std::function<void()>>> &registry() {
-    static std::vector<std::pair<std::string, std::function<void()>>> r;
-    return r;
-}
-static int g_failures = 0;
-#define TEST(name)                                                                                                   \
-    static void name();                                                                                              \
-    static const bool reg_##name = (registry().emplace_back(#name, name), true);                                     \
-    static void name()
-#define EXPECT(cond)                                                                                                 \
-    do {                                                                                                             \
-        if (!(cond)) {                                                                                               \
-            std::fprintf(stderr, "  %s:%d: EXPECT(%s) failed\n", __FILE__, __LINE__, #cond);                         \
-            ++g_failures;                                                                                            \
-        }                                                                                                            \
-    } while (0)
+#include "harness.hpp"
 
 template<typename P>
 static P roundtrip(const P &p) {
