@@ -52,6 +52,7 @@ def _args():
                          "8 peers x 2 stripes measured fastest on one MI355X box (profiles/r2/ring_sweep.md)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
+    ap.add_argument("--extras-child", default="", help=argparse.SUPPRESS)  # internal: run only the extras, write JSON
     return ap.parse_args()
 
 
@@ -68,8 +69,10 @@ class Job:
         local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
         same_gpu = os.environ.get("PCCL_BENCH_SAME_GPU") == "1"  # rehearsal of the N>1 path on a 1-GPU box
         if self.world > 1:
+            import datetime
+
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
             self.dist = dist
         self.gpu = 0 if same_gpu else local_rank
         torch.cuda.set_device(self.gpu)
@@ -306,30 +309,13 @@ def rejoin_latency(job):
     return out.get("s")
 
 
-def main():
-    a = _args()
-    job = Job(a)
-    nbytes = a.mib << 20
-    P = job.total
-    extra = {}
-
-    # ---- headline: TCP device ring, P peers x 1 GiB bf16
-    ring = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=not a.quick,
-                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20))
+def run_extras(job, a, nbytes):
+    """The measurements that go into ``extra`` besides the headline: the xGMI/IPC path at the same peers, its size
+    sweep, 2 peers over IPC (N == 1), small-message latencies and the peer-rejoin latency."""
     import pccl_amd as pccl
-    alg, bus = _bw(nbytes, ring["t"], P)
-    path_name = pccl.ReducePath(ring["path"]).name
-    extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
-                  "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
-                  "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": a.pool,
-                  "result_exact": ring.get("ok")})
-    sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
-                                                    "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
-                             for b, t in ring["sweep"].items()}}
-    sweep["DEVICE_RING"][f"{a.mib}MiB"] = {"ms": round(ring["t"] * 1e3, 3), "bus_bw_per_peer_GBps": round(bus, 3)}
-
-    if not a.quick and not a.no_ipc_extra:
-        # ---- same job over the xGMI/IPC path (default for same-host GPU peers)
+    P = job.total
+    extra, sweep = {}, {}
+    if not a.no_ipc_extra:
         ipc = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
                       sweep=(1 << 20, 16 << 20, 256 << 20))
         ialg, ibus = _bw(nbytes, ipc["t"], P)
@@ -346,10 +332,81 @@ def main():
             talg, tbus = _bw(nbytes, two["t"], 2)
             extra["ipc_2_peers_1gpu"] = {"ms_per_op": round(two["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(tbus, 3),
                                          "reduce_path": pccl.ReducePath(two["path"]).name}
-    if not a.quick and job.world == 1:
+    if job.world == 1:
         extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
+    return extra, sweep
+
+
+def extras_in_child(job, a):
+    """Runs run_extras() in a child process per rank (its own gloo group on MASTER_PORT + 11): a failure there (e.g.
+    a GPU fault on an xGMI path never exercised on this node) is reported in ``extra`` instead of losing the
+    headline. Returns (extra, sweep) on rank 0, ({}, {}) elsewhere."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"pccl_bench_extras_{os.getpid()}_{job.rank}.json")
+    args = [sys.executable, os.path.abspath(__file__), "--gpus", str(a.gpus), "--steps", str(a.steps), "--warmup",
+            str(a.warmup), "--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--extras-child", out]
+    if a.no_ipc_extra:
+        args.append("--no-ipc-extra")
+    env = dict(os.environ)
+    if job.world > 1:
+        env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 11)
+        # under torchrun the process group joins the elastic agent's store as a client; the child's group needs its
+        # own store (hosted by rank 0's child on the new port)
+        env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
+    try:
+        rc = subprocess.run(args, env=env, timeout=900).returncode
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+    res = {}
+    if job.rank == 0:
+        try:
+            with open(out) as f:
+                res = json.load(f)
+            os.unlink(out)
+        except (OSError, ValueError):
+            res = {}
+        if rc != 0:
+            res.setdefault("extra", {})["extras_error"] = f"extras child exited with {rc}"
+    return res.get("extra", {}), res.get("sweep", {})
+
+
+def main():
+    a = _args()
+    job = Job(a)
+    nbytes = a.mib << 20
+    P = job.total
+    if a.extras_child:
+        extra, sweep = run_extras(job, a, nbytes)
+        if job.rank == 0:
+            with open(a.extras_child, "w") as f:
+                json.dump({"extra": extra, "sweep": sweep}, f)
+        if job.dist is not None:
+            job.dist.barrier()
+            job.dist.destroy_process_group()
+        return
+    extra = {}
+
+    # ---- headline: TCP device ring, P peers x 1 GiB bf16
+    ring = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=not a.quick,
+                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20))
+    import pccl_amd as pccl
+    alg, bus = _bw(nbytes, ring["t"], P)
+    path_name = pccl.ReducePath(ring["path"]).name
+    extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
+                  "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
+                  "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": a.pool,
+                  "result_exact": ring.get("ok")})
+    sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
+                                                    "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
+                             for b, t in ring["sweep"].items()}}
+    sweep["DEVICE_RING"][f"{a.mib}MiB"] = {"ms": round(ring["t"] * 1e3, 3), "bus_bw_per_peer_GBps": round(bus, 3)}
+    if not a.quick:
+        x_extra, x_sweep = extras_in_child(job, a)
+        extra.update(x_extra)
+        sweep.update(x_sweep)
     extra["sweep"] = sweep
 
     cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "

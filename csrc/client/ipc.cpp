@@ -110,6 +110,23 @@ static std::map<std::pair<const IpcArena *, uint64_t>, OpCtx> g_ctx;
 static std::mutex g_attempt_mtx;
 static std::map<uint64_t, int> g_attempts;
 
+int ipc_grid_budget(const std::vector<uint64_t> &gpu_uids, size_t rank) {
+    int sharing = 0;
+    for (uint64_t u : gpu_uids) sharing += u == gpu_uids[rank] ? 1 : 0;
+    return std::max(256, 512 / std::max(1, sharing));
+}
+
+int ipc_unreachable_peer(const std::vector<uint64_t> &gpu_uids, size_t rank, int my_device,
+                         const std::function<int(uint64_t)> &device_of_uid,
+                         const std::function<bool(int, int)> &can_access_peer) {
+    for (size_t k = 0; k < gpu_uids.size(); ++k) {
+        if (k == rank || gpu_uids[k] == gpu_uids[rank]) continue;
+        const int d = device_of_uid(gpu_uids[k]);
+        if (d >= 0 && !can_access_peer(my_device, d)) return static_cast<int>(k);
+    }
+    return -1;
+}
+
 std::shared_ptr<IpcArena> IpcArena::create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
                                            uint32_t group) {
     const size_t W = ring.size();
@@ -582,6 +599,19 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         release_buffer(outb);
         return kUseRing;
     }
+    {
+        std::vector<uint64_t> uids(ring_.size());
+        for (size_t k = 0; k < ring_.size(); ++k) uids[k] = shm_->op(slot, static_cast<uint32_t>(k))->gpu_uid;
+        const int bad = ipc_unreachable_peer(
+            uids, rank_, device, [be](uint64_t u) { return be->device_of_uid(u); },
+            [be](int d, int p) { return be->can_access_peer(d, p); });
+        if (bad >= 0) {
+            LOG(ERR) << "IPC: GPU of peer " << bad << " is not peer-accessible from device " << device
+                     << "; using the TCP ring for later ops";
+            map_failed_.store(true, std::memory_order_relaxed);
+            return abort_voted(kAborted);
+        }
+    }
     OpCtx ctx;
     ctx.bytes = bytes;
     ctx.in_buf = inb;
@@ -700,13 +730,9 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     std::vector<void *> dsts(W);
     // workgroup budget: 512 per GPU (2 per CU, the measured optimum for these streaming kernels), split between the
     // peers whose kernels run concurrently on this GPU, but not below 256 per kernel (fewer cannot saturate HBM)
-    int sharing = 0;
-    {
-        const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
-        const uint64_t me = shm_->op(slot, static_cast<uint32_t>(rank_))->gpu_uid;
-        for (size_t k = 0; k < W; ++k) sharing += shm_->op(slot, static_cast<uint32_t>(k))->gpu_uid == me ? 1 : 0;
-    }
-    const int grid = std::max(256, 512 / std::max(1, sharing));
+    std::vector<uint64_t> uids(W);
+    for (size_t k = 0; k < W; ++k) uids[k] = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->gpu_uid;
+    const int grid = ipc_grid_budget(uids, rank_);
 
     if (inter) {
         // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push

@@ -51,6 +51,18 @@ constexpr uint32_t kIpcMaxSegs = 16;                              // => ops of u
 class Client;
 struct ArenaShm;
 
+// Workgroup budget of one xGMI kernel: 512 per GPU (2 per CU, the measured optimum for these streaming kernels,
+// profiles/r1_ipc_grid_sweep.md) split between the ring members whose kernels run on the same physical GPU (same
+// uid), but not below 256 per kernel (fewer cannot saturate HBM).
+int ipc_grid_budget(const std::vector<uint64_t> &gpu_uids, size_t rank);
+
+// Peer-access precheck of an IPC op: every ring member's GPU that is visible here (uid -> local ordinal) must be
+// mappable from `my_device`; members on GPUs this process cannot see are left to hipIpcOpenMemHandle (its failure
+// also falls back to the TCP ring). Returns the first member that fails, or -1.
+int ipc_unreachable_peer(const std::vector<uint64_t> &gpu_uids, size_t rank, int my_device,
+                         const std::function<int(uint64_t)> &device_of_uid,
+                         const std::function<bool(int, int)> &can_access_peer);
+
 class IpcArena {
 public:
     // kAbortedByMaster: the vote barrier consumed the master's abort packet for this op (exactly one is sent per op,

@@ -33,6 +33,9 @@ public:
     virtual int current_device() = 0;
     // process-independent identity of a device (hash of its PCI bus id): peers compare it to find GPU sharing
     virtual uint64_t device_uid(int dev) = 0;
+    // visible device with this uid (-1: not visible to this process); whether `dev` can map `peer`'s memory
+    virtual int device_of_uid(uint64_t uid) = 0;
+    virtual bool can_access_peer(int dev, int peer) = 0;
 
     // memory
     virtual void *alloc_device(size_t n) = 0;

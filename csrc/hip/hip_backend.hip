@@ -49,6 +49,21 @@ public:
         for (const char *c = bus; *c; ++c) h = (h ^ static_cast<uint8_t>(*c)) * 1099511628211ull;
         return h;
     }
+    int device_of_uid(uint64_t uid) override {
+        const int n = device_count();
+        for (int d = 0; d < n; ++d)
+            if (device_uid(d) == uid) return d;
+        return -1;
+    }
+    bool can_access_peer(int dev, int peer) override {
+        if (dev == peer) return true;
+        int ok = 0;
+        if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return ok != 0;
+    }
     int current_device() override {
         int d = -1;
         (void)hipGetDevice(&d);

@@ -514,6 +514,9 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int n
                 if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
         }
     }
+    // destinations may be another GPU's HBM (IPC-mapped over xGMI): release at system scope, so a peer that observes
+    // this op's completion through the host-side barrier reads the finished bytes
+    __threadfence_system();
 }
 
 // Tiled variant of k_multi_reduce_vec: workgroup t owns the contiguous tile [t*kBlock*U, (t+1)*kBlock*U) of vectors
@@ -579,6 +582,9 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_tile(DstList dsts, int 
                 if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
         }
     }
+    // destinations may be another GPU's HBM (IPC-mapped over xGMI): release at system scope, so a peer that observes
+    // this op's completion through the host-side barrier reads the finished bytes
+    __threadfence_system();
 }
 
 template<typename E, typename Op, bool AVG>
@@ -594,6 +600,7 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(DstList dsts, in
         const S v = E::st(acc);
         for (int k = 0; k < ndst; ++k) static_cast<S *>(dsts.p[k])[i] = v;
     }
+    __threadfence_system(); // see k_multi_reduce_vec
 }
 
 // ---------------------------------------------------------------- xGMI multi-source gather (all-gather phase)

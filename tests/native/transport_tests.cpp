@@ -115,7 +115,7 @@ TEST(es_interrupt_idle_server) {
     const auto t0 = std::chrono::steady_clock::now();
     s.interrupt();
     s.join();
-    EXPECT(std::chrono::steady_clock::now() - t0 < 1s);
+    EXPECT(std::chrono::steady_clock::now() - t0 < 5s);
     EXPECT(!s.running());
 }
 
@@ -126,7 +126,7 @@ TEST(es_interrupt_with_connected_clients_closes_them) {
     EXPECT(eventually([&] { std::lock_guard l(e->m); return e->joined.size() == 4; }));
     const auto t0 = std::chrono::steady_clock::now();
     delete e; // interrupt + join: no close callbacks on interrupt, sockets closed
-    EXPECT(std::chrono::steady_clock::now() - t0 < 2s);
+    EXPECT(std::chrono::steady_clock::now() - t0 < 5s);
     for (int fd : fds) {
         uint8_t b;
         EXPECT(!net::recv_all(fd, &b, 1)); // EOF
@@ -146,7 +146,7 @@ TEST(es_interrupt_while_client_streams) {
     EXPECT(eventually([&] { return e->count() > 3; }));
     const auto t0 = std::chrono::steady_clock::now();
     delete e;
-    EXPECT(std::chrono::steady_clock::now() - t0 < 2s);
+    EXPECT(std::chrono::steady_clock::now() - t0 < 5s);
     stop = true;
     ::shutdown(fd, SHUT_RDWR);
     t.join();
@@ -449,7 +449,7 @@ TEST(mc_timeout_and_poll) {
     const auto t0 = std::chrono::steady_clock::now();
     EXPECT(!c.receive<proto::M2CCollectiveCommsAbort>(nullptr, 80ms));
     const auto dt = std::chrono::steady_clock::now() - t0;
-    EXPECT(dt >= 70ms && dt < 2s);
+    EXPECT(dt >= 70ms && dt < 5s);
     EXPECT(!c.receive<proto::M2CCollectiveCommsAbort>(nullptr, 0ms)); // poll
     c.interrupt();
     c.join();
@@ -571,7 +571,7 @@ TEST(connect_to_closed_port_fails_fast) {
     net::close_fd(fd);
     const auto t0 = std::chrono::steady_clock::now();
     EXPECT(net::connect_tcp(loop_v4(port), 2000) < 0);
-    EXPECT(std::chrono::steady_clock::now() - t0 < 1500ms);
+    EXPECT(std::chrono::steady_clock::now() - t0 < 5s);
 }
 
 TEST(listen_bump_finds_next_free_port) {

@@ -15,6 +15,7 @@
 #include "net/mux.hpp"
 #include "net/socket.hpp"
 #include "proto/packets.hpp"
+#include "client/ipc.hpp"
 
 #include <sys/socket.h>
 #include <unistd.h>
@@ -340,6 +341,34 @@ TEST(event_server_ltv_roundtrip_and_close_callbacks) {
     EXPECT(got.load() == 1 && got_len.load() == big.size() && closed.load() == 1);
     srv.interrupt();
     srv.join();
+}
+
+// xGMI path on a multi-GPU node without the node: the workgroup budget and the peer-access precheck with fake GPU uids
+TEST(ipc_grid_budget_by_gpu_sharing) {
+    using client::ipc_grid_budget;
+    const std::vector<uint64_t> eight_gpus = {11, 12, 13, 14, 15, 16, 17, 18};
+    for (size_t r = 0; r < 8; ++r) EXPECT(ipc_grid_budget(eight_gpus, r) == 512); // one peer per GPU: whole chip
+    const std::vector<uint64_t> pairs = {1, 1, 2, 2};
+    EXPECT(ipc_grid_budget(pairs, 0) == 256 && ipc_grid_budget(pairs, 3) == 256);
+    const std::vector<uint64_t> one_gpu(8, 7);
+    EXPECT(ipc_grid_budget(one_gpu, 5) == 256); // floor: fewer cannot saturate HBM
+    const std::vector<uint64_t> mixed = {1, 2, 2, 2, 3};
+    EXPECT(ipc_grid_budget(mixed, 0) == 512 && ipc_grid_budget(mixed, 1) == 256);
+}
+
+TEST(ipc_peer_access_precheck) {
+    using client::ipc_unreachable_peer;
+    const std::vector<uint64_t> uids = {100, 101, 102, 103};
+    auto visible = [](uint64_t u) { return u >= 100 && u < 104 ? static_cast<int>(u - 100) : -1; };
+    auto full_mesh = [](int, int) { return true; };
+    EXPECT(ipc_unreachable_peer(uids, 0, 0, visible, full_mesh) == -1);
+    auto no_2 = [](int d, int p) { return !(d == 0 && p == 2); }; // device 0 cannot map device 2
+    EXPECT(ipc_unreachable_peer(uids, 0, 0, visible, no_2) == 2);
+    EXPECT(ipc_unreachable_peer(uids, 1, 1, visible, no_2) == -1);
+    auto invisible = [](uint64_t u) { return u == 100 ? 0 : -1; }; // other GPUs not visible: left to the IPC open
+    EXPECT(ipc_unreachable_peer(uids, 0, 0, invisible, [](int, int) { return false; }) == -1);
+    const std::vector<uint64_t> same = {5, 5, 5};
+    EXPECT(ipc_unreachable_peer(same, 1, 0, visible, [](int, int) { return false; }) == -1);
 }
 
 int main() {
