@@ -733,6 +733,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     std::vector<uint64_t> uids(W);
     for (size_t k = 0; k < W; ++k) uids[k] = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->gpu_uid;
     const int grid = ipc_grid_budget(uids, rank_);
+    bool remote = false; // a destination lives on another GPU: system-scope release at kernel end
+    for (uint64_t u : uids) remote = remote || u != uids[rank_];
 
     if (inter) {
         // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push
@@ -758,7 +760,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
             for (size_t k = 0; k < W; ++k) dsts[k] = ctx.out[k].at(a);
             const void *one = pbase + (a - b0);
             return be->multi_reduce(dsts.data(), static_cast<int>(W), &one, 1, (b - a) / es, dtype, ReduceOp::Sum, st,
-                                    grid);
+                                    grid, remote);
         });
         if (!bcast || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: host-local broadcast failed";
@@ -775,7 +777,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
                 dsts[k] = ctx.out[k].at(a);
             }
             return be->multi_reduce(dsts.data(), static_cast<int>(W), srcs.data(), static_cast<int>(W), (b - a) / es,
-                                    dtype, op, st, grid);
+                                    dtype, op, st, grid, remote);
         });
         fault_point("ipc_kernel", seq); // the kernels of every peer are in flight here
         if (!launched || !be->stream_sync(st)) {

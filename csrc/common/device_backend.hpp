@@ -79,9 +79,10 @@ public:
     // Intra-node xGMI kernels. srcs[k] points to shard `count` elements in peer k's buffer (IPC-mapped);
     // every dsts[0..ndst) receives op(srcs[0..n)) reduced in order 0..n-1 (the own output and, in the one-shot push
     // all-reduce, the IPC-mapped outputs of the peers). Avg divides by n at the end.
-    // max_grid: workgroup budget of this launch (0 = default); peers sharing one GPU split the chip between them
+    // max_grid: workgroup budget of this launch (0 = default); peers sharing one GPU split the chip between them.
+    // release_system: a destination is another GPU's memory (system-scope release at kernel end)
     virtual bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
-                              ReduceOp op, DevStream s, int max_grid = 0) = 0;
+                              ReduceOp op, DevStream s, int max_grid = 0, bool release_system = false) = 0;
     // dst regions gathered from n sources: dst[k*stride ...] = srcs[k] for k != skip (count elements each,
     // segment k has counts[k] elements at element offset offsets[k]).
     virtual bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,

@@ -195,8 +195,9 @@ public:
         return hipk::launch_finalize_avg(dst, count, t, ws, static_cast<hipStream_t>(s));
     }
     bool multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t, ReduceOp op,
-                      DevStream s, int max_grid) override {
-        return hipk::launch_multi_reduce(dsts, ndst, srcs, n, count, t, op, static_cast<hipStream_t>(s), max_grid);
+                      DevStream s, int max_grid, bool release_system) override {
+        return hipk::launch_multi_reduce(dsts, ndst, srcs, n, count, t, op, static_cast<hipStream_t>(s), max_grid,
+                                         release_system);
     }
     bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n, int skip,
                       DType t, DevStream s) override {

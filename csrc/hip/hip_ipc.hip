@@ -14,7 +14,7 @@ static int env_int(const char *name, int dflt) {
 }
 
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
-                         ReduceOp op, hipStream_t st, int max_grid_hint) {
+                         ReduceOp op, hipStream_t st, int max_grid_hint, bool release) {
     if (count == 0) return true;
     if (n < 1 || n > kMaxSrc || ndst < 1 || ndst > kMaxSrc) return false;
     SrcList sl{};
@@ -58,10 +58,10 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
                     auto go = [&](auto avg_c, auto u_c) {
                         if (tiled)
                             k_multi_reduce_tile<E, O, decltype(avg_c)::value, decltype(u_c)::value>
-                                <<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
+                                <<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec, release ? 1 : 0);
                         else
                             k_multi_reduce_vec<E, O, decltype(avg_c)::value, decltype(u_c)::value>
-                                <<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec);
+                                <<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, nvec, release ? 1 : 0);
                     };
                     using T2 = std::integral_constant<int, 2>;
                     using T4 = std::integral_constant<int, 4>;
@@ -82,11 +82,11 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
                 ok = launch_ok([&] {
                     if constexpr (std::is_same_v<O, OpSum>) {
                         if (avg) {
-                            k_multi_reduce_scalar<E, O, true><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin);
+                            k_multi_reduce_scalar<E, O, true><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin, release ? 1 : 0);
                             return;
                         }
                     }
-                    k_multi_reduce_scalar<E, O, false><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin);
+                    k_multi_reduce_scalar<E, O, false><<<grid, kBlock, 0, st>>>(dl, ndst, sl, n, count, begin, release ? 1 : 0);
                 });
             }
             return ok;

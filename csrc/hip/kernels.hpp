@@ -459,8 +459,18 @@ struct DstList {
 // every peer gets bit-identical bytes) and stores the result to every destination. In the one-shot IPC all-reduce the
 // destinations are the receive buffers of all peers (remote ones over xGMI: posted writes, so the outbound direction
 // of the links carries the all-gather while the inbound direction carries the reduce-scatter reads).
+// End of an xGMI kernel whose destinations include another GPU's HBM (IPC-mapped): one system-scope release per
+// workgroup (after every wave's stores issued) makes them visible to a peer that observes this op's completion through
+// the host-side barrier. Launched only when a destination is remote: per workgroup it costs ~5% of the kernel's
+// bandwidth, per thread 15-35% (profiles/r2/kernels_fence.md); same-GPU destinations need no more than kernel end.
+__device__ __forceinline__ void ipc_release_system() {
+    __syncthreads();
+    if (threadIdx.x == 0) __threadfence_system();
+}
+
 template<typename E, typename Op, bool AVG, int U = 2>
-__global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec) {
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec,
+                                                          int release) {
     // U vectors (i, i + stride, ...) per thread and iteration: U x nsrc 16-byte loads in flight
     using S = typename E::S;
     using C = typename E::C;
@@ -514,9 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int n
                 if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
         }
     }
-    // destinations may be another GPU's HBM (IPC-mapped over xGMI): release at system scope, so a peer that observes
-    // this op's completion through the host-side barrier reads the finished bytes
-    __threadfence_system();
+    if (release) ipc_release_system(); // uniform per launch
 }
 
 // Tiled variant of k_multi_reduce_vec: workgroup t owns the contiguous tile [t*kBlock*U, (t+1)*kBlock*U) of vectors
@@ -524,7 +532,8 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_vec(DstList dsts, int n
 // streamed operands do not evict each other from L2; U x nsrc loads in flight per thread. Same fixed peer order and
 // single rounding as k_multi_reduce_vec (bit-identical results).
 template<typename E, typename Op, bool AVG, int U = 4>
-__global__ __launch_bounds__(kBlock) void k_multi_reduce_tile(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec) {
+__global__ __launch_bounds__(kBlock) void k_multi_reduce_tile(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t nvec,
+                                                           int release) {
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = Vec<E>::N;
@@ -582,14 +591,12 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_tile(DstList dsts, int 
                 if (has[u]) nt_store(static_cast<uint4 *>(dsts.p[k]) + idx[u], out[u]);
         }
     }
-    // destinations may be another GPU's HBM (IPC-mapped over xGMI): release at system scope, so a peer that observes
-    // this op's completion through the host-side barrier reads the finished bytes
-    __threadfence_system();
+    if (release) ipc_release_system(); // uniform per launch
 }
 
 template<typename E, typename Op, bool AVG>
 __global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(DstList dsts, int ndst, SrcList srcs, int nsrc, size_t n,
-                                                                size_t begin) {
+                                                                size_t begin, int release) {
     using S = typename E::S;
     using C = typename E::C;
     const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
@@ -600,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_multi_reduce_scalar(DstList dsts, in
         const S v = E::st(acc);
         for (int k = 0; k < ndst; ++k) static_cast<S *>(dsts.p[k])[i] = v;
     }
-    __threadfence_system(); // see k_multi_reduce_vec
+    if (release) ipc_release_system(); // uniform per launch
 }
 
 // ---------------------------------------------------------------- xGMI multi-source gather (all-gather phase)

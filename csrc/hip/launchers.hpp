@@ -27,7 +27,7 @@ bool launch_minmax(const void *src, size_t count, DType vtype, double *partial_s
 
 // hip_ipc.hip
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
-                         ReduceOp op, hipStream_t s, int max_grid = 0);
+                         ReduceOp op, hipStream_t s, int max_grid = 0, bool release = false);
 bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
                          int skip, DType t, hipStream_t s);
 
