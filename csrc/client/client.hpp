@@ -201,6 +201,9 @@ private:
     // shared state
     void serve_shared_state(int fd, SockAddr peer);
     bool hash_entry(const SSEntry &e, uint64_t &hash, HashType &type);
+    // Hashes many entries: device simplehashes are queued on one pooled stream per GPU (results into pinned words,
+    // one sync per GPU at the end) while host entries hash on the CPU meanwhile.
+    bool hash_entries(const std::vector<const SSEntry *> &entries, std::vector<uint64_t> &hashes, HashType &type);
 
     ClientConfig cfg_;
     net::MasterConnection master_;

@@ -36,6 +36,58 @@ static HashType announced_hash_type() {
     return t;
 }
 
+bool Client::hash_entries(const std::vector<const SSEntry *> &entries, std::vector<uint64_t> &hashes, HashType &type) {
+    type = announced_hash_type();
+    hashes.assign(entries.size(), 0);
+    DeviceBackend *be = device_backend();
+    if (type != HashType::Simple || !be) {
+        for (size_t i = 0; i < entries.size(); ++i)
+            if (!hash_entry(*entries[i], hashes[i], type)) return false;
+        return true;
+    }
+    struct DevBatch {
+        std::unique_ptr<StreamLease> stream;
+        std::vector<size_t> idx;
+    };
+    std::map<int, DevBatch> batches;
+    std::vector<size_t> host_idx;
+    std::vector<DevPtrInfo> info(entries.size());
+    for (size_t i = 0; i < entries.size(); ++i) {
+        be->pointer_info(entries[i]->data, info[i]);
+        if (entries[i]->bytes > 0 && info[i].is_device) batches[info[i].device].idx.push_back(i);
+        else host_idx.push_back(i);
+    }
+    Lease words(pinned_pool(), std::max<size_t>(entries.size(), 1) * sizeof(uint32_t));
+    auto *out = reinterpret_cast<uint32_t *>(words.data());
+    std::vector<Lease> temps; // 16-byte aligned copies of misaligned tensors (alive until the sync)
+    bool ok = out != nullptr;
+    for (auto &[dev, b] : batches) {
+        if (!ok) break;
+        be->set_device(dev);
+        b.stream = std::make_unique<StreamLease>(dev);
+        const DevStream st = b.stream->get();
+        for (size_t i : b.idx) {
+            const SSEntry &e = *entries[i];
+            const void *p = e.data;
+            if (reinterpret_cast<uintptr_t>(p) % 16 != 0) {
+                temps.emplace_back(device_pool(), e.bytes, dev);
+                be->memcpy_async(temps.back().data(), p, e.bytes, st);
+                p = temps.back().data();
+            }
+            ok = ok && be->simplehash_async(p, e.bytes, out + i, st);
+        }
+    }
+    for (size_t i : host_idx) // CPU entries hash while the GPUs work
+        ok = ok && hash_entry(*entries[i], hashes[i], type);
+    for (auto &[dev, b] : batches) {
+        if (!b.stream) continue;
+        be->set_device(dev);
+        ok = be->stream_sync(b.stream->get()) && ok;
+        for (size_t i : b.idx) hashes[i] = out[i];
+    }
+    return ok;
+}
+
 bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
     type = announced_hash_type();
     if (e.bytes == 0) {
@@ -48,8 +100,9 @@ bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
     if (type == HashType::Crc32) {
         if (pi.is_device) {
             be->set_device(pi.device);
+            StreamLease stream(pi.device);
             bool ok = true;
-            hash = device_crc32c(be, e.data, e.bytes, nullptr, &ok);
+            hash = device_crc32c(be, e.data, e.bytes, stream.get(), &ok);
             return ok;
         }
         if (e.device == DeviceType::Gpu) {
@@ -60,13 +113,16 @@ bool Client::hash_entry(const SSEntry &e, uint64_t &hash, HashType &type) {
         return true;
     }
     if (pi.is_device) {
+        // a pooled non-blocking stream (never the null stream: that would serialise against every stream of the
+        // application); the Python layer / caller has already synchronised the tensor's producer
         be->set_device(pi.device);
+        StreamLease stream(pi.device);
         if (reinterpret_cast<uintptr_t>(e.data) % 16 != 0) {
             Lease tmp(device_pool(), e.bytes, pi.device);
-            be->memcpy_sync(tmp.data(), e.data, e.bytes);
-            hash = be->simplehash(tmp.data(), e.bytes, nullptr);
+            be->memcpy_async(tmp.data(), e.data, e.bytes, stream.get());
+            hash = be->simplehash(tmp.data(), e.bytes, stream.get());
         } else {
-            hash = be->simplehash(e.data, e.bytes, nullptr);
+            hash = be->simplehash(e.data, e.bytes, stream.get());
         }
         return true;
     }
@@ -123,6 +179,13 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
     C2MSyncSharedState vote;
     vote.revision = ss.revision;
     vote.strategy = ss.strategy;
+    std::vector<const SSEntry *> to_hash;
+    for (const auto &e : ss.entries)
+        if (!e.allow_content_inequality) to_hash.push_back(&e);
+    std::vector<uint64_t> hashes;
+    HashType htype = HashType::Simple;
+    if (!hash_entries(to_hash, hashes, htype)) return false;
+    size_t hi = 0;
     for (const auto &e : ss.entries) {
         SharedStateHashEntry he;
         he.key = e.key;
@@ -130,7 +193,8 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         he.num_elements = e.count;
         he.allow_content_inequality = e.allow_content_inequality;
         if (!e.allow_content_inequality) {
-            if (!hash_entry(e, he.hash, he.hash_type)) return false;
+            he.hash = hashes[hi++];
+            he.hash_type = htype;
         }
         vote.entries.push_back(he);
     }
@@ -150,8 +214,9 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             c->serving_ = nullptr;
             // a requester reports completion once it holds the bytes, possibly before our sender thread returned
             // from its last send: wait for the serves so the caller may modify its tensors and tx_bytes is final
-            if (!c->ss_cv_.wait_for(l, std::chrono::seconds(30), [&] { return c->ss_active_serves_ == 0; }))
+            if (!c->ss_cv_.wait_for(l, std::chrono::seconds(30), [&] { return c->ss_active_serves_ == 0; })) {
                 LOG(WARN) << "Shared state sync: a serve to a peer is still running after 30 s";
+            }
         }
     } guard(this, &ss); // serve requests from the moment we vote (peers may be faster than our master packet)
 

@@ -88,8 +88,11 @@ public:
     virtual bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
                               int skip, DType t, DevStream s) = 0;
 
-    // Simple hash of device memory (bit-identical to kernels::simplehash_host). Synchronous.
+    // Simple hash of device memory (bit-identical to kernels::simplehash_host). Synchronous (syncs `s` only).
     virtual uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) = 0;
+    // Asynchronous variant: the final kernel writes the hash to `out_pinned` (pinned host memory) when `s` reaches
+    // it; several hashes can be queued on one stream and collected with a single stream_sync. 16-byte aligned input.
+    virtual bool simplehash_async(const void *dev_ptr, size_t n_bytes, uint32_t *out_pinned, DevStream s) = 0;
     // CRC-32C kernel pass over n_tiles 16 KiB tiles at a 16-byte aligned device pointer. Returns one raw CRC partial
     // per workgroup (each covers tiles_per_wg tiles, the last one the remainder). `tables` = 12 x 256 words (8 slicing
     // tables + the 16 KiB tile-shift table), `levels` = the 8 tree multipliers. Synchronous. Use device_crc32c().

@@ -216,6 +216,18 @@ public:
         }
         return out[0];
     }
+    bool simplehash_async(const void *dev_ptr, size_t n_bytes, uint32_t *out_pinned, DevStream s) override {
+        if (n_bytes == 0) {
+            *out_pinned = 0;
+            return true;
+        }
+        // the per-stream partials are reused by the next hash on the same stream only after this one's final kernel
+        // (stream order), so only the launch itself is serialised
+        Scratch &sc = scratch_for(s);
+        std::lock_guard l(*sc.mtx);
+        return hipk::launch_simplehash(dev_ptr, n_bytes, reinterpret_cast<uint32_t *>(sc.dev), out_pinned,
+                                       static_cast<hipStream_t>(s));
+    }
     bool crc32c_tiles(const void *dev_ptr, size_t n_tiles, const uint32_t *tables, const uint32_t *levels,
                       uint32_t *partials, size_t max_partials, size_t &n_partials, size_t &tiles_per_wg,
                       DevStream s) override {
@@ -260,7 +272,7 @@ public:
 
 private:
     struct Scratch {
-        double *dev = nullptr;  // 2 x 1024 doubles: min/max partials, or 960 hash partials
+        double *dev = nullptr;  // 2 x 1024 doubles: min/max partials, or 960 hash partials, or 4096 CRC partials
         double *host = nullptr; // pinned result words
         std::shared_ptr<std::mutex> mtx = std::make_shared<std::mutex>();
     };

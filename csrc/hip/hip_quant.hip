@@ -89,7 +89,7 @@ bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, 
         using S = typename E::S;
         constexpr int V = vec_width<S>();
         const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}});
-        const int grid = std::min(grid_for(count, pl.vec ? V : 1), 1024);
+        const int grid = std::min(grid_ew(count, pl, V), 1024); // <= 1024 partials (scratch size)
         return launch_ok([&] {
             k_minmax_partial<E><<<grid, kBlock, 0, st>>>(static_cast<const S *>(src), count, partial, pl.head, pl.vec);
             k_minmax_final<><<<1, kBlock, 0, st>>>(partial, grid, count, out2);

@@ -268,18 +268,21 @@ __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ d
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = vec_width<S>();
-    ew_loop<V>(
+    struct DQ {
+        Pack<S, V> d;
+        Pack<Q, V> q;
+    };
+    ew_loop_ls<V, kEwUnroll>(
         n, head, vec,
         [&](size_t i) {
             dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps(static_cast<int64_t>(src[i]), p))));
         },
-        [&](size_t b) {
-            auto d = ldp<S, V>(dst + b);
-            const auto q = ldp<Q, V>(src + b);
+        [&](size_t b) { return DQ{ldp_nt<S, V>(dst + b), ldp<Q, V>(src + b)}; },
+        [&](size_t b, DQ x) {
 #pragma unroll
             for (int e = 0; e < V; ++e)
-                d.v[e] = E::st(apply_op<Op, C>(E::ld(d.v[e]), static_cast<C>(dq_zps(static_cast<int64_t>(q.v[e]), p))));
-            stp<S, V>(dst + b, d);
+                x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), static_cast<C>(dq_zps(static_cast<int64_t>(x.q.v[e]), p))));
+            stp_nt<S, V>(dst + b, x.d);
         });
 }
 
@@ -336,10 +339,10 @@ __global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typ
                                                   QuantParams p, size_t head, int vec) {
     using S = typename E::S;
     constexpr int V = vec_width<S>();
-    ew_loop<V>(
+    ew_loop_ls<V, kEwUnroll>(
         n, head, vec, [&](size_t i) { dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p)); },
-        [&](size_t b) {
-            const auto s = ldp<S, V>(src + b);
+        [&](size_t b) { return ldp_nt<S, V>(src + b); },
+        [&](size_t b, const Pack<S, V> &s) {
             Pack<Q, V> q;
 #pragma unroll
             for (int e = 0; e < V; ++e) q.v[e] = static_cast<Q>(q_zps(static_cast<float>(E::ld(s.v[e])), p));
@@ -360,6 +363,26 @@ __device__ __forceinline__ void wave_minmax(C &lo, C &hi) {
     }
 }
 
+template<typename C>
+__device__ __forceinline__ void block_minmax(C &lo, C &hi, C *s_lo, C *s_hi) {
+    wave_minmax(lo, hi);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            lo = s_lo[k] < lo ? s_lo[k] : lo;
+            hi = s_hi[k] > hi ? s_hi[k] : hi;
+        }
+    }
+}
+
+// Pass 1: every workgroup reduces its tiles to a (min, max) partial. A single-launch variant (last workgroup folds
+// the partials behind a device-scope ticket) measured slower on MI355X - each workgroup's agent-scope release is an
+// L2 write-back (`buffer_wbl2`), 1024 of them cost more than the second launch (profiles/r2/kernels_polish.md).
 template<typename E>
 __global__ __launch_bounds__(kBlock) void k_minmax_partial(const typename E::S *__restrict__ src, size_t n,
                                                            double *__restrict__ partial, size_t head, int vec) {
@@ -378,23 +401,14 @@ __global__ __launch_bounds__(kBlock) void k_minmax_partial(const typename E::S *
 #pragma unroll
             for (int e = 0; e < V; ++e) take(E::ld(s.v[e]));
         });
-    wave_minmax(lo, hi);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        s_lo[w] = lo;
-        s_hi[w] = hi;
-    }
-    __syncthreads();
+    block_minmax(lo, hi, s_lo, s_hi);
     if (threadIdx.x == 0) {
-        for (int k = 1; k < kBlock / 64; ++k) {
-            lo = s_lo[k] < lo ? s_lo[k] : lo;
-            hi = s_hi[k] > hi ? s_hi[k] : hi;
-        }
         partial[2 * blockIdx.x] = static_cast<double>(lo);
         partial[2 * blockIdx.x + 1] = static_cast<double>(hi);
     }
 }
 
+// Pass 2 (one workgroup): fold the partials, write {min, max} to `out` (pinned host words)
 template<int Unused = 0>
 __global__ __launch_bounds__(kBlock) void k_minmax_final(const double *__restrict__ partial, int nblocks, size_t n,
                                                          double *__restrict__ out) {
@@ -404,18 +418,8 @@ __global__ __launch_bounds__(kBlock) void k_minmax_final(const double *__restric
         lo = partial[2 * i] < lo ? partial[2 * i] : lo;
         hi = partial[2 * i + 1] > hi ? partial[2 * i + 1] : hi;
     }
-    wave_minmax(lo, hi);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        s_lo[w] = lo;
-        s_hi[w] = hi;
-    }
-    __syncthreads();
+    block_minmax(lo, hi, s_lo, s_hi);
     if (threadIdx.x == 0) {
-        for (int k = 1; k < kBlock / 64; ++k) {
-            lo = s_lo[k] < lo ? s_lo[k] : lo;
-            hi = s_hi[k] > hi ? s_hi[k] : hi;
-        }
         out[0] = n ? lo : 0.0;
         out[1] = n ? hi : 0.0;
     }

@@ -23,7 +23,7 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
                            const kernels::QuantParams &p, hipStream_t s);
 bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
                      const kernels::QuantParams &p, hipStream_t s);
-bool launch_minmax(const void *src, size_t count, DType vtype, double *partial_scratch, double *out2, hipStream_t s);
+bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, double *out2, hipStream_t st);
 
 // hip_ipc.hip
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,

@@ -1,3 +1,5 @@
+#include <atomic>
+#include <immintrin.h>
 #include "host_kernels.hpp"
 
 #include <algorithm>
@@ -199,7 +201,9 @@ proto::QuantMeta host_quantize(void *dst_q, const void *src, size_t count, DType
         case DType::F16: ok = quantize_v<EF16>(dst_q, src, count, qtype, p); break;
         default: break;
     }
-    if (!ok) LOG(ERR) << "host_quantize: unsupported combination " << dtype_name(vtype) << " -> " << dtype_name(qtype);
+    if (!ok) {
+        LOG(ERR) << "host_quantize: unsupported combination " << dtype_name(vtype) << " -> " << dtype_name(qtype);
+    }
     return meta;
 }
 
@@ -516,14 +520,132 @@ __attribute__((target("sse4.2"))) uint32_t crc32c_hw3(const void *data, size_t n
     return ~c32;
 }
 
-bool crc32c_has_hw() {
-    if (g_spoof_no_hw) return false;
-    return __builtin_cpu_supports("sse4.2");
+// PCLMUL combine (reference crc32_amd64_sse42_pcmul.cpp): shifting a CRC by L bytes is a multiplication by a
+// constant; one carry-less multiply of the 32-bit CRC by a 64-bit constant K followed by one crc32q of the product
+// gives it. K is not hard-coded: g_K(c) = crc32q(0, clmul(c, K)) is linear in K and in c, so K is solved at first use
+// from the 32 x 32 equations g_K(e_i) = shift(e_i, L) by Gaussian elimination over GF(2) (and checked).
+namespace {
+// fold with a 128-bit product: crc32q over the low qword, then xor in the high qword's contribution
+__attribute__((target("sse4.2,pclmul"))) uint32_t clmul_apply(uint32_t c, uint64_t k) {
+    const __m128i prod = _mm_clmulepi64_si128(_mm_cvtsi32_si128(static_cast<int>(c)), _mm_cvtsi64_si128(static_cast<long long>(k)), 0x00);
+    const uint64_t lo = static_cast<uint64_t>(_mm_cvtsi128_si64(prod));
+    const uint64_t hi = static_cast<uint64_t>(_mm_extract_epi64(prod, 1));
+    return static_cast<uint32_t>(_mm_crc32_u64(0, lo)) ^ static_cast<uint32_t>(hi);
 }
+
+struct ClmulConst {
+    uint64_t k = 0;
+    bool ok = false;
+};
+
+// solves g_K = shift(., bytes) for K (64 unknown bits); needs pclmul + sse4.2 at run time
+__attribute__((target("sse4.2,pclmul"))) ClmulConst solve_clmul_const(uint64_t bytes) {
+    const uint32_t m = crc32c_x8n(bytes);
+    // equations: for every input bit i (c = 1 << i) and output bit r: xor_j K_j * bit_r(g_{e_j}(e_i)) = bit_r(f(e_i))
+    std::vector<std::pair<uint64_t, int>> rows; // (coefficients over the 64 K bits, rhs)
+    for (int i = 0; i < 32; ++i) {
+        uint32_t col[64];
+        for (int j = 0; j < 64; ++j) col[j] = clmul_apply(1u << i, 1ull << j);
+        const uint32_t want = crc32c_gf_mul(m, 1u << i);
+        for (int r = 0; r < 32; ++r) {
+            uint64_t coef = 0;
+            for (int j = 0; j < 64; ++j) coef |= static_cast<uint64_t>((col[j] >> r) & 1u) << j;
+            rows.emplace_back(coef, static_cast<int>((want >> r) & 1u));
+        }
+    }
+    ClmulConst out;
+    // Gauss-Jordan elimination
+    size_t rank = 0;
+    std::vector<int> pivot_col;
+    for (int col = 0; col < 64 && rank < rows.size(); ++col) {
+        size_t piv = rank;
+        while (piv < rows.size() && !((rows[piv].first >> col) & 1)) ++piv;
+        if (piv == rows.size()) continue;
+        std::swap(rows[piv], rows[rank]);
+        for (size_t r = 0; r < rows.size(); ++r)
+            if (r != rank && ((rows[r].first >> col) & 1)) {
+                rows[r].first ^= rows[rank].first;
+                rows[r].second ^= rows[rank].second;
+            }
+        pivot_col.push_back(col);
+        ++rank;
+    }
+    for (size_t r = rank; r < rows.size(); ++r)
+        if (rows[r].second) return out; // inconsistent: no such K
+    for (size_t r = 0; r < rank; ++r)
+        if (rows[r].second) out.k |= 1ull << pivot_col[r];
+    for (int i = 0; i < 32; ++i) // verify on the basis
+        if (clmul_apply(1u << i, out.k) != crc32c_gf_mul(m, 1u << i)) return out;
+    out.ok = true;
+    return out;
+}
+} // namespace
+
+static const ClmulConst &clmul_lane(int k) {
+    static const ClmulConst by_lane = solve_clmul_const(kCrcLane), by_2lanes = solve_clmul_const(2 * kCrcLane);
+    return k == 1 ? by_lane : by_2lanes;
+}
+
+bool crc32c_clmul_ready() {
+    return __builtin_cpu_supports("sse4.2") && __builtin_cpu_supports("pclmul") && clmul_lane(1).ok && clmul_lane(2).ok;
+}
+
+__attribute__((target("sse4.2,pclmul"))) uint32_t crc32c_hw3_clmul(const void *data, size_t n) {
+    const ClmulConst &by_lane = clmul_lane(1), &by_2lanes = clmul_lane(2);
+    if (!by_lane.ok || !by_2lanes.ok) return crc32c_hw3(data, n);
+    const auto *p = static_cast<const uint8_t *>(data);
+    uint64_t c0 = 0xffffffffu;
+    while (n >= 3 * kCrcLane) {
+        uint64_t c1 = 0, c2 = 0;
+        for (size_t i = 0; i < kCrcLane; i += 8) {
+            uint64_t a, b, d;
+            std::memcpy(&a, p + i, 8);
+            std::memcpy(&b, p + kCrcLane + i, 8);
+            std::memcpy(&d, p + 2 * kCrcLane + i, 8);
+            c0 = _mm_crc32_u64(c0, a);
+            c1 = _mm_crc32_u64(c1, b);
+            c2 = _mm_crc32_u64(c2, d);
+        }
+        c0 = clmul_apply(static_cast<uint32_t>(c0), by_2lanes.k) ^ clmul_apply(static_cast<uint32_t>(c1), by_lane.k) ^
+             static_cast<uint32_t>(c2);
+        p += 3 * kCrcLane;
+        n -= 3 * kCrcLane;
+    }
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        c0 = _mm_crc32_u64(c0, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t c32 = static_cast<uint32_t>(c0);
+    while (n--) c32 = _mm_crc32_u8(c32, *p++);
+    return ~c32;
+}
+
+// Runtime dispatch with spoofable CPU features (reference crc32_cpu.cpp + crc32_cpu_test.cpp:139-185): tests force a
+// lower tier to check every implementation on one machine.
+static std::atomic<int> g_crc_tier_cap{3};
+
+int crc32c_tier() {
+    int t = 0;
+    if (!g_spoof_no_hw && __builtin_cpu_supports("sse4.2")) t = __builtin_cpu_supports("pclmul") ? 2 : 1;
+    return std::min(t, g_crc_tier_cap.load(std::memory_order_relaxed));
+}
+
+void crc32c_spoof_tier(int max_tier) { g_crc_tier_cap.store(max_tier < 0 ? 3 : max_tier, std::memory_order_relaxed); }
+
+bool crc32c_has_hw() { return crc32c_tier() >= 1; }
 
 void crc32c_spoof_no_hw(bool no_hw) { g_spoof_no_hw = no_hw; }
 
-uint32_t crc32c(const void *data, size_t n) { return crc32c_has_hw() ? crc32c_hw3(data, n) : crc32c_sw(data, n); }
+uint32_t crc32c(const void *data, size_t n) {
+    switch (crc32c_tier()) {
+        case 2: return crc32c_hw3_clmul(data, n);
+        case 1: return crc32c_hw3(data, n);
+        default: return crc32c_sw(data, n);
+    }
+}
 
 
 // ------------------------------------------------------------------------------------------------------------------

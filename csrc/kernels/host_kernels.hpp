@@ -44,7 +44,13 @@ uint32_t crc32c(const void *data, size_t n_bytes);
 uint32_t crc32c_sw(const void *data, size_t n_bytes);
 uint32_t crc32c_hw(const void *data, size_t n_bytes);  // one crc32q chain
 uint32_t crc32c_hw3(const void *data, size_t n_bytes); // three interleaved chains + table-driven combine (default)
+uint32_t crc32c_hw3_clmul(const void *data, size_t n_bytes); // three chains + PCLMUL combine (default on EPYC)
+bool crc32c_clmul_ready(); // PCLMUL tier usable (CPU features + fold constants solved and verified)
 void crc32c_spoof_no_hw(bool no_hw); // test hook: force the software path
+// implementation tier picked by crc32c(): 0 table (slicing-by-8), 1 SSE4.2 (3 chains, table combine),
+// 2 SSE4.2 + PCLMUL; crc32c_spoof_tier(t) caps it for tests (-1 restores), like the reference's spoofed features
+int crc32c_tier();
+void crc32c_spoof_tier(int max_tier);
 bool crc32c_has_hw();
 
 // CRC-32C algebra for split computation (HIP kernel partials, hip_hash.hip). A "raw" CRC has no initial value and no

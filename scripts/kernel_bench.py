@@ -46,6 +46,11 @@ def main():
         n * 2 * 2 + n)
     row("dequant_reduce u8->bf16 sum (pccl)", timeit(lambda: K.dequant_reduce(x, q, meta, "min_max", "sum"), a.iters),
         n + 2 * n * 2)
+    qz, mz = K.quantize(y, torch.uint8, "zero_point_scale")
+    row("quantize bf16->u8 zero-point-scale (pccl)",
+        timeit(lambda: K.quantize(y, torch.uint8, "zero_point_scale"), a.iters), n * 2 * 2 + n)
+    row("dequant_reduce u8 zps->bf16 sum (pccl)",
+        timeit(lambda: K.dequant_reduce(x, qz, mz, "zero_point_scale", "sum"), a.iters), n + 2 * n * 2)
     if hasattr(torch, "float8_e4m3fn"):
         q8, m8 = K.quantize(y, torch.float8_e4m3fn, "min_max")
         row("quantize bf16->fp8 e4m3 (pccl)", timeit(lambda: K.quantize(y, torch.float8_e4m3fn, "min_max"), a.iters),

@@ -343,6 +343,39 @@ TEST(event_server_ltv_roundtrip_and_close_callbacks) {
     srv.join();
 }
 
+// every CRC-32C implementation tier agrees with the table version (sizes around the 3 x 8 KiB block, odd offsets)
+TEST(crc32c_tiers_agree) {
+    std::vector<uint8_t> buf((1 << 20) + 64);
+    std::mt19937 rng(7);
+    for (auto &b : buf) b = static_cast<uint8_t>(rng());
+    const int native = kernels::crc32c_tier();
+    if (native >= 2) EXPECT(kernels::crc32c_clmul_ready()); // the solved fold constants were found and verified
+    const size_t sizes[] = {0, 1, 7, 8, 9, 24575, 24576, 24577, 49152 + 13, 100000, 1 << 20};
+    for (size_t n : sizes)
+        for (size_t off : {0, 1, 3}) {
+            const uint32_t want = kernels::crc32c_sw(buf.data() + off, n);
+            EXPECT(kernels::crc32c_hw3(buf.data() + off, n) == want);
+            EXPECT(kernels::crc32c_hw3_clmul(buf.data() + off, n) == want);
+            for (int tier = 0; tier <= 2; ++tier) {
+                kernels::crc32c_spoof_tier(tier);
+                EXPECT(kernels::crc32c_tier() == std::min(tier, native));
+                EXPECT(kernels::crc32c(buf.data() + off, n) == want);
+            }
+            kernels::crc32c_spoof_tier(-1);
+        }
+    EXPECT(kernels::crc32c("123456789", 9) == 0xE3069283u); // CRC-32C check value
+    // throughput of each tier on this host (informational)
+    std::vector<uint8_t> big(64 << 20, 0x5A);
+    auto rate = [&](auto fn) {
+        const auto t0 = std::chrono::steady_clock::now();
+        volatile uint32_t sink = fn(big.data(), big.size());
+        (void)sink;
+        return big.size() / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 1e9;
+    };
+    std::printf("  crc32c GB/s: table %.2f, sse4.2 x3 %.2f, sse4.2 x3 + pclmul %.2f\n", rate(kernels::crc32c_sw),
+                rate(kernels::crc32c_hw3), rate(kernels::crc32c_hw3_clmul));
+}
+
 // xGMI path on a multi-GPU node without the node: the workgroup budget and the peer-access precheck with fake GPU uids
 TEST(ipc_grid_budget_by_gpu_sharing) {
     using client::ipc_grid_budget;

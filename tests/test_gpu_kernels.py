@@ -84,6 +84,21 @@ def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
     assert torch.equal(rd.cpu(), rh)
 
 
+@pytest.mark.parametrize("n", [1, 1000, (1 << 22) + 3, 300_000_001])
+def test_device_minmax_single_launch_repeated(hip, n):
+    """min/max is one launch with a last-workgroup fold and a re-armed ticket: repeated calls on the same stream
+    (all-negative data, then shifted data, tails, > 1024 workgroups of tiles) must equal the host."""
+    for shift in (-50.0, 3.0, 0.0):
+        if n < (1 << 23):
+            xd = (_rand(n, torch.float32, 7 + int(shift)) * 4 - 10.0 + shift).bfloat16().to(hip)
+        else:
+            xd = (torch.arange(n, device=hip, dtype=torch.float32).remainder_(977.0) - 500.0 + shift).bfloat16()
+        _, md = K.quantize(xd, torch.uint8, "min_max")
+        torch.cuda.synchronize()
+        xf = xd.float()
+        assert md[0] == float(xf.min()) and md[1] == float(xf.max()), (md, shift)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32])
 @pytest.mark.parametrize("nsrc", [2, 3, 5, 8, 16])
 @pytest.mark.parametrize("op", ["sum", "avg", "max"])
