@@ -106,8 +106,8 @@ def main():
     ap.add_argument("--deadline", type=float, default=0)
     ap.add_argument("--stop-after-optimize", type=int, default=20)
     ap.add_argument("--no-ipc", action="store_true",
-                    help="device ring over TCP instead of the xGMI IPC path (see docs/PERFORMANCE.md: a peer killed "
-                         "while a kernel of another peer accesses its exported HBM)")
+                    help="device ring over TCP instead of the xGMI IPC path (default: IPC, which survives a peer "
+                         "SIGKILLed mid-kernel since round 2; tests/test_fault_tolerance.py::test_gpu_ipc_sigkill_mid_op)")
     ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
     a = ap.parse_args()
     if a.rank is not None:
@@ -118,7 +118,7 @@ def main():
     deadline = time.time() + 240
     common = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
               "--deadline", str(deadline), "--stop-after-optimize", str(a.stop_after_optimize)]
-    env = {"PCCL_BENCHMARK_MILLIS": "300", "PCCL_NUM_BENCHMARK_CONNECTIONS": "2"}
+    env = {"PCCL_BENCHMARK_MILLIS": "300", "PCCL_NUM_BENCHMARK_CONNECTIONS": "2", "PCCL_SAME_HOST_MBPS": "0"}
     if a.no_ipc:
         env["PCCL_DISABLE_IPC"] = "1"
     lines = []

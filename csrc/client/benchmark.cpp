@@ -18,8 +18,9 @@ namespace pccl::client {
 using namespace std::chrono;
 
 BenchResult benchmark_send(const Uuid &self, const SockAddr &endpoint, double &mbps_out) {
-    const int n_conn = static_cast<int>(std::max<size_t>(1, env_size("PCCL_NUM_BENCHMARK_CONNECTIONS", 8)));
-    const double seconds = static_cast<double>(env_size("PCCL_BENCHMARK_MILLIS", 2000)) / 1000.0;
+    // reference defaults: 16 connections x 10 s of 8 MiB sends (benchmark_runner.cpp:11-13)
+    const int n_conn = static_cast<int>(std::max<size_t>(1, env_size("PCCL_NUM_BENCHMARK_CONNECTIONS", 16)));
+    const double seconds = static_cast<double>(env_size("PCCL_BENCHMARK_MILLIS", 10000)) / 1000.0;
     constexpr size_t kBuf = 8 << 20;
     std::vector<int> fds;
     for (int i = 0; i < n_conn; ++i) {
@@ -76,7 +77,7 @@ BenchResult benchmark_send(const Uuid &self, const SockAddr &endpoint, double &m
 }
 
 void benchmark_receive(int fd, const SockAddr &peer) {
-    const double seconds = static_cast<double>(env_size("PCCL_BENCHMARK_MILLIS", 2000)) / 1000.0 + 8.0;
+    const double seconds = static_cast<double>(env_size("PCCL_BENCHMARK_MILLIS", 10000)) / 1000.0 + 8.0;
     std::vector<uint8_t> buf(1 << 20);
     const auto t0 = steady_clock::now();
     while (duration<double>(steady_clock::now() - t0).count() < seconds) {

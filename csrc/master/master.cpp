@@ -530,6 +530,10 @@ void Master::handle_optimize(const SockAddr &addr) {
     check_optimize_consensus();
 }
 
+double Master::same_host_mbps() { // ~xGMI link class; read per round (tests switch it)
+    return static_cast<double>(env_size("PCCL_SAME_HOST_MBPS", 1000000));
+}
+
 void Master::check_optimize_consensus() {
     for (const auto &[_, c] : clients_)
         if (c.phase == Phase::Accepted && c.state != State::VoteOptimizeTopology) return;
@@ -549,6 +553,13 @@ void Master::check_optimize_consensus() {
             if (un != unreachable_.end() && un->second.count(e.to)) continue;
             const ClientInfo *to = client_by_uuid(e.to);
             if (!to || to->phase != Phase::Accepted) continue;
+            if (same_host_mbps() > 0 && !c.host_token.empty() && c.host_token == to->host_token) {
+                // same host (boot id + hostname): the pair talks over loopback or xGMI, never over the NIC, so it
+                // is not benchmarked (reference benchmarks every pair for 10 s); a fixed, NIC-beating cost makes
+                // the ATSP keep co-located peers adjacent (PCCL_SAME_HOST_MBPS, 0 = measure as usual)
+                groups_[c.group].bw.store(u, e.to, same_host_mbps());
+                continue;
+            }
             resp.requests.push_back(BenchmarkRequest{u, e.to, to->bm});
         }
         server_.send_packet(c.addr, resp);

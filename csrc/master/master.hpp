@@ -128,6 +128,7 @@ private:
     bool check_p2p_established();
     void check_pending_query_consensus();
     void check_optimize_consensus();
+    static double same_host_mbps();
     void check_optimize_complete_consensus();
     bool check_sync_consensus(uint32_t group);
     void check_sync_complete_consensus(uint32_t group);

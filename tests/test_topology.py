@@ -12,6 +12,7 @@ from pccl_amd.utils import local_master, run_threaded_peers
 def test_optimize_topology_then_reduce(world, monkeypatch):
     monkeypatch.setenv("PCCL_BENCHMARK_MILLIS", "150")
     monkeypatch.setenv("PCCL_NUM_BENCHMARK_CONNECTIONS", "2")
+    monkeypatch.setenv("PCCL_SAME_HOST_MBPS", "0")  # benchmark same-host pairs too (every test peer is local)
 
     def fn(rank, comm):
         comm.optimize_topology()
@@ -27,3 +28,24 @@ def test_optimize_topology_then_reduce(world, monkeypatch):
         res = run_threaded_peers(world, fn, address=addr, timeout=180)
     assert all(r[0] == world * (world + 1) / 2 and r[1] == world for r in res)
     assert sorted(r[3] for r in res) == list(range(world))  # a valid ring: every position taken once
+
+
+def test_optimize_topology_same_host_pairs_not_benchmarked(monkeypatch):
+    """Pairs on one host (same boot id + hostname) get a fixed xGMI-class cost instead of a 10 s loopback benchmark:
+    with the reference defaults (16 connections x 10 s) a 3-peer optimisation would take >= 60 s of benchmarks."""
+    import time
+    monkeypatch.delenv("PCCL_BENCHMARK_MILLIS", raising=False)
+    monkeypatch.delenv("PCCL_SAME_HOST_MBPS", raising=False)
+
+    def fn(rank, comm):
+        t0 = time.perf_counter()
+        comm.optimize_topology()
+        dt = time.perf_counter() - t0
+        x = torch.full((1000,), float(rank + 1))
+        comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)
+        return dt, float(x[0])
+
+    with local_master() as addr:
+        res = run_threaded_peers(3, fn, address=addr, timeout=120)
+    assert all(r[1] == 6.0 for r in res)
+    assert max(r[0] for r in res) < 8.0, res
