@@ -1,6 +1,11 @@
 """Elastic stress test: peers with cross-step background reduces are killed (SIGKILL) and respawned at random while
 the run continues (reference python/tests/stress_tests/*/stresstest_orchestrator.py). Asserts: no wrong reduce result
-ever, survivors keep making progress, every peer alive at the end exits cleanly."""
+ever, survivors keep making progress, every peer alive at the end exits cleanly.
+
+Soak mode (the reference orchestrator runs 8 h): PCCL_STRESS_SECONDS=28800 [PCCL_STRESS_PEERS=8] runs the same loop
+for that long with the reference's schedule (every 0.5-2 s: spawn with p = 0.6, SIGKILL with p = 0.4, never below 2
+alive); the GPU variant puts every peer's tensors on cuda:0 (xGMI/IPC path, kills land mid-kernel).
+"""
 import json
 import os
 import random
@@ -8,52 +13,84 @@ import signal
 import subprocess
 import time
 
+import pytest
+
 from pccl_amd.utils import local_master, spawn_python
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PEER = os.path.join(HERE, "workers", "stress_peer.py")
 
 
-def test_random_kill_respawn(tmp_path):
+def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
     rng = random.Random(1234)
     stop = tmp_path / "stop"
-    duration, target = 25.0, 4
     procs, killed = [], 0
     with local_master() as addr:
         def spawn():
-            procs.append(spawn_python([PEER, addr, str(stop)], env={"OMP_NUM_THREADS": "1"},
-                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+            # stdout to a file: a long soak must never block a peer on a full pipe
+            out = open(tmp_path / f"peer{len(procs)}.out", "w+")
+            procs.append((spawn_python([PEER, addr, str(stop)], env={"OMP_NUM_THREADS": "1", "STRESS_DEVICE": device},
+                                       stdout=out, stderr=subprocess.STDOUT, text=True), out))
         for _ in range(target):
             spawn()
         t_end = time.time() + duration
         while time.time() < t_end:
+            alive = [p for p, _ in procs if p.poll() is None]
+            if soak:  # reference schedule
+                time.sleep(rng.uniform(0.5, 2.0))
+                if rng.random() < 0.4 and len(alive) > 2:
+                    rng.choice(alive).send_signal(signal.SIGKILL)
+                    killed += 1
+                if rng.random() < 0.6 and len(alive) < 2 * target:
+                    spawn()
+                continue
             time.sleep(rng.uniform(2.0, 4.0))
-            alive = [p for p in procs if p.poll() is None]
             if len(alive) > 2:
                 victim = rng.choice(alive)
                 victim.send_signal(signal.SIGKILL)
                 killed += 1
-            if len([p for p in procs if p.poll() is None]) < target:
+            if len([p for p, _ in procs if p.poll() is None]) < target:
                 spawn()
         stop.write_text("1")
-        outs = []
-        for p in procs:
+        for p, out in procs:
             try:
-                outs.append(p.communicate(timeout=90))
+                p.wait(timeout=90)
             except subprocess.TimeoutExpired:
                 p.send_signal(signal.SIGUSR1)  # faulthandler: dump every thread's Python stack
                 time.sleep(1)
                 p.kill()
-                o, e = p.communicate()
-                raise AssertionError("peer did not stop:\n" + e[-6000:])
+                p.wait()
+                out.seek(0)
+                raise AssertionError("peer did not stop:\n" + out.read()[-6000:])
     summaries = []
-    for p, (o, e) in zip(procs, outs):
+    for p, out in procs:
+        out.seek(0)
+        text = out.read()
+        out.close()
         if p.returncode == -signal.SIGKILL:
             continue
-        assert p.returncode == 0, e[-3000:]
-        lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
-        assert lines, e[-2000:]
+        assert p.returncode == 0, text[-3000:]
+        lines = [json.loads(x) for x in text.splitlines() if x.startswith("{")]
+        assert lines, text[-2000:]
         summaries.append(lines[-1])
+    return killed, summaries
+
+
+def test_random_kill_respawn(tmp_path):
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "25"))
+    soak = duration > 60
+    killed, summaries = _run_stress(tmp_path, duration, int(os.environ.get("PCCL_STRESS_PEERS", "4")), soak=soak)
+    assert killed >= 3
+    assert summaries and all(s["bad"] == 0 for s in summaries), summaries
+    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+
+
+@pytest.mark.gpu
+def test_random_kill_respawn_gpu_ipc(tmp_path, hip):
+    """Device tensors on cuda:0: the peers reduce over the xGMI/IPC path, so SIGKILLs land during IPC votes and
+    kernels; no wrong result, survivors progress, everyone alive at the end exits cleanly."""
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
+    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
     assert sum(s["ok_ops"] for s in summaries) > 10, summaries

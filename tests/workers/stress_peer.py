@@ -26,11 +26,14 @@ def main():
     torch.set_num_threads(1)
     master, stop_file = sys.argv[1], sys.argv[2]
     n_tensors = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+    dev = torch.device(os.environ.get("STRESS_DEVICE", "cpu"))  # cuda:0 -> device tensors (xGMI/IPC path)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
     comm = pccl.Communicator(master, 0, p2p_connection_pool_size=2)
     comm.connect(n_attempts=30)
-    weights = torch.zeros(4096)
+    weights = torch.zeros(4096, device=dev)
     state = pccl.SharedState([pccl.TensorInfo.from_torch(weights, "weights")])
-    grads = [torch.ones(64 * 64 * (k + 1)) for k in range(n_tensors)]
+    grads = [torch.ones(64 * 64 * (k + 1) * (64 if dev.type == "cuda" else 1), device=dev) for k in range(n_tensors)]
     bad, ok_ops, failed_ops, steps, syncs = 0, 0, 0, 0, 0
     reduce_thread = None
     result = {}
