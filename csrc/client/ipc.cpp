@@ -18,6 +18,7 @@
 #include "../common/log.hpp"
 #include "client.hpp"
 #include "pools.hpp"
+#include "vmm_share.hpp"
 #include "../common/trace.hpp"
 
 namespace pccl::client {
@@ -247,17 +248,36 @@ std::shared_ptr<IpcArena> IpcArena::create(Client &c, const std::vector<Uuid> &r
     return arena;
 }
 
+bool IpcArena::safe_mode() {
+    static const bool safe = [] {
+        const char *v = std::getenv("PCCL_IPC_MODE");
+        return !(v && std::strcmp(v, "fast") == 0);
+    }();
+    return safe;
+}
+
+void IpcArena::release_mapping(const MapKey &key, Mapping &m) {
+    DeviceBackend *be = device_backend();
+    be->set_device(std::get<2>(key));
+    if (m.vmm) be->vmm_unmap(m.ptr);
+    else be->ipc_close(m.ptr);
+}
+
 IpcArena::~IpcArena() {
     DeviceBackend *be = device_backend();
     if (be) {
         const int cur = be->current_device();
-        for (auto &[key, m] : mappings_) {
-            be->set_device(std::get<2>(key));
-            be->ipc_close(m.ptr);
-        }
+        for (auto &[key, m] : mappings_) release_mapping(key, m);
         for (auto &b : bufs_) {
             be->set_device(b->device);
-            for (void *p : b->segs) be->free_device(p);
+            for (size_t k = 0; k < b->segs.size(); ++k) {
+                if (b->share_ids[k]) {
+                    VmmShare::instance().retract(b->share_ids[k]);
+                    be->vmm_free(b->segs[k]);
+                } else {
+                    be->free_device(b->segs[k]);
+                }
+            }
         }
         if (cur >= 0) be->set_device(cur);
     }
@@ -280,20 +300,57 @@ IpcArena::CommBuf *IpcArena::acquire_buffer(size_t bytes, int device) {
     be->set_device(device);
     const size_t nseg = bytes <= kIpcSegBytes ? 1 : (bytes + kIpcSegBytes - 1) / kIpcSegBytes;
     const size_t seg_cap = nseg == 1 ? std::max<size_t>(bytes, 1 << 20) : kIpcSegBytes;
+    const bool vmm = safe_mode();
     auto undo = [&] {
-        for (void *p : b->segs) be->free_device(p);
+        for (size_t k = 0; k < b->segs.size(); ++k) {
+            if (b->share_ids[k]) {
+                VmmShare::instance().retract(b->share_ids[k]);
+                be->vmm_free(b->segs[k]);
+            } else {
+                be->free_device(b->segs[k]);
+            }
+        }
     };
     for (size_t k = 0; k < nseg; ++k) {
-        void *p = be->alloc_device(seg_cap);
         std::array<uint8_t, kIpcHandleBytes> h{};
-        if (!p || !be->ipc_export(p, h.data())) {
-            if (p) be->free_device(p);
+        void *p = nullptr;
+        uint64_t id = 0;
+        if (vmm) { // fault-safe: VMM allocation shared as an fd (importers hold their own reference)
+            int fd = -1;
+            size_t alloc = 0;
+            p = be->vmm_alloc(seg_cap, device, &fd, &alloc);
+            if (p) {
+                id = VmmShare::instance().publish(fd);
+                if (id == 0) {
+                    ::close(fd);
+                    be->vmm_free(p);
+                    p = nullptr;
+                }
+            }
+            if (p) {
+                VmmHandle vh;
+                vh.pid = static_cast<int32_t>(getpid());
+                vh.nonce = VmmShare::instance().nonce();
+                vh.id = id;
+                vh.size = alloc;
+                std::memcpy(h.data(), &vh, sizeof(vh));
+            }
+        } else {
+            p = be->alloc_device(seg_cap);
+            if (p && !be->ipc_export(p, h.data())) {
+                be->free_device(p);
+                p = nullptr;
+            }
+        }
+        if (!p) {
             undo();
-            LOG(ERR) << "IPC arena: failed to allocate/export a " << seg_cap << "-byte comm buffer segment";
+            LOG(ERR) << "IPC arena: failed to allocate/export a " << seg_cap << "-byte comm buffer segment"
+                     << (vmm ? " (VMM)" : "");
             return nullptr;
         }
         b->segs.push_back(p);
         b->handles.push_back(h);
+        b->share_ids.push_back(id);
     }
     b->cap = nseg * seg_cap;
     b->busy = true;
@@ -320,9 +377,19 @@ void *IpcArena::pin_mapping(int peer, const uint8_t *handle, int my_device, MapK
     }
     DeviceBackend *be = device_backend();
     be->set_device(my_device);
-    void *p = be->ipc_open(handle);
+    void *p = nullptr;
+    VmmHandle vh;
+    const bool vmm = VmmHandle::decode(handle, vh);
+    if (vmm) {
+        const int fd = VmmShare::fetch(vh.pid, vh.nonce, vh.id);
+        if (fd < 0) return nullptr;
+        p = be->vmm_import(fd, vh.size, my_device);
+        ::close(fd);
+    } else {
+        p = be->ipc_open(handle);
+    }
     if (!p) return nullptr;
-    mappings_[key] = Mapping{p, 1, ++map_clock_};
+    mappings_[key] = Mapping{p, vmm, 1, ++map_clock_};
     // bound the number of open mappings (user allocations come and go): close the least recently used ones that no
     // op holds (an op's kernels may be reading / writing through every mapping it pinned)
     constexpr size_t kMaxMappings = 256;
@@ -331,8 +398,7 @@ void *IpcArena::pin_mapping(int peer, const uint8_t *handle, int my_device, MapK
         for (auto m = mappings_.begin(); m != mappings_.end(); ++m)
             if (m->second.refs == 0 && (victim == mappings_.end() || m->second.used < victim->second.used)) victim = m;
         if (victim == mappings_.end()) break; // everything is pinned by in-flight ops
-        be->set_device(std::get<2>(victim->first));
-        be->ipc_close(victim->second.ptr);
+        release_mapping(victim->first, victim->second);
         mappings_.erase(victim);
     }
     be->set_device(my_device);
@@ -480,13 +546,27 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
 }
 
 namespace {
-// staged comm buffer segments <-> a contiguous device buffer (copies on `st`, not synchronised)
+// PCCL_IPC_COPY=memcpy: staged copies with hipMemcpyAsync instead of the copy kernel
+bool copy_with_memcpy() {
+    static const bool m = [] {
+        const char *v = std::getenv("PCCL_IPC_COPY");
+        return v && std::strcmp(v, "memcpy") == 0;
+    }();
+    return m;
+}
+
+// staged comm buffer segments <-> a contiguous device buffer (copies on `st`, not synchronised). By default the
+// copies run as a kernel (same-device kernel -> kernel ordering on one stream, no copy-engine path for VMM memory).
 bool copy_staged(DeviceBackend *be, const std::vector<void *> &segs, uint8_t *user, size_t bytes, bool to_user,
                  DevStream st) {
     for (size_t k = 0, off = 0; off < bytes; ++k, off += kIpcSegBytes) {
         const size_t n = std::min(kIpcSegBytes, bytes - off);
         uint8_t *seg = static_cast<uint8_t *>(segs[k]);
-        if (!(to_user ? be->memcpy_async(user + off, seg, n, st) : be->memcpy_async(seg, user + off, n, st)))
+        void *d = to_user ? static_cast<void *>(user + off) : static_cast<void *>(seg);
+        const void *s = to_user ? static_cast<const void *>(seg) : static_cast<const void *>(user + off);
+        const size_t zero = 0;
+        if (!(copy_with_memcpy() ? be->memcpy_async(d, s, n, st)
+                                 : be->multi_gather(d, &s, &zero, &n, 1, -1, DType::U8, st)))
             return false;
     }
     return true;
@@ -519,7 +599,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         // Direct (zero-copy) access to the caller's buffers where HIP IPC can export them. An in-place op always
         // stages its input: peers read the staged copy while results land in the caller's buffer, and the copy is
         // the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
-        const bool allow_direct = !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
+        const bool allow_direct = !safe_mode() && !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
         if (allow_direct && src != dst)
             in_direct = export_user(const_cast<void *>(src), device, mine->in_handle[0], mine->in_off);
         if (allow_direct) out_direct = export_user(dst, device, mine->out_handle[0], mine->out_off);
@@ -646,11 +726,12 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
             map_failed_.store(true, std::memory_order_relaxed);
             return abort_voted(kAborted);
         }
-        if (PCCL_LOG_ENABLED(DEBUG))
+        if (PCCL_LOG_ENABLED(DEBUG)) {
             LOG(DEBUG) << "IPC seq " << seq << " peer " << k << " pid " << pids_[k] << " in "
                        << static_cast<const void *>(ctx.in[k].seg[0]) << " (" << ctx.in[k].seg.size() << " segs) out "
                        << static_cast<const void *>(ctx.out[k].seg[0]) << " (" << ctx.out[k].seg.size()
                        << " segs) bytes " << bytes;
+        }
     }
     ctx.pins = std::move(pins);
     {
@@ -733,8 +814,14 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     std::vector<uint64_t> uids(W);
     for (size_t k = 0; k < W; ++k) uids[k] = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->gpu_uid;
     const int grid = ipc_grid_budget(uids, rank_);
-    bool remote = false; // a destination lives on another GPU: system-scope release at kernel end
-    for (uint64_t u : uids) remote = remote || u != uids[rank_];
+    // system-scope release at kernel end when a destination lives on another GPU, or is a staged buffer that the
+    // copy-out reads with a copy engine: without it whole 4 KiB workgroup tiles of the result were still zero in the
+    // copy (measured: test_device_ipc_modes, 6144 stale floats in 6 tiles of a 12 MB op)
+    bool remote = false;
+    for (size_t k = 0; k < W; ++k) {
+        const OpPeerShm *p = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k));
+        remote = remote || uids[k] != uids[rank_] || !(p->zero_copy & 2u);
+    }
 
     if (inter) {
         // hierarchical: host-local reduce of my shard into scratch, inter-host ring on the scratch, local push
@@ -790,7 +877,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         const bool reduced = for_pieces(lo[rank_], n[rank_], [&](size_t a, size_t b) {
             for (size_t k = 0; k < W; ++k) srcs[k] = ctx.in[k].at(a);
             void *d0 = ctx.out[rank_].at(a);
-            return be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), (b - a) / es, dtype, op, st, grid);
+            return be->multi_reduce(&d0, 1, srcs.data(), static_cast<int>(W), (b - a) / es, dtype, op, st, grid,
+                                    remote);
         });
         if (!reduced || !be->stream_sync(st)) {
             LOG(ERR) << "IPC: multi-source reduce failed";
@@ -806,7 +894,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
             gathered = for_pieces(lo[k], n[k], [&](size_t a, size_t b) {
                 const void *s = ctx.out[k].at(a);
                 const size_t off = 0, cnt = (b - a) / es;
-                return be->multi_gather(ctx.out[rank_].at(a), &s, &off, &cnt, 1, -1, dtype, st);
+                return be->multi_gather(ctx.out[rank_].at(a), &s, &off, &cnt, 1, -1, dtype, st, ctx.out_staged);
             });
         }
         if (!gathered || !be->stream_sync(st)) {

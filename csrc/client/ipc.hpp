@@ -23,9 +23,14 @@
 // and kernels run in pieces that never cross a segment boundary (boundaries are multiples of kIpcSegBytes in op
 // byte space, the same for every peer). User buffers in larger allocations are staged.
 //
-// Buffer lifetime under faults: a mapping is pinned (reference-counted) by every op that uses it and is only closed
-// when unpinned; after an abort a peer waits until every live peer is past its kernels for that op before it
-// restores / releases buffers or returns (a dead peer's queues are gone once its process is).
+// Buffer lifetime under faults (PCCL_IPC_MODE, default "safe"): every exported buffer is a VMM allocation
+// (hipMemCreate) shared as a POSIX fd (vmm_share.hpp); an importer maps it into its own address space and holds its own
+// reference to the physical memory, so a peer SIGKILLed while the others' kernels read its input / write its output
+// leaves valid memory behind (profiles/r2/ipc/vmm_exporter_death_probe.log). hipIpc handles of the caller's buffers
+// are faster (no copy-in / copy-out) but a dead exporter's memory can vanish under a running kernel (GPU memory fault
+// in the 8-peer kill + rejoin benchmark, profiles/r2/ipc/): "fast" opts into them. A mapping is pinned
+// (reference-counted) by every op that uses it and is only closed when unpinned; after an abort a peer waits until
+// every live peer is past its kernels for that op before it restores / releases buffers or returns.
 #pragma once
 
 #include <array>
@@ -103,6 +108,7 @@ private:
     struct CommBuf {
         std::vector<void *> segs;
         std::vector<std::array<uint8_t, kIpcHandleBytes>> handles;
+        std::vector<uint64_t> share_ids; // VMM mode: ids of the fds published with VmmShare (0 = hipIpc export)
         size_t cap = 0;
         int device = -1;
         bool busy = false;
@@ -111,6 +117,7 @@ private:
     void release_buffer(CommBuf *b);
     struct Mapping {
         void *ptr = nullptr;
+        bool vmm = false;  // imported VMM allocation (unmap) vs hipIpc mapping (close)
         int refs = 0;      // ops that hold this mapping (never closed while > 0)
         uint64_t used = 0; // LRU stamp
     };
@@ -127,6 +134,9 @@ private:
     void drain_peers(Client &c, uint64_t seq);
     // PCCL_IPC_ALGO: "push" (default, one-shot reduce + broadcast) or "two_shot" (reduce-scatter, then gather)
     static bool push_algorithm();
+    // PCCL_IPC_MODE: "safe" (default: VMM-shared staging buffers only) or "fast" (hipIpc, zero-copy user buffers)
+    static bool safe_mode();
+    void release_mapping(const MapKey &key, Mapping &m);
 
     std::vector<Uuid> ring_;
     size_t rank_ = 0;

@@ -45,6 +45,14 @@ public:
     virtual bool ipc_export(void *dev_ptr, uint8_t handle[kIpcHandleBytes]) = 0;
     virtual void *ipc_open(const uint8_t handle[kIpcHandleBytes]) = 0;
     virtual void ipc_close(void *mapped) = 0;
+    // Fault-safe inter-process sharing (virtual memory management): device memory created with hipMemCreate and
+    // exported as a POSIX fd. An importer maps the fd into its own address space and holds its own reference to the
+    // physical memory, so the memory stays valid when the exporter dies mid-kernel (profiles/r2/ipc/). `size` is
+    // rounded up to the allocation granularity (returned in *alloc_size / expected by the others).
+    virtual void *vmm_alloc(size_t n, int device, int *fd_out, size_t *alloc_size) = 0;
+    virtual void vmm_free(void *p) = 0;                                // exporter side: unmap + release
+    virtual void *vmm_import(int fd, size_t size, int device) = 0;    // importer side (does not take the fd)
+    virtual void vmm_unmap(void *p) = 0;                               // importer side
     // allocation containing `p` (IPC handles always map the allocation base; offsets travel separately)
     virtual bool address_range(const void *p, void **base, size_t *size) = 0;
 
@@ -86,7 +94,7 @@ public:
     // dst regions gathered from n sources: dst[k*stride ...] = srcs[k] for k != skip (count elements each,
     // segment k has counts[k] elements at element offset offsets[k]).
     virtual bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
-                              int skip, DType t, DevStream s) = 0;
+                              int skip, DType t, DevStream s, bool release_system = false) = 0;
 
     // Simple hash of device memory (bit-identical to kernels::simplehash_host). Synchronous (syncs `s` only).
     virtual uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) = 0;

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <vector>
 #include <memory>
 #include <mutex>
 
@@ -107,6 +108,89 @@ public:
     void ipc_close(void *mapped) override {
         if (mapped) (void)hipIpcCloseMemHandle(mapped);
     }
+
+    void *vmm_alloc(size_t n, int device, int *fd_out, size_t *alloc_size) override {
+        hipMemAllocationProp prop = vmm_prop(device);
+        size_t gran = 0;
+        if (!HIP_OK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum)) || gran == 0)
+            return nullptr;
+        const size_t size = (std::max<size_t>(n, 1) + gran - 1) / gran * gran;
+        void *p = nullptr;
+        VmmMap m{size, {}, true, device};
+        {
+            // a retained allocation of this device that fits (at most 2x): still mapped, re-exported below
+            std::lock_guard l(vmm_mtx_);
+            auto best = retained_.end();
+            for (auto it = retained_.begin(); it != retained_.end(); ++it)
+                if (it->second.device == device && it->second.size >= size && it->second.size <= 2 * size &&
+                    (best == retained_.end() || it->second.size < best->second.size))
+                    best = it;
+            if (best != retained_.end()) {
+                p = best->first;
+                m = best->second;
+                retained_bytes_ -= m.size;
+                retained_.erase(best);
+            }
+        }
+        if (!p) {
+            if (!HIP_OK(hipMemCreate(&m.handle, size, &prop, 0))) return nullptr;
+            p = vmm_map(m.handle, size, device, gran);
+            if (!p) {
+                (void)hipMemRelease(m.handle);
+                return nullptr;
+            }
+        }
+        int fd = -1;
+        if (!HIP_OK(hipMemExportToShareableHandle(&fd, m.handle, hipMemHandleTypePosixFileDescriptor, 0)) || fd < 0) {
+            vmm_unmap_raw(p, m.size);
+            (void)hipMemRelease(m.handle);
+            return nullptr;
+        }
+        {
+            std::lock_guard l(vmm_mtx_);
+            vmm_[p] = m;
+        }
+        *fd_out = fd;
+        *alloc_size = m.size;
+        return p;
+    }
+    void vmm_free(void *p) override {
+        VmmMap m;
+        {
+            std::lock_guard l(vmm_mtx_);
+            auto it = vmm_.find(p);
+            if (it == vmm_.end()) return;
+            m = it->second;
+            vmm_.erase(it);
+            // exported comm buffers outlive their communicator in this cache (mapped, VA kept): unmapping is what
+            // costs address space (see vmm_unmap_raw)
+            if (m.owns_handle && retained_bytes_ + m.size <= vmm_retain_cap()) {
+                retained_bytes_ += m.size;
+                retained_[p] = m;
+                return;
+            }
+        }
+        vmm_unmap_raw(p, m.size);
+        if (m.owns_handle) (void)hipMemRelease(m.handle);
+    }
+    void *vmm_import(int fd, size_t size, int device) override {
+        hipMemGenericAllocationHandle_t h{};
+        int fd_copy = fd; // the runtime takes a pointer to the fd
+        if (!HIP_OK(hipMemImportFromShareableHandle(&h, &fd_copy, hipMemHandleTypePosixFileDescriptor))) return nullptr;
+        hipMemAllocationProp prop = vmm_prop(device);
+        size_t gran = 0;
+        if (!HIP_OK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum)) || gran == 0) {
+            (void)hipMemRelease(h);
+            return nullptr;
+        }
+        void *p = vmm_map(h, size, device, gran);
+        (void)hipMemRelease(h); // the mapping keeps the physical memory alive (even after the exporter's death)
+        if (!p) return nullptr;
+        std::lock_guard l(vmm_mtx_);
+        vmm_[p] = VmmMap{size, h, false, device};
+        return p;
+    }
+    void vmm_unmap(void *p) override { vmm_free(p); }
     bool address_range(const void *p, void **base, size_t *size) override {
         hipDeviceptr_t b = nullptr;
         size_t n = 0;
@@ -200,8 +284,9 @@ public:
                                          release_system);
     }
     bool multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n, int skip,
-                      DType t, DevStream s) override {
-        return hipk::launch_multi_gather(dst, srcs, offsets, counts, n, skip, t, static_cast<hipStream_t>(s));
+                      DType t, DevStream s, bool release_system) override {
+        return hipk::launch_multi_gather(dst, srcs, offsets, counts, n, skip, t, static_cast<hipStream_t>(s),
+                                         release_system);
     }
     uint32_t simplehash(const void *dev_ptr, size_t n_bytes, DevStream s) override {
         if (n_bytes == 0) return 0;
@@ -271,6 +356,63 @@ public:
     }
 
 private:
+    struct VmmMap {
+        size_t size = 0;
+        hipMemGenericAllocationHandle_t handle{};
+        bool owns_handle = false;
+        int device = 0;
+    };
+    std::mutex vmm_mtx_;
+    std::map<void *, VmmMap> vmm_;
+    std::map<void *, VmmMap> retained_; // freed exported allocations kept mapped for reuse
+    size_t retained_bytes_ = 0;
+    static size_t vmm_retain_cap() {
+        static const size_t cap = [] {
+            const char *v = std::getenv("PCCL_VMM_RETAIN_BYTES");
+            return v ? static_cast<size_t>(std::strtoull(v, nullptr, 10)) : (size_t{16} << 30);
+        }();
+        return cap;
+    }
+    static hipMemAllocationProp vmm_prop(int device) {
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = device;
+        prop.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+        return prop;
+    }
+    // reserve + map + read/write access for every visible device that can reach `device` (peers on other GPUs of this
+    // process may access it too)
+    void *vmm_map(hipMemGenericAllocationHandle_t h, size_t size, int device, size_t gran) {
+        void *p = nullptr;
+        if (!HIP_OK(hipMemAddressReserve(&p, size, gran, nullptr, 0))) return nullptr;
+        if (!HIP_OK(hipMemMap(p, size, 0, h, 0))) {
+            (void)hipMemAddressFree(p, size);
+            return nullptr;
+        }
+        std::vector<hipMemAccessDesc> acc;
+        const int n = device_count();
+        for (int d = 0; d < n; ++d) {
+            if (d != device && !can_access_peer(d, device)) continue;
+            hipMemAccessDesc a{};
+            a.location.type = hipMemLocationTypeDevice;
+            a.location.id = d;
+            a.flags = hipMemAccessFlagsProtReadWrite;
+            acc.push_back(a);
+        }
+        if (!HIP_OK(hipMemSetAccess(p, size, acc.data(), acc.size()))) {
+            vmm_unmap_raw(p, size);
+            return nullptr;
+        }
+        return p;
+    }
+    // Unmaps but never frees the address range. Measured on MI355X with both the ROCm 7.2 and PyTorch's bundled HIP
+    // runtime (csrc/tools/vmm_churn_probe.hip, profiles/r2/ipc/vmm_churn.md): once a range is hipMemAddressFree'd
+    // and handed out again by hipMemAddressReserve, kernels and copies on the new mapping read and write the wrong
+    // pages (146 of 150 rounds corrupted; live allocations overwritten), and with the range kept reserved, 0 of 150.
+    // A leaked range costs virtual address space only (the physical memory is released).
+    static void vmm_unmap_raw(void *p, size_t size) { (void)hipMemUnmap(p, size); }
+
     struct Scratch {
         double *dev = nullptr;  // 2 x 1024 doubles: min/max partials, or 960 hash partials, or 4096 CRC partials
         double *host = nullptr; // pinned result words

@@ -95,7 +95,7 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
 }
 
 bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
-                         int skip, DType t, hipStream_t st) {
+                         int skip, DType t, hipStream_t st, bool release) {
     if (n < 1 || n > kMaxSrc) return false;
     GatherList g{};
     size_t maxb = 0;
@@ -108,7 +108,8 @@ bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offse
     }
     if (maxb == 0) return true;
     const int gx = std::max(1, std::min(grid_for(maxb / 16 + 1, 4), 1024 / std::max(1, n - 1)));
-    return launch_ok([&] { k_multi_gather<><<<dim3(gx, n), kBlock, 0, st>>>(static_cast<uint8_t *>(dst), g, n, skip); });
+    return launch_ok([&] { k_multi_gather<><<<dim3(gx, n), kBlock, 0, st>>>(static_cast<uint8_t *>(dst), g, n, skip,
+                                                                         release ? 1 : 0); });
 }
 
 } // namespace pccl::hipk

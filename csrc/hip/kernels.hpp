@@ -622,7 +622,8 @@ struct GatherList {
 };
 
 template<int Unused = 0>
-__global__ __launch_bounds__(kBlock) void k_multi_gather(uint8_t *__restrict__ dst, GatherList g, int n, int skip) {
+__global__ __launch_bounds__(kBlock) void k_multi_gather(uint8_t *__restrict__ dst, GatherList g, int n, int skip,
+                                                          int release) {
     // blockIdx.y selects the segment (every peer's segment streams concurrently over its own xGMI link); within a
     // segment each workgroup copies one contiguous chunk, 4 x 16 B per thread in flight, non-temporal both ways
     const int k = blockIdx.y;
@@ -654,6 +655,7 @@ __global__ __launch_bounds__(kBlock) void k_multi_gather(uint8_t *__restrict__ d
         const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
         for (size_t b = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; b < bytes; b += stride) d[b] = src[b];
     }
+    if (release) ipc_release_system(); // uniform per launch (the early return above is per workgroup)
 }
 
 // ---------------------------------------------------------------- simplehash

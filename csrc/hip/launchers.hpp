@@ -29,7 +29,7 @@ bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, 
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
                          ReduceOp op, hipStream_t s, int max_grid = 0, bool release = false);
 bool launch_multi_gather(void *dst, const void *const *srcs, const size_t *offsets, const size_t *counts, int n,
-                         int skip, DType t, hipStream_t s);
+                         int skip, DType t, hipStream_t s, bool release = false);
 
 // hip_optim.hip
 bool launch_pseudo_grad(float *pg, const float *outer, const void *local, size_t count, DType lt, hipStream_t s);

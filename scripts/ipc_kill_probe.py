@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ipc_kill"))
     ap.add_argument("--inplace", action="store_true")
     ap.add_argument("--log-level", default="INFO")
+    ap.add_argument("--respawn", action="store_true", help="start a replacement peer after the kill (it joins the "
+                                                            "running ring: new IPC arena with a fresh process)")
     ap.add_argument("--inject", default="", help="PCCL_FAULT_INJECT for the victim (e.g. ipc_kernel:200): it kills "
                                                  "itself at that protocol point instead of the parent's timed SIGKILL")
     a = ap.parse_args()
@@ -87,6 +89,15 @@ def main():
             summary["victim_rc"] = ps[0].wait(timeout=60)
         except subprocess.TimeoutExpired:
             summary["victim_rc"] = "timeout"
+        if a.respawn and not summary.get("hung_before_kill"):
+            r = a.world
+            fo = open(os.path.join(a.out, f"peer{r}.out"), "w")
+            fe = open(os.path.join(a.out, f"peer{r}.err"), "w")
+            files += [fo, fe]
+            args = [sys.executable, "-u", worker, addr, str(a.world), str(r), "--const", "--n", str(a.n), "--dtype",
+                    "bf16", "--duration", str(max(2.0, a.duration / 2)), "--device", "cuda:0", "--reuse",
+                    "--check-every", "16", "--no-wait"] + (["--inplace"] if a.inplace else [])
+            ps.append(subprocess.Popen(args, stdout=fo, stderr=fe, env=env))
         rcs = []
         deadline = time.time() + a.duration + 30
         for p in ps[1:]:
@@ -106,7 +117,7 @@ def main():
         for f in files:
             f.close()
     summary["survivor_rcs"] = rcs
-    for r in range(a.world):
+    for r in range(len(ps)):
         with open(os.path.join(a.out, f"peer{r}.out")) as f:
             lines = [json.loads(x) for x in f if x.startswith("{")]
         oks = [x for x in lines if "error" not in x]
@@ -119,7 +130,7 @@ def main():
         summary[f"peer{r}"]["fault_lines"] = [ln for ln in err.splitlines() if "fault" in ln.lower()][:5]
     summary["killed_after_start_s"] = round(killed_at - t0, 2)
     print(json.dumps(summary), flush=True)
-    ok = all(rc == 0 for rc in rcs) and all(summary[f"peer{r}"]["bad"] == 0 for r in range(1, a.world))
+    ok = all(rc == 0 for rc in rcs) and all(summary[f"peer{r}"]["bad"] == 0 for r in range(1, len(ps)))
     sys.exit(0 if ok else 1)
 
 

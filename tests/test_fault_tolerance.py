@@ -104,21 +104,28 @@ def test_gpu_peer_crash_survivors_continue(hip):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("point,inplace", [("ipc_kernel", False), ("ipc_kernel", True), ("ipc_vote", True)])
-def test_gpu_ipc_sigkill_mid_op(hip, point, inplace):
+@pytest.mark.parametrize("point,inplace,respawn", [("ipc_kernel", False, False), ("ipc_kernel", True, False),
+                                                   ("ipc_vote", True, False), ("ipc_kernel", False, True)])
+def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn):
     """xGMI/IPC path, 3 processes on one GPU, 512 MiB bf16: peer 0 SIGKILLs itself at a fixed protocol point of op
     300 (PCCL_FAULT_INJECT) - right after launching its push kernel (every peer's kernel is then reading / writing the
     victim's exported HBM) or right after publishing its vote. Survivors must abort that op, re-form the ring and
-    keep producing exact results on the IPC path, with no GPU memory fault."""
+    keep producing exact results on the IPC path, with no GPU memory fault; with `respawn` a fresh replacement process
+    joins the running ring afterwards (new arena, the BASELINE config 5 sequence)."""
     import sys
     probe = os.path.join(os.path.dirname(HERE), "scripts", "ipc_kill_probe.py")
-    out = os.path.join(os.path.dirname(HERE), "gpurun_out", f"pytest_ipc_kill_{point}_{int(inplace)}")
-    args = [sys.executable, probe, "--inject", f"{point}:300", "--duration", "4", "--n", str(1 << 28), "--out", out]
-    r = subprocess.run(args + (["--inplace"] if inplace else []), capture_output=True, text=True, timeout=150)
+    out = os.path.join(os.path.dirname(HERE), "gpurun_out", f"pytest_ipc_kill_{point}_{int(inplace)}_{int(respawn)}")
+    args = [sys.executable, probe, "--inject", f"{point}:300", "--duration", "12" if respawn else "4", "--n",
+            str(1 << 28), "--out", out]
+    args += (["--inplace"] if inplace else []) + (["--respawn"] if respawn else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=150)
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["victim_rc"] == -9, summary
-    assert summary["survivor_rcs"] == [0, 0], (summary, r.stderr[-2000:])
+    assert summary["survivor_rcs"] == [0, 0] + ([0] if respawn else []), (summary, r.stderr[-2000:])
+    if respawn:
+        j = summary["peer3"]
+        assert j["bad"] == 0 and not j["fault_lines"] and j["ops_ok"] > 0 and 3 in j["worlds"], j
     for k in (1, 2):
         s_k = summary[f"peer{k}"]
         assert s_k["bad"] == 0 and not s_k["fault_lines"], s_k
-        assert s_k["worlds"] == [2, 3] and s_k["ops_ok"] > 300 and s_k["paths"] == [3], s_k
+        assert 2 in s_k["worlds"] and 3 in s_k["worlds"] and s_k["ops_ok"] > 300 and s_k["paths"] == [3], s_k

@@ -165,16 +165,18 @@ def test_device_shared_state(hip):
     assert [r[1] for r in res] == [0, n * 4, 0]
 
 
+@pytest.mark.parametrize("ipc_mode", ["safe", "fast"])
 @pytest.mark.parametrize("mode", ["zero_copy", "inplace", "mixed"])
-def test_two_process_ipc(hip, mode):
-    """Two processes on cuda:0 exchange device buffers through hipIpc handles (the intra-node xGMI path):
-    out-of-place ops export the caller's buffers (zero-copy, interior offsets), in-place ops a staged comm buffer."""
+def test_two_process_ipc(hip, mode, ipc_mode):
+    """Two processes on cuda:0 exchange device buffers (the intra-node xGMI path). safe (default): staged VMM
+    buffers shared as fds; fast: hipIpc handles, out-of-place ops export the caller's buffers (zero-copy, interior
+    offsets), in-place ops a staged comm buffer."""
     def extra(r):
         return ["--inplace"] if mode == "inplace" or (mode == "mixed" and r == 1) else []
     with local_master() as addr:
         procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, "2", str(r), "--n",
                                str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3",
-                               *extra(r)],
+                               *extra(r)], env={"PCCL_IPC_MODE": ipc_mode},
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
         outs = [p.communicate(timeout=240) for p in procs]
     for p, (o, e) in zip(procs, outs):
@@ -216,15 +218,21 @@ def test_device_ipc_modes(hip, inplace, no_zc, monkeypatch):
         monkeypatch.setenv("PCCL_IPC_NO_ZERO_COPY", "1")
     n = 3_000_001
     big = [torch.randn(n + 1000, device=hip) for _ in range(2)]
+    orig = [b[777:777 + n].cpu() for b in big]
+    expect_all = (big[0][777:777 + n] + big[1][777:777 + n]).clone()  # before any peer reduces in place
+    torch.cuda.synchronize()
 
     def fn(rank, comm):
         x = big[rank][777:777 + n]  # interior view: the IPC handle maps the allocation base
-        expect = (big[0][777:777 + n] + big[1][777:777 + n]).clone()
+        expect = expect_all
         y = x if inplace[rank] else torch.empty_like(x)
         comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
         torch.cuda.synchronize()
         return y.cpu(), expect.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
 
-    for y, expect, path in _run(2, fn):
+    for rank, (y, expect, path) in enumerate(_run(2, fn)):
         assert path == pccl.ReducePath.DEVICE_IPC.value
-        assert torch.equal(y, expect)
+        bad = (y != expect).nonzero().flatten()
+        assert bad.numel() == 0, dict(rank=rank, wrong=bad.numel(), first=bad[:4].tolist(), last=bad[-4:].tolist(),
+                                      zeros=int((y[bad] == 0).sum()), own_input=int((y[bad] == orig[rank][bad]).sum()),
+                                      peer_input=int((y[bad] == orig[1 - rank][bad]).sum()))
