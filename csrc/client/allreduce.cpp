@@ -21,6 +21,7 @@
 #include <cstring>
 
 #include "../common/log.hpp"
+#include "../common/spin.hpp"
 #include "../kernels/host_kernels.hpp"
 #include "client.hpp"
 #include "../common/trace.hpp"
@@ -149,6 +150,7 @@ bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
 
 void Client::run_op(const std::shared_ptr<OpState> &op) {
     const uint64_t tag = op->req.tag;
+    low_timer_slack();
     fault_delay(tag);
     OpTrace trace;
     current_trace() = trace_ops_enabled() ? &trace : nullptr;

@@ -2,6 +2,8 @@
 // Bounded busy-wait used before blocking on a condition variable in the latency-critical waits (master packets,
 // P2P sink progress): a futex wake-up of a sleeping thread costs 10-50 us on a loaded host, several times the
 // loopback round trip of a small collective. PCCL_SPIN_US (default 50, 0 disables) bounds the spin per wait.
+#include <sys/prctl.h>
+
 #include <chrono>
 #include <cstddef>
 
@@ -12,6 +14,13 @@ namespace pccl {
 inline long spin_budget_us() {
     static const long us = static_cast<long>(env_size("PCCL_SPIN_US", 50));
     return us;
+}
+
+/// The short sleeps of the op threads (IPC barriers: 5 us) would otherwise round up to the default 50 us timer
+/// slack; 1 us for the calling thread, once per thread.
+inline void low_timer_slack() {
+    static thread_local const bool done = [] { return prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0) == 0; }();
+    (void)done;
 }
 
 /// Spins until pred() is true or the budget is spent; returns pred()'s last value.

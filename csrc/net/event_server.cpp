@@ -83,6 +83,7 @@ void EventServer::loop() {
             if (errno == EINTR) continue;
             break;
         }
+        corked_ = true;
         for (int i = 0; i < n && !stop_; ++i) {
             const int fd = events[i].data.fd;
             if (fd == listen_fd_) {
@@ -101,6 +102,7 @@ void EventServer::loop() {
             if (events[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) handle_readable(c);
             if (!c.closing && (events[i].events & EPOLLOUT)) flush(c);
         }
+        flush_dirty();
         process_pending_closes();
         std::vector<std::function<void()>> posted;
         {
@@ -109,8 +111,11 @@ void EventServer::loop() {
         }
         for (auto &f : posted)
             if (!stop_) f();
+        flush_dirty();
         if (!posted.empty()) process_pending_closes();
         if (tick_cb_ && !stop_) tick_cb_();
+        flush_dirty();
+        corked_ = false;
     }
     // shutdown: close all clients (no callbacks on interrupt)
     for (auto &[fd, c] : clients_by_fd_) ::close(fd);
@@ -197,10 +202,32 @@ bool EventServer::send_raw(const SockAddr &client, uint16_t id, std::vector<uint
     Client &c = *clients_by_fd_.at(it->second);
     if (c.closing) return false;
     auto h = ltv_header(id, payload.size());
-    h.insert(h.end(), payload.begin(), payload.end());
-    c.wq.push_back(std::move(h));
-    flush(c);
+    if (corked_ && !c.wq.empty()) { // append to the pending buffer: one send() for the batch
+        auto &back = c.wq.back();
+        back.insert(back.end(), h.begin(), h.end());
+        back.insert(back.end(), payload.begin(), payload.end());
+    } else {
+        h.insert(h.end(), payload.begin(), payload.end());
+        c.wq.push_back(std::move(h));
+    }
+    if (!corked_) {
+        flush(c);
+    } else if (!c.dirty) {
+        c.dirty = true;
+        dirty_.push_back(c.fd);
+    }
     return true;
+}
+
+void EventServer::flush_dirty() {
+    for (int fd : dirty_) {
+        auto it = clients_by_fd_.find(fd);
+        if (it == clients_by_fd_.end()) continue;
+        Client &c = *it->second;
+        c.dirty = false;
+        if (!c.closing) flush(c);
+    }
+    dirty_.clear();
 }
 
 void EventServer::flush(Client &c) {
@@ -228,7 +255,7 @@ void EventServer::flush(Client &c) {
 
 void EventServer::update_events(Client &c) {
     epoll_event ev{};
-    ev.events = EPOLLIN | (c.want_out ? EPOLLOUT : 0);
+    ev.events = EPOLLIN | (c.want_out ? static_cast<uint32_t>(EPOLLOUT) : 0u);
     ev.data.fd = c.fd;
     epoll_ctl(epoll_fd_, EPOLL_CTL_MOD, c.fd, &ev);
 }

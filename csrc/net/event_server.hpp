@@ -62,6 +62,7 @@ private:
         size_t woff = 0;
         bool want_out = false;
         bool closing = false;
+        bool dirty = false; // queued bytes not yet handed to the socket (flushed at the end of the batch)
     };
 
     void loop();
@@ -70,6 +71,7 @@ private:
     void flush(Client &c);
     void process_pending_closes();
     void update_events(Client &c);
+    void flush_dirty();
 
     SockAddr listen_addr_;
     bool bump_;
@@ -84,6 +86,10 @@ private:
     std::unordered_map<int, std::unique_ptr<Client>> clients_by_fd_;
     std::unordered_map<SockAddrKey, int, SockAddrKeyHash> fd_by_addr_;
     std::vector<int> pending_close_;
+    // Sends issued while handling one batch of events are coalesced per client and flushed once at the end of the
+    // batch: a consensus that answers every peer (Abort + Complete to 8 peers) costs one send() per peer, not two.
+    bool corked_ = false;
+    std::vector<int> dirty_;
     std::mutex posted_mtx_;
     std::vector<std::function<void()>> posted_;
     ReadCb read_cb_;
