@@ -216,10 +216,16 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
     total = peers or job.total
 
     def fn(i, comm):
+        import contextlib
+
+        import pccl_amd as pccl
         g = torch.Generator(device=job.dev).manual_seed(job.first + i)
         n = nbytes // 2
-        x = torch.randn(n, device=job.dev, dtype=torch.bfloat16, generator=g)
-        y = torch.empty_like(x)
+        # xGMI path: buffers in fd-shareable memory (pccl_amd.memory), the documented way to get zero-copy fault-safe
+        # ops between processes; the TCP ring does not care where the buffers live
+        with pccl.memory.maybe_shareable(job.dev) if ipc else contextlib.nullcontext():
+            x = torch.randn(n, device=job.dev, dtype=torch.bfloat16, generator=g)
+            y = torch.empty_like(x)
         r = {"main": _timed(job, i, comm, x, y, steps, warmup)}
         tag = 10_000
         for b in sweep:

@@ -18,6 +18,7 @@
 #include "../common/log.hpp"
 #include "client.hpp"
 #include "pools.hpp"
+#include "shareable.hpp"
 #include "vmm_share.hpp"
 #include "../common/trace.hpp"
 
@@ -104,6 +105,10 @@ struct OpCtx {
     std::vector<IpcArena::MapKey> pins; // mappings this op holds
     size_t bytes = 0;
 };
+
+// per-process counters of how op buffers were handed to the peers (pcclxIpcStats): [0] direct inputs, [1] direct
+// outputs, [2] staged inputs, [3] staged outputs
+static std::atomic<uint64_t> g_buf_stats[4];
 
 // per-process bookkeeping
 static std::mutex g_ctx_mtx;
@@ -596,13 +601,32 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         }
     };
     if (device_ok) {
-        // Direct (zero-copy) access to the caller's buffers where HIP IPC can export them. An in-place op always
-        // stages its input: peers read the staged copy while results land in the caller's buffer, and the copy is
-        // the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
-        const bool allow_direct = !safe_mode() && !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
-        if (allow_direct && src != dst)
-            in_direct = export_user(const_cast<void *>(src), device, mine->in_handle[0], mine->in_off);
-        if (allow_direct) out_direct = export_user(dst, device, mine->out_handle[0], mine->out_off);
+        // Direct (zero-copy) access to the caller's buffers where that is fault-safe or opted into:
+        //   * every ring member is a thread of this process: raw pointers (no process can die alone);
+        //   * the buffer lies in shareable memory (shareable.hpp, VMM + fd): peers import it like a staged buffer;
+        //   * PCCL_IPC_MODE=fast: hipIpc export of the caller's allocation.
+        // An in-place op always stages its input: peers read the staged copy while results land in the caller's
+        // buffer, and the copy is the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
+        const bool allow_direct = !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
+        const bool all_local = std::all_of(pids_.begin(), pids_.end(), [&](int p) { return p == pids_[rank_]; });
+        auto direct = [&](const void *p, uint8_t *handle, uint64_t &off) {
+            if (!allow_direct) return false;
+            if (all_local) {
+                std::memset(handle, 0, kIpcHandleBytes);
+                off = 0;
+                return true;
+            }
+            shareable::Share s;
+            if (shareable::lookup(p, bytes, s) && s.device == device && s.size <= kIpcMaxExport) {
+                std::memset(handle, 0, kIpcHandleBytes);
+                std::memcpy(handle, &s.handle, sizeof(s.handle));
+                off = s.offset;
+                return true;
+            }
+            return !safe_mode() && export_user(const_cast<void *>(p), device, handle, off);
+        };
+        if (src != dst) in_direct = direct(src, mine->in_handle[0], mine->in_off);
+        out_direct = direct(dst, mine->out_handle[0], mine->out_off);
         if (in_direct) {
             mine->in_segs = 1;
             mine->in_raw[0] = reinterpret_cast<uint64_t>(src);
@@ -734,6 +758,8 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         }
     }
     ctx.pins = std::move(pins);
+    ++g_buf_stats[in_direct ? 0 : 2];
+    ++g_buf_stats[out_direct ? 1 : 3];
     {
         std::lock_guard l(g_ctx_mtx);
         g_ctx[{this, seq}] = std::move(ctx);
@@ -958,3 +984,7 @@ std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint6
 }
 
 } // namespace pccl::client
+
+extern "C" __attribute__((visibility("default"))) void pcclxIpcStats(uint64_t *out4) {
+    for (int k = 0; k < 4; ++k) out4[k] = pccl::client::g_buf_stats[k].load(std::memory_order_relaxed);
+}

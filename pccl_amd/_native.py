@@ -16,6 +16,7 @@ except ImportError:
     pass
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = ""  # the libpccl.so this process loaded (torch's pluggable allocator dlopens the same file)
 
 
 class IPv4(Structure):
@@ -114,6 +115,8 @@ def _load() -> ctypes.CDLL:
             f"libpccl.so not found at {path}; build it first: python -c 'import __graft_entry__ as g; g.build()' "
             f"(or cmake -S . -B build -G Ninja && ninja -C build)")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    global LIB_PATH
+    LIB_PATH = path
     p = POINTER
     sig = {
         "pcclInit": ([], c_int),
@@ -153,6 +156,10 @@ def _load() -> ctypes.CDLL:
         "pcclxPseudoGrad": ([c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int], c_int),
         "pcclxOuterSgd": ([c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_float, c_float, c_float, c_float,
                            c_int, c_int, c_int], c_int),
+        # shareable (VMM + fd) device memory and xGMI/IPC buffer-mode counters (pccl_amd.memory)
+        "pcclxShareableQuery": ([c_void_p, c_size_t, p(c_uint64), p(c_size_t)], c_int),
+        "pcclxShareableLiveBytes": ([], c_size_t),
+        "pcclxIpcStats": ([p(c_uint64)], None),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

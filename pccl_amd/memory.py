@@ -1,0 +1,139 @@
+"""Shareable device memory for the fault-safe zero-copy xGMI path.
+
+Same-host peers all-reduce device tensors over xGMI (``csrc/client/ipc.cpp``). In the default fault-safe mode
+(``PCCL_IPC_MODE=safe``) a peer process may only touch another process's memory through a VMM allocation shared as
+a file descriptor: the importer holds its own reference to the physical pages, so a peer that is SIGKILLed while the
+others' kernels read its input or write its output leaves valid memory behind. Ordinary PyTorch tensors are
+therefore staged — copied into such a buffer before the op and out of one after it, three times the HBM traffic of
+the all-reduce kernel alone. Tensors allocated here are fd-shareable from the start and are reduced in place::
+
+    import pccl_amd as pccl
+    with pccl.shareable_memory():                 # torch.cuda.MemPool backed by libpccl's VMM allocator
+        grads = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    comm.all_reduce(grads, out, ...)              # out-of-place ops read / write both buffers directly
+
+``DataParallel`` and ``DiLoCo`` (``pccl_amd.parallel``) allocate their communication buffers here automatically.
+The reference has no counterpart (its CUDA path is a TCP ring); this is the MI355X-native design that makes the
+xGMI fast path both zero-copy and safe under peer death.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import threading
+
+from . import _native
+
+_lock = threading.Lock()
+_allocator = None
+_pools: dict = {}
+
+
+def _immortal(obj) -> None:
+    """Keeps `obj` alive until the process exits. Measured on MI355X (scripts/probes/shareable_exit_probe.py): when
+    the interpreter's final garbage collection destroys a MemPool backed by a pluggable allocator, the process dies
+    with SIGSEGV; deleting it earlier or never is fine. The OS reclaims the memory at exit."""
+    ctypes.pythonapi.Py_IncRef(ctypes.py_object(obj))
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def available() -> bool:
+    """True when shareable allocations can be made here (HIP device present and torch's MemPool API available)."""
+    torch = _torch()
+    return bool(torch.cuda.is_available() and hasattr(torch.cuda, "MemPool") and _native.C.pcclxHipDeviceCount() > 0)
+
+
+def _get_allocator():
+    global _allocator
+    with _lock:
+        if _allocator is None:
+            from torch.cuda.memory import CUDAPluggableAllocator
+            # the same file the ctypes bindings loaded: dlopen returns that handle, so the allocation registry that
+            # the all-reduce consults is the one these entry points fill
+            _allocator = CUDAPluggableAllocator(_native.LIB_PATH, "pcclxShareableMalloc", "pcclxShareableFree")
+            _immortal(_allocator)
+        return _allocator
+
+
+def shareable_pool(device=None):
+    """The process-wide ``torch.cuda.MemPool`` of shareable memory for ``device`` (default: the current device)."""
+    torch = _torch()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _lock:
+        pool = _pools.get(idx)
+    if pool is None:
+        alloc = _get_allocator()
+        with torch.cuda.device(idx):
+            pool = torch.cuda.MemPool(alloc.allocator())
+        with _lock:
+            if idx not in _pools:
+                _immortal(pool)
+            pool = _pools.setdefault(idx, pool)
+    return pool
+
+
+@contextlib.contextmanager
+def shareable_memory(device=None):
+    """Context manager: CUDA tensors allocated inside come from the shareable pool of ``device``."""
+    torch = _torch()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    pool = shareable_pool(dev)
+    with torch.cuda.use_mem_pool(pool, dev):
+        yield pool
+
+
+def empty(*size, dtype=None, device=None):
+    """``torch.empty`` in shareable memory (``device`` must be a HIP device)."""
+    torch = _torch()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    with shareable_memory(dev):
+        return torch.empty(*size, dtype=dtype, device=dev)
+
+
+def zeros(*size, dtype=None, device=None):
+    t = empty(*size, dtype=dtype, device=device)
+    t.zero_()
+    return t
+
+
+def empty_like(t):
+    return empty(t.shape, dtype=t.dtype, device=t.device)
+
+
+def is_shareable(t) -> bool:
+    """True if all of ``t``'s bytes lie in one live shareable allocation."""
+    if getattr(t, "device", None) is None or t.device.type != "cuda":
+        return False
+    off = ctypes.c_uint64()
+    size = ctypes.c_size_t()
+    return bool(_native.C.pcclxShareableQuery(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                              ctypes.byref(off), ctypes.byref(size)))
+
+
+def live_bytes() -> int:
+    """Bytes currently held in shareable allocations by this process (PyTorch's cache included)."""
+    return int(_native.C.pcclxShareableLiveBytes())
+
+
+def ipc_buffer_stats() -> dict:
+    """How this process's xGMI/IPC ops handed their buffers to the peers since start: direct (zero-copy) vs staged
+    (copy-in / copy-out through VMM comm buffers), per input and output."""
+    out = (ctypes.c_uint64 * 4)()
+    _native.C.pcclxIpcStats(out)
+    return {"direct_in": out[0], "direct_out": out[1], "staged_in": out[2], "staged_out": out[3]}
+
+
+def maybe_shareable(device) -> contextlib.AbstractContextManager:
+    """``shareable_memory(device)`` for HIP devices when available, a no-op context otherwise (CPU tensors, no GPU,
+    or PCCL_SHAREABLE_BUFFERS=0)."""
+    import os
+    torch = _torch()
+    dev = torch.device(device)
+    if dev.type != "cuda" or os.environ.get("PCCL_SHAREABLE_BUFFERS", "1") == "0" or not available():
+        return contextlib.nullcontext()
+    return shareable_memory(dev)

@@ -27,6 +27,7 @@ import torch
 
 from ..api import (Communicator, DataType, DistributionHint, PCCLError, QuantizationAlgorithm, QuantizationOptions,
                    ReduceOp, ReduceOperandDescriptor)
+from ..memory import maybe_shareable
 from .elastic import RetryResult, all_reduce_multiple_with_retry, world_size
 
 
@@ -42,7 +43,8 @@ class GradBuckets:
         self.views: Dict[torch.nn.Parameter, torch.Tensor] = {}
         for key, ps in groups.items():
             total = sum(p.numel() for p in ps)
-            buf = torch.zeros(total, device=key[0], dtype=key[1])
+            with maybe_shareable(key[0]):  # fd-shareable: the xGMI path reduces it without a staged copy-out
+                buf = torch.zeros(total, device=key[0], dtype=key[1])
             off = 0
             for p in ps:
                 v = buf[off:off + p.numel()].view_as(p)

@@ -22,6 +22,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from ..api import Communicator, QuantizationOptions, ReduceOp, SharedState, SharedStateSyncStrategy, TensorInfo
+from ..memory import maybe_shareable
 from ..ops import kernels as K
 from .elastic import RetryResult, all_reduce_multiple_with_retry
 
@@ -77,8 +78,14 @@ class DiLoCo:
             self.local = [t.view(-1) for t in tensors]
         self.outer = [b.detach().float().clone() for b in self.local]
         self.mom = [torch.zeros_like(o) for o in self.outer]
-        self.pg = [torch.empty_like(o) for o in self.outer]
+        self.pg = [self._comm_buffer_like(o) for o in self.outer]
         self.outer_steps = torch.zeros(1, dtype=torch.int64)  # shared: decides the momentum bootstrap on every peer
+
+    @staticmethod
+    def _comm_buffer_like(t: torch.Tensor) -> torch.Tensor:
+        """All-reduced buffers live in fd-shareable memory on HIP devices (zero-copy on the xGMI path)."""
+        with maybe_shareable(t.device):
+            return torch.empty_like(t)
 
     # --- shared state ------------------------------------------------------------------------------------------
     def state_tensors(self) -> Dict[str, torch.Tensor]:
@@ -153,7 +160,7 @@ class AsyncDiLoCo(DiLoCo):
 
     def __init__(self, *args, **kw):
         super().__init__(*args, **kw)
-        self.pg_next = [torch.empty_like(o) for o in self.outer]
+        self.pg_next = [self._comm_buffer_like(o) for o in self.outer]
         self._thread: Optional[threading.Thread] = None
         self._result: Optional[RetryResult] = None
         self._error: Optional[BaseException] = None

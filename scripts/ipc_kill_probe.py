@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--duration", type=float, default=10.0, help="seconds each peer keeps running ops")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ipc_kill"))
     ap.add_argument("--inplace", action="store_true")
+    ap.add_argument("--shareable", action="store_true", help="peers allocate their buffers in fd-shareable memory "
+                                                              "(zero-copy safe mode)")
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--respawn", action="store_true", help="start a replacement peer after the kill (it joins the "
                                                             "running ring: new IPC arena with a fresh process)")
@@ -51,6 +53,8 @@ def main():
                     "bf16", "--duration", str(a.duration), "--device", "cuda:0", "--reuse", "--check-every", "16"]
             if a.inplace:
                 args.append("--inplace")
+            if a.shareable:
+                args.append("--shareable")
             penv = dict(env, PCCL_FAULT_INJECT=a.inject) if (r == 0 and a.inject) else env
             ps.append(subprocess.Popen(args, stdout=fo, stderr=fe, env=penv))
         # wait until the victim has completed a few ops, then kill it at an arbitrary point
@@ -96,7 +100,8 @@ def main():
             files += [fo, fe]
             args = [sys.executable, "-u", worker, addr, str(a.world), str(r), "--const", "--n", str(a.n), "--dtype",
                     "bf16", "--duration", str(max(2.0, a.duration / 2)), "--device", "cuda:0", "--reuse",
-                    "--check-every", "16", "--no-wait"] + (["--inplace"] if a.inplace else [])
+                    "--check-every", "16", "--no-wait"] + (["--inplace"] if a.inplace else []) + \
+                (["--shareable"] if a.shareable else [])
             ps.append(subprocess.Popen(args, stdout=fo, stderr=fe, env=env))
         rcs = []
         deadline = time.time() + a.duration + 30
@@ -124,7 +129,8 @@ def main():
         summary[f"peer{r}"] = {"ops_ok": len(oks), "errors": len(lines) - len(oks),
                                "bad": sum(1 for x in oks if x.get("bad")),
                                "worlds": sorted({x["world"] for x in oks}),
-                               "paths": sorted({x["path"] for x in oks})}
+                               "paths": sorted({x["path"] for x in oks}),
+                               "ipc_bufs": oks[-1].get("ipc_bufs") if oks else None}
         with open(os.path.join(a.out, f"peer{r}.err")) as f:
             err = f.read()
         summary[f"peer{r}"]["fault_lines"] = [ln for ln in err.splitlines() if "fault" in ln.lower()][:5]

@@ -104,20 +104,25 @@ def test_gpu_peer_crash_survivors_continue(hip):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("point,inplace,respawn", [("ipc_kernel", False, False), ("ipc_kernel", True, False),
-                                                   ("ipc_vote", True, False), ("ipc_kernel", False, True)])
-def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn):
+@pytest.mark.parametrize("point,inplace,respawn,shareable", [
+    ("ipc_kernel", False, False, False), ("ipc_kernel", True, False, False), ("ipc_vote", True, False, False),
+    ("ipc_kernel", False, True, False), ("ipc_kernel", False, False, True), ("ipc_kernel", True, False, True)])
+def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn, shareable):
     """xGMI/IPC path, 3 processes on one GPU, 512 MiB bf16: peer 0 SIGKILLs itself at a fixed protocol point of op
     300 (PCCL_FAULT_INJECT) - right after launching its push kernel (every peer's kernel is then reading / writing the
     victim's exported HBM) or right after publishing its vote. Survivors must abort that op, re-form the ring and
     keep producing exact results on the IPC path, with no GPU memory fault; with `respawn` a fresh replacement process
-    joins the running ring afterwards (new arena, the BASELINE config 5 sequence)."""
+    joins the running ring afterwards (new arena, the BASELINE config 5 sequence). With `shareable` the peers' buffers
+    live in fd-shareable memory (pccl_amd.memory): the kernels read / write the victim's own tensors (zero-copy), and
+    those must survive its death just as the staged comm buffers do."""
     import sys
     probe = os.path.join(os.path.dirname(HERE), "scripts", "ipc_kill_probe.py")
-    out = os.path.join(os.path.dirname(HERE), "gpurun_out", f"pytest_ipc_kill_{point}_{int(inplace)}_{int(respawn)}")
+    out = os.path.join(os.path.dirname(HERE), "gpurun_out",
+                       f"pytest_ipc_kill_{point}_{int(inplace)}_{int(respawn)}_{int(shareable)}")
     args = [sys.executable, probe, "--inject", f"{point}:300", "--duration", "12" if respawn else "4", "--n",
             str(1 << 28), "--out", out]
-    args += (["--inplace"] if inplace else []) + (["--respawn"] if respawn else [])
+    args += (["--inplace"] if inplace else []) + (["--respawn"] if respawn else []) + \
+        (["--shareable"] if shareable else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=150)
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["victim_rc"] == -9, summary
@@ -129,3 +134,7 @@ def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn):
         s_k = summary[f"peer{k}"]
         assert s_k["bad"] == 0 and not s_k["fault_lines"], s_k
         assert 2 in s_k["worlds"] and 3 in s_k["worlds"] and s_k["ops_ok"] > 300 and s_k["paths"] == [3], s_k
+        if shareable:  # the output (and, out of place, the input) went to the peers directly
+            b = s_k["ipc_bufs"]
+            assert b["direct_out"] > 300 and b["staged_out"] == 0, b
+            assert (b["direct_in"] > 300 and b["staged_in"] == 0) if not inplace else b["direct_in"] == 0, b

@@ -166,13 +166,15 @@ def test_device_shared_state(hip):
 
 
 @pytest.mark.parametrize("ipc_mode", ["safe", "fast"])
-@pytest.mark.parametrize("mode", ["zero_copy", "inplace", "mixed"])
+@pytest.mark.parametrize("mode", ["zero_copy", "inplace", "mixed", "shareable", "shareable_inplace"])
 def test_two_process_ipc(hip, mode, ipc_mode):
     """Two processes on cuda:0 exchange device buffers (the intra-node xGMI path). safe (default): staged VMM
     buffers shared as fds; fast: hipIpc handles, out-of-place ops export the caller's buffers (zero-copy, interior
-    offsets), in-place ops a staged comm buffer."""
+    offsets), in-place ops a staged comm buffer. shareable*: the tensors live in fd-shareable memory
+    (pccl_amd.memory) and are handed to the peer directly in either mode."""
     def extra(r):
-        return ["--inplace"] if mode == "inplace" or (mode == "mixed" and r == 1) else []
+        e = ["--inplace"] if mode in ("inplace", "shareable_inplace") or (mode == "mixed" and r == 1) else []
+        return e + (["--shareable"] if mode.startswith("shareable") else [])
     with local_master() as addr:
         procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, "2", str(r), "--n",
                                str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3",
@@ -187,6 +189,13 @@ def test_two_process_ipc(hip, mode, ipc_mode):
             expect = float(1 + 2 + 2 * ln["step"])
             assert ln["lo"] == ln["hi"] == expect
             assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value
+        b = lines[-1]["ipc_bufs"]
+        if mode.startswith("shareable") or (mode == "zero_copy" and ipc_mode == "fast"):
+            assert b["direct_out"] == 3 and b["staged_out"] == 0, b
+        if mode == "shareable" or (mode == "zero_copy" and ipc_mode == "fast"):
+            assert b["direct_in"] == 3 and b["staged_in"] == 0, b
+        if ipc_mode == "safe" and mode in ("zero_copy", "inplace", "mixed"):  # plain torch memory: staged
+            assert b["direct_in"] == 0 and b["direct_out"] == 0, b
 
 
 @pytest.mark.parametrize("gib", [1.25, 2.5])
@@ -236,3 +245,40 @@ def test_device_ipc_modes(hip, inplace, no_zc, monkeypatch):
         assert bad.numel() == 0, dict(rank=rank, wrong=bad.numel(), first=bad[:4].tolist(), last=bad[-4:].tolist(),
                                       zeros=int((y[bad] == 0).sum()), own_input=int((y[bad] == orig[rank][bad]).sum()),
                                       peer_input=int((y[bad] == orig[1 - rank][bad]).sum()))
+
+
+def test_shareable_memory_module(hip):
+    """pccl_amd.memory: tensors allocated in the shareable pool resolve to a live VMM allocation (interior views
+    included); ordinary tensors do not; the pool serves repeated allocations."""
+    before = pccl.memory.live_bytes()
+    with pccl.shareable_memory(hip):
+        a = torch.arange(1 << 22, device=hip, dtype=torch.float32)
+        b = torch.empty(3_000_001, device=hip, dtype=torch.bfloat16)
+    c = torch.empty(1 << 20, device=hip)
+    assert pccl.memory.is_shareable(a) and pccl.memory.is_shareable(b) and pccl.memory.is_shareable(a[12345:])
+    assert not pccl.memory.is_shareable(c) and not pccl.memory.is_shareable(torch.empty(4))
+    assert pccl.memory.live_bytes() > before
+    assert torch.equal(a.cpu(), torch.arange(1 << 22, dtype=torch.float32))
+    d = pccl.memory.empty(1000, dtype=torch.float16, device=hip)
+    assert pccl.memory.is_shareable(d) and d.dtype == torch.float16
+
+
+def test_threaded_peers_skip_staging(hip):
+    """Peers that are threads of one process cannot die independently: safe mode hands them the caller's buffers
+    directly (no copy-in / copy-out), in-place ops still stage the input (abort backup)."""
+    n = 1 << 20
+    s0 = pccl.memory.ipc_buffer_stats()
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(rank + 1), device=hip)
+        y = torch.empty_like(x)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=1)
+        torch.cuda.synchronize()
+        return float(y.min()), float(y.max()), float(x.min()), float(x.max())
+
+    for lo, hi, xlo, xhi in _run(2, fn):
+        assert lo == hi == 3.0 and xlo == xhi == 3.0
+    s1 = pccl.memory.ipc_buffer_stats()
+    d = {k: s1[k] - s0[k] for k in s0}
+    assert d == {"direct_in": 2, "direct_out": 4, "staged_in": 2, "staged_out": 0}, d

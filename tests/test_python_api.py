@@ -132,3 +132,20 @@ def test_profiler_nested_sessions_report_and_trace(tmp_path):
     col.chrome_trace(str(path))
     ev = json.loads(path.read_text())["traceEvents"]
     assert len(ev) == 6 and all(e["ph"] == "X" and e["dur"] > 0 for e in ev)
+
+
+def test_shareable_memory_api_on_cpu():
+    """pccl_amd.memory without a GPU: no shareable pool, CPU tensors are never shareable, the parallel modules fall
+    back to ordinary allocations, and the IPC buffer counters are readable."""
+    import contextlib
+
+    import torch
+
+    import pccl_amd as pccl
+    assert not pccl.memory.is_shareable(torch.empty(16))
+    assert isinstance(pccl.memory.maybe_shareable("cpu"), contextlib.nullcontext)
+    st = pccl.memory.ipc_buffer_stats()
+    assert set(st) == {"direct_in", "direct_out", "staged_in", "staged_out"} and all(v >= 0 for v in st.values())
+    assert pccl.memory.live_bytes() >= 0
+    if not torch.cuda.is_available():
+        assert not pccl.memory.available()

@@ -2,11 +2,13 @@
 
 usage: allreduce_peer.py MASTER WORLD RANK [--n N] [--dtype f32|bf16|f16|i32] [--device cpu|cuda:0] [--steps K]
                          [--die-at STEP] [--const] [--no-wait] [--inplace] [--op sum|avg|max] [--quant none|u8]
+                         [--shareable]
 Each step all-reduces a tensor and checks the result; prints one JSON line per attempt.
   default: x = rank + 1 + step, tag = step (all peers start together)
   --const: x = 1, tag 0, result must equal the op's world size (membership may change between steps)
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -41,6 +43,7 @@ def main():
     ap.add_argument("--check-every", type=int, default=1, help="verify the result every k-th step only")
     ap.add_argument("--reuse", action="store_true", help="allocate x / y once (back-to-back ops, no refill)")
     ap.add_argument("--duration", type=float, default=0.0, help="run steps until this many seconds passed instead")
+    ap.add_argument("--shareable", action="store_true", help="allocate x / y in fd-shareable memory (pccl_amd.memory)")
     a = ap.parse_args()
     op = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[a.op]
     qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant == "u8" \
@@ -66,8 +69,9 @@ def main():
             continue
         val = 1.0 if a.const else float(a.rank + 1 + step)
         if not a.reuse or step == 0 or a.inplace:
-            x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
-            y = x if a.inplace else torch.empty_like(x)
+            with pccl.memory.maybe_shareable(dev) if a.shareable else contextlib.nullcontext():
+                x = torch.full((a.n,), val, dtype=DT[a.dtype], device=dev)
+                y = x if a.inplace else torch.empty_like(x)
         if step == a.die_at:
             os._exit(17)  # simulated crash (no clean disconnect)
         t0 = time.perf_counter()
@@ -91,6 +95,8 @@ def main():
         rec = {"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
                "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
                "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
+        if dev.type == "cuda":
+            rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
         if a.const and not (lo == hi == float(info.local_world_size)):
             rec["bad"] = True
         print(json.dumps(rec), flush=True)
