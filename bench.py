@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import statistics
 import sys
 import threading
@@ -184,6 +185,7 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
     torch.cuda.synchronize()
     job.sync(i)
     t0 = time.perf_counter()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     tx = rx = 0
     for s in range(steps):
         info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + warmup + s)
@@ -191,7 +193,12 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
         rx += info.rx_bytes
     torch.cuda.synchronize()
     job.sync(i)
-    return time.perf_counter() - t0, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+    dt = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    # CPU seconds of the whole process (every peer thread of this rank) over the timed ops: the loopback-TCP ring is
+    # CPU work (kernel socket copies), so cpu_s / dt shows how many cores it kept busy
+    cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), cpu
 
 
 def _check(job, i, comm, x, y, peers):
@@ -203,6 +210,24 @@ def _check(job, i, comm, x, y, peers):
     want = peers * (peers + 1) / 2
     lo, hi = float(y.min()), float(y.max())
     return lo == hi == want
+
+
+def _log(msg):
+    """Progress on stderr (the JSON result line is the only stdout output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')} rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _cpu_quota():
+    """CPUs this process may use: the cgroup v2 quota (cpu.max) if set, else the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        if q != "max":
+            return round(min(n, int(q) / int(period)), 2)
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _bw(nbytes, t, n):
@@ -237,10 +262,12 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
             r["ok"] = _check(job, i, comm, x, y, total)
         return r
 
+    _log(f"phase {'xGMI/IPC' if ipc else 'TCP device ring'}: {total} peers x {nbytes >> 20} MiB, {steps} steps")
     res = job.phase(fn, ipc=ipc, peers=peers)
     dt = job.max_over_job([r["main"][0] for r in res])
+    _log(f"  done: {dt / steps * 1e3:.3f} ms/op")
     out = {"t": dt / steps, "tx": res[0]["main"][1] / steps, "rx": res[0]["main"][2] / steps,
-           "path": res[0]["main"][3], "sweep": {}}
+           "path": res[0]["main"][3], "sweep": {}, "cpu_cores": res[0]["main"][4] / max(dt, 1e-9)}
     for b in sweep:
         out["sweep"][b] = job.max_over_job([r[b] for r in res])
     if check:
@@ -381,6 +408,9 @@ def extras_in_child(job, a):
 
 def main():
     a = _args()
+    if os.environ.get("PCCL_BENCH_WATCHDOG"):  # periodic Python stacks of every thread (hang diagnosis)
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["PCCL_BENCH_WATCHDOG"]), repeat=True)
     job = Job(a)
     nbytes = a.mib << 20
     P = job.total
@@ -404,6 +434,7 @@ def main():
     extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
                   "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
                   "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": a.pool,
+                  "cpu_cores_busy_rank0": round(ring["cpu_cores"], 2), "cpus_available": _cpu_quota(),
                   "result_exact": ring.get("ok")})
     sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
                                                     "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}

@@ -809,7 +809,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
                                        [](size_t v, const Staged &x) { return v < x.a; });
             if (it == lst.begin()) return false;
             --it;
-            return end <= it->b && be->event_sync(it->e);
+            return end <= it->b && event_wait_polling(be, it->e);
         };
     };
     auto always_ready = [](size_t) { return true; };
@@ -826,7 +826,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
         const auto [ts, te] = bounds[tx_idx];
         const auto [rs, re] = bounds[rx_idx];
-        if (sink_free[cur]) be->event_sync(sink_free[cur]);
+        if (sink_free[cur]) event_wait_polling(be, sink_free[cur]);
         if (step == 0) { // own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
             ready[cur].clear();
             txshift[cur] = 0;
@@ -867,7 +867,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         const size_t inc = (cur_chunk + ws - 1) % ws;
         const auto [ts, te] = bounds[cur_chunk];
         const auto [rs, re] = bounds[inc];
-        if (sink_free[cur]) be->event_sync(sink_free[cur]);
+        if (sink_free[cur]) event_wait_polling(be, sink_free[cur]);
         uint8_t *sink = rxbuf[cur], *region = dst + rs * es;
         auto consume = [&](size_t a, size_t b) {
             be->memcpy_async(region + a * es, sink + a * es, (b - a) * es, pq.h2d);
@@ -968,7 +968,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         }
         return m;
     };
-    auto quant_ready = [&](size_t end) { return end == 0 || be->event_sync(ev((end - 1) / (piece_el * qs))); };
+    auto quant_ready = [&](size_t end) { return end == 0 || event_wait_polling(be, ev((end - 1) / (piece_el * qs))); };
     auto always_ready = [](size_t) { return true; };
 
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,

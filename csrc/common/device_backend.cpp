@@ -3,9 +3,11 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../kernels/host_kernels.hpp"
@@ -56,6 +58,18 @@ DeviceBackend *device_backend() {
 }
 
 bool device_backend_available() { return device_backend() != nullptr; }
+
+bool event_wait_polling(DeviceBackend *be, DevEvent e) {
+    static const bool poll = env_size("PCCL_EVENT_POLL", 1) != 0;
+    if (!poll) return be->event_sync(e);
+    unsigned us = 2;
+    while (true) {
+        const int r = be->event_query(e);
+        if (r != 0) return r == 1;
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+        us = std::min(us * 2, 100u);
+    }
+}
 
 uint32_t device_crc32c(DeviceBackend *be, const void *dev_ptr, size_t n, DevStream s, bool *ok) {
     constexpr size_t kChunk = 64, kTile = 256 * kChunk, kMaxPartials = 1024;

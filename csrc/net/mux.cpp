@@ -156,7 +156,7 @@ bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n)
 }
 
 bool MuxConn::read_into(uint8_t *dst, size_t n, Sink *progress_sink) {
-    constexpr size_t kPiece = 1 << 20;
+    constexpr size_t kPiece = 4 << 20;
     size_t done = 0;
     while (done < n) {
         const size_t want = std::min(kPiece, n - done);
@@ -169,11 +169,15 @@ bool MuxConn::read_into(uint8_t *dst, size_t n, Sink *progress_sink) {
         done += static_cast<size_t>(k);
         rx_total_.fetch_add(static_cast<uint64_t>(k), std::memory_order_relaxed);
         if (progress_sink != nullptr) {
-            progress_sink->received.fetch_add(static_cast<size_t>(k), std::memory_order_release);
-            {
-                std::lock_guard l(mtx_);
+            // seq_cst pairs with wait_sink (store wake_at, then re-read received): one of the two sides sees the
+            // other's write, so a waiter is never left sleeping past its threshold
+            const size_t now = progress_sink->received.fetch_add(static_cast<size_t>(k)) + static_cast<size_t>(k);
+            if (now >= progress_sink->wake_at.load()) {
+                {
+                    std::lock_guard l(mtx_);
+                }
+                cv_.notify_all();
             }
-            cv_.notify_all();
         }
     }
     return true;
@@ -321,8 +325,12 @@ size_t MuxConn::wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds t
             l.lock();
             continue;
         }
-        if (cv_.wait_until(l, deadline) == std::cv_status::timeout)
-            return it->second->received.load(std::memory_order_acquire);
+        Sink *sink = it->second.get();
+        sink->wake_at.store(want);
+        if (sink->received.load() >= want) continue;
+        const bool timed_out = cv_.wait_until(l, deadline) == std::cv_status::timeout;
+        sink->wake_at.store(SIZE_MAX); // the sink outlives the wait: only its own op removes it
+        if (timed_out) return sink->received.load(std::memory_order_acquire);
     }
 }
 

@@ -83,6 +83,9 @@ private:
         uint8_t *dst = nullptr;
         size_t capacity = 0;
         std::atomic<size_t> received{0};
+        // the waiter's threshold (wait_sink): the RX thread wakes it only once `received` reaches it (one wake-up
+        // per awaited batch instead of one per recv() call)
+        std::atomic<size_t> wake_at{SIZE_MAX};
         bool busy = false; // RX thread is writing into dst
     };
     struct Frame {

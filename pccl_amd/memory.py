@@ -24,7 +24,7 @@ import threading
 
 from . import _native
 
-_lock = threading.Lock()
+_lock = threading.RLock()
 _allocator = None
 _pools: dict = {}
 
@@ -64,27 +64,47 @@ def shareable_pool(device=None):
     torch = _torch()
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    with _lock:
+    with _lock:  # one pool per device even when several peer threads ask at once
         pool = _pools.get(idx)
-    if pool is None:
-        alloc = _get_allocator()
-        with torch.cuda.device(idx):
-            pool = torch.cuda.MemPool(alloc.allocator())
-        with _lock:
-            if idx not in _pools:
-                _immortal(pool)
-            pool = _pools.setdefault(idx, pool)
+        if pool is None:
+            alloc = _get_allocator()
+            with torch.cuda.device(idx):
+                pool = torch.cuda.MemPool(alloc.allocator())
+            _immortal(pool)
+            _pools[idx] = pool
     return pool
+
+
+_ctx_locks: dict = {}
+_tls = threading.local()
 
 
 @contextlib.contextmanager
 def shareable_memory(device=None):
-    """Context manager: CUDA tensors allocated inside come from the shareable pool of ``device``."""
+    """Context manager: CUDA tensors allocated inside come from the shareable pool of ``device``.
+
+    PyTorch lets only one thread at a time route allocations to a given MemPool ("already recording to mempool_id"),
+    so threads entering this context for the same device take turns (keep the body to allocations); nested use in
+    one thread is a no-op."""
     torch = _torch()
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     pool = shareable_pool(dev)
-    with torch.cuda.use_mem_pool(pool, dev):
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    active = getattr(_tls, "active", None)
+    if active is None:
+        active = _tls.active = set()
+    if idx in active:
         yield pool
+        return
+    with _lock:
+        lk = _ctx_locks.setdefault(idx, threading.Lock())
+    with lk:
+        active.add(idx)
+        try:
+            with torch.cuda.use_mem_pool(pool, dev):
+                yield pool
+        finally:
+            active.discard(idx)
 
 
 def empty(*size, dtype=None, device=None):

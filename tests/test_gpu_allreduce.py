@@ -282,3 +282,22 @@ def test_threaded_peers_skip_staging(hip):
     s1 = pccl.memory.ipc_buffer_stats()
     d = {k: s1[k] - s0[k] for k in s0}
     assert d == {"direct_in": 2, "direct_out": 4, "staged_in": 2, "staged_out": 0}, d
+
+
+def test_shareable_memory_concurrent_threads(hip):
+    """Peer threads of one process allocate in the shareable pool at the same time (PyTorch allows one thread per
+    MemPool context: the context serialises them) and reduce over the xGMI path with direct buffers."""
+    n = 1 << 20
+
+    def fn(rank, comm):
+        with pccl.shareable_memory(hip):
+            with pccl.shareable_memory(hip):  # nested: no-op
+                x = torch.full((n,), float(rank + 1), device=hip)
+            y = torch.empty_like(x)
+        assert pccl.memory.is_shareable(x) and pccl.memory.is_shareable(y)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        torch.cuda.synchronize()
+        return float(y.min()), float(y.max())
+
+    for lo, hi in _run(4, fn):
+        assert lo == hi == 10.0
