@@ -1,5 +1,5 @@
 // Point-to-point bandwidth benchmark used by topology optimization (reference: ccoip/src/cpp/benchmark_runner.cpp).
-// The sender opens PCCL_NUM_BENCHMARK_CONNECTIONS (default 8) parallel TCP streams to the peer's benchmark port and
+// The sender opens PCCL_NUM_BENCHMARK_CONNECTIONS (default 16, as the reference) parallel TCP streams to the peer's benchmark port and
 // streams 8 MiB buffers for PCCL_BENCHMARK_SECONDS (default 2 s; the reference fixed 10 s), reporting the summed
 // goodput in Mbit/s.
 #pragma once
