@@ -1,6 +1,6 @@
 // Point-to-point bandwidth benchmark used by topology optimization (reference: ccoip/src/cpp/benchmark_runner.cpp).
-// The sender opens PCCL_NUM_BENCHMARK_CONNECTIONS (default 16, as the reference) parallel TCP streams to the peer's benchmark port and
-// streams 8 MiB buffers for PCCL_BENCHMARK_SECONDS (default 2 s; the reference fixed 10 s), reporting the summed
+// The sender opens PCCL_NUM_BENCHMARK_CONNECTIONS (default 16) parallel TCP streams to the peer's benchmark port and
+// streams 8 MiB buffers for PCCL_BENCHMARK_MILLIS (default 10000), the reference's defaults, reporting the summed
 // goodput in Mbit/s.
 #pragma once
 
