@@ -253,13 +253,15 @@ std::shared_ptr<IpcArena> IpcArena::create(Client &c, const std::vector<Uuid> &r
     return arena;
 }
 
-bool IpcArena::safe_mode() {
+bool ipc_safe_mode() {
     static const bool safe = [] {
         const char *v = std::getenv("PCCL_IPC_MODE");
         return !(v && std::strcmp(v, "fast") == 0);
     }();
     return safe;
 }
+
+bool IpcArena::safe_mode() { return ipc_safe_mode(); }
 
 void IpcArena::release_mapping(const MapKey &key, Mapping &m) {
     DeviceBackend *be = device_backend();

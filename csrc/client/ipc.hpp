@@ -56,6 +56,11 @@ constexpr uint32_t kIpcMaxSegs = 16;                              // => ops of u
 class Client;
 struct ArenaShm;
 
+// PCCL_IPC_MODE: "safe" (default) — buffers cross processes only as VMM allocations shared as fds (the importer keeps
+// the pages alive if the exporter dies); "fast" — hipIpc exports of plain allocations are allowed too. Shared by the
+// all-reduce arena and the same-host shared-state hand-off.
+bool ipc_safe_mode();
+
 // Workgroup budget of one xGMI kernel: 512 per GPU (2 per CU, the measured optimum for these streaming kernels,
 // profiles/r1_ipc_grid_sweep.md) split between the ring members whose kernels run on the same physical GPU (same
 // uid), but not below 256 per kernel (fewer cannot saturate HBM).

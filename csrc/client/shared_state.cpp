@@ -9,16 +9,21 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 
 #include "../common/log.hpp"
 #include "../common/trace.hpp"
 #include "../kernels/host_kernels.hpp"
 #include "../net/socket.hpp"
 #include "client.hpp"
+#include "ipc.hpp"
 #include "pools.hpp"
+#include "shareable.hpp"
+#include "vmm_share.hpp"
 
 namespace pccl::client {
 
@@ -311,6 +316,80 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         }
         ss.revision = sresp->revision;
         bool ok = true;
+        const bool same_process = sresp->pid == static_cast<uint32_t>(getpid());
+        // phase 1: map the source of every handed-over entry (VMM imports hold their own reference to the pages, so
+        // from here on the distributor may die without invalidating them)
+        struct Mapped {
+            void *ptr;
+            bool vmm;
+            int device;
+        };
+        std::vector<Mapped> mapped;
+        struct Unmap { // every exit path releases the mappings
+            DeviceBackend *be;
+            std::vector<Mapped> &m;
+            ~Unmap() {
+                for (const auto &x : m) {
+                    be->set_device(x.device);
+                    if (x.vmm) be->vmm_unmap(x.ptr);
+                    else be->ipc_close(x.ptr);
+                }
+            }
+        } unmap{be, mapped};
+        std::vector<std::vector<const uint8_t *>> srcs(sresp->entries.size());
+        std::vector<int> devs(sresp->entries.size(), 0);
+        for (size_t i = 0; ok && i < sresp->entries.size(); ++i) {
+            const auto &se = sresp->entries[i];
+            if (se.mode == 0) continue;
+            SSEntry *dst = lookup(i, se.key, se.size_bytes);
+            if (!dst) {
+                ok = false;
+                break;
+            }
+            if (!be) {
+                LOG(ERR) << "Shared state sync: IPC entry " << se.key << " but no HIP backend";
+                ok = false;
+                break;
+            }
+            DevPtrInfo pi{};
+            be->pointer_info(dst->data, pi);
+            const int dev = devs[i] = pi.is_device ? pi.device : std::max(0, se.device);
+            be->set_device(dev);
+            if (same_process) {
+                srcs[i].push_back(reinterpret_cast<const uint8_t *>(se.raw_ptr)); // plain pointer
+            } else if (se.mode == 1) {
+                void *m = be->ipc_open(se.handle);
+                if (m) {
+                    mapped.push_back({m, false, dev});
+                    srcs[i].push_back(static_cast<const uint8_t *>(m) + se.offset);
+                }
+            } else {
+                std::vector<const uint8_t *> hs{se.handle};
+                for (const auto &h : se.more_handles) hs.push_back(h.data());
+                for (size_t j = 0; j < hs.size(); ++j) {
+                    VmmHandle vh;
+                    int vfd = -1;
+                    void *m = nullptr;
+                    if (VmmHandle::decode(hs[j], vh) && (vfd = VmmShare::fetch(vh.pid, vh.nonce, vh.id)) >= 0) {
+                        m = be->vmm_import(vfd, vh.size, dev);
+                        ::close(vfd);
+                    }
+                    if (!m) {
+                        srcs[i].clear();
+                        break;
+                    }
+                    mapped.push_back({m, true, dev});
+                    srcs[i].push_back(static_cast<const uint8_t *>(m) + (j == 0 ? se.offset : 0));
+                }
+            }
+            if (srcs[i].empty()) {
+                LOG(ERR) << "Shared state sync: cannot map the distributor's copy of " << se.key;
+                ok = false;
+            }
+        }
+        if (const size_t ms = env_size("PCCL_SS_COPY_DELAY_MS", 0)) // tests: let the distributor die in between
+            std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+        // phase 2: copy / receive every entry in order, hash-verify it
         for (size_t i = 0; ok && i < sresp->entries.size(); ++i) {
             const auto &se = sresp->entries[i];
             SSEntry *dst = lookup(i, se.key, se.size_bytes);
@@ -318,24 +397,26 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 ok = false;
                 break;
             }
-            if (se.mode == 1 && !be) {
-                LOG(ERR) << "Shared state sync: IPC entry " << se.key << " but no HIP backend";
-                ok = false;
-            } else if (se.mode == 1) {
-                DevPtrInfo pi{};
-                be->pointer_info(dst->data, pi);
-                const int dev = pi.is_device ? pi.device : std::max(0, se.device);
-                be->set_device(dev);
-                void *mapped = nullptr;
-                const uint8_t *src = nullptr;
-                if (sresp->pid == static_cast<uint32_t>(getpid())) {
-                    src = reinterpret_cast<const uint8_t *>(se.raw_ptr); // same process: plain pointer
-                } else {
-                    mapped = be->ipc_open(se.handle);
-                    if (mapped) src = static_cast<const uint8_t *>(mapped) + se.offset;
+            if (se.mode != 0) {
+                be->set_device(devs[i]);
+                const size_t nseg = se.seg_bytes ? (dst->bytes + se.seg_bytes - 1) / se.seg_bytes : 0;
+                if (se.mode == 1 || same_process) {
+                    ok = be->memcpy_sync(dst->data, srcs[i][0], dst->bytes);
+                } else if (nseg == 0 || nseg > srcs[i].size()) {
+                    LOG(ERR) << "Shared state sync: malformed segment list for " << se.key;
+                    ok = false;
+                } else { // VMM imports: copy kernel (no copy-engine path for imported VMM memory)
+                    StreamLease stream(devs[i]);
+                    ok = stream.get() != nullptr;
+                    for (size_t j = 0, off = 0; ok && off < dst->bytes; ++j, off += se.seg_bytes) {
+                        const size_t n = std::min<size_t>(se.seg_bytes, dst->bytes - off);
+                        const void *src = srcs[i][j];
+                        const size_t zero = 0;
+                        ok = be->multi_gather(static_cast<uint8_t *>(dst->data) + off, &src, &zero, &n, 1, -1, DType::U8,
+                                              stream.get());
+                    }
+                    ok = ok && be->stream_sync(stream.get());
                 }
-                ok = src && be->memcpy_sync(dst->data, src, dst->bytes);
-                if (mapped) be->ipc_close(mapped);
                 if (!ok) {
                     LOG(ERR) << "Shared state sync: IPC copy of " << se.key << " failed";
                 }
@@ -438,6 +519,7 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
     if (!pkt) return;
     std::vector<std::string> keys;
     bool ipc_request = false, same_host = false;
+    uint32_t ipc_pid = 0;
     if (pkt->id == C2SRequestSharedState::kId) {
         auto req = decode_payload<C2SRequestSharedState>(pkt->payload.data(), pkt->payload.size());
         if (!req) return;
@@ -448,6 +530,7 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         keys = std::move(req->keys);
         ipc_request = true;
         same_host = req->host_token == net::host_token();
+        ipc_pid = req->pid;
     } else {
         return;
     }
@@ -535,36 +618,87 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         return;
     }
 
-    // IPC request: export HBM entries (same host only), stream the rest, keep the exports valid until the
-    // requester reports that its copies are done
+    // IPC request: hand HBM entries over (same host only), stream the rest, keep what was handed over valid until
+    // the requester reports that its copies are done. Fault-safe (PCCL_IPC_MODE=safe, default): only VMM fd shares
+    // cross the process boundary — the entry's own allocation if it lies in shareable memory, else a staged copy in
+    // kIpcSegBytes VMM segments — so a distributor that dies mid-copy leaves valid memory behind. "fast": hipIpc
+    // export of the entry's allocation (no staging copy, but the requester's copy faults if we die under it).
     S2CSharedStateIpcResponse resp;
     resp.status = status;
     resp.revision = revision;
     resp.pid = static_cast<uint32_t>(getpid());
     uint64_t ipc_bytes = 0;
+    std::vector<void *> staged; // VMM staging segments of this request
+    struct StagedGuard {
+        std::vector<void *> &v;
+        ~StagedGuard() {
+            for (void *p : v) shareable::free(p);
+        }
+    } staged_guard{staged};
+    const bool same_process = ipc_pid == static_cast<uint32_t>(getpid());
     for (const auto &e : to_send) {
         SharedStateIpcEntry ie;
         ie.key = e.key;
         ie.size_bytes = e.bytes;
         DevPtrInfo pi{};
         if (be && same_host && e.bytes > 0) be->pointer_info(e.data, pi);
+        if (!pi.is_device) {
+            resp.entries.push_back(ie);
+            continue;
+        }
+        be->set_device(pi.device);
+        shareable::Share sh;
         void *base = nullptr;
         size_t size = 0;
-        if (pi.is_device && be->address_range(e.data, &base, &size) && base) {
-            be->set_device(pi.device);
-            if (be->ipc_export(base, ie.handle)) {
-                ie.mode = 1;
-                ie.device = pi.device;
-                ie.offset = static_cast<uint64_t>(static_cast<const uint8_t *>(e.data) - static_cast<uint8_t *>(base));
-                ie.raw_ptr = reinterpret_cast<uint64_t>(e.data);
-                ipc_bytes += e.bytes;
+        if (same_process) {
+            ie.mode = 1; // the requester reads through raw_ptr
+        } else if (shareable::lookup(e.data, e.bytes, sh) && sh.size <= kIpcMaxExport) {
+            ie.mode = 2; // zero-copy and fault-safe: the tensor itself is fd-shareable
+            std::memcpy(ie.handle, &sh.handle, sizeof(sh.handle));
+            ie.offset = sh.offset;
+            ie.seg_bytes = e.bytes;
+        } else if (ipc_safe_mode()) {
+            StreamLease stream(pi.device);
+            bool ok = stream.get() != nullptr;
+            std::vector<std::array<uint8_t, 64>> hs;
+            for (size_t off = 0; ok && off < e.bytes; off += kIpcSegBytes) {
+                const size_t n = std::min(kIpcSegBytes, e.bytes - off);
+                void *seg = shareable::alloc(n, pi.device);
+                ok = seg != nullptr && shareable::lookup(seg, n, sh);
+                if (!ok) break;
+                staged.push_back(seg);
+                std::array<uint8_t, 64> h{};
+                std::memcpy(h.data(), &sh.handle, sizeof(sh.handle));
+                hs.push_back(h);
+                const void *src = static_cast<const uint8_t *>(e.data) + off;
+                const size_t zero = 0;
+                ok = be->multi_gather(seg, &src, &zero, &n, 1, -1, DType::U8, stream.get());
             }
+            ok = ok && be->stream_sync(stream.get());
+            if (ok && !hs.empty()) {
+                ie.mode = 2;
+                std::memcpy(ie.handle, hs[0].data(), hs[0].size());
+                ie.more_handles.assign(hs.begin() + 1, hs.end());
+                ie.seg_bytes = kIpcSegBytes;
+                ie.offset = 0;
+            } else {
+                LOG(WARN) << "Shared state: staging " << e.key << " for the IPC hand-off failed; streaming it";
+            }
+        } else if (be->address_range(e.data, &base, &size) && base && be->ipc_export(base, ie.handle)) {
+            ie.mode = 1;
+            ie.offset = static_cast<uint64_t>(static_cast<const uint8_t *>(e.data) - static_cast<uint8_t *>(base));
+        }
+        if (ie.mode != 0) {
+            ie.device = pi.device;
+            ie.raw_ptr = reinterpret_cast<uint64_t>(e.data);
+            ipc_bytes += e.bytes;
         }
         resp.entries.push_back(ie);
     }
     if (!net::send_packet(fd, resp)) return;
+    fault_point("ss_serve", revision); // tests: die while the requester maps / copies what was handed over
     for (size_t i = 0; i < to_send.size(); ++i) {
-        if (resp.entries[i].mode == 1) continue;
+        if (resp.entries[i].mode != 0) continue;
         if (!stream_entry(to_send[i])) {
             LOG(WARN) << "Shared state: streaming " << to_send[i].key << " to " << sockaddr_str(peer) << " failed";
             return;

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <fcntl.h>
 #include <random>
 #include <string>
@@ -129,7 +130,13 @@ void fault_point(const char *point, uint64_t seq) {
     if (std::strtoull(spec.c_str() + colon + 1, nullptr, 10) != seq) return;
     std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu\n", point, static_cast<unsigned long long>(seq));
     std::fflush(stderr);
-    ::kill(::getpid(), SIGKILL);
+    if (const char *d = std::getenv("PCCL_FAULT_INJECT_DELAY_MS")) // die a little later (the point's work goes on)
+        std::thread([ms = std::atol(d)] {
+            ::usleep(static_cast<useconds_t>(ms) * 1000);
+            ::kill(::getpid(), SIGKILL);
+        }).detach();
+    else
+        ::kill(::getpid(), SIGKILL);
 }
 
 void fault_delay(uint64_t tag) {

@@ -149,7 +149,10 @@ void EventServer::accept_all() {
 void EventServer::handle_readable(Client &c) {
     uint8_t tmp[65536];
     bool closed = false;
-    while (true) {
+    // at most 1 MiB per readiness event: a client that streams faster than we drain would otherwise keep every recv()
+    // full, so the loop never reached the dispatch below (rbuf grew without bound and no packet was handled; seen in
+    // transport_tests es_interrupt_while_client_streams). epoll is level-triggered: the rest is read next round.
+    for (int rounds = 0; rounds < 16; ++rounds) {
         const ssize_t k = ::recv(c.fd, tmp, sizeof(tmp), 0);
         if (k > 0) {
             c.rbuf.insert(c.rbuf.end(), tmp, tmp + k);

@@ -390,6 +390,11 @@ void S2CSharedStateIpcResponse::encode(WBuf &w) const {
         w.u64(e.offset);
         w.u64(e.raw_ptr);
         w.bytes(e.handle, sizeof(e.handle));
+        if (e.mode == 2) {
+            w.u64(e.seg_bytes);
+            w.u32(static_cast<uint32_t>(e.more_handles.size()));
+            for (const auto &h : e.more_handles) w.bytes(h.data(), h.size());
+        }
     }
 }
 
@@ -408,6 +413,13 @@ bool S2CSharedStateIpcResponse::decode(RBuf &r) {
         e.offset = r.u64();
         e.raw_ptr = r.u64();
         r.bytes(e.handle, sizeof(e.handle));
+        if (e.mode == 2) {
+            e.seg_bytes = r.u64();
+            const uint32_t m = r.u32();
+            if (!r.plausible_count(m, 64)) return false;
+            e.more_handles.resize(m);
+            for (auto &h : e.more_handles) r.bytes(h.data(), h.size());
+        }
     }
     return r.ok();
 }

@@ -5,6 +5,7 @@
 // Packets carried inside multiplexed P2P frames: u16 id | payload (no length; the frame carries it).
 #pragma once
 
+#include <array>
 #include <cstdint>
 #include <optional>
 #include <string>
@@ -409,11 +410,17 @@ struct C2SRequestSharedStateIpc {
 struct SharedStateIpcEntry {
     std::string key;
     uint64_t size_bytes = 0;
-    uint8_t mode = 0; // 0: bytes follow on the stream, 1: IPC handle
+    // 0: bytes follow on the stream, 1: hipIpc handle of the allocation (PCCL_IPC_MODE=fast), 2: VMM fd shares
+    // (fault-safe: the importer keeps the pages alive if the distributor dies mid-copy) — `handle` is the first
+    // segment, `more_handles` the rest; the entry's bytes are the segments back to back, `seg_bytes` each (the last
+    // one shorter), starting at `offset` inside the first
+    uint8_t mode = 0;
     int32_t device = -1;
     uint64_t offset = 0;   // byte offset of the entry inside the exported allocation
     uint64_t raw_ptr = 0;  // the distributor's pointer (usable directly when both peers share a process)
-    uint8_t handle[64]{};  // hipIpcMemHandle_t of the allocation
+    uint8_t handle[64]{};  // hipIpcMemHandle_t of the allocation / VmmHandle of the first segment
+    uint64_t seg_bytes = 0;                          // mode 2 only (encoded only then)
+    std::vector<std::array<uint8_t, 64>> more_handles; // mode 2 only
 };
 
 struct S2CSharedStateIpcResponse {

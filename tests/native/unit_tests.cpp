@@ -121,6 +121,24 @@ TEST(packet_extensions_backward_compatible) {
     EXPECT(q.revision == 9 && q.pid == 1234 && q.entries.size() == 1 && q.entries[0].key == "w" &&
            q.entries[0].mode == 1 && q.entries[0].device == 2 && q.entries[0].offset == 512 &&
            q.entries[0].raw_ptr == 0xdeadbeef && q.entries[0].handle[0] == 7 && q.entries[0].handle[63] == 9);
+    // mode 2 (VMM fd shares): segment size and the extra segment handles travel too; mode 0/1 entries carry none
+    proto::SharedStateIpcEntry v = ie;
+    v.key = "big";
+    v.mode = 2;
+    v.seg_bytes = 1 << 30;
+    v.more_handles.resize(2);
+    v.more_handles[0][5] = 11;
+    v.more_handles[1][63] = 13;
+    s.entries.push_back(v);
+    proto::SharedStateIpcEntry plain;
+    plain.key = "cpu";
+    plain.size_bytes = 8;
+    s.entries.push_back(plain);
+    auto q2 = roundtrip(s);
+    EXPECT(q2.entries.size() == 3 && q2.entries[1].mode == 2 && q2.entries[1].seg_bytes == (1u << 30) &&
+           q2.entries[1].more_handles.size() == 2 && q2.entries[1].more_handles[0][5] == 11 &&
+           q2.entries[1].more_handles[1][63] == 13 && q2.entries[0].more_handles.empty() &&
+           q2.entries[2].key == "cpu" && q2.entries[2].mode == 0 && q2.entries[2].seg_bytes == 0);
     proto::C2SRequestSharedStateIpc rq;
     rq.keys = {"a", "b"};
     rq.host_token = "t";

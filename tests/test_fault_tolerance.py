@@ -138,3 +138,33 @@ def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn, shareable):
             b = s_k["ipc_bufs"]
             assert b["direct_out"] > 300 and b["staged_out"] == 0, b
             assert (b["direct_in"] > 300 and b["staged_in"] == 0) if not inplace else b["direct_in"] == 0, b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shareable", [False, True])
+def test_gpu_shared_state_distributor_sigkill_mid_handoff(hip, shareable):
+    """Same-host shared-state hand-off (HBM entries passed as VMM fd shares): the distributor SIGKILLs itself 300 ms
+    after sending its IPC response (PCCL_FAULT_INJECT=ss_serve:5 + PCCL_FAULT_INJECT_DELAY_MS) while the joiner has
+    mapped its copy and waits 1 s before copying (PCCL_SS_COPY_DELAY_MS). The joiner's import holds its own reference
+    to the pages, so the copy reads valid memory of a dead process: exact data, no GPU fault, and the survivors then
+    all-reduce in the shrunken world. Both distributors carry the injection; only the one that serves dies."""
+    worker = os.path.join(HERE, "workers", "ss_peer.py")
+    extra = ["--n", str(1 << 26)] + (["--shareable"] if shareable else [])
+    kill = {"PCCL_FAULT_INJECT": "ss_serve:5", "PCCL_FAULT_INJECT_DELAY_MS": "300"}
+    with local_master() as addr:
+        ds = [spawn_python([worker, addr, "dist", *extra], env=kill, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True) for _ in range(2)]
+        time.sleep(1.0)
+        j = spawn_python([worker, addr, "join", *extra], env={"PCCL_SS_COPY_DELAY_MS": "1000"},
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        outs = [p.communicate(timeout=180) for p in ds + [j]]
+    rcs = [p.returncode for p in ds + [j]]
+    assert sorted(rcs[:2]) == [-9, 0], (rcs, [o[1][-2000:] for o in outs])
+    assert rcs[2] == 0, outs[2][1][-3000:]
+    for _, err in outs:
+        assert "memory access fault" not in err.lower() and "illegal address" not in err.lower(), err[-2000:]
+    jl = _lines(outs[2][0])
+    sync = next(x for x in jl if x["phase"] == "sync")
+    assert sync["lo"] == sync["hi"] == 7.0 and sync["rx"] == (1 << 26) * 4 and sync["revision"] == 5, jl
+    ar = next(x for x in jl if x["phase"] == "all_reduce")
+    assert ar["world"] == 2 and ar["lo"] == ar["hi"] == 2.0, jl
