@@ -9,7 +9,9 @@ Two peer processes and an in-process master on 127.0.0.1:
     trainer's content, the joiner pulls every tensor and re-hashes it.
 Reported: the joiner's wall time for that call (hash + master election + transfer + verification) and the payload
 throughput. ``--transport ipc`` (default on GPUs) hands HBM tensors over with HIP IPC (device-to-device copy);
-``tcp`` streams them through pinned staging buffers over loopback TCP (the reference's only transport).
+``tcp`` streams them through pinned staging buffers over loopback TCP (the reference's only transport). The IPC
+hand-off is fault-safe: the trainer's tensors are staged into VMM segments shared as fds unless ``--shareable`` puts
+them in fd-shareable memory from the start (zero-copy).
 The reference publishes no number for this configuration; its transfer path is the TCP stream.
 """
 from __future__ import annotations
@@ -25,12 +27,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _state(torch, pccl, n_params, n_tensors, device, fill):
+def _state(torch, pccl, n_params, n_tensors, device, fill, shareable=False):
+    import contextlib
     per = n_params // n_tensors
     tensors = []
     for i in range(n_tensors):
         numel = per if i < n_tensors - 1 else n_params - per * (n_tensors - 1)
-        t = torch.empty(numel, dtype=torch.float32, device=device)
+        with pccl.memory.maybe_shareable(device) if shareable else contextlib.nullcontext():
+            t = torch.empty(numel, dtype=torch.float32, device=device)
         if fill == "random":
             g = torch.Generator(device=device).manual_seed(1234 + i)
             t.normal_(generator=g)
@@ -51,7 +55,7 @@ def peer(a):
     comm = pccl.Communicator(a.master, 0)
     comm.connect(n_attempts=60)
     if a.role == "trainer":
-        tensors, st = _state(torch, pccl, a.params, a.tensors, dev, "random")
+        tensors, st = _state(torch, pccl, a.params, a.tensors, dev, "random", a.shareable)
         for rev in range(3):  # train alone for a few revisions
             st.revision = rev
             comm.sync_shared_state(st)
@@ -94,6 +98,8 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--transport", default="ipc", choices=["ipc", "tcp"])
     ap.add_argument("--role", default=None, choices=["trainer", "joiner"])
+    ap.add_argument("--shareable", action="store_true", help="the trainer's state lives in fd-shareable memory "
+                    "(pccl_amd.memory): the fault-safe IPC hand-off is zero-copy instead of staged")
     ap.add_argument("--master", default=None)
     a = ap.parse_args()
     a.params = int(a.params)
@@ -102,7 +108,8 @@ def main():
 
     from pccl_amd.utils import local_master, spawn_python
     env = {"PCCL_SS_NO_IPC": "1"} if a.transport == "tcp" else {}
-    common = ["--params", str(a.params), "--tensors", str(a.tensors), "--device", a.device]
+    common = ["--params", str(a.params), "--tensors", str(a.tensors), "--device", a.device] + \
+        (["--shareable"] if a.shareable else [])
     with local_master() as addr:
         me = os.path.abspath(__file__)
         trainer = spawn_python([me, "--role", "trainer", "--master", addr, *common], env=env,
@@ -121,7 +128,7 @@ def main():
     print(json.dumps({
         "metric": "shared-state late-joiner catch-up", "config": "Shared-state sync: 1B-param fp32 state, "
         "late-joining peer catches up from rev 0", "params": a.params, "tensors": a.tensors, "device": a.device,
-        "transport": a.transport, "seconds": round(j["seconds"], 4), "bytes": j["bytes"],
+        "transport": a.transport, "shareable_state": a.shareable, "seconds": round(j["seconds"], 4), "bytes": j["bytes"],
         "GBps": round(j["bytes"] / j["seconds"] / 1e9, 3), "joiner_rx_bytes": j["rx_bytes"],
         "trainer_tx_bytes": t["tx_bytes"], "adopted_revision": j["revision"], "content_ok": j["sums"] == t["sums"]}),
         flush=True)

@@ -16,8 +16,9 @@ run() { # name timeout cmd...
 STEPS=${STEPS:-tests,ss_ipc,ss_tcp,wan,ft,basic}
 [[ $STEPS == *tests* ]] && { run tests 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_benchmarks.py tests/test_gpu_allreduce.py || exit $?; }
 [[ $STEPS == *ss_ipc* ]] && { run ss_ipc 300 python benchmarks/shared_state_sync.py --params 1e9 --transport ipc || exit $?; }
+[[ $STEPS == *ss_shr* ]] && { run ss_shr 300 python benchmarks/shared_state_sync.py --params 1e9 --transport ipc --shareable || exit $?; }
 [[ $STEPS == *ss_tcp* ]] && { run ss_tcp 300 python benchmarks/shared_state_sync.py --params 1e9 --transport tcp || exit $?; }
 [[ $STEPS == *wan* ]] && { run wan 400 python benchmarks/wan_quantized.py || exit $?; }
-[[ $STEPS == *ft* ]] && { run ft 300 python benchmarks/fault_tolerance.py --no-ipc --log-dir gpurun_out/ft_logs || exit $?; }
+[[ $STEPS == *ft* ]] && { run ft 300 python benchmarks/fault_tolerance.py --log-dir gpurun_out/ft_logs || exit $?; }
 [[ $STEPS == *basic* ]] && { run basic 300 python benchmarks/basic_reduce.py || exit $?; }
 exit 0
