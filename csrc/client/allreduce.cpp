@@ -534,6 +534,37 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
     return 0;
 }
 
+// Small all-reduces (at most PCCL_SMALL_ALLREDUCE_BYTES per peer, default 256 KiB; must match on every peer): the
+// whole vector travels W-1 ring hops (all-gather) and every peer reduces the W vectors locally in ring-index order,
+// instead of 2(W-1) hops of 1/W pieces. Such ops are bound by per-hop latency (socket wake-ups), not bytes, so this
+// halves their critical path; every peer reduces the same vectors in the same order, so results stay bit-identical
+// across peers. Returns 0 ok, 1 io failure, 2 abort; `dst` is written only after every hop succeeded.
+size_t small_allreduce_bytes() { return env_size("PCCL_SMALL_ALLREDUCE_BYTES", 256u << 10); }
+
+int small_allgather_reduce(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
+                           const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
+                           const void *src, void *dst, size_t count, DType dt, ReduceOp op, size_t ws, size_t rank,
+                           const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
+                           std::atomic<uint64_t> &rx_ctr) {
+    const size_t es = dtype_size(dt), bytes = count * es;
+    Lease all(host_pool(), std::max<size_t>(ws * bytes, 64));
+    if (!all.ok()) return 1;
+    uint8_t *v = all.data();
+    std::memcpy(v + rank * bytes, src, bytes);
+    for (size_t step = 0; step + 1 < ws; ++step) {
+        const size_t send_idx = (rank + ws - step) % ws, recv_idx = (rank + ws - step - 1) % ws;
+        const int rc = striped_step(txs, rxs, tag, seq, v + send_idx * bytes, bytes, [](size_t) { return true; },
+                                    v + recv_idx * bytes, bytes, es, std::max<size_t>(bytes, 1),
+                                    [](size_t, size_t) {}, aborted, tx_ctr, rx_ctr);
+        if (rc) return rc;
+    }
+    std::memcpy(dst, v, bytes);
+    for (size_t k = 1; k < ws; ++k)
+        if (!kernels::host_reduce(dst, v + k * bytes, count, dt, op)) return 1;
+    if (op == ReduceOp::Avg) kernels::host_finalize_avg(dst, count, dt, ws);
+    return 0;
+}
+
 } // namespace
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -551,6 +582,13 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
 
     StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
     auto aborted = [&] { return abort_received(q.tag); };
+
+    if (!quant && bytes <= small_allreduce_bytes()) {
+        const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
+                                              aborted, op.tx, op.rx);
+        trace_mark("allgather_reduce");
+        return {rc == 0, rc == 2};
+    }
 
     Lease backup;
     if (q.src == q.dst) {
@@ -726,6 +764,17 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     StreamLease stream(device);
     DevStream st = stream.get();
     if (!st) return {false, false};
+    if (bytes <= small_allreduce_bytes()) { // latency-bound: one D2H, host all-gather + reduce, one H2D
+        Lease hin(pinned_pool(), std::max<size_t>(bytes, 64)), hout(pinned_pool(), std::max<size_t>(bytes, 64));
+        if (!hin.ok() || !hout.ok()) return {false, false};
+        if (!be->memcpy_async(hin.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};
+        const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, hin.data(), hout.data(), q.count, q.dtype,
+                                              q.op, ws, rank, [&] { return abort_received(q.tag); }, op.tx, op.rx);
+        if (rc) return {false, rc == 2};
+        if (!be->memcpy_async(dst, hout.data(), bytes, st) || !be->stream_sync(st)) return {false, false};
+        trace_mark("allgather_reduce");
+        return {true, false};
+    }
     PcieQueues pq;
     StreamLease own_h2d(device), own_d2h(device);
     if (env_size("PCCL_SHARED_COPY_QUEUES", 1) != 0) {

@@ -282,3 +282,44 @@ def test_striped_large_all_reduce(world, pool, quant, monkeypatch):
     expect = _expected(inputs, pccl.ReduceOp.SUM).float()
     tol = 3 * world * max(float(t.max() - t.min()) for t in inputs) / 255 if quant else 1e-4
     assert (res[0] - expect).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("small_limit", [0, 1 << 18])
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.int32])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_small_message_allgather_path(small_limit, world, dtype, inplace, monkeypatch):
+    """Ops up to PCCL_SMALL_ALLREDUCE_BYTES take the all-gather + local-reduce path (W-1 hops instead of 2(W-1));
+    0 forces the ring. Both must give the same (exact for integer-valued data) sums, bit-identical on every peer,
+    for every op incl. AVG, in place or not, and sizes that do not divide by the world."""
+    monkeypatch.setenv("PCCL_SMALL_ALLREDUCE_BYTES", str(small_limit))
+    n = 1003
+    lim = 4 if dtype == torch.bfloat16 else 8  # products of 4 values stay exactly representable in bf16
+    inputs = [torch.randint(-lim, lim, (n,), generator=torch.Generator().manual_seed(7 + r)).to(dtype)
+              for r in range(world)]
+    ops = [pccl.ReduceOp.SUM, pccl.ReduceOp.MAX, pccl.ReduceOp.MIN, pccl.ReduceOp.PROD]
+    if dtype.is_floating_point:
+        ops.append(pccl.ReduceOp.AVG)
+
+    def fn(rank, comm):
+        outs = []
+        for k, op in enumerate(ops):
+            x = inputs[rank].clone()
+            y = x if inplace else torch.empty_like(x)
+            info = comm.all_reduce(x, y, op=op, tag=k)
+            outs.append((y, info.tx_bytes))
+        return outs
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr)
+    for k, op in enumerate(ops):
+        expect = _expected(inputs, op)
+        for r in range(world):
+            y, tx = res[r][k]
+            assert torch.equal(y, res[0][k][0]), "peers must agree bit-for-bit"
+            if dtype == torch.bfloat16 and op == pccl.ReduceOp.AVG:
+                torch.testing.assert_close(y.double(), expect, rtol=1e-2, atol=1e-2)
+            else:
+                assert torch.equal(y.double(), expect.double()), (op, y[:8], expect[:8])
+            nbytes = n * inputs[0].element_size()
+            assert tx == (nbytes * (world - 1) if small_limit else tx), tx  # all-gather sends W-1 whole vectors

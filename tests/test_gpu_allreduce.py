@@ -301,3 +301,24 @@ def test_shareable_memory_concurrent_threads(hip):
 
     for lo, hi in _run(4, fn):
         assert lo == hi == 10.0
+
+
+@pytest.mark.parametrize("n", [1, 1000, 65536, 300_000])
+def test_device_ring_small_messages(hip, n, monkeypatch):
+    """Device tensors over the TCP ring below PCCL_SMALL_ALLREDUCE_BYTES (256 KiB): one D2H, host all-gather +
+    ring-order reduce, one H2D; 300k fp32 (1.2 MB) takes the pipelined ring. Exact, identical on every peer."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+
+    def fn(rank, comm):
+        x = torch.arange(n, device=hip, dtype=torch.float32) % 7 + rank
+        y = torch.empty_like(x)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        comm.all_reduce(x, x, op=pccl.ReduceOp.MAX, tag=1)
+        torch.cuda.synchronize()
+        return y.cpu(), x.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    res = _run(3, fn)
+    base = torch.arange(n, dtype=torch.float32) % 7
+    for y, x, path in res:
+        assert path == pccl.ReducePath.DEVICE_RING.value
+        assert torch.equal(y, 3 * base + 3) and torch.equal(x, base + 2)
