@@ -534,12 +534,18 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
     return 0;
 }
 
-// Small all-reduces (at most PCCL_SMALL_ALLREDUCE_BYTES per peer, default 256 KiB; must match on every peer): the
-// whole vector travels W-1 ring hops (all-gather) and every peer reduces the W vectors locally in ring-index order,
-// instead of 2(W-1) hops of 1/W pieces. Such ops are bound by per-hop latency (socket wake-ups), not bytes, so this
-// halves their critical path; every peer reduces the same vectors in the same order, so results stay bit-identical
-// across peers. Returns 0 ok, 1 io failure, 2 abort; `dst` is written only after every hop succeeded.
-size_t small_allreduce_bytes() { return env_size("PCCL_SMALL_ALLREDUCE_BYTES", 256u << 10); }
+// Small all-reduces: the whole vector travels W-1 ring hops (all-gather) and every peer reduces the W vectors locally
+// in ring-index order, instead of 2(W-1) hops of 1/W pieces. Such ops are bound by per-hop latency (socket wake-ups,
+// and on the device ring per-step staging copies), not bytes, so this halves their critical path; every peer reduces
+// the same vectors in the same order, so results stay bit-identical across peers. Taken when the vector is at most
+// PCCL_SMALL_ALLREDUCE_BYTES (default 1 MiB; must match on every peer) and the all-gather sends at most 8x that
+// (W-1 copies). Measured on MI355X, 8 peers, TCP device ring (profiles/r2/small_messages/): 64 KiB 1770 -> 547 us,
+// 256 KiB 2822 -> 921 us, 1 MiB 2968 -> 2496 us, 4 MiB 4182 -> 10277 us (hence the cap).
+// Returns 0 ok, 1 io failure, 2 abort; `dst` is written only after every hop succeeded.
+bool use_small_path(size_t bytes, size_t ws) {
+    const size_t lim = env_size("PCCL_SMALL_ALLREDUCE_BYTES", 1u << 20);
+    return bytes <= lim && bytes * (ws - 1) <= 8 * lim;
+}
 
 int small_allgather_reduce(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                            const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq,
@@ -583,7 +589,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
     auto aborted = [&] { return abort_received(q.tag); };
 
-    if (!quant && bytes <= small_allreduce_bytes()) {
+    if (!quant && use_small_path(bytes, ws)) {
         const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
                                               aborted, op.tx, op.rx);
         trace_mark("allgather_reduce");
@@ -764,7 +770,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     StreamLease stream(device);
     DevStream st = stream.get();
     if (!st) return {false, false};
-    if (bytes <= small_allreduce_bytes()) { // latency-bound: one D2H, host all-gather + reduce, one H2D
+    if (use_small_path(bytes, ws)) { // latency-bound: one D2H, host all-gather + reduce, one H2D
         Lease hin(pinned_pool(), std::max<size_t>(bytes, 64)), hout(pinned_pool(), std::max<size_t>(bytes, 64));
         if (!hin.ok() || !hout.ok()) return {false, false};
         if (!be->memcpy_async(hin.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};

@@ -305,7 +305,7 @@ def test_shareable_memory_concurrent_threads(hip):
 
 @pytest.mark.parametrize("n", [1, 1000, 65536, 300_000])
 def test_device_ring_small_messages(hip, n, monkeypatch):
-    """Device tensors over the TCP ring below PCCL_SMALL_ALLREDUCE_BYTES (256 KiB): one D2H, host all-gather +
+    """Device tensors over the TCP ring below PCCL_SMALL_ALLREDUCE_BYTES (1 MiB): one D2H, host all-gather +
     ring-order reduce, one H2D; 300k fp32 (1.2 MB) takes the pipelined ring. Exact, identical on every peer."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
 
