@@ -336,6 +336,7 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 }
             }
         } unmap{be, mapped};
+        std::map<std::pair<std::array<uint8_t, 64>, int>, void *> imported; // (handle, device) -> mapping
         std::vector<std::vector<const uint8_t *>> srcs(sresp->entries.size());
         std::vector<int> devs(sresp->entries.size(), 0);
         for (size_t i = 0; ok && i < sresp->entries.size(); ++i) {
@@ -367,18 +368,30 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 std::vector<const uint8_t *> hs{se.handle};
                 for (const auto &h : se.more_handles) hs.push_back(h.data());
                 for (size_t j = 0; j < hs.size(); ++j) {
-                    VmmHandle vh;
-                    int vfd = -1;
+                    // packed entries share segments: import each one once per fetch (an import reserves VA space
+                    // for the whole allocation, and VMM ranges are never freed, hip_backend.hip)
+                    std::array<uint8_t, 64> hk;
+                    std::memcpy(hk.data(), hs[j], hk.size());
                     void *m = nullptr;
-                    if (VmmHandle::decode(hs[j], vh) && (vfd = VmmShare::fetch(vh.pid, vh.nonce, vh.id)) >= 0) {
-                        m = be->vmm_import(vfd, vh.size, dev);
-                        ::close(vfd);
+                    auto hit = imported.find({hk, dev});
+                    if (hit != imported.end()) {
+                        m = hit->second;
+                    } else {
+                        VmmHandle vh;
+                        int vfd = -1;
+                        if (VmmHandle::decode(hs[j], vh) && (vfd = VmmShare::fetch(vh.pid, vh.nonce, vh.id)) >= 0) {
+                            m = be->vmm_import(vfd, vh.size, dev);
+                            ::close(vfd);
+                        }
+                        if (m) {
+                            mapped.push_back({m, true, dev});
+                            imported[{hk, dev}] = m;
+                        }
                     }
                     if (!m) {
                         srcs[i].clear();
                         break;
                     }
-                    mapped.push_back({m, true, dev});
                     srcs[i].push_back(static_cast<const uint8_t *>(m) + (j == 0 ? se.offset : 0));
                 }
             }
@@ -636,6 +649,86 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         }
     } staged_guard{staged};
     const bool same_process = ipc_pid == static_cast<uint32_t>(getpid());
+    // Staging (safe mode, entries not in shareable memory): entries up to kPackMax are packed back to back into
+    // shared VMM segments (one allocation / fd / import per segment instead of per tensor: a model's state has
+    // hundreds of small tensors); larger ones get their own kIpcSegBytes segments. Copies run on one stream per
+    // device and are synchronised once, before the response goes out.
+    constexpr size_t kPackMax = 64u << 20, kPackAlign = 256;
+    struct PackSeg {
+        uint8_t *seg = nullptr;
+        size_t cap = 0, used = 0;
+        std::array<uint8_t, 64> h{};
+    };
+    std::map<int, PackSeg> pack;           // open pack segment per device
+    std::map<int, size_t> small_left;      // bytes of small staged entries still to place, per device
+    std::map<int, std::unique_ptr<StreamLease>> streams;
+    auto stream_for = [&](int dev) -> DevStream {
+        auto &sl = streams[dev];
+        if (!sl) sl = std::make_unique<StreamLease>(dev);
+        return sl->get();
+    };
+    auto new_seg = [&](size_t n, int dev, std::array<uint8_t, 64> &h) -> uint8_t * {
+        void *seg = shareable::alloc(n, dev);
+        shareable::Share sh;
+        if (!seg || !shareable::lookup(seg, n, sh)) {
+            if (seg) shareable::free(seg);
+            return nullptr;
+        }
+        staged.push_back(seg);
+        h.fill(0);
+        std::memcpy(h.data(), &sh.handle, sizeof(sh.handle));
+        return static_cast<uint8_t *>(seg);
+    };
+    auto copy_into = [&](uint8_t *dst, const uint8_t *src, size_t n, int dev) {
+        const void *s = src;
+        const size_t zero = 0;
+        const DevStream st = stream_for(dev);
+        return st && be->multi_gather(dst, &s, &zero, &n, 1, -1, DType::U8, st);
+    };
+    auto stage = [&](const SSEntry &e, SharedStateIpcEntry &ie, int dev) -> bool {
+        const auto *src = static_cast<const uint8_t *>(e.data);
+        if (e.bytes <= kPackMax) {
+            PackSeg &p = pack[dev];
+            size_t off = (p.used + kPackAlign - 1) / kPackAlign * kPackAlign;
+            if (!p.seg || off + e.bytes > p.cap) {
+                p = PackSeg{};
+                p.cap = std::max(e.bytes, std::min(small_left[dev], kIpcSegBytes));
+                if (!(p.seg = new_seg(p.cap, dev, p.h))) return false;
+                off = 0;
+            }
+            if (!copy_into(p.seg + off, src, e.bytes, dev)) return false;
+            p.used = off + e.bytes;
+            small_left[dev] -= std::min(small_left[dev], (e.bytes + kPackAlign - 1) / kPackAlign * kPackAlign);
+            ie.mode = 2;
+            std::memcpy(ie.handle, p.h.data(), p.h.size());
+            ie.offset = off;
+            ie.seg_bytes = e.bytes;
+            return true;
+        }
+        std::vector<std::array<uint8_t, 64>> hs;
+        for (size_t off = 0; off < e.bytes; off += kIpcSegBytes) {
+            const size_t n = std::min(kIpcSegBytes, e.bytes - off);
+            std::array<uint8_t, 64> h{};
+            uint8_t *seg = new_seg(n, dev, h);
+            if (!seg || !copy_into(seg, src + off, n, dev)) return false;
+            hs.push_back(h);
+        }
+        ie.mode = 2;
+        std::memcpy(ie.handle, hs[0].data(), hs[0].size());
+        ie.more_handles.assign(hs.begin() + 1, hs.end());
+        ie.seg_bytes = kIpcSegBytes;
+        ie.offset = 0;
+        return true;
+    };
+    if (!same_process && ipc_safe_mode() && be && same_host) // pass 1: how much will be packed, per device
+        for (const auto &e : to_send) {
+            DevPtrInfo pi{};
+            shareable::Share sh;
+            if (e.bytes == 0 || e.bytes > kPackMax) continue;
+            be->pointer_info(e.data, pi);
+            if (pi.is_device && !(shareable::lookup(e.data, e.bytes, sh) && sh.size <= kIpcMaxExport))
+                small_left[pi.device] += (e.bytes + kPackAlign - 1) / kPackAlign * kPackAlign;
+        }
     for (const auto &e : to_send) {
         SharedStateIpcEntry ie;
         ie.key = e.key;
@@ -658,30 +751,7 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
             ie.offset = sh.offset;
             ie.seg_bytes = e.bytes;
         } else if (ipc_safe_mode()) {
-            StreamLease stream(pi.device);
-            bool ok = stream.get() != nullptr;
-            std::vector<std::array<uint8_t, 64>> hs;
-            for (size_t off = 0; ok && off < e.bytes; off += kIpcSegBytes) {
-                const size_t n = std::min(kIpcSegBytes, e.bytes - off);
-                void *seg = shareable::alloc(n, pi.device);
-                ok = seg != nullptr && shareable::lookup(seg, n, sh);
-                if (!ok) break;
-                staged.push_back(seg);
-                std::array<uint8_t, 64> h{};
-                std::memcpy(h.data(), &sh.handle, sizeof(sh.handle));
-                hs.push_back(h);
-                const void *src = static_cast<const uint8_t *>(e.data) + off;
-                const size_t zero = 0;
-                ok = be->multi_gather(seg, &src, &zero, &n, 1, -1, DType::U8, stream.get());
-            }
-            ok = ok && be->stream_sync(stream.get());
-            if (ok && !hs.empty()) {
-                ie.mode = 2;
-                std::memcpy(ie.handle, hs[0].data(), hs[0].size());
-                ie.more_handles.assign(hs.begin() + 1, hs.end());
-                ie.seg_bytes = kIpcSegBytes;
-                ie.offset = 0;
-            } else {
+            if (!stage(e, ie, pi.device)) {
                 LOG(WARN) << "Shared state: staging " << e.key << " for the IPC hand-off failed; streaming it";
             }
         } else if (be->address_range(e.data, &base, &size) && base && be->ipc_export(base, ie.handle)) {
@@ -694,6 +764,15 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
             ipc_bytes += e.bytes;
         }
         resp.entries.push_back(ie);
+    }
+    for (auto &[dev, sl] : streams) { // staged copies complete before anyone is told where they are
+        be->set_device(dev);
+        if (!sl->get() || !be->stream_sync(sl->get())) {
+            LOG(ERR) << "Shared state: staging copies for the IPC hand-off failed";
+            resp.status = SharedStateStatus::NotDistributed;
+            resp.entries.clear();
+            break;
+        }
     }
     if (!net::send_packet(fd, resp)) return;
     fault_point("ss_serve", revision); // tests: die while the requester maps / copies what was handed over

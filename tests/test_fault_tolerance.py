@@ -168,3 +168,22 @@ def test_gpu_shared_state_distributor_sigkill_mid_handoff(hip, shareable):
     assert sync["lo"] == sync["hi"] == 7.0 and sync["rx"] == (1 << 26) * 4 and sync["revision"] == 5, jl
     ar = next(x for x in jl if x["phase"] == "all_reduce")
     assert ar["world"] == 2 and ar["lo"] == ar["hi"] == 2.0, jl
+
+
+@pytest.mark.gpu
+def test_gpu_shared_state_many_tensors_packed_handoff(hip):
+    """A joiner in another process receives 300 small HBM tensors of odd sizes plus one 256 MiB tensor over the
+    fault-safe IPC hand-off: the small ones are packed into shared VMM segments (one fd / import per segment), the
+    large one has its own; every byte arrives."""
+    worker = os.path.join(HERE, "workers", "ss_peer.py")
+    extra = ["--n", str(1 << 26), "--extra-tensors", "300"]
+    with local_master() as addr:
+        ds = [spawn_python([worker, addr, "dist", *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for _ in range(2)]
+        time.sleep(1.0)
+        j = spawn_python([worker, addr, "join", *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        outs = [p.communicate(timeout=180) for p in ds + [j]]
+    assert [p.returncode for p in ds + [j]] == [0, 0, 0], [o[1][-2000:] for o in outs]
+    sync = next(x for x in _lines(outs[2][0]) if x["phase"] == "sync")
+    assert sync["lo"] == sync["hi"] == 7.0 and sync["extra_ok"] and sync["revision"] == 5, sync
+    assert sync["sec"] < 5.0, sync

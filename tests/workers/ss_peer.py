@@ -26,11 +26,15 @@ def main():
     ap.add_argument("role", choices=["dist", "join"])
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--shareable", action="store_true")
+    ap.add_argument("--extra-tensors", type=int, default=0, help="add K small tensors of odd sizes (packed staging)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     with pccl.memory.maybe_shareable(dev) if a.shareable else contextlib.nullcontext():
         w = torch.full((a.n,), 7.0 if a.role == "dist" else 0.0, device=dev)
-    st = pccl.SharedState([pccl.TensorInfo.from_torch(w, "w")])
+        extra = [torch.full((1 + (k * 997) % 50000,), float(k % 13) if a.role == "dist" else -1.0, device=dev)
+                 for k in range(a.extra_tensors)]
+    st = pccl.SharedState([pccl.TensorInfo.from_torch(w, "w")] +
+                          [pccl.TensorInfo.from_torch(t, f"x{k}") for k, t in enumerate(extra)])
     st.revision = 5 if a.role == "dist" else 0
     comm = pccl.Communicator(a.master, 0)
     comm.connect(n_attempts=60)
@@ -40,10 +44,14 @@ def main():
             if comm.are_peers_pending():
                 comm.update_topology()
             time.sleep(0.01)
+    t0 = time.perf_counter()
     info = comm.sync_shared_state(st)
     torch.cuda.synchronize()
-    print(json.dumps({"role": a.role, "phase": "sync", "rx": info.rx_bytes, "tx": info.tx_bytes,
-                      "lo": float(w.min()), "hi": float(w.max()), "revision": st.revision}), flush=True)
+    dt = time.perf_counter() - t0
+    extra_ok = all(bool((t == float(k % 13)).all()) for k, t in enumerate(extra))
+    print(json.dumps({"role": a.role, "phase": "sync", "rx": info.rx_bytes, "tx": info.tx_bytes, "sec": dt,
+                      "lo": float(w.min()), "hi": float(w.max()), "revision": st.revision, "extra_ok": extra_ok}),
+          flush=True)
     g = torch.ones(1 << 20, device=dev)
     out = torch.empty_like(g)
     for attempt in range(100):  # the ring loses the killed distributor: retry until the new world completes
