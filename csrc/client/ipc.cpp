@@ -717,6 +717,18 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
             map_failed_.store(true, std::memory_order_relaxed);
             return abort_voted(kAborted);
         }
+        // peers in this process are reached through raw pointers (possibly plain hipMalloc memory of another GPU):
+        // my kernels need peer access to their devices
+        for (size_t k = 0; k < ring_.size(); ++k) {
+            if (k == rank_ || pids_[k] != pids_[rank_] || uids[k] == uids[rank_]) continue;
+            const int pd = be->device_of_uid(uids[k]);
+            if (pd < 0 || !be->enable_peer_access(device, pd)) {
+                LOG(ERR) << "IPC: cannot enable peer access from device " << device << " to the GPU of peer " << k
+                         << "; using the TCP ring for later ops";
+                map_failed_.store(true, std::memory_order_relaxed);
+                return abort_voted(kAborted);
+            }
+        }
     }
     OpCtx ctx;
     ctx.bytes = bytes;

@@ -36,6 +36,8 @@ public:
     // visible device with this uid (-1: not visible to this process); whether `dev` can map `peer`'s memory
     virtual int device_of_uid(uint64_t uid) = 0;
     virtual bool can_access_peer(int dev, int peer) = 0;
+    // kernels on `dev` may dereference plain (hipMalloc) pointers of `peer` from now on (idempotent)
+    virtual bool enable_peer_access(int dev, int peer) = 0;
 
     // memory
     virtual void *alloc_device(size_t n) = 0;

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <vector>
 #include <memory>
 #include <mutex>
@@ -64,6 +65,20 @@ public:
             return false;
         }
         return ok != 0;
+    }
+    bool enable_peer_access(int dev, int peer) override {
+        if (dev == peer) return true;
+        std::lock_guard l(peer_mtx_);
+        if (peer_enabled_.count({dev, peer})) return true;
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+        (void)hipGetLastError();
+        if (cur >= 0) (void)hipSetDevice(cur);
+        const bool ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+        if (ok) peer_enabled_.insert({dev, peer});
+        return ok;
     }
     int current_device() override {
         int d = -1;
@@ -429,6 +444,8 @@ private:
     }
 
     int n_devices_ = 0;
+    std::mutex peer_mtx_;
+    std::set<std::pair<int, int>> peer_enabled_;
     std::mutex scratch_mtx_;
     std::map<DevStream, Scratch> scratch_;
     std::map<int, void *> crc_tables_; // per device, uploaded on first use
