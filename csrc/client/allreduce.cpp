@@ -747,11 +747,201 @@ void step_mark(bool reduce_scatter, size_t step) {
     if (step < 16) trace_mark(reduce_scatter ? rs[step] : ag[step]);
 }
 
-// payload bytes [a, b) of a pinned staging buffer become valid once `e` has completed
+// payload bytes [a, b) of a pinned staging buffer become valid once `e` has completed (nullptr: already valid)
 struct Staged {
     size_t a, b;
     DevEvent e;
 };
+
+// Readiness of one ring step's payload, shared between the op thread that produces it (staging copies, the fused
+// reduce, received bytes) and the connections' sender threads that send it, possibly while it is still being
+// produced (send-ahead). Ranges of one stripe are added in order and their events are recorded on one in-order stream,
+// so once the range holding byte end-1 is complete, every earlier byte of that stripe is readable.
+struct ReadyRanges {
+    std::mutex m;
+    std::vector<Staged> v;
+    void clear() {
+        std::lock_guard l(m);
+        v.clear();
+    }
+    void add(size_t a, size_t b, DevEvent e) {
+        std::lock_guard l(m);
+        v.push_back({a, b, e});
+    }
+    // blocks until byte end-1 is readable; false if `cancel` became non-zero first
+    bool wait(size_t end, DeviceBackend *be, const std::atomic<int> &cancel) {
+        if (end == 0) return true;
+        unsigned us = 2;
+        while (true) {
+            bool found = false;
+            DevEvent e = nullptr;
+            {
+                std::lock_guard l(m);
+                for (const auto &r : v)
+                    if (r.a <= end - 1 && end - 1 < r.b) {
+                        found = true;
+                        e = r.e;
+                        break;
+                    }
+            }
+            if (found) return e == nullptr || event_wait_polling(be, e);
+            if (cancel.load(std::memory_order_relaxed) != 0) return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(us));
+            us = std::min(us * 2, 200u);
+        }
+    }
+};
+
+// The send side of one device-ring op: one thread per stripe for the whole op (not per step), each sending its
+// stripe of every step in order over connection (seq + k) % pool. The op thread publishes step g (payload, bytes,
+// readiness) as soon as step g may start sending — with send-ahead while step g-1 still receives — and a stripe thread
+// streams each piece once it is readable. Per-op threads instead of the connections' shared sender threads: a stripe
+// thread may wait on its op's network progress (the previous peer's data), which must never hold up another op's
+// sends queued on the same connection (two peers with concurrent ops could otherwise wait on each other).
+class OpSenders {
+public:
+    struct Step {
+        const uint8_t *payload = nullptr;
+        size_t bytes = 0;
+        ReadyRanges *ready = nullptr;
+    };
+    OpSenders(const std::vector<std::shared_ptr<net::MuxConn>> &txs, uint64_t tag, uint64_t seq, size_t frame,
+              size_t nsteps, size_t max_stripes, DeviceBackend *be, std::atomic<uint64_t> &tx_ctr)
+        : txs_(txs), tag_(tag), seq_(seq), frame_(frame), be_(be), tx_ctr_(tx_ctr), steps_(nsteps),
+          done_(nsteps) {
+        for (size_t k = 0; k < max_stripes; ++k) th_.emplace_back([this, k] { run(k); });
+    }
+    ~OpSenders() {
+        cancel();
+        for (auto &t : th_) t.join();
+    }
+    // step g may be sent from now on (steps are published in order)
+    void publish(size_t g, const Step &st) {
+        const StripePlan tp = plan_stripes(st.bytes, txs_.size());
+        size_t n = 0;
+        for (size_t k = 0; k < tp.off.size(); ++k)
+            if (tp.len[k] > 0) ++n;
+        {
+            std::lock_guard l(m_);
+            steps_[g] = st;
+            done_[g] = n;
+            published_ = g + 1;
+        }
+        cv_.notify_all();
+    }
+    bool published(size_t g) {
+        std::lock_guard l(m_);
+        return published_ > g;
+    }
+    // blocks until every stripe of step g is sent; false on failure / cancel
+    bool wait(size_t g) {
+        std::unique_lock l(m_);
+        cv_.wait(l, [&] { return rc_.load() != 0 || (published_ > g && done_[g] == 0); });
+        return rc_.load() == 0;
+    }
+    void cancel() {
+        rc_.store(1);
+        std::lock_guard l(m_);
+        cv_.notify_all();
+    }
+    bool failed() const { return rc_.load() != 0; }
+    const std::atomic<int> &rc() const { return rc_; }
+
+private:
+    void run(size_t k) {
+        for (size_t g = 0; g < steps_.size(); ++g) {
+            Step st;
+            {
+                std::unique_lock l(m_);
+                cv_.wait(l, [&] { return rc_.load() != 0 || published_ > g; });
+                if (rc_.load() != 0) return;
+                st = steps_[g];
+            }
+            const StripePlan tp = plan_stripes(st.bytes, txs_.size());
+            if (k >= tp.off.size() || tp.len[k] == 0) continue;
+            net::MuxConn *c = txs_[(seq_ + k) % txs_.size()].get();
+            const size_t base = tp.off[k], len = tp.len[k];
+            for (size_t sent = 0; sent < len;) {
+                const size_t n = std::min(frame_, len - sent);
+                if (!st.ready->wait(base + sent + n, be_, rc_) || !c->send_frame(tag_, seq_, st.payload + base + sent, n)) {
+                    cancel();
+                    return;
+                }
+                sent += n;
+                tx_ctr_ += n;
+            }
+            {
+                std::lock_guard l(m_);
+                --done_[g];
+            }
+            cv_.notify_all();
+        }
+    }
+    const std::vector<std::shared_ptr<net::MuxConn>> &txs_;
+    const uint64_t tag_, seq_;
+    const size_t frame_;
+    DeviceBackend *be_;
+    std::atomic<uint64_t> &tx_ctr_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::vector<Step> steps_;
+    std::vector<size_t> done_;
+    size_t published_ = 0;
+    std::atomic<int> rc_{0};
+    std::vector<std::thread> th_;
+};
+
+// The receive half of a ring step: posts the sinks, calls `consume(a, b)` for newly complete elements (batches of at
+// least `gran` bytes unless a stripe ends) and removes the sinks. `send_rc` (may be null) != 0 aborts the wait (a send
+// of this op failed). Returns 0 ok, 1 io failure, 2 abort.
+int receive_step(const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq, uint8_t *sink,
+                 size_t rx_bytes, size_t elem, size_t gran, const std::function<void(size_t, size_t)> &consume,
+                 const std::function<bool()> &aborted, const std::atomic<int> *send_rc, std::atomic<uint64_t> &rx_ctr) {
+    const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
+    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
+    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    const size_t gran_el = std::max<size_t>(1, gran / elem);
+    std::vector<size_t> done(rp.off.size(), 0);
+    size_t remaining = 0;
+    for (size_t k = 0; k < rp.off.size(); ++k)
+        if (rp.len[k] > 0) ++remaining;
+    int rc = 0;
+    size_t idle = 0, rr = 0;
+    while (remaining > 0) {
+        bool progress = false;
+        for (size_t k = 0; k < rp.off.size(); ++k) {
+            const size_t want = rp.len[k] / elem;
+            if (done[k] >= want) continue;
+            const size_t have = rx_conn(k)->sink_progress(tag) / elem;
+            if (have > done[k] && (have - done[k] >= gran_el || have >= want)) {
+                const size_t e0 = rp.off[k] / elem;
+                consume(e0 + done[k], e0 + have);
+                done[k] = have;
+                progress = true;
+                if (done[k] >= want) --remaining;
+            }
+        }
+        if (remaining == 0 || progress) {
+            idle = 0;
+            continue;
+        }
+        size_t k = rr++ % rp.off.size();
+        while (done[k] >= rp.len[k] / elem) k = rr++ % rp.off.size();
+        net::MuxConn *c = rx_conn(k);
+        c->wait_sink(tag, std::min(rp.len[k], (done[k] + gran_el) * elem), 5ms);
+        if (!c->is_open() || (send_rc && send_rc->load() != 0)) {
+            rc = 1;
+            break;
+        }
+        if (++idle % 8 == 0 && aborted()) {
+            rc = 2;
+            break;
+        }
+    }
+    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->remove_sink(tag);
+    if (rc == 0) rx_ctr += rx_bytes;
+    return rc;
+}
 
 } // namespace
 
@@ -850,93 +1040,101 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     uint8_t *txbuf[2] = {txa.data(), txb.data()};
     uint8_t *rxbuf[2] = {rxa.data(), rxb.data()};
     uint8_t *rxdev[2] = {da.data(), db.data()};
-    std::vector<Staged> ready[2]; // staged payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
-    size_t txshift[2] = {0, 0};   // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
+    ReadyRanges txready[2];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    ReadyRanges rxready[2];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
+    size_t txshift[2] = {0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
     DevEvent sink_free[2] = {nullptr, nullptr}; // last H2D copy reading rxbuf[i]
 
-    // tx_ready over a staged payload: the sender of a stripe asks for [.., end); the range holding byte end-1 was
-    // queued after every earlier range of that stripe on the (in-order) D2H queue, so its event covers them all
-    auto ready_fn = [&](std::vector<Staged> &lst) {
-        std::sort(lst.begin(), lst.end(), [](const Staged &x, const Staged &y) { return x.a < y.a; });
-        return [&lst, be](size_t end) {
-            if (end == 0) return true;
-            auto it = std::upper_bound(lst.begin(), lst.end(), end - 1,
-                                       [](size_t v, const Staged &x) { return v < x.a; });
-            if (it == lst.begin()) return false;
-            --it;
-            return end <= it->b && event_wait_polling(be, it->e);
-        };
+    // Steps g = 0 .. 2(W-1)-1: reduce-scatter, then all-gather. With send-ahead (PCCL_RING_SEND_AHEAD=1) step g+1's
+    // sends start while step g still receives, so each piece of the next payload leaves as soon as it exists. Measured
+    // (profiles/r2/ring_send_ahead/): 8 peers 366 -> 370 ms, 2 peers 79 -> 119 ms (the receiver has not posted the
+    // next step's sinks yet, so early frames are queued and copied once more) — off by default.
+    const bool ahead = env_size("PCCL_RING_SEND_AHEAD", 0) != 0;
+    const size_t nsteps = 2 * (ws - 1);
+    auto chunk_tx = [&](size_t g) { // chunk index this peer sends at global step g
+        return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
     };
-    auto always_ready = [](size_t) { return true; };
-    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
-                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume) {
-        return striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, es, piece, consume,
-                            aborted, op.tx, op.rx, {}, piece);
+    auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
+    size_t max_stripes = 1;
+    for (size_t g = 0; g < nsteps; ++g) {
+        const auto [ts, te] = bounds[chunk_tx(g)];
+        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, rv.tx.size()).off.size());
+    }
+    // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
+    OpSenders senders(rv.tx, q.tag, seq, piece, nsteps, max_stripes, be, op.tx);
+    auto start = [&](size_t g) {
+        const auto [ts, te] = bounds[chunk_tx(g)];
+        const bool rs_or_ag0 = g < ws; // reduce-scatter steps and all-gather step 0 send staged txbuf payloads
+        OpSenders::Step stp;
+        stp.payload = rs_or_ag0 ? txbuf[g % 2] + txshift[g % 2] : rxbuf[(g + 1) % 2];
+        stp.bytes = (te - ts) * es;
+        stp.ready = rs_or_ag0 ? &txready[g % 2] : &rxready[(g + 1) % 2];
+        senders.publish(g, stp);
+    };
+    auto fail_all = [&](int code) {
+        senders.cancel();
+        return fail(code);
     };
 
-    size_t g = 0; // global step (reduce-scatter and all-gather): alternates the double buffers
-    // ---- reduce-scatter
-    for (size_t step = 0; step + 1 < ws; ++step, ++g) {
+    for (size_t g = 0; g < nsteps; ++g) {
         const size_t cur = g % 2, nxt = cur ^ 1;
-        const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
-        const auto [ts, te] = bounds[tx_idx];
-        const auto [rs, re] = bounds[rx_idx];
+        const bool rs = g + 1 < ws;
+        // step g-1's sends read the buffers this step refills (txbuf[nxt] for reduce-scatter, rxbuf[cur] through
+        // step g+1's forwarding): they must be done first
+        if (g > 0 && !senders.wait(g - 1)) return fail_all(1);
         if (sink_free[cur]) event_wait_polling(be, sink_free[cur]);
-        if (step == 0) { // own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
-            ready[cur].clear();
+        if (g == 0) { // own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+            const auto [ts, te] = bounds[chunk_tx(0)];
+            txready[cur].clear();
             txshift[cur] = 0;
             for (size_t off = 0; off < (te - ts) * es; off += piece) {
                 const size_t n = std::min(piece, (te - ts) * es - off);
                 be->memcpy_async(txbuf[cur] + off, static_cast<const uint8_t *>(q.src) + ts * es + off, n, pq.d2h);
                 last_d2h = record(pq.d2h);
-                ready[cur].push_back({off, off + n, last_d2h});
+                txready[cur].add(off, off + n, last_d2h);
             }
         }
-        ready[nxt].clear();
-        uint8_t *region = dst + rs * es;
-        // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
+        const auto [rs0, re0] = bounds[chunk_rx(g)];
+        uint8_t *region = dst + rs0 * es;
         const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
-        txshift[nxt] = shift;
-        uint8_t *sink = rxbuf[cur], *stage = rxdev[cur] + shift, *out = txbuf[nxt] + shift;
-        const int rc = run_step(txbuf[cur] + txshift[cur], (te - ts) * es, ready_fn(ready[cur]), sink,
-                                (re - rs) * es, [&](size_t a, size_t b) {
-            const size_t off = a * es, n = (b - a) * es;
-            be->memcpy_async(stage + off, sink + off, n, pq.h2d);
-            last_h2d = record(pq.h2d);
-            be->stream_wait_event(st, last_h2d);
-            be->reduce_copy(region + off, stage + off, out + off, b - a, q.dtype, q.op, st);
-            ready[nxt].push_back({off, off + n, record(st)});
-        });
+        if (rs) { // the reduced pieces become the next step's payload in txbuf[nxt]
+            txready[nxt].clear();
+            txshift[nxt] = shift;
+        } else { // this step's received bytes are forwarded by the next all-gather step
+            rxready[cur].clear();
+        }
+        if (!senders.published(g)) start(g);
+        if (ahead && g + 1 < nsteps) start(g + 1);
+        uint8_t *sink = rxbuf[cur];
+        std::function<void(size_t, size_t)> consume;
+        if (rs) {
+            // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
+            uint8_t *stage = rxdev[cur] + shift, *out = txbuf[nxt] + shift;
+            consume = [&, stage, out, sink, region](size_t a, size_t b) {
+                const size_t off = a * es, n = (b - a) * es;
+                be->memcpy_async(stage + off, sink + off, n, pq.h2d);
+                last_h2d = record(pq.h2d);
+                be->stream_wait_event(st, last_h2d);
+                be->reduce_copy(region + off, stage + off, out + off, b - a, q.dtype, q.op, st);
+                txready[nxt].add(off, off + n, record(st));
+            };
+        } else {
+            consume = [&, sink, region, cur](size_t a, size_t b) {
+                be->memcpy_async(region + a * es, sink + a * es, (b - a) * es, pq.h2d);
+                last_h2d = record(pq.h2d);
+                rxready[cur].add(a * es, b * es, nullptr); // in host memory: forwardable at once
+            };
+        }
+        const int rc = receive_step(rv.rx, q.tag, seq, sink, (re0 - rs0) * es, es, piece, consume, aborted,
+                                    &senders.rc(), op.rx);
         sink_free[cur] = last_h2d;
-        if (rc) return fail(rc);
-        step_mark(true, step);
-        if (step == 0) fault_point("ring_step", seq);
+        if (rc) return fail_all(rc);
+        if (!ahead && !senders.wait(g)) return fail_all(1); // classic schedule: a step ends when its sends are done
+        step_mark(rs, rs ? g : g - (ws - 1));
+        if (g == 0) fault_point("ring_step", seq);
+        if (g + 2 == ws) trace_mark("reduce_scatter");
     }
-
-    trace_mark("reduce_scatter");
-    // ---- all-gather: step 0 sends the owned chunk (staged by the last reduce-scatter step), later steps forward the
-    // previous step's received bytes verbatim from pinned memory; received bytes go to HBM on the H2D queue
-    size_t cur_chunk = (rank + 1) % ws;
-    for (size_t step = 0; step + 1 < ws; ++step, ++g) {
-        const size_t cur = g % 2, prev = cur ^ 1;
-        const size_t inc = (cur_chunk + ws - 1) % ws;
-        const auto [ts, te] = bounds[cur_chunk];
-        const auto [rs, re] = bounds[inc];
-        if (sink_free[cur]) event_wait_polling(be, sink_free[cur]);
-        uint8_t *sink = rxbuf[cur], *region = dst + rs * es;
-        auto consume = [&](size_t a, size_t b) {
-            be->memcpy_async(region + a * es, sink + a * es, (b - a) * es, pq.h2d);
-            last_h2d = record(pq.h2d);
-        };
-        const int rc = step == 0
-                           ? run_step(txbuf[cur] + txshift[cur], (te - ts) * es, ready_fn(ready[cur]), sink,
-                                      (re - rs) * es, consume)
-                           : run_step(rxbuf[prev], (te - ts) * es, always_ready, sink, (re - rs) * es, consume);
-        sink_free[cur] = last_h2d;
-        if (rc) return fail(rc);
-        step_mark(false, step);
-        cur_chunk = inc;
-    }
+    if (!senders.wait(nsteps - 1)) return fail_all(1);
     if (last_h2d) be->stream_wait_event(st, last_h2d);
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
     if (!be->stream_sync(st)) return {false, false};
