@@ -293,6 +293,13 @@ class ReduceOpDescriptor:
         c.recvbuf = self.recvbuf_ptr
         self.reduce_descriptor.fill(c.descriptor)
 
+    to_c_inpl = fill  # reference name (python/framework/pccl/_pccl.py:319)
+
+    def to_c(self) -> _native.ReduceOpDescriptorC:
+        c = _native.ReduceOpDescriptorC()
+        self.fill(c)
+        return c
+
 
 class TensorInfo:
     def __init__(self, name: str, data_ptr: int, *, numel: int, dtype: DataType, device_type: DeviceType,
