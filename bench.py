@@ -49,8 +49,9 @@ def _args():
     ap.add_argument("--peers", type=int, default=8, help="total peers of the job (config: 8)")
     ap.add_argument("--mib", type=int, default=1024, help="buffer per peer in MiB (config: 1024)")
     ap.add_argument("--pool", type=int, default=0,
-                    help="P2P connections per ring neighbour (ring stripes); 0 = 16 / peers on the host, in [1, 8]: "
-                         "8 peers x 2 stripes measured fastest on one MI355X box (profiles/r2/ring_sweep.md)")
+                    help="P2P connections per ring neighbour (ring stripes); 0 = CPUs available / peers on the host, "
+                         "in [1, 8]: on the 16-CPU MI355X box 8 peers x 2 stripes measured fastest "
+                         "(profiles/r2/ring_sweep.md, profiles/r2/tcp_loopback/)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     ap.add_argument("--extras-child", default="", help=argparse.SUPPRESS)  # internal: run only the extras, write JSON
@@ -84,8 +85,8 @@ class Job:
         self.first = self.rank * self.local
         self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
         self.bar = threading.Barrier(self.local)
-        if a.pool <= 0:
-            a.pool = max(1, min(8, 16 // self.total))
+        if a.pool <= 0:  # connections per ring neighbour: the box's CPU share over the host's peers, in [1, 8]
+            a.pool = max(1, min(8, int(_cpu_quota()) // self.total))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
