@@ -49,7 +49,7 @@ def main():
     it_local = 0
     timer = Timer()
     while True:
-        prof = Profiler()
+        prof = Profiler(sync_cuda=device.type == "cuda")  # phase times include the GPU work queued in them
         with prof.session("update_topology"):
             maybe_update_topology(comm, it_local)
         it_local += 1
@@ -86,7 +86,8 @@ def main():
         iter_num += 1
         state.revision += 1
         dt = timer.lap()
-        rec = {"iter": it, "loss": round(loss_acc, 4), "world": ws, "ms": round(dt * 1e3, 1),
+        phase_ms = {k: round(v * 1e3, 2) for k, v in prof.totals().items() if k in ("forward_backward", "all_reduce")}
+        rec = {"iter": it, "loss": round(loss_acc, 4), "world": ws, "ms": round(dt * 1e3, 1), "phase_ms": phase_ms,
                "tok_s": round(tokens_per_iter / dt, 1), "mfu": round(model.estimate_mfu(tokens_per_iter, dt), 4),
                "ss_rx": info.rx_bytes, "ar_tx": res.tx_bytes if res else 0}
         if a.eval_interval and it % a.eval_interval == 0:
