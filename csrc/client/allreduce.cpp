@@ -863,7 +863,12 @@ private:
             const size_t base = tp.off[k], len = tp.len[k];
             for (size_t sent = 0; sent < len;) {
                 const size_t n = std::min(frame_, len - sent);
-                if (!st.ready->wait(base + sent + n, be_, rc_) || !c->send_frame(tag_, seq_, st.payload + base + sent, n)) {
+                if (!st.ready->wait(base + sent + n, be_, rc_)) {
+                    cancel();
+                    return;
+                }
+                RoctxIoRange io("send");
+                if (!c->send_frame(tag_, seq_, st.payload + base + sent, n)) {
                     cancel();
                     return;
                 }

@@ -96,6 +96,13 @@ const Roctx &roctx() {
     }();
     return r;
 }
+bool roctx_io_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("PCCL_ROCTX_IO");
+        return e != nullptr && e[0] == '1';
+    }();
+    return v;
+}
 OpTrace *&current_trace() {
     thread_local OpTrace *t = nullptr;
     return t;

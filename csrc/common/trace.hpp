@@ -55,6 +55,21 @@ struct RoctxRange {
     RoctxRange &operator=(const RoctxRange &) = delete;
 };
 
+// Per-frame I/O ranges (device-ring sends), only with PCCL_ROCTX_IO=1: thousands per large op, for timelines that
+// show socket sends against copies and kernels (scripts/ring_overlap.py).
+bool roctx_io_enabled();
+struct RoctxIoRange {
+    bool on;
+    explicit RoctxIoRange(const char *name) : on(roctx_io_enabled() && roctx().push != nullptr) {
+        if (on) roctx().push(name);
+    }
+    ~RoctxIoRange() {
+        if (on) roctx().pop();
+    }
+    RoctxIoRange(const RoctxIoRange &) = delete;
+    RoctxIoRange &operator=(const RoctxIoRange &) = delete;
+};
+
 inline void trace_mark(const char *what) {
     if (OpTrace *t = current_trace()) t->mark(what);
     if (const Roctx &r = roctx(); r.mark) r.mark(what);

@@ -1,5 +1,7 @@
 #include "mux.hpp"
 
+#include "../common/trace.hpp"
+
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -216,7 +218,11 @@ void MuxConn::rx_loop() {
             }
         }
         if (sink != nullptr) {
-            const bool ok = read_into(sink->dst + offset, n, sink);
+            bool ok;
+            {
+                RoctxIoRange io("recv");
+                ok = read_into(sink->dst + offset, n, sink);
+            }
             {
                 std::lock_guard l(mtx_);
                 sink->busy = false;
