@@ -370,7 +370,34 @@ def run_extras(job, a, nbytes):
         extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
+    elif job.n_gpus > 1 and os.environ.get("PCCL_BENCH_RCCL", "1") == "1":
+        extra["rccl_reference"] = rccl_reference(job, a, nbytes)
     return extra, sweep
+
+
+def rccl_reference(job, a, nbytes):
+    """RCCL (torch.distributed "nccl" backend) all-reduce of the same 1 GiB bf16 buffer, one rank per GPU: the
+    MI355X vendor collective as a yardstick for the xGMI path (RCCL has no elastic membership, so it is not an
+    alternative for PCCL's use case). N > 1 distinct GPUs only."""
+    torch = job.torch
+    dist = job.dist
+    try:
+        g = dist.new_group(backend="nccl")
+        x = torch.randn(nbytes // 2, device=job.dev, dtype=torch.bfloat16)
+        for _ in range(max(2, a.warmup)):
+            dist.all_reduce(x, group=g)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            dist.all_reduce(x, group=g)
+        torch.cuda.synchronize()
+        dt = job.max_over_job([time.perf_counter() - t0]) / a.steps
+        dist.destroy_process_group(g)
+        n = job.world
+        return {"ranks": n, "ms_per_op": round(dt * 1e3, 4), "bus_bw_per_rank_GBps": round(_bw(nbytes, dt, n)[1], 3)}
+    except Exception as e:  # noqa: BLE001 - a yardstick: report, never fail the bench
+        return {"error": repr(e)[:300]}
 
 
 def extras_in_child(job, a):
