@@ -34,8 +34,13 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
         for _ in range(target):
             spawn()
         t_end = time.time() + duration
+        t_report = time.time() + 30
         while time.time() < t_end:
             alive = [p for p, _ in procs if p.poll() is None]
+            if soak and time.time() >= t_report:  # progress of a long soak (run pytest with -s to see it live)
+                t_report = time.time() + 30
+                print(f"[soak] {duration - (t_end - time.time()):.0f}/{duration:.0f} s: {len(alive)} alive, "
+                      f"{killed} killed, {len(procs)} spawned", flush=True)
             if soak:  # reference schedule
                 time.sleep(rng.uniform(0.5, 2.0))
                 if rng.random() < 0.4 and len(alive) > 2:
