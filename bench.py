@@ -18,8 +18,9 @@ busBW = (bytes / t) * 2 (n - 1) / n; ``extra.bus_bw_per_peer_GBps`` is the per-p
 reference tests/basic_reduce_test/main.cpp:141-143).
 
 ``extra`` also carries, measured in the same run: the xGMI/IPC path at the same peers (the library's default for
-same-host peers), 2 peers over IPC (N == 1), a busBW-vs-size sweep for both paths, small-message latencies
-(2-peer 4-element CPU all-reduce = BASELINE config 1; 1 MiB over IPC) and the peer-rejoin latency.
+same-host peers), 2 peers over IPC (N == 1), a busBW-vs-size sweep for both paths, the 1 GiB busBW at 2 / 4 / 8
+peers for both paths (``extra.peer_curve``, N == 1), small-message latencies (2-peer 4-element CPU all-reduce =
+BASELINE config 1; 1 MiB over IPC) and the peer-rejoin latency.
 
 vs_baseline is null: the reference publishes only WAN throughputs (25 / 45 Gbit/s), which are not
 comparable with a single-host loopback/HBM measurement.
@@ -54,6 +55,7 @@ def _args():
                          "(profiles/r2/ring_sweep.md, profiles/r2/tcp_loopback/)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
+    ap.add_argument("--no-peer-curve", action="store_true", help="skip the 2 / 4 peer points of the 1 GiB curve")
     ap.add_argument("--extras-child", default="", help=argparse.SUPPRESS)  # internal: run only the extras, write JSON
     return ap.parse_args()
 
@@ -85,8 +87,14 @@ class Job:
         self.first = self.rank * self.local
         self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
         self.bar = threading.Barrier(self.local)
-        if a.pool <= 0:  # connections per ring neighbour: the box's CPU share over the host's peers, in [1, 8]
-            a.pool = max(1, min(8, int(_cpu_quota()) // self.total))
+        self.auto_pool = a.pool <= 0
+        a.pool = self.pool_for(self.total)
+
+    def pool_for(self, peers: int) -> int:
+        """Connections per ring neighbour: --pool, or the box's CPU share over the host's peers, in [1, 8]."""
+        if not self.auto_pool:
+            return self.a.pool
+        return max(1, min(8, int(_cpu_quota()) // peers))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
@@ -138,7 +146,7 @@ class Job:
         def body(i):
             try:
                 self.torch.cuda.set_device(self.dev)
-                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.a.pool, **ports[i])
+                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.pool_for(total), **ports[i])
                 comms[i] = c
                 c.connect(n_attempts=30)
                 wait_for_world(c, total, timeout=300)
@@ -234,6 +242,10 @@ def _cpu_quota():
 def _bw(nbytes, t, n):
     alg = nbytes / t / 1e9
     return alg, alg * 2 * (n - 1) / n
+
+
+def _curve_point(nbytes, t, n):
+    return {"ms": round(t * 1e3, 4), "bus_bw_per_peer_GBps": round(_bw(nbytes, t, n)[1], 3)}
 
 
 def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
@@ -348,7 +360,7 @@ def run_extras(job, a, nbytes):
     sweep, 2 peers over IPC (N == 1), small-message latencies and the peer-rejoin latency."""
     import pccl_amd as pccl
     P = job.total
-    extra, sweep = {}, {}
+    extra, sweep, curve = {}, {}, {}
     if not a.no_ipc_extra:
         ipc = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
                       sweep=(1 << 20, 16 << 20, 256 << 20))
@@ -366,6 +378,20 @@ def run_extras(job, a, nbytes):
             talg, tbus = _bw(nbytes, two["t"], 2)
             extra["ipc_2_peers_1gpu"] = {"ms_per_op": round(two["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(tbus, 3),
                                          "reduce_path": pccl.ReducePath(two["path"]).name}
+            curve.setdefault("DEVICE_IPC", {})["2"] = _curve_point(nbytes, two["t"], 2)
+            curve["DEVICE_IPC"][str(P)] = _curve_point(nbytes, ipc["t"], P)
+    if job.world == 1 and not a.no_peer_curve:
+        # the metric's "2/4/8 peers": the same 1 GiB all-reduce at fewer peers (8 is the headline / ipc_same_peers)
+        for p in (2, 4):
+            if p >= P:
+                continue
+            r = measure(job, ipc=False, nbytes=nbytes, steps=max(3, a.steps // 2), warmup=1, peers=p)
+            curve.setdefault("DEVICE_RING", {})[str(p)] = _curve_point(nbytes, r["t"], p)
+            if not a.no_ipc_extra and p != 2:
+                r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p)
+                curve.setdefault("DEVICE_IPC", {})[str(p)] = _curve_point(nbytes, r["t"], p)
+    if curve:
+        extra["peer_curve"] = curve
     if job.world == 1:
         extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         r = rejoin_latency(job)
@@ -408,9 +434,12 @@ def extras_in_child(job, a):
     import tempfile
     out = os.path.join(tempfile.gettempdir(), f"pccl_bench_extras_{os.getpid()}_{job.rank}.json")
     args = [sys.executable, os.path.abspath(__file__), "--gpus", str(a.gpus), "--steps", str(a.steps), "--warmup",
-            str(a.warmup), "--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--extras-child", out]
+            str(a.warmup), "--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(0 if job.auto_pool else a.pool),
+            "--extras-child", out]
     if a.no_ipc_extra:
         args.append("--no-ipc-extra")
+    if a.no_peer_curve:
+        args.append("--no-peer-curve")
     env = dict(os.environ)
     if job.world > 1:
         env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 11)
@@ -418,7 +447,7 @@ def extras_in_child(job, a):
         # own store (hosted by rank 0's child on the new port)
         env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
     try:
-        rc = subprocess.run(args, env=env, timeout=900).returncode
+        rc = subprocess.run(args, env=env, timeout=float(os.environ.get("PCCL_BENCH_EXTRAS_TIMEOUT", "300"))).returncode
     except subprocess.TimeoutExpired:
         rc = "timeout"
     res = {}
@@ -472,6 +501,8 @@ def main():
         x_extra, x_sweep = extras_in_child(job, a)
         extra.update(x_extra)
         sweep.update(x_sweep)
+        if "peer_curve" in extra:
+            extra["peer_curve"].setdefault("DEVICE_RING", {})[str(P)] = _curve_point(nbytes, ring["t"], P)
     extra["sweep"] = sweep
 
     cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--device", default="cuda" if os.environ.get("MNIST_USE_CUDA") == "1" else "cpu")
     ap.add_argument("--max-steps", type=int, default=int(os.environ.get("MAX_STEPS", "256")))
     ap.add_argument("--min-world", type=int, default=int(os.environ.get("DONT_EXIT_BEFORE_REACHED_WORLD_SIZE", "0")))
+    ap.add_argument("--start-world", type=int, default=int(os.environ.get("PCCL_START_WORLD", "2")),
+                    help="train only once this many peers have formed the run (elastic afterwards)")
     ap.add_argument("--batch-size", type=int, default=32)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--hidden", type=int, nargs="+", default=[128])
@@ -56,7 +58,7 @@ def main():
         it += 1
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
         world_seen = max(world_seen, ws)
-        if ws < 2:
+        if ws < 2 or world_seen < a.start_world:
             time.sleep(0.05)
             continue
         comm.sync_shared_state(state)

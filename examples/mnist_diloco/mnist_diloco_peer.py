@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--outer-steps", type=int, default=10)
     ap.add_argument("--inner-steps", type=int, default=8)
     ap.add_argument("--min-world", type=int, default=0)
+    ap.add_argument("--start-world", type=int, default=int(os.environ.get("PCCL_START_WORLD", "2")),
+                    help="train only once this many peers have formed the run (elastic afterwards)")
     a = ap.parse_args()
     torch.set_num_threads(1)
     torch.manual_seed(a.rank)
@@ -48,7 +50,7 @@ def main():
         it += 1
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
         world_seen = max(world_seen, ws)
-        if ws < 2:
+        if ws < 2 or world_seen < a.start_world:
             time.sleep(0.05)
             continue
         info = comm.sync_shared_state(state)

@@ -7,6 +7,7 @@ the bench and the smoke check can run side by side on one host.
 from __future__ import annotations
 
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -16,6 +17,9 @@ from contextlib import contextmanager
 from typing import Callable, Dict, Iterator, List, Optional, Sequence
 
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# sent to peers that overran their deadline before they are killed: every thread's native backtrace on stderr
+# (spawn_python turns on PCCL_DEBUG_BACKTRACE_SIGNAL)
+DIAG_SIGNALS = (signal.SIGUSR2,)
 
 
 def free_port(host: str = "127.0.0.1") -> int:
@@ -124,6 +128,48 @@ def spawn_python(args: Sequence[str], env: Optional[Dict[str, str]] = None, **kw
     e = dict(os.environ)
     e["PYTHONPATH"] = REPO_ROOT + os.pathsep + e.get("PYTHONPATH", "")
     e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    e.setdefault("PCCL_DEBUG_BACKTRACE_SIGNAL", "1")
     if env:
         e.update(env)
     return subprocess.Popen([sys.executable, *args], env=e, **kw)
+
+
+def communicate_all(procs: Sequence[subprocess.Popen], timeout: float,
+                    diag_signals: Sequence[int] = ()) -> List[tuple]:
+    """``communicate()`` on every process at once: each one's pipes are drained by its own thread, so a peer that
+    writes more than a pipe buffer while another is being waited on cannot block (and stall the collective that the
+    waited-on peer is in). On timeout the live processes get ``diag_signals`` (e.g. SIGUSR1 for a faulthandler
+    dump, SIGUSR2 for PCCL_DEBUG_BACKTRACE_SIGNAL), then SIGKILL, and ``TimeoutError`` is raised with every
+    process's output tail in its message."""
+    outs: List[Optional[tuple]] = [None] * len(procs)
+
+    def drain(k: int):
+        outs[k] = procs[k].communicate()
+
+    threads = [threading.Thread(target=drain, args=(k,), daemon=True) for k in range(len(procs))]
+    for t in threads:
+        t.start()
+    deadline = time.time() + timeout
+    for t in threads:
+        t.join(timeout=max(0.0, deadline - time.time()))
+    if any(t.is_alive() for t in threads):
+        for sig in diag_signals:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        p.send_signal(sig)
+                    except OSError:
+                        pass
+            time.sleep(2.0)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for t in threads:
+            t.join(timeout=30)
+        tails = []
+        for k, o in enumerate(outs):
+            o = o or ("", "")
+            tails.append(f"--- process {k} (rc {procs[k].returncode}) stdout:\n{str(o[0])[-3000:]}\n"
+                         f"--- stderr:\n{str(o[1])[-6000:]}")
+        raise TimeoutError(f"processes did not finish within {timeout} s\n" + "\n".join(tails))
+    return [o if o is not None else ("", "") for o in outs]

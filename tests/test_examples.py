@@ -7,7 +7,7 @@ import sys
 
 import pytest
 
-from pccl_amd.utils import local_master, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EX = os.path.join(ROOT, "examples", "nanogpt")
@@ -21,7 +21,7 @@ def _run(script, extra, device="cpu", world=2, timeout=300):
                               env={"OMP_NUM_THREADS": "2"}, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for _ in range(world)]
         try:
-            outs = [p.communicate(timeout=timeout) for p in procs]
+            outs = communicate_all(procs, timeout, DIAG_SIGNALS)
         finally:
             for p in procs:
                 if p.poll() is None:
@@ -76,7 +76,7 @@ def test_diloco_fsdp_two_nodes():
                               stderr=subprocess.PIPE, text=True)
                  for k in range(2)]
         try:
-            outs = [p.communicate(timeout=300) for p in nodes]
+            outs = communicate_all(nodes, 300, DIAG_SIGNALS)
         finally:
             for p in nodes:
                 if p.poll() is None:

@@ -11,7 +11,7 @@ import time
 
 import pytest
 
-from pccl_amd.utils import local_master, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "workers", "allreduce_peer.py")
@@ -37,7 +37,7 @@ def test_peer_crash_survivors_continue(n):
     with local_master() as addr:
         ps = [_spawn(addr, 3, r, "--const", "--n", str(n), "--steps", "40", "--step-sleep", "0.01",
                      *(["--die-at", "10"] if r == 1 else [])) for r in range(3)]
-        outs = [p.communicate(timeout=240) for p in ps]
+        outs = communicate_all(ps, 240, DIAG_SIGNALS)
     assert ps[1].returncode == 17
     for r in (0, 2):
         assert ps[r].returncode == 0, outs[r][1][-3000:]
@@ -55,9 +55,9 @@ def test_crash_and_rejoin():
         while ps[2].poll() is None and time.time() < deadline:
             time.sleep(0.1)
         assert ps[2].returncode == 17
-        joiner = _spawn(addr, 3, 3, "--const", "--n", "4096", "--steps", "20", "--no-wait")
-        jo, je = joiner.communicate(timeout=240)
-        outs = [p.communicate(timeout=240) for p in ps[:2]]
+        joiner = _spawn(addr, 3, 3, "--const", "--n", "4096", "--steps", "20", "--no-wait", "--leave-when-alone")
+        (jo, je), = communicate_all([joiner], 150, DIAG_SIGNALS)
+        outs = communicate_all(ps[:2], 240, DIAG_SIGNALS)
     assert joiner.returncode == 0, je[-3000:]
     jl = _check_ok(_lines(jo))
     assert all(ln["world"] == 3 for ln in jl)
@@ -95,7 +95,7 @@ def test_gpu_peer_crash_survivors_continue(hip):
     with local_master() as addr:
         ps = [_spawn(addr, 3, r, "--const", "--n", str(1 << 22), "--dtype", "bf16", "--steps", "30",
                      *(["--die-at", "8"] if r == 0 else []), device="cuda:0") for r in range(3)]
-        outs = [p.communicate(timeout=300) for p in ps]
+        outs = communicate_all(ps, 300, DIAG_SIGNALS)
     assert ps[0].returncode == 17
     for r in (1, 2):
         assert ps[r].returncode == 0, outs[r][1][-3000:]
@@ -157,7 +157,7 @@ def test_gpu_shared_state_distributor_sigkill_mid_handoff(hip, shareable):
         time.sleep(1.0)
         j = spawn_python([worker, addr, "join", *extra], env={"PCCL_SS_COPY_DELAY_MS": "1000"},
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-        outs = [p.communicate(timeout=180) for p in ds + [j]]
+        outs = communicate_all(ds + [j], 180, DIAG_SIGNALS)
     rcs = [p.returncode for p in ds + [j]]
     assert sorted(rcs[:2]) == [-9, 0], (rcs, [o[1][-2000:] for o in outs])
     assert rcs[2] == 0, outs[2][1][-3000:]
@@ -182,7 +182,7 @@ def test_gpu_shared_state_many_tensors_packed_handoff(hip):
               for _ in range(2)]
         time.sleep(1.0)
         j = spawn_python([worker, addr, "join", *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-        outs = [p.communicate(timeout=180) for p in ds + [j]]
+        outs = communicate_all(ds + [j], 180, DIAG_SIGNALS)
     assert [p.returncode for p in ds + [j]] == [0, 0, 0], [o[1][-2000:] for o in outs]
     sync = next(x for x in _lines(outs[2][0]) if x["phase"] == "sync")
     assert sync["lo"] == sync["hi"] == 7.0 and sync["extra_ok"] and sync["revision"] == 5, sync

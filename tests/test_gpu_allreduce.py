@@ -11,7 +11,7 @@ import pytest
 import torch
 
 import pccl_amd as pccl
-from pccl_amd.utils import local_master, run_threaded_peers, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, run_threaded_peers, spawn_python
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -180,7 +180,7 @@ def test_two_process_ipc(hip, mode, ipc_mode):
                                str((1 << 24) + 1), "--dtype", "bf16", "--device", "cuda:0", "--steps", "3",
                                *extra(r)], env={"PCCL_IPC_MODE": ipc_mode},
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
-        outs = [p.communicate(timeout=240) for p in procs]
+        outs = communicate_all(procs, 240, DIAG_SIGNALS)
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
         lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
@@ -209,7 +209,7 @@ def test_two_process_ipc_large(hip, gib):
                                "--dtype", "bf16", "--device", "cuda:0", "--steps", "2",
                                *(["--inplace"] if r == 1 else [])],
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
-        outs = [p.communicate(timeout=200) for p in procs]
+        outs = communicate_all(procs, 200, DIAG_SIGNALS)
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
         lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]

@@ -13,7 +13,7 @@ import subprocess
 import pytest
 
 import pccl_amd as pccl
-from pccl_amd.utils import local_master, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "workers", "allreduce_peer.py")
@@ -28,7 +28,7 @@ def _run(hosts, per_host, device, extra=(), n=(1 << 20) + 37, dtype="f32", steps
                     "--steps", str(steps), *extra, *(per_rank(r) if per_rank else [])]
             procs.append(spawn_python(args, env={"PCCL_HOST_TOKEN": f"simhost{r // per_host}"},
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
-        outs = [p.communicate(timeout=300) for p in procs]
+        outs = communicate_all(procs, 300, DIAG_SIGNALS)
     res = []
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
@@ -98,7 +98,7 @@ def test_peer_crash_with_host_layout(device, request):
                     "--steps", "12", "--const", *(["--die-at", "4"] if r == 3 else [])]
             procs.append(spawn_python(args, env={"PCCL_HOST_TOKEN": f"simhost{r // 2}"},
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
-        outs = [p.communicate(timeout=300) for p in procs]
+        outs = communicate_all(procs, 300, DIAG_SIGNALS)
     assert procs[3].returncode == 17
     for r in range(3):
         assert procs[r].returncode == 0, outs[r][1][-3000:]

@@ -8,17 +8,19 @@ import time
 
 import pytest
 
-from pccl_amd.utils import local_master, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PEER = os.path.join(ROOT, "examples", "mnist_ddp", "mnist_peer.py")
 
 
-def _run(world, device="cpu", steps=60, late_joiner=False, timeout=300):
+def _run(world, device="cpu", steps=60, late_joiner=False, timeout=150):
     with local_master() as addr:
         procs = []
         n0 = world - 1 if late_joiner else world
-        extra = ["--min-world", str(world)] if late_joiner else []
+        # a late joiner arrives mid-run; otherwise every peer waits for the whole world before training (no peer
+        # may finish the run before the last one has even registered)
+        extra = ["--min-world", str(world)] if late_joiner else ["--start-world", str(world)]
         for r in range(n0):
             procs.append(spawn_python([PEER, "--master", addr, "--rank", str(r), "--device", device, "--max-steps",
                                        str(steps), *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
@@ -29,10 +31,8 @@ def _run(world, device="cpu", steps=60, late_joiner=False, timeout=300):
             procs.append(spawn_python([PEER, "--master", addr, "--rank", str(world - 1), "--device", device,
                                        "--max-steps", str(steps)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True))
-        outs = []
         try:
-            for p in procs:
-                outs.append(p.communicate(timeout=timeout))
+            outs = communicate_all(procs, timeout, DIAG_SIGNALS)
         finally:
             for p in procs:
                 if p.poll() is None:
@@ -80,7 +80,9 @@ def _run_diloco(world, device="cpu", late_joiner=False):
     with local_master() as addr:
         procs = []
         n0 = world - 1 if late_joiner else world
-        extra = ["--min-world", str(world)] if late_joiner else []
+        # a late joiner arrives mid-run; otherwise every peer waits for the whole world before training (no peer
+        # may finish the run before the last one has even registered)
+        extra = ["--min-world", str(world)] if late_joiner else ["--start-world", str(world)]
         for r in range(n0):
             procs.append(spawn_python([DILOCO_PEER, "--master", addr, "--rank", str(r), "--device", device, *extra],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -89,7 +91,7 @@ def _run_diloco(world, device="cpu", late_joiner=False):
             procs.append(spawn_python([DILOCO_PEER, "--master", addr, "--rank", str(world - 1), "--device", device],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
         try:
-            outs = [p.communicate(timeout=300) for p in procs]
+            outs = communicate_all(procs, 300, DIAG_SIGNALS)
         finally:
             for p in procs:
                 if p.poll() is None:

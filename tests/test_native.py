@@ -8,7 +8,7 @@ import sys
 
 import pytest
 
-from pccl_amd.utils import free_port
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "build")
@@ -40,7 +40,7 @@ def test_c_api_peers_with_standalone_master(world, num_ops, n, pool, inflight):
         assert "listening" in m.stdout.readline()
         peers = [subprocess.Popen([peer, str(port), str(world), "3", str(num_ops), str(n), str(pool), str(inflight)],
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(world)]
-        outs = [p.communicate(timeout=180) for p in peers]
+        outs = communicate_all(peers, 180, DIAG_SIGNALS)
         for p, (o, e) in zip(peers, outs):
             assert p.returncode == 0, e[-2000:]
             steps = [json.loads(x) for x in o.splitlines() if x.startswith("{")]

@@ -10,7 +10,7 @@ import textwrap
 
 import pytest
 
-from pccl_amd.utils import local_master, spawn_python
+from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
 
 PEER = textwrap.dedent(r"""
     import json, sys, time
@@ -38,7 +38,7 @@ def _timed(world, quant, pool, wan="10:400"):
         ps = [spawn_python(["-c", PEER, addr, str(world), quant, str(pool)],
                            env={"PCCL_SIM_WAN": wan, "OMP_NUM_THREADS": "1", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)},
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(world)]
-        outs = [p.communicate(timeout=300) for p in ps]
+        outs = communicate_all(ps, 300, DIAG_SIGNALS)
     res = []
     for p, (o, e) in zip(ps, outs):
         assert p.returncode == 0, e[-2000:]

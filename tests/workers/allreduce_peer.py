@@ -2,7 +2,7 @@
 
 usage: allreduce_peer.py MASTER WORLD RANK [--n N] [--dtype f32|bf16|f16|i32] [--device cpu|cuda:0] [--steps K]
                          [--die-at STEP] [--const] [--no-wait] [--inplace] [--op sum|avg|max] [--quant none|u8]
-                         [--shareable]
+                         [--shareable] [--leave-when-alone]
 Each step all-reduces a tensor and checks the result; prints one JSON line per attempt.
   default: x = rank + 1 + step, tag = step (all peers start together)
   --const: x = 1, tag 0, result must equal the op's world size (membership may change between steps)
@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--reuse", action="store_true", help="allocate x / y once (back-to-back ops, no refill)")
     ap.add_argument("--duration", type=float, default=0.0, help="run steps until this many seconds passed instead")
     ap.add_argument("--shareable", action="store_true", help="allocate x / y in fd-shareable memory (pccl_amd.memory)")
+    ap.add_argument("--leave-when-alone", action="store_true",
+                    help="exit 0 once every other peer has left after this one completed a step (a joiner whose "
+                         "partners finished their run first cannot complete more steps)")
     a = ap.parse_args()
     op = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[a.op]
     qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant == "u8" \
@@ -65,6 +68,8 @@ def main():
         it += 1
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
         if ws < 2:
+            if a.leave_when_alone and step > 0:
+                break
             time.sleep(0.05)
             continue
         val = 1.0 if a.const else float(a.rank + 1 + step)
