@@ -18,7 +18,7 @@ step() { # name timeout cmd...
 }
 S=${STEPS:-smoke,pytest,bench,prof,benchmarks}
 [[ $S == *smoke* ]] && step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
-[[ $S == *pytest* ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -rf
+[[ $S == *pytest* ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 170 --timeout-method thread -rf
 [[ $S == *bench* ]] && step bench 600 python -u bench.py --steps 10 --warmup 3
 if [[ $S == *prof* ]]; then
   (cd /tmp && export TMPDIR=/tmp && step_name=prof && \
