@@ -88,13 +88,8 @@ class Job:
         self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
         self.bar = threading.Barrier(self.local)
         self.auto_pool = a.pool <= 0
-        a.pool = self.pool_for(self.total)
-
-    def pool_for(self, peers: int) -> int:
-        """Connections per ring neighbour: --pool, or the box's CPU share over the host's peers, in [1, 8]."""
-        if not self.auto_pool:
-            return self.a.pool
-        return max(1, min(8, int(_cpu_quota()) // peers))
+        if self.auto_pool:  # connections per ring neighbour: the box's CPU share over the job's peers, in [1, 8]
+            a.pool = max(1, min(8, int(_cpu_quota()) // self.total))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
@@ -146,7 +141,7 @@ class Job:
         def body(i):
             try:
                 self.torch.cuda.set_device(self.dev)
-                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.pool_for(total), **ports[i])
+                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.a.pool, **ports[i])
                 comms[i] = c
                 c.connect(n_attempts=30)
                 wait_for_world(c, total, timeout=300)
