@@ -78,14 +78,16 @@ class Job:
             import torch.distributed as dist
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
             self.dist = dist
-        self.gpu = 0 if same_gpu else local_rank
+        ndev = max(1, torch.cuda.device_count())
+        # one GPU per rank; with fewer GPUs than ranks the ranks share them round-robin (labelled by distinct devices)
+        self.gpu = 0 if same_gpu else local_rank % ndev
         torch.cuda.set_device(self.gpu)
         self.dev = torch.device("cuda", self.gpu)
         self.total = max(a.peers, self.world)
         self.total += (-self.total) % self.world  # equal peers per process
         self.local = self.total // self.world
         self.first = self.rank * self.local
-        self.n_gpus = 1 if (same_gpu or self.world == 1) else self.world
+        self.n_gpus = 1 if same_gpu else min(self.world, ndev)
         self.bar = threading.Barrier(self.local)
         self.auto_pool = a.pool <= 0
         if self.auto_pool:  # connections per ring neighbour: the box's CPU share over the job's peers, in [1, 8]
