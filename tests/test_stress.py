@@ -24,7 +24,7 @@ PEER = os.path.join(HERE, "workers", "stress_peer.py")
 def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
     rng = random.Random(1234)
     stop = tmp_path / "stop"
-    procs, killed = [], 0
+    procs, killed, signalled = [], 0, set()
     with local_master() as addr:
         def spawn():
             # stdout to a file: a long soak must never block a peer on a full pipe
@@ -36,7 +36,8 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
         t_end = time.time() + duration
         t_report = time.time() + 30
         while time.time() < t_end:
-            alive = [p for p, _ in procs if p.poll() is None]
+            # a SIGKILLed GPU process can take a while to exit: never pick (or count) it twice
+            alive = [p for p, _ in procs if p.poll() is None and p.pid not in signalled]
             if soak and time.time() >= t_report:  # progress of a long soak (run pytest with -s to see it live)
                 t_report = time.time() + 30
                 print(f"[soak] {duration - (t_end - time.time()):.0f}/{duration:.0f} s: {len(alive)} alive, "
@@ -44,7 +45,9 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
             if soak:  # reference schedule
                 time.sleep(rng.uniform(0.5, 2.0))
                 if rng.random() < 0.4 and len(alive) > 2:
-                    rng.choice(alive).send_signal(signal.SIGKILL)
+                    victim = rng.choice(alive)
+                    victim.send_signal(signal.SIGKILL)
+                    signalled.add(victim.pid)
                     killed += 1
                 if rng.random() < 0.6 and len(alive) < 2 * target:
                     spawn()
@@ -53,8 +56,9 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
             if len(alive) > 2:
                 victim = rng.choice(alive)
                 victim.send_signal(signal.SIGKILL)
+                signalled.add(victim.pid)
                 killed += 1
-            if len([p for p, _ in procs if p.poll() is None]) < target:
+            if len([p for p, _ in procs if p.poll() is None and p.pid not in signalled]) < target:
                 spawn()
         stop.write_text("1")
         for p, out in procs:
