@@ -149,3 +149,37 @@ def test_shareable_memory_api_on_cpu():
     assert pccl.memory.live_bytes() >= 0
     if not torch.cuda.is_available():
         assert not pccl.memory.available()
+
+
+def test_communicate_all_drains_every_pipe_concurrently():
+    """A process blocked on a full stdout pipe must not stall the wait for another one (the sequential
+    ``communicate()`` pattern deadlocks when the process waited on first needs the other one to progress)."""
+    import subprocess
+    import sys
+
+    from pccl_amd.utils import communicate_all
+    big = "import sys; sys.stdout.write('x' * (1 << 20)); sys.stdout.flush()"
+    # the first process only exits once the second has written its megabyte (the file appears after the write)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        flag = f"{d}/done"
+        waiter = ("import os, time\nwhile not os.path.exists(%r): time.sleep(0.01)\nprint('ok')" % flag)
+        writer = big + "; open(%r, 'w').close()" % flag
+        ps = [subprocess.Popen([sys.executable, "-c", c], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for c in (waiter, writer)]
+        outs = communicate_all(ps, 60)
+    assert outs[0][0].strip() == "ok" and len(outs[1][0]) == 1 << 20
+
+
+def test_communicate_all_deadline_reports_output():
+    import subprocess
+    import sys
+
+    import pytest
+
+    from pccl_amd.utils import communicate_all
+    p = subprocess.Popen([sys.executable, "-c", "import time; print('started', flush=True); time.sleep(60)"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    with pytest.raises(TimeoutError, match="started"):
+        communicate_all([p], 2.0)
+    assert p.poll() is not None
