@@ -462,6 +462,11 @@ def extras_in_child(job, a):
 
 def main():
     a = _args()
+    # stdout carries exactly one line, the result JSON: everything else any library, child process or the gloo
+    # rendezvous writes to fd 1 goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if os.environ.get("PCCL_BENCH_WATCHDOG"):  # periodic Python stacks of every thread (hang diagnosis)
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["PCCL_BENCH_WATCHDOG"]), repeat=True)
@@ -517,7 +522,7 @@ def main():
         "extra": extra,
     }
     if job.rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if job.dist is not None:
         job.dist.barrier()
         job.dist.destroy_process_group()
