@@ -51,8 +51,9 @@ def _args():
     ap.add_argument("--mib", type=int, default=1024, help="buffer per peer in MiB (config: 1024)")
     ap.add_argument("--pool", type=int, default=0,
                     help="P2P connections per ring neighbour (ring stripes); 0 = CPUs available / peers on the host, "
-                         "in [1, 8]: on the 16-CPU MI355X box 8 peers x 2 stripes measured fastest "
-                         "(profiles/r2/ring_sweep.md, profiles/r2/tcp_loopback/)")
+                         "in [1, 4]: on the 16-CPU MI355X box 8 peers x 2 stripes measured fastest, and 8 stripes "
+                         "per peer were slower than 2 even with 8 CPUs per peer (profiles/r2/ring_sweep.md, "
+                         "profiles/r2/tcp_loopback/, profiles/r2/pool_probe/)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     ap.add_argument("--no-peer-curve", action="store_true", help="skip the 2 / 4 peer points of the 1 GiB curve")
@@ -90,8 +91,8 @@ class Job:
         self.n_gpus = 1 if same_gpu else min(self.world, ndev)
         self.bar = threading.Barrier(self.local)
         self.auto_pool = a.pool <= 0
-        if self.auto_pool:  # connections per ring neighbour: the box's CPU share over the job's peers, in [1, 8]
-            a.pool = max(1, min(8, int(_cpu_quota()) // self.total))
+        if self.auto_pool:  # connections per ring neighbour: the box's CPU share over the job's peers, in [1, 4]
+            a.pool = max(1, min(4, int(_cpu_quota()) // self.total))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
