@@ -12,8 +12,9 @@ The total work (8 x 1 GiB) is fixed as N grows, so ``scaling`` is "strong".
 
 Headline (``value``): the TCP device ring (PCCL_DISABLE_IPC=1 — peers do not short-circuit to xGMI): every ring step
 stages HBM -> pinned host (hipMemcpyAsync), sends over loopback TCP and reduces the received bytes into HBM with the
-HIP reduce kernel. ``value`` is the whole-job aggregate bus bandwidth = sum over the peers of the nccl-tests busBW,
-busBW = (bytes / t) * 2 (n - 1) / n; ``extra.bus_bw_per_peer_GBps`` is the per-peer busBW and
+HIP reduce kernel. ``value`` is the per-peer nccl-tests bus bandwidth, busBW = (bytes / t) * 2 (n - 1) / n, of the
+first timed window; ``extra.aggregate_bus_bw_GBps`` is its sum over the peers, ``extra.windows_ms`` the ms per op of
+``--windows`` timed windows (min / median next to it), ``extra.op_ms_rank0`` the per-op spread, and
 ``extra.ref_metric_rx_plus_tx_per_peer_GBps`` the reference's own metric ((rx + tx) / t per peer,
 reference tests/basic_reduce_test/main.cpp:141-143).
 
@@ -50,10 +51,12 @@ def _args():
     ap.add_argument("--peers", type=int, default=8, help="total peers of the job (config: 8)")
     ap.add_argument("--mib", type=int, default=1024, help="buffer per peer in MiB (config: 1024)")
     ap.add_argument("--pool", type=int, default=0,
-                    help="P2P connections per ring neighbour (ring stripes); 0 = CPUs available / peers on the host, "
-                         "in [1, 4]: on the 16-CPU MI355X box 8 peers x 2 stripes measured fastest, and 8 stripes "
-                         "per peer were slower than 2 even with 8 CPUs per peer (profiles/r2/ring_sweep.md, "
-                         "profiles/r2/tcp_loopback/, profiles/r2/pool_probe/)")
+                    help="P2P connections per ring neighbour (ring stripes); 0 = per phase, CPUs available / peers in "
+                         "this process, in [1, 8]: on the 16-CPU MI355X box 8 peers x 2, 4 peers x 4 and 2 peers x 8 "
+                         "stripes measured fastest with the send-ahead ring (profiles/r3/ring_ab/)")
+    ap.add_argument("--windows", type=int, default=3,
+                    help="timed windows of --steps ops for the headline (the first is the reported one; all of them "
+                         "give extra.windows_ms min / median)")
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     ap.add_argument("--no-peer-curve", action="store_true", help="skip the 2 / 4 peer points of the 1 GiB curve")
@@ -91,8 +94,12 @@ class Job:
         self.n_gpus = 1 if same_gpu else min(self.world, ndev)
         self.bar = threading.Barrier(self.local)
         self.auto_pool = a.pool <= 0
-        if self.auto_pool:  # connections per ring neighbour: the box's CPU share over the job's peers, in [1, 4]
-            a.pool = max(1, min(4, int(_cpu_quota()) // self.total))
+
+    def pool_for(self, local_peers: int) -> int:
+        """Connections per ring neighbour for a phase with `local_peers` peer threads in this process."""
+        if not self.auto_pool:
+            return self.a.pool
+        return max(1, min(8 if self.world == 1 else 4, int(_cpu_quota()) // max(1, local_peers)))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
@@ -140,11 +147,15 @@ class Job:
         comms = [None] * local
         bar = threading.Barrier(local)
         self.bar = bar
+        # the xGMI path moves no data over the TCP pool: keep it small there (8 connections per neighbour measured
+        # 0.88 -> 1.25 ms for 2 peers x 1 GiB over IPC, setup and vote traffic only)
+        pool = min(2, self.pool_for(local)) if ipc else self.pool_for(local)
+        self.phase_pool = pool
 
         def body(i):
             try:
                 self.torch.cuda.set_device(self.dev)
-                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=self.a.pool, **ports[i])
+                c = pccl.Communicator(addr, 0, p2p_connection_pool_size=pool, **ports[i])
                 comms[i] = c
                 c.connect(n_attempts=30)
                 wait_for_world(c, total, timeout=300)
@@ -177,8 +188,9 @@ class Job:
         return out
 
 
-def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
-    """warmup + `steps` timed all-reduces between job-wide barriers; returns (seconds, tx, rx, path)."""
+def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None):
+    """warmup + `steps` timed all-reduces between job-wide barriers; returns (seconds, tx, rx, path, cpu seconds).
+    `ops` (optional list) receives the wall time of every timed op as seen by this peer."""
     import pccl_amd as pccl
     torch = job.torch
     for s in range(warmup):
@@ -191,11 +203,15 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
                     raise
     torch.cuda.synchronize()
     job.sync(i)
+    tc0 = _task_cpu() if i == 0 and tag0 == 0 else None  # the phase's main window only
     t0 = time.perf_counter()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     tx = rx = 0
     for s in range(steps):
+        ta = time.perf_counter()
         info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + warmup + s)
+        if ops is not None:
+            ops.append(time.perf_counter() - ta)
         tx += info.tx_bytes
         rx += info.rx_bytes
     torch.cuda.synchronize()
@@ -205,7 +221,46 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0):
     # CPU seconds of the whole process (every peer thread of this rank) over the timed ops: the loopback-TCP ring is
     # CPU work (kernel socket copies), so cpu_s / dt shows how many cores it kept busy
     cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    if tc0 is not None:
+        job.cpu_by_thread = _cpu_by_thread(tc0, _task_cpu(), cpu, dt)
     return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), cpu
+
+
+def _task_cpu():
+    """{tid: (thread name, user s, sys s)} of this process's live threads (Linux /proc)."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return out
+    for t in tids:
+        try:
+            with open(f"/proc/self/task/{t}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        out[t] = (name, int(f[11]) / tick, int(f[12]) / tick)
+    return out
+
+
+def _cpu_by_thread(before, after, total_cpu, wall):
+    """Cores kept busy per thread name over a window: live threads' deltas grouped by name (pccl threads are named by
+    libpccl: pccl-mux-rx = socket receives, pccl-stripe-tx = ring sends, pccl-op = op threads, ...); threads that
+    exited inside the window (per-op sender threads) only show in the remainder ``exited_or_unnamed``."""
+    agg = {}
+    for tid, (name, u, s) in after.items():
+        u0, s0 = before.get(tid, (name, 0.0, 0.0))[1:]
+        key = name if name.startswith("pccl") else "other"
+        a = agg.setdefault(key, [0.0, 0.0])
+        a[0] += u - u0
+        a[1] += s - s0
+    seen = sum(u + s for u, s in agg.values())
+    res = {k: {"user_cores": round(u / wall, 2), "sys_cores": round(s / wall, 2)} for k, (u, s) in sorted(agg.items())}
+    res["exited_threads_cores"] = round(max(0.0, total_cpu - seen) / wall, 2)
+    return res
 
 
 def _check(job, i, comm, x, y, peers):
@@ -246,8 +301,9 @@ def _curve_point(nbytes, t, n):
     return {"ms": round(t * 1e3, 4), "bus_bw_per_peer_GBps": round(_bw(nbytes, t, n)[1], 3)}
 
 
-def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
-    """Runs one phase; returns {"t": s/op (max over the job), "tx", "rx", "path", "sweep": {bytes: s/op}, "ok"}."""
+def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, windows=1):
+    """Runs one phase; returns {"t": s/op (max over the job), "tx", "rx", "path", "sweep": {bytes: s/op}, "ok",
+    "windows": [s/op of each timed window (the first is "t")], "op_ms": per-op wall times of peer 0 in window 1}."""
     torch = job.torch
     total = peers or job.total
 
@@ -262,7 +318,12 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
         with pccl.memory.maybe_shareable(job.dev) if ipc else contextlib.nullcontext():
             x = torch.randn(n, device=job.dev, dtype=torch.bfloat16, generator=g)
             y = torch.empty_like(x)
-        r = {"main": _timed(job, i, comm, x, y, steps, warmup)}
+        ops = []
+        r = {"main": _timed(job, i, comm, x, y, steps, warmup, ops=ops), "ops": ops, "win": []}
+        tag = 5_000
+        for _w in range(1, windows):  # further windows of the same ops (the first one is the reported value)
+            r["win"].append(_timed(job, i, comm, x, y, steps, 0, tag0=tag)[0])
+            tag += steps + 10
         tag = 10_000
         for b in sweep:
             m = b // 2
@@ -278,7 +339,9 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False):
     dt = job.max_over_job([r["main"][0] for r in res])
     _log(f"  done: {dt / steps * 1e3:.3f} ms/op")
     out = {"t": dt / steps, "tx": res[0]["main"][1] / steps, "rx": res[0]["main"][2] / steps,
-           "path": res[0]["main"][3], "sweep": {}, "cpu_cores": res[0]["main"][4] / max(dt, 1e-9)}
+           "path": res[0]["main"][3], "sweep": {}, "cpu_cores": res[0]["main"][4] / max(dt, 1e-9),
+           "op_ms": [round(v * 1e3, 2) for v in res[0]["ops"]], "pool": job.phase_pool}
+    out["windows"] = [out["t"]] + [job.max_over_job([r["win"][w] for r in res]) / steps for w in range(windows - 1)]
     for b in sweep:
         out["sweep"][b] = job.max_over_job([r[b] for r in res])
     if check:
@@ -327,7 +390,7 @@ def rejoin_latency(job):
         joiner = None
         if i == 0:
             def join():
-                c = pccl.Communicator(job.addr, 0, p2p_connection_pool_size=job.a.pool)
+                c = pccl.Communicator(job.addr, 0, p2p_connection_pool_size=job.phase_pool)
                 t0 = time.perf_counter()
                 c.connect(n_attempts=30)
                 yy = torch.empty_like(small)
@@ -383,7 +446,7 @@ def run_extras(job, a, nbytes):
         for p in (2, 4):
             if p >= P:
                 continue
-            r = measure(job, ipc=False, nbytes=nbytes, steps=max(3, a.steps // 2), warmup=1, peers=p)
+            r = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p)
             curve.setdefault("DEVICE_RING", {})[str(p)] = _curve_point(nbytes, r["t"], p)
             if not a.no_ipc_extra and p != 2:
                 r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p)
@@ -487,14 +550,21 @@ def main():
 
     # ---- headline: TCP device ring, P peers x 1 GiB bf16
     ring = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=not a.quick,
-                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20))
+                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20), windows=max(1, a.windows))
     import pccl_amd as pccl
     alg, bus = _bw(nbytes, ring["t"], P)
     path_name = pccl.ReducePath(ring["path"]).name
-    extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "alg_bw_GBps": round(alg, 3),
+    wins = sorted(ring["windows"])
+    ops = sorted(ring["op_ms"])
+    extra.update({"bus_bw_per_peer_GBps": round(bus, 3), "aggregate_bus_bw_GBps": round(bus * P, 3),
+                  "alg_bw_GBps": round(alg, 3),
+                  "windows_ms": [round(w * 1e3, 2) for w in ring["windows"]],
+                  "windows_ms_min": round(wins[0] * 1e3, 2), "windows_ms_median": round(statistics.median(wins) * 1e3, 2),
+                  "op_ms_rank0": {"min": ops[0], "median": round(statistics.median(ops), 2), "max": ops[-1]},
                   "ref_metric_rx_plus_tx_per_peer_GBps": round((ring["tx"] + ring["rx"]) / ring["t"] / 1e9, 3),
-                  "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": a.pool,
+                  "reduce_path": path_name, "peers_per_gpu": job.local, "p2p_connections_per_neighbour": ring["pool"],
                   "cpu_cores_busy_rank0": round(ring["cpu_cores"], 2), "cpus_available": _cpu_quota(),
+                  "cpu_by_thread_rank0": getattr(job, "cpu_by_thread", None),
                   "result_exact": ring.get("ok")})
     sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
                                                     "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
@@ -511,8 +581,8 @@ def main():
     cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "
                  f"{'loopback TCP device ring' if path_name == 'DEVICE_RING' else path_name}")
     line = {
-        "metric": METRIC, "value": round(bus * P, 3),
-        "unit": "GB/s (job aggregate: sum over peers of per-peer busBW)",
+        "metric": METRIC, "value": round(bus, 3),
+        "unit": "GB/s (per-peer nccl-tests busBW of the 1 GiB all-reduce; job aggregate in extra)",
         "n_gpus": job.n_gpus, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ring["t"] * 1e3, 4),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (torch.randn bf16 on device)",

@@ -99,7 +99,10 @@ void OpWorkers::submit(std::function<void()> fn) {
     std::lock_guard l(m_);
     q_.push_back(std::move(fn));
     if (q_.size() > idle_ && threads_.size() < max_workers()) {
-        threads_.emplace_back([this] { loop(); });
+        threads_.emplace_back([this] {
+            name_thread("pccl-op");
+            loop();
+        });
     } else {
         cv_.notify_one();
     }
@@ -754,9 +757,10 @@ struct Staged {
 };
 
 // Readiness of one ring step's payload, shared between the op thread that produces it (staging copies, the fused
-// reduce, received bytes) and the connections' sender threads that send it, possibly while it is still being
-// produced (send-ahead). Ranges of one stripe are added in order and their events are recorded on one in-order stream,
-// so once the range holding byte end-1 is complete, every earlier byte of that stripe is readable.
+// reduce, received bytes) and the connections' sender threads that send it while it is still being produced
+// (send-ahead). A range is readable once its event (nullptr: none) has completed. Ranges arrive in any order across
+// the producer's stripes, and the sender's stripe plan need not match the producer's (neighbours may run different
+// connection pool sizes), so a wait covers the whole byte range it sends.
 struct ReadyRanges {
     std::mutex m;
     std::vector<Staged> v;
@@ -768,23 +772,36 @@ struct ReadyRanges {
         std::lock_guard l(m);
         v.push_back({a, b, e});
     }
-    // blocks until byte end-1 is readable; false if `cancel` became non-zero first
-    bool wait(size_t end, DeviceBackend *be, const std::atomic<int> &cancel) {
-        if (end == 0) return true;
+    // blocks until every byte of [begin, end) is readable; false if `cancel` became non-zero first
+    bool wait(size_t begin, size_t end, DeviceBackend *be, const std::atomic<int> &cancel) {
+        if (end <= begin) return true;
         unsigned us = 2;
+        std::vector<std::pair<size_t, size_t>> iv;
+        std::vector<DevEvent> evs;
         while (true) {
-            bool found = false;
-            DevEvent e = nullptr;
+            bool covered = false;
             {
                 std::lock_guard l(m);
+                iv.clear();
+                evs.clear();
                 for (const auto &r : v)
-                    if (r.a <= end - 1 && end - 1 < r.b) {
-                        found = true;
-                        e = r.e;
-                        break;
+                    if (r.b > begin && r.a < end) {
+                        iv.emplace_back(r.a, r.b);
+                        if (r.e) evs.push_back(r.e);
                     }
+                std::sort(iv.begin(), iv.end());
+                size_t cur = begin;
+                for (const auto &[a, b] : iv) {
+                    if (a > cur) break;
+                    cur = std::max(cur, b);
+                }
+                covered = cur >= end;
             }
-            if (found) return e == nullptr || event_wait_polling(be, e);
+            if (covered) {
+                for (DevEvent e : evs)
+                    if (!event_wait_polling(be, e)) return false;
+                return true;
+            }
             if (cancel.load(std::memory_order_relaxed) != 0) return false;
             std::this_thread::sleep_for(std::chrono::microseconds(us));
             us = std::min(us * 2, 200u);
@@ -809,7 +826,10 @@ public:
               size_t nsteps, size_t max_stripes, DeviceBackend *be, std::atomic<uint64_t> &tx_ctr)
         : txs_(txs), tag_(tag), seq_(seq), frame_(frame), be_(be), tx_ctr_(tx_ctr), steps_(nsteps),
           done_(nsteps) {
-        for (size_t k = 0; k < max_stripes; ++k) th_.emplace_back([this, k] { run(k); });
+        for (size_t k = 0; k < max_stripes; ++k) th_.emplace_back([this, k] {
+            name_thread("pccl-stripe-tx");
+            run(k);
+        });
     }
     ~OpSenders() {
         cancel();
@@ -832,6 +852,11 @@ public:
     bool published(size_t g) {
         std::lock_guard l(m_);
         return published_ > g;
+    }
+    // every stripe of step g has been sent (non-blocking)
+    bool sent(size_t g) {
+        std::lock_guard l(m_);
+        return published_ > g && done_[g] == 0;
     }
     // blocks until every stripe of step g is sent; false on failure / cancel
     bool wait(size_t g) {
@@ -863,7 +888,7 @@ private:
             const size_t base = tp.off[k], len = tp.len[k];
             for (size_t sent = 0; sent < len;) {
                 const size_t n = std::min(frame_, len - sent);
-                if (!st.ready->wait(base + sent + n, be_, rc_)) {
+                if (!st.ready->wait(base + sent, base + sent + n, be_, rc_)) {
                     cancel();
                     return;
                 }
@@ -896,58 +921,6 @@ private:
     std::vector<std::thread> th_;
 };
 
-// The receive half of a ring step: posts the sinks, calls `consume(a, b)` for newly complete elements (batches of at
-// least `gran` bytes unless a stripe ends) and removes the sinks. `send_rc` (may be null) != 0 aborts the wait (a send
-// of this op failed). Returns 0 ok, 1 io failure, 2 abort.
-int receive_step(const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq, uint8_t *sink,
-                 size_t rx_bytes, size_t elem, size_t gran, const std::function<void(size_t, size_t)> &consume,
-                 const std::function<bool()> &aborted, const std::atomic<int> *send_rc, std::atomic<uint64_t> &rx_ctr) {
-    const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
-    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
-    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
-    const size_t gran_el = std::max<size_t>(1, gran / elem);
-    std::vector<size_t> done(rp.off.size(), 0);
-    size_t remaining = 0;
-    for (size_t k = 0; k < rp.off.size(); ++k)
-        if (rp.len[k] > 0) ++remaining;
-    int rc = 0;
-    size_t idle = 0, rr = 0;
-    while (remaining > 0) {
-        bool progress = false;
-        for (size_t k = 0; k < rp.off.size(); ++k) {
-            const size_t want = rp.len[k] / elem;
-            if (done[k] >= want) continue;
-            const size_t have = rx_conn(k)->sink_progress(tag) / elem;
-            if (have > done[k] && (have - done[k] >= gran_el || have >= want)) {
-                const size_t e0 = rp.off[k] / elem;
-                consume(e0 + done[k], e0 + have);
-                done[k] = have;
-                progress = true;
-                if (done[k] >= want) --remaining;
-            }
-        }
-        if (remaining == 0 || progress) {
-            idle = 0;
-            continue;
-        }
-        size_t k = rr++ % rp.off.size();
-        while (done[k] >= rp.len[k] / elem) k = rr++ % rp.off.size();
-        net::MuxConn *c = rx_conn(k);
-        c->wait_sink(tag, std::min(rp.len[k], (done[k] + gran_el) * elem), 5ms);
-        if (!c->is_open() || (send_rc && send_rc->load() != 0)) {
-            rc = 1;
-            break;
-        }
-        if (++idle % 8 == 0 && aborted()) {
-            rc = 2;
-            break;
-        }
-    }
-    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->remove_sink(tag);
-    if (rc == 0) rx_ctr += rx_bytes;
-    return rc;
-}
-
 } // namespace
 
 std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
@@ -958,8 +931,11 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     const size_t es = dtype_size(q.dtype);
     auto *dst = static_cast<uint8_t *>(q.dst);
     const size_t bytes = q.count * es;
-    // copy granularity: >= 4 MiB keeps the copy engines near their peak (1 MiB copies: ~37 GB/s)
-    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20)) / es * es;
+    // Copy / reduce / frame granularity. >= 4 MiB keeps the copy engines near their peak (1 MiB copies: ~37 GB/s);
+    // with the send-ahead pipeline the step fill no longer scales with the piece, and 32 MiB measured fastest at
+    // 8 peers x 1 GiB on one MI355X (8 MiB 391-409 ms, 16 MiB 345-421, 32 MiB 331-346 in most runs;
+    // profiles/r3/ring_ab/): fewer copies, kernels, events and socket wake-ups per byte.
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 32u << 20)) / es * es;
 
     be->set_device(device);
     StreamLease stream(device);
@@ -999,6 +975,30 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         be->event_record(e, s);
         return e;
     };
+
+    const auto bounds = chunk_bounds(q.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t stage_bytes = max_chunk * es + 64;
+    // Staging rings of kNb buffers: step g receives into rxbuf[g % kNb] (HBM twin rxdev[g % kNb] for the reduce) and
+    // its reduce writes the next payload into txbuf[(g + 1) % kNb]. Three deep, because step g+1's sinks are posted
+    // while step g still receives and step g+1's sends run while step g's do: a buffer is refilled only after the
+    // step two back finished with it.
+    constexpr size_t kNb = 3;
+    Lease txl[kNb], rxl[kNb], dvl[kNb];
+    uint8_t *txbuf[kNb], *rxbuf[kNb], *rxdev[kNb];
+    for (size_t i = 0; i < kNb; ++i) {
+        txl[i] = Lease(pinned_pool(), stage_bytes);
+        rxl[i] = Lease(pinned_pool(), stage_bytes);
+        dvl[i] = Lease(device_pool(), stage_bytes, device);
+        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return {false, false};
+        txbuf[i] = txl[i].data();
+        rxbuf[i] = rxl[i].data();
+        rxdev[i] = dvl[i].data();
+    }
+    Lease backup;
+    // declared after every staging lease: destroyed first, so nothing of this op still reads or writes them when
+    // they go back to the pools (also on the early returns below)
     struct Drain { // runs on every exit: nothing of this op may still touch its staging buffers / dst afterwards
         DeviceBackend *be;
         DevStream st;
@@ -1011,8 +1011,6 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
             for (auto e : *ev) event_pool().put(e);
         }
     } drain{be, st, &last_h2d, &last_d2h, &owned};
-
-    Lease backup;
     if (q.src == q.dst && !q.scratch) {
         backup = Lease(device_pool(), bytes, device);
         if (!backup.ok()) return {false, false};
@@ -1034,32 +1032,29 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         return {code == 2, code == 2};
     };
 
-    const auto bounds = chunk_bounds(q.count, ws);
-    size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
-    const size_t stage_bytes = max_chunk * es + 64;
-    Lease txa(pinned_pool(), stage_bytes), txb(pinned_pool(), stage_bytes);
-    Lease rxa(pinned_pool(), stage_bytes), rxb(pinned_pool(), stage_bytes);
-    Lease da(device_pool(), stage_bytes, device), db(device_pool(), stage_bytes, device);
-    if (!txa.ok() || !txb.ok() || !rxa.ok() || !rxb.ok() || !da.ok() || !db.ok()) return {false, false};
-    uint8_t *txbuf[2] = {txa.data(), txb.data()};
-    uint8_t *rxbuf[2] = {rxa.data(), rxb.data()};
-    uint8_t *rxdev[2] = {da.data(), db.data()};
-    ReadyRanges txready[2];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
-    ReadyRanges rxready[2];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
-    size_t txshift[2] = {0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
-    DevEvent sink_free[2] = {nullptr, nullptr}; // last H2D copy reading rxbuf[i]
+    ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
+    size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
+    DevEvent h2d_done[kNb] = {nullptr, nullptr, nullptr}; // last H2D copy reading rxbuf[i] / writing rxdev[i]
+    DevEvent red_done[kNb] = {nullptr, nullptr, nullptr}; // last reduce kernel reading rxdev[i]
 
-    // Steps g = 0 .. 2(W-1)-1: reduce-scatter, then all-gather. With send-ahead (PCCL_RING_SEND_AHEAD=1) step g+1's
-    // sends start while step g still receives, so each piece of the next payload leaves as soon as it exists. Measured
-    // (profiles/r2/ring_send_ahead/): 8 peers 366 -> 370 ms, 2 peers 79 -> 119 ms (the receiver has not posted the
-    // next step's sinks yet, so early frames are queued and copied once more) — off by default.
-    const bool ahead = env_size("PCCL_RING_SEND_AHEAD", 0) != 0;
+    // Steps g = 0 .. 2(W-1)-1: reduce-scatter, then all-gather, run as one continuous pipeline (send-ahead): step
+    // g+1's sinks are posted and its sends published while step g still receives, so every connection streams the
+    // steps back to back and each piece of the next payload leaves the moment it has been reduced (or, all-gather,
+    // received). PCCL_RING_SEND_AHEAD=0 restores the step-synchronous schedule (A/B).
+    const bool ahead = env_size("PCCL_RING_SEND_AHEAD", 1) != 0;
+    // step-0 payload (own input chunk -> pinned): on the process-wide D2H copy queue (default; FIFO across the peers
+    // of this process) or on the op's stream (PCCL_RING_STEP0_OP_STREAM=1: blit kernels, per-peer copies run
+    // concurrently). 8 peers x 1 GiB, 32 MiB pieces, 3 runs each: queue 358 / 337 / 341 ms, op stream 331 / 429 /
+    // 388 ms (profiles/r3/ring_ab/summary.txt).
+    const bool step0_on_op_stream = env_size("PCCL_RING_STEP0_OP_STREAM", 0) != 0;
     const size_t nsteps = 2 * (ws - 1);
+    auto is_rs = [&](size_t g) { return g + 1 < ws; };
     auto chunk_tx = [&](size_t g) { // chunk index this peer sends at global step g
         return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
     };
     auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
+    auto region_of = [&](size_t g) { return dst + bounds[chunk_rx(g)].first * es; };
     size_t max_stripes = 1;
     for (size_t g = 0; g < nsteps; ++g) {
         const auto [ts, te] = bounds[chunk_tx(g)];
@@ -1067,13 +1062,14 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     }
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
     OpSenders senders(rv.tx, q.tag, seq, piece, nsteps, max_stripes, be, op.tx);
-    auto start = [&](size_t g) {
+    auto publish = [&](size_t g) {
+        if (senders.published(g)) return;
         const auto [ts, te] = bounds[chunk_tx(g)];
-        const bool rs_or_ag0 = g < ws; // reduce-scatter steps and all-gather step 0 send staged txbuf payloads
+        const bool staged = g < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
         OpSenders::Step stp;
-        stp.payload = rs_or_ag0 ? txbuf[g % 2] + txshift[g % 2] : rxbuf[(g + 1) % 2];
+        stp.payload = staged ? txbuf[g % kNb] + txshift[g % kNb] : rxbuf[(g - 1) % kNb];
         stp.bytes = (te - ts) * es;
-        stp.ready = rs_or_ag0 ? &txready[g % 2] : &rxready[(g + 1) % 2];
+        stp.ready = staged ? &txready[g % kNb] : &rxready[(g - 1) % kNb];
         senders.publish(g, stp);
     };
     auto fail_all = [&](int code) {
@@ -1081,59 +1077,161 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         return fail(code);
     };
 
+    // ---- receive side: one set of sinks per step, posted up to one step early
+    struct StepRx {
+        StripePlan rp;
+        std::vector<net::MuxConn::SinkRef> sinks;
+        std::vector<size_t> done; // elements consumed per stripe
+        size_t remaining = 0;
+        bool posted = false;
+    };
+    std::vector<StepRx> srx(nsteps);
+    auto rx_conn = [&](size_t k) { return rv.rx[(seq + k) % rv.rx.size()].get(); };
+    // rxbuf[g % kNb] may take step g's bytes once the step that used it before (g - kNb) is finished with it: its H2D
+    // copies and reduce kernels completed and (all-gather) the step after it has forwarded its bytes
+    auto can_post = [&](size_t g) {
+        if (g < kNb) return true;
+        const size_t b = g % kNb, prev = g - kNb;
+        if (h2d_done[b] && be->event_query(h2d_done[b]) == 0) return false;
+        if (red_done[b] && be->event_query(red_done[b]) == 0) return false;
+        if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
+        return true;
+    };
+    auto post = [&](size_t g) {
+        StepRx &r = srx[g];
+        const size_t b = g % kNb;
+        h2d_done[b] = red_done[b] = nullptr;
+        if (!is_rs(g)) rxready[b].clear();
+        const auto [rs0, re0] = bounds[chunk_rx(g)];
+        r.rp = plan_stripes((re0 - rs0) * es, rv.rx.size());
+        r.sinks.resize(r.rp.off.size());
+        r.done.assign(r.rp.off.size(), 0);
+        r.remaining = 0;
+        for (size_t k = 0; k < r.rp.off.size(); ++k) {
+            if (r.rp.len[k] == 0) continue;
+            r.sinks[k] = rx_conn(k)->post_sink(q.tag, seq, rxbuf[b] + r.rp.off[k], r.rp.len[k]);
+            ++r.remaining;
+        }
+        r.posted = true;
+    };
+    auto unpost = [&](size_t g) {
+        StepRx &r = srx[g];
+        if (!r.posted) return;
+        for (size_t k = 0; k < r.sinks.size(); ++k)
+            if (r.sinks[k]) rx_conn(k)->remove_sink(q.tag, r.sinks[k]);
+        r.sinks.clear();
+        r.posted = false;
+    };
+    struct Unposter { // sinks must never outlive their buffers (also on failure)
+        std::function<void()> fn;
+        ~Unposter() { fn(); }
+    } unposter{[&] {
+        for (size_t g = 0; g < nsteps; ++g) unpost(g);
+    }};
+
     for (size_t g = 0; g < nsteps; ++g) {
-        const size_t cur = g % 2, nxt = cur ^ 1;
-        const bool rs = g + 1 < ws;
-        // step g-1's sends read the buffers this step refills (txbuf[nxt] for reduce-scatter, rxbuf[cur] through
-        // step g+1's forwarding): they must be done first
-        if (g > 0 && !senders.wait(g - 1)) return fail_all(1);
-        if (sink_free[cur]) event_wait_polling(be, sink_free[cur]);
-        if (g == 0) { // own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+        const size_t b = g % kNb, nb = (g + 1) % kNb;
+        const bool rs = is_rs(g);
+        if (!ahead && g > 0 && !senders.wait(g - 1)) return fail_all(1);
+        // 1. step g's sinks (normally posted during step g-1)
+        while (!srx[g].posted) {
+            if (can_post(g)) {
+                post(g);
+                break;
+            }
+            if (senders.failed()) return fail_all(1);
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
+        uint8_t *region = region_of(g);
+        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
+        if (rs) {
+            if (g >= 2 && !senders.wait(g - 2)) return fail_all(1);
+            txready[nb].clear();
+            txshift[nb] = shift;
+        }
+        // 3. own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+        if (g == 0) {
             const auto [ts, te] = bounds[chunk_tx(0)];
-            txready[cur].clear();
-            txshift[cur] = 0;
+            txready[0].clear();
+            txshift[0] = 0;
+            DevStream q0 = step0_on_op_stream ? st : pq.d2h;
             for (size_t off = 0; off < (te - ts) * es; off += piece) {
                 const size_t n = std::min(piece, (te - ts) * es - off);
-                be->memcpy_async(txbuf[cur] + off, static_cast<const uint8_t *>(q.src) + ts * es + off, n, pq.d2h);
-                last_d2h = record(pq.d2h);
-                txready[cur].add(off, off + n, last_d2h);
+                be->memcpy_async(txbuf[0] + off, static_cast<const uint8_t *>(q.src) + ts * es + off, n, q0);
+                DevEvent e = record(q0);
+                if (!step0_on_op_stream) last_d2h = e;
+                txready[0].add(off, off + n, e);
             }
         }
-        const auto [rs0, re0] = bounds[chunk_rx(g)];
-        uint8_t *region = dst + rs0 * es;
-        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
-        if (rs) { // the reduced pieces become the next step's payload in txbuf[nxt]
-            txready[nxt].clear();
-            txshift[nxt] = shift;
-        } else { // this step's received bytes are forwarded by the next all-gather step
-            rxready[cur].clear();
-        }
-        if (!senders.published(g)) start(g);
-        if (ahead && g + 1 < nsteps) start(g + 1);
-        uint8_t *sink = rxbuf[cur];
+        publish(g);
+        if (ahead && g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
+        // 4. receive + consume step g
+        StepRx &r = srx[g];
+        uint8_t *sink = rxbuf[b];
+        DevEvent last_red = nullptr;
         std::function<void(size_t, size_t)> consume;
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
-            uint8_t *stage = rxdev[cur] + shift, *out = txbuf[nxt] + shift;
-            consume = [&, stage, out, sink, region](size_t a, size_t b) {
-                const size_t off = a * es, n = (b - a) * es;
+            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
+            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
+                const size_t off = a * es, n = (e - a) * es;
                 be->memcpy_async(stage + off, sink + off, n, pq.h2d);
                 last_h2d = record(pq.h2d);
                 be->stream_wait_event(st, last_h2d);
-                be->reduce_copy(region + off, stage + off, out + off, b - a, q.dtype, q.op, st);
-                txready[nxt].add(off, off + n, record(st));
+                be->reduce_copy(region + off, stage + off, out + off, e - a, q.dtype, q.op, st);
+                last_red = record(st);
+                txready[nb].add(off, off + n, last_red);
             };
         } else {
-            consume = [&, sink, region, cur](size_t a, size_t b) {
-                be->memcpy_async(region + a * es, sink + a * es, (b - a) * es, pq.h2d);
+            consume = [&, sink, region, b](size_t a, size_t e) {
+                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d);
                 last_h2d = record(pq.h2d);
-                rxready[cur].add(a * es, b * es, nullptr); // in host memory: forwardable at once
+                rxready[b].add(a * es, e * es, nullptr); // in host memory: forwardable at once
             };
         }
-        const int rc = receive_step(rv.rx, q.tag, seq, sink, (re0 - rs0) * es, es, piece, consume, aborted,
-                                    &senders.rc(), op.rx);
-        sink_free[cur] = last_h2d;
+        const size_t gran_el = std::max<size_t>(1, piece / es);
+        int rc = 0;
+        size_t idle = 0, rr = 0;
+        while (r.remaining > 0) {
+            bool progress = false;
+            for (size_t k = 0; k < r.sinks.size(); ++k) {
+                if (!r.sinks[k]) continue;
+                const size_t want = r.rp.len[k] / es;
+                if (r.done[k] >= want) continue;
+                const size_t have = net::MuxConn::sink_progress(r.sinks[k]) / es;
+                if (have > r.done[k] && (have - r.done[k] >= gran_el || have >= want)) {
+                    const size_t e0 = r.rp.off[k] / es;
+                    consume(e0 + r.done[k], e0 + have);
+                    r.done[k] = have;
+                    progress = true;
+                    if (r.done[k] >= want) --r.remaining;
+                }
+            }
+            // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
+            if (ahead && g + 1 < nsteps && !srx[g + 1].posted && can_post(g + 1)) post(g + 1);
+            if (r.remaining == 0 || progress) {
+                idle = 0;
+                continue;
+            }
+            size_t k = rr++ % r.sinks.size();
+            while (!r.sinks[k] || r.done[k] >= r.rp.len[k] / es) k = rr++ % r.sinks.size();
+            net::MuxConn *c = rx_conn(k);
+            c->wait_sink(r.sinks[k], std::min(r.rp.len[k], (r.done[k] + gran_el) * es), 5ms);
+            if (!c->is_open() || senders.failed()) {
+                rc = 1;
+                break;
+            }
+            if (++idle % 8 == 0 && aborted()) {
+                rc = 2;
+                break;
+            }
+        }
+        h2d_done[b] = last_h2d;
+        red_done[b] = last_red;
         if (rc) return fail_all(rc);
+        op.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
+        unpost(g);
         if (!ahead && !senders.wait(g)) return fail_all(1); // classic schedule: a step ends when its sends are done
         step_mark(rs, rs ? g : g - (ws - 1));
         if (g == 0) fault_point("ring_step", seq);

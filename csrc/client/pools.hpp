@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../common/device_backend.hpp"
+#include "../common/types.hpp"
 
 namespace pccl::client {
 
@@ -40,6 +41,7 @@ public:
             if (best != SIZE_MAX) {
                 Buf b = free_[bi];
                 free_.erase(free_.begin() + static_cast<long>(bi));
+                free_bytes_ -= b.cap;
                 return b;
             }
         }
@@ -55,11 +57,18 @@ public:
         return b;
     }
 
+    // Returned buffers stay cached up to kMaxFree buffers and PCCL_POOL_MAX_FREE_MIB (default 32 GiB) per pool,
+    // oldest released first. The cap must cover a whole op's working set: the device ring holds 9 staging buffers
+    // per peer (8 threaded peers x 1 GiB: 6 GiB of pinned memory), and a pool that trims below that frees and
+    // re-allocates pinned memory on every op (hipHostFree / hipHostMalloc of 128 MiB cost milliseconds each).
     void put(const Buf &b) {
         if (b.p == nullptr) return;
+        static const size_t max_bytes = env_size("PCCL_POOL_MAX_FREE_MIB", 32u << 10) << 20;
         std::lock_guard l(mtx_);
         free_.push_back(b);
-        if (free_.size() > 32) {
+        free_bytes_ += b.cap;
+        while (free_.size() > 1 && (free_.size() > kMaxFree || free_bytes_ > max_bytes)) {
+            free_bytes_ -= free_.front().cap;
             release(free_.front());
             free_.erase(free_.begin());
         }
@@ -83,9 +92,11 @@ private:
                 break;
         }
     }
+    static constexpr size_t kMaxFree = 256;
     Kind kind_;
     std::mutex mtx_;
     std::vector<Buf> free_;
+    size_t free_bytes_ = 0;
 };
 
 // RAII lease of a pooled buffer.

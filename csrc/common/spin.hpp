@@ -23,6 +23,10 @@ inline void low_timer_slack() {
     (void)done;
 }
 
+/// Names the calling thread (at most 15 characters; shown in /proc/<pid>/task/*/comm): per-thread CPU accounting of
+/// the ring (bench.py extra.cpu_by_thread) groups the process's threads by these names.
+inline void name_thread(const char *name) { prctl(PR_SET_NAME, reinterpret_cast<unsigned long>(name), 0, 0, 0); }
+
 /// Spins until pred() is true or the budget is spent; returns pred()'s last value.
 template <class Pred> inline bool spin_until(Pred &&pred) {
     const long budget = spin_budget_us();

@@ -25,7 +25,10 @@ bool MasterConnection::connect() {
     timeval tv{10, 0}; // bounded sends (reference: SO_SNDTIMEO 10 s)
     setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
     open_ = true;
-    rx_thread_ = std::thread([this] { rx_loop(); });
+    rx_thread_ = std::thread([this] {
+        name_thread("pccl-master-rx");
+        rx_loop();
+    });
     return true;
 }
 

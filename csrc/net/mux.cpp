@@ -99,7 +99,10 @@ MuxConn::~MuxConn() {
 
 bool MuxConn::start() {
     open_.store(true, std::memory_order_release);
-    if (mode_ == Mode::Rx) rx_thread_ = std::thread([this] { rx_loop(); });
+    if (mode_ == Mode::Rx) rx_thread_ = std::thread([this] {
+        name_thread("pccl-mux-rx");
+        rx_loop();
+    });
     return true;
 }
 
@@ -126,7 +129,10 @@ void MuxConn::join() {
 void MuxConn::post_send_job(std::function<void()> job) {
     std::lock_guard l(job_mtx_);
     jobs_.push_back(std::move(job));
-    if (!tx_job_thread_.joinable() && !jobs_stop_) tx_job_thread_ = std::thread([this] { tx_job_loop(); });
+    if (!tx_job_thread_.joinable() && !jobs_stop_) tx_job_thread_ = std::thread([this] {
+            name_thread("pccl-mux-tx");
+            tx_job_loop();
+        });
     job_cv_.notify_one();
 }
 
@@ -201,20 +207,16 @@ void MuxConn::rx_loop() {
         size_t offset = 0;
         {
             std::lock_guard l(mtx_);
-            auto it = sinks_.find(tag);
-            if (it != sinks_.end() && it->second->ctr == ctr &&
-                it->second->received.load(std::memory_order_relaxed) + n <= it->second->capacity) {
-                // only deliver directly if nothing for this tag/ctr is still queued ahead of us (FIFO)
-                auto qit = queued_.find(tag);
-                bool queued_ahead = false;
-                if (qit != queued_.end())
-                    for (const auto &f : qit->second)
-                        if (f.ctr == ctr) queued_ahead = true;
-                if (!queued_ahead) {
-                    sink = it->second.get();
-                    sink->busy = true;
-                    offset = sink->received.load(std::memory_order_relaxed);
-                }
+            // deliver directly only if nothing for this tag/ctr is still queued ahead of this frame (FIFO)
+            auto qit = queued_.find(tag);
+            bool queued_ahead = false;
+            if (qit != queued_.end())
+                for (const auto &f : qit->second)
+                    if (f.ctr == ctr) queued_ahead = true;
+            if (!queued_ahead) sink = sink_for_locked(tag, ctr, n);
+            if (sink != nullptr) {
+                sink->busy = true;
+                offset = sink->received.load(std::memory_order_relaxed);
             }
         }
         if (sink != nullptr) {
@@ -236,18 +238,11 @@ void MuxConn::rx_loop() {
         {
             std::lock_guard l(mtx_);
             auto it = sinks_.find(tag);
-            if (it != sinks_.end() && ctr < it->second->ctr) {
-                // stale frame of an aborted earlier op with the same tag
-            } else if (it != sinks_.end() && it->second->ctr == ctr && !it->second->busy &&
-                       it->second->received.load(std::memory_order_relaxed) + n <= it->second->capacity &&
-                       (queued_.find(tag) == queued_.end() || queued_[tag].empty())) {
-                // the sink was posted while we were reading this frame: deliver it now (keeps FIFO order)
-                Sink *s = it->second.get();
-                const size_t off = s->received.load(std::memory_order_relaxed);
-                std::memcpy(s->dst + off, buf.data(), n);
-                s->received.store(off + n, std::memory_order_release);
-            } else {
+            const bool stale = it != sinks_.end() && !it->second.empty() && ctr < it->second.front()->ctr;
+            if (!stale) { // (stale: a frame of an aborted earlier op with the same tag)
                 queued_[tag].push_back(Frame{ctr, std::move(buf)});
+                // a sink may have been posted while this frame was read: deliver now (keeps FIFO order)
+                drain_queued_locked(tag, ctr);
             }
         }
         cv_.notify_all();
@@ -284,79 +279,124 @@ std::optional<std::vector<uint8_t>> MuxConn::recv_frame(uint64_t tag, uint64_t c
     }
 }
 
-void MuxConn::post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n) {
+MuxConn::Sink *MuxConn::sink_for_locked(uint64_t tag, uint64_t ctr, size_t n) {
+    auto it = sinks_.find(tag);
+    if (it == sinks_.end()) return nullptr;
+    for (auto &s : it->second) {
+        if (s->ctr != ctr) continue;
+        const size_t have = s->received.load(std::memory_order_relaxed);
+        if (have >= s->capacity) continue; // full: the frame belongs to a later sink
+        return have + n <= s->capacity && !s->busy ? s.get() : nullptr;
+    }
+    return nullptr;
+}
+
+void MuxConn::drain_queued_locked(uint64_t tag, uint64_t ctr) {
+    auto it = queued_.find(tag);
+    if (it == queued_.end()) return;
+    auto &q = it->second;
+    auto sk = sinks_.find(tag);
+    if (sk != sinks_.end() && !sk->second.empty()) {
+        const uint64_t cur = sk->second.front()->ctr;
+        while (!q.empty() && q.front().ctr < cur) q.pop_front(); // stale frames of an aborted earlier op
+    }
+    while (!q.empty() && q.front().ctr == ctr) {
+        Sink *s = sink_for_locked(tag, ctr, q.front().data.size());
+        if (s == nullptr) break;
+        const auto &f = q.front().data;
+        const size_t have = s->received.load(std::memory_order_relaxed);
+        std::memcpy(s->dst + have, f.data(), f.size());
+        s->received.store(have + f.size(), std::memory_order_release);
+        q.pop_front();
+    }
+    if (q.empty()) queued_.erase(it);
+}
+
+MuxConn::SinkRef MuxConn::post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n) {
     std::lock_guard l(mtx_);
-    auto s = std::make_unique<Sink>();
+    auto s = std::make_shared<Sink>();
     s->ctr = ctr;
     s->dst = dst;
     s->capacity = n;
-    auto it = queued_.find(tag);
-    if (it != queued_.end()) {
-        auto &q = it->second;
-        while (!q.empty() && q.front().ctr < ctr) q.pop_front();
-        while (!q.empty() && q.front().ctr == ctr) {
-            const auto &f = q.front().data;
-            const size_t have = s->received.load(std::memory_order_relaxed);
-            if (have + f.size() > n) break;
-            std::memcpy(dst + have, f.data(), f.size());
-            s->received.store(have + f.size(), std::memory_order_release);
-            q.pop_front();
-        }
-        if (q.empty()) queued_.erase(it);
-    }
-    sinks_[tag] = std::move(s);
+    auto &dq = sinks_[tag];
+    // sinks of an older ctr left behind (an aborted op that never removed them) no longer receive anything
+    while (!dq.empty() && dq.front()->ctr < ctr && !dq.front()->busy) dq.pop_front();
+    dq.push_back(s);
+    drain_queued_locked(tag, ctr);
+    return s;
 }
 
 size_t MuxConn::sink_progress(uint64_t tag) {
     std::lock_guard l(mtx_);
     auto it = sinks_.find(tag);
-    if (it == sinks_.end()) return 0;
-    return it->second->received.load(std::memory_order_acquire);
+    if (it == sinks_.end() || it->second.empty()) return 0;
+    return it->second.front()->received.load(std::memory_order_acquire);
 }
 
 size_t MuxConn::wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout) {
+    SinkRef s;
+    {
+        std::lock_guard l(mtx_);
+        auto it = sinks_.find(tag);
+        if (it == sinks_.end() || it->second.empty()) return 0;
+        s = it->second.front();
+    }
+    return wait_sink(s, want, timeout);
+}
+
+size_t MuxConn::wait_sink(const SinkRef &sr, size_t want, std::chrono::milliseconds timeout) {
+    if (!sr) return 0;
+    Sink *sink = sr.get(); // kept alive by the caller's reference
+    if (sink->received.load(std::memory_order_acquire) >= want || !is_open())
+        return sink->received.load(std::memory_order_acquire);
+    // spin briefly without the lock, then sleep on the condition variable with the waiter's threshold published
+    spin_until([&] { return sink->received.load(std::memory_order_acquire) >= want || !is_open(); });
     std::unique_lock l(mtx_);
     const auto deadline = std::chrono::steady_clock::now() + timeout;
-    bool spun = false;
     while (true) {
-        auto it = sinks_.find(tag);
-        if (it == sinks_.end()) return 0;
-        const size_t have = it->second->received.load(std::memory_order_acquire);
+        const size_t have = sink->received.load(std::memory_order_acquire);
         if (have >= want || !is_open()) return have;
-        if (!spun) { // spin once without the lock, then re-check under it before sleeping (no lost notify)
-            spun = true;
-            Sink *sink = it->second.get(); // only the waiter's own op removes its sink
-            l.unlock();
-            spin_until([&] { return sink->received.load(std::memory_order_acquire) >= want || !is_open(); });
-            l.lock();
-            continue;
-        }
-        Sink *sink = it->second.get();
         sink->wake_at.store(want);
         if (sink->received.load() >= want) continue;
         const bool timed_out = cv_.wait_until(l, deadline) == std::cv_status::timeout;
-        sink->wake_at.store(SIZE_MAX); // the sink outlives the wait: only its own op removes it
+        sink->wake_at.store(SIZE_MAX);
         if (timed_out) return sink->received.load(std::memory_order_acquire);
     }
 }
 
 void MuxConn::remove_sink(uint64_t tag) {
+    SinkRef s;
+    {
+        std::lock_guard l(mtx_);
+        auto it = sinks_.find(tag);
+        if (it == sinks_.end() || it->second.empty()) return;
+        s = it->second.front();
+    }
+    remove_sink(tag, s);
+}
+
+void MuxConn::remove_sink(uint64_t tag, const SinkRef &s) {
+    if (!s) return;
     std::unique_lock l(mtx_);
-    auto it = sinks_.find(tag);
-    if (it == sinks_.end()) return;
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
     bool interrupted = false;
-    while (it->second->busy) {
+    while (s->busy) {
         cv_.wait_for(l, std::chrono::milliseconds(50));
         if (std::chrono::steady_clock::now() > deadline && !interrupted) {
             LOG(WARN) << "MuxConn: sink still being written after 10 s; interrupting connection";
             interrupted = true;
             if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
         }
-        it = sinks_.find(tag);
-        if (it == sinks_.end()) return;
     }
-    sinks_.erase(it);
+    auto it = sinks_.find(tag);
+    if (it == sinks_.end()) return;
+    auto &dq = it->second;
+    for (auto d = dq.begin(); d != dq.end(); ++d)
+        if (d->get() == s.get()) {
+            dq.erase(d);
+            break;
+        }
+    if (dq.empty()) sinks_.erase(it);
 }
 
 } // namespace pccl::net

@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <optional>
 #include <thread>
@@ -67,17 +68,9 @@ public:
     }
 
     // Posts a sink of exactly `n` bytes at `dst` for (tag, ctr). Already-queued matching frames are copied in.
-    void post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n);
-    // Bytes delivered into the sink so far (acquire). 0 if no sink.
-    size_t sink_progress(uint64_t tag);
-    // Waits until progress >= want, the connection closed, or timeout. Returns current progress.
-    size_t wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout);
-    // Removes the sink; waits for an in-flight write into it to finish (interrupts the connection if it hangs).
-    void remove_sink(uint64_t tag);
-
-    uint64_t rx_bytes_total() const { return rx_total_.load(std::memory_order_relaxed); }
-
-private:
+    // Sinks of one tag form a FIFO: frames fill the oldest sink that still has room, so a ring op can post the next
+    // step's sinks while the current step is still receiving (the sender streams both steps back to back on this
+    // connection) and early frames land in place instead of being queued and copied once more.
     struct Sink {
         uint64_t ctr = 0;
         uint8_t *dst = nullptr;
@@ -88,6 +81,22 @@ private:
         std::atomic<size_t> wake_at{SIZE_MAX};
         bool busy = false; // RX thread is writing into dst
     };
+    using SinkRef = std::shared_ptr<Sink>;
+    SinkRef post_sink(uint64_t tag, uint64_t ctr, uint8_t *dst, size_t n);
+    // Bytes delivered into the sink so far (acquire).
+    static size_t sink_progress(const SinkRef &s) { return s ? s->received.load(std::memory_order_acquire) : 0; }
+    // Waits until progress >= want, the connection closed, or timeout. Returns current progress.
+    size_t wait_sink(const SinkRef &s, size_t want, std::chrono::milliseconds timeout);
+    // Removes the sink; waits for an in-flight write into it to finish (interrupts the connection if it hangs).
+    void remove_sink(uint64_t tag, const SinkRef &s);
+    // Tag-keyed forms acting on the oldest sink of the tag (single-sink users)
+    size_t sink_progress(uint64_t tag);
+    size_t wait_sink(uint64_t tag, size_t want, std::chrono::milliseconds timeout);
+    void remove_sink(uint64_t tag);
+
+    uint64_t rx_bytes_total() const { return rx_total_.load(std::memory_order_relaxed); }
+
+private:
     struct Frame {
         uint64_t ctr;
         std::vector<uint8_t> data;
@@ -113,7 +122,11 @@ private:
 
     std::mutex mtx_;
     std::condition_variable cv_;
-    std::unordered_map<uint64_t, std::unique_ptr<Sink>> sinks_;
+    // oldest sink of `tag` with room for `n` more bytes (full ones are skipped; a partly filled one without room for
+    // the whole frame stops the search: frames never straddle sinks); nullptr if none. Caller holds mtx_.
+    Sink *sink_for_locked(uint64_t tag, uint64_t ctr, size_t n);
+    void drain_queued_locked(uint64_t tag, uint64_t ctr);
+    std::unordered_map<uint64_t, std::deque<SinkRef>> sinks_;
     std::unordered_map<uint64_t, std::deque<Frame>> queued_;
     std::atomic<uint64_t> rx_total_{0};
 };

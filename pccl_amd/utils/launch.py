@@ -80,8 +80,10 @@ def wait_for_world(comm, world_size: int, timeout: float = 60.0, poll: float = 0
 
 def run_threaded_peers(n: int, fn: Callable[[int, object], object], *, address: str, timeout: float = 120.0,
                        peer_group: int = 0, connect_stagger: float = 0.0,
-                       comm_kwargs: Optional[Dict[str, object]] = None) -> List[object]:
+                       comm_kwargs=None) -> List[object]:
     """Runs ``fn(rank, communicator)`` on n peers, one thread each, all connected to ``address``.
+
+    ``comm_kwargs``: Communicator keyword arguments, a dict for every peer or a callable ``rank -> dict``.
 
     Each peer waits until the world has n members before calling ``fn``. Exceptions are re-raised in the caller.
     """
@@ -93,7 +95,8 @@ def run_threaded_peers(n: int, fn: Callable[[int, object], object], *, address: 
 
     def body(r: int):
         try:
-            c = Communicator(address, peer_group, **ports[r], **(comm_kwargs or {}))
+            kw = comm_kwargs(r) if callable(comm_kwargs) else comm_kwargs
+            c = Communicator(address, peer_group, **ports[r], **(kw or {}))
             comms[r] = c
             c.connect(n_attempts=10)
             wait_for_world(c, n, timeout=timeout)

@@ -316,6 +316,44 @@ TEST(mux_stale_ctr_frames_dropped_and_tags_independent) {
     delete rx;
 }
 
+TEST(mux_sink_fifo_fills_oldest_sink_first) {
+    // a ring op posts step g+1's sink while step g's still receives: frames fill the sinks in posting order
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> s1(3000), s2(2000), d1(3000, 0), d2(2000, 0);
+    for (size_t i = 0; i < s1.size(); ++i) s1[i] = static_cast<uint8_t>(i * 3 + 1);
+    for (size_t i = 0; i < s2.size(); ++i) s2[i] = static_cast<uint8_t>(i * 5 + 2);
+    auto h1 = rx->post_sink(4, 2, d1.data(), d1.size());
+    auto h2 = rx->post_sink(4, 2, d2.data(), d2.size());
+    tx->send_frame(4, 2, s1.data(), 1000);
+    tx->send_frame(4, 2, s1.data() + 1000, 2000);
+    tx->send_frame(4, 2, s2.data(), 2000);
+    EXPECT(rx->wait_sink(h1, d1.size(), 5s) == d1.size());
+    EXPECT(rx->wait_sink(h2, d2.size(), 5s) == d2.size());
+    EXPECT(d1 == s1 && d2 == s2);
+    rx->remove_sink(4, h1);
+    rx->remove_sink(4, h2);
+    delete tx;
+    delete rx;
+}
+
+TEST(mux_sink_fifo_late_second_sink_takes_queued_frames) {
+    // frames of the next step arrive before its sink exists: queued, then copied in when it is posted
+    auto [tx, rx] = mux_pair();
+    std::vector<uint8_t> a(4096, 7), b(1024, 9), d1(4096, 0), d2(1024, 0);
+    auto h1 = rx->post_sink(6, 1, d1.data(), d1.size());
+    tx->send_frame(6, 1, a.data(), a.size());
+    tx->send_frame(6, 1, b.data(), b.size());
+    EXPECT(rx->wait_sink(h1, d1.size(), 5s) == d1.size());
+    std::this_thread::sleep_for(50ms); // the second frame is queued (sink 1 full, no sink 2 yet)
+    rx->remove_sink(6, h1);
+    auto h2 = rx->post_sink(6, 1, d2.data(), d2.size());
+    EXPECT(rx->wait_sink(h2, d2.size(), 5s) == d2.size());
+    EXPECT(d1 == a && d2 == b);
+    rx->remove_sink(6, h2);
+    delete tx;
+    delete rx;
+}
+
 TEST(mux_peer_close_is_detected) {
     auto [tx, rx] = mux_pair();
     std::vector<uint8_t> dst(128);

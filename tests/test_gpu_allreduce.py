@@ -119,6 +119,38 @@ def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, mon
         assert torch.equal(y, expect)
 
 
+@pytest.mark.parametrize("ahead,step0_op", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, monkeypatch):
+    """Neighbours with different P2P connection pool sizes (1 / 3 / 2 stripes) and chunks that are no multiple of the
+    staging piece: a TX stripe of the next step then spans several RX stripes of this one, and the send-ahead
+    pipeline must send no byte before it has been received and reduced (advisor round 2, high)."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_RING_SEND_AHEAD", ahead)
+    monkeypatch.setenv("PCCL_RING_STEP0_OP_STREAM", step0_op)
+    world, n = 3, 9_000_011
+    pools = [1, 3, 2]
+    base = (torch.arange(n, dtype=torch.int64) % 29).float()
+    inputs = [(base * (r + 1) + r).to(torch.bfloat16) for r in range(world)]
+    expect = torch.stack([x.float() for x in inputs]).sum(0).to(torch.bfloat16)
+
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        y = torch.empty_like(x)
+        for tag in range(3):  # later ops reuse pooled staging buffers, events and the connections' sink queues
+            comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+        torch.cuda.synchronize()
+        return y.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, timeout=180,
+                                 comm_kwargs=lambda r: {"p2p_connection_pool_size": pools[r]})
+    for y, path in res:
+        assert path == pccl.ReducePath.DEVICE_RING.value
+        assert torch.equal(y, expect)
+
+
 @pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
 def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
