@@ -524,7 +524,39 @@ def extras_in_child(job, a):
     return res.get("extra", {}), res.get("sweep", {})
 
 
+def _numa_bind():
+    """PCCL_BENCH_NUMA_BIND=1: restrict the process to the CPUs of cuda:LOCAL_RANK's NUMA node (sysfs; before any GPU
+    call). Returns a description for extra, or None."""
+    if os.environ.get("PCCL_BENCH_NUMA_BIND") != "1":
+        return None
+    import glob
+    try:
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        nodes = []
+        for card in sorted(glob.glob("/sys/class/drm/card*/device/numa_node")):
+            with open(os.path.join(os.path.dirname(card), "vendor")) as f:
+                if f.read().strip() != "0x1002":
+                    continue
+            with open(card) as f:
+                nodes.append(int(f.read().strip()))
+        node = nodes[local_rank % len(nodes)] if nodes else -1
+        if node < 0:
+            return {"numa_bind": "no node"}
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        cpus &= os.sched_getaffinity(0)
+        os.sched_setaffinity(0, cpus)
+        return {"numa_node": node, "cpus": len(cpus)}
+    except (OSError, ValueError) as e:
+        return {"numa_bind_error": repr(e)[:200]}
+
+
 def main():
+    numa = _numa_bind()
     a = _args()
     # stdout carries exactly one line, the result JSON: everything else any library, child process or the gloo
     # rendezvous writes to fd 1 goes to stderr
@@ -577,6 +609,8 @@ def main():
         if "peer_curve" in extra:
             extra["peer_curve"].setdefault("DEVICE_RING", {})[str(P)] = _curve_point(nbytes, ring["t"], P)
     extra["sweep"] = sweep
+    if numa is not None:
+        extra["numa_bind"] = numa
 
     cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "
                  f"{'loopback TCP device ring' if path_name == 'DEVICE_RING' else path_name}")

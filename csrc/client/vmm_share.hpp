@@ -3,7 +3,8 @@
 // ("\0pccl-vmm-<pid>-<nonce>"), fds travel with SCM_RIGHTS. A peer asks for an allocation id and receives its own
 // copy of the fd, imports it (DeviceBackend::vmm_import) and closes the copy. The per-process random nonce is part of
 // the socket name and of every handle, so a handle of a dead process never resolves in a new process that happens to
-// reuse its pid.
+// reuse its pid. Only callers with this process's uid are served, and allocation ids are 64-bit random capabilities
+// known only to the ring's peers (the socket name itself is public in /proc/net/unix).
 #pragma once
 
 #include <cstdint>

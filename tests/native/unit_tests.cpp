@@ -16,6 +16,7 @@
 #include "net/socket.hpp"
 #include "proto/packets.hpp"
 #include "client/ipc.hpp"
+#include "client/vmm_share.hpp"
 
 #include <sys/socket.h>
 #include <unistd.h>
@@ -352,6 +353,32 @@ TEST(mux_sink_fifo_late_second_sink_takes_queued_frames) {
     rx->remove_sink(6, h2);
     delete tx;
     delete rx;
+}
+
+TEST(vmm_share_serves_fds_by_random_id_only) {
+    // the fd service is generic over fds: a pipe stands in for an exported VMM allocation
+    int p[2];
+    EXPECT(::pipe(p) == 0);
+    auto &svc = client::VmmShare::instance();
+    const uint64_t id = svc.publish(p[1]); // the service owns the write end now
+    const uint64_t id2 = svc.publish(::dup(p[1]));
+    EXPECT(id != 0 && id2 != 0 && id != id2);
+    EXPECT(id2 != id + 1 && id != id2 + 1); // random capabilities, not a sequence
+    const int got = client::VmmShare::fetch(::getpid(), svc.nonce(), id, 2000);
+    EXPECT(got >= 0);
+    if (got >= 0) {
+        const char msg[] = "vmm";
+        EXPECT(::write(got, msg, 3) == 3); // the duplicate refers to the published pipe
+        char buf[4] = {};
+        EXPECT(::read(p[0], buf, 3) == 3 && std::string(buf) == "vmm");
+        ::close(got);
+    }
+    EXPECT(client::VmmShare::fetch(::getpid(), svc.nonce(), id ^ 0x5a5a5a5aULL, 2000) < 0); // unknown id
+    EXPECT(client::VmmShare::fetch(::getpid(), svc.nonce() ^ 1, id, 500) < 0);             // wrong socket
+    svc.retract(id);
+    EXPECT(client::VmmShare::fetch(::getpid(), svc.nonce(), id, 2000) < 0); // retracted
+    svc.retract(id2);
+    ::close(p[0]);
 }
 
 TEST(mux_peer_close_is_detected) {
