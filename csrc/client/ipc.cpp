@@ -1,5 +1,6 @@
 #include "ipc.hpp"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/mman.h>
@@ -108,7 +109,9 @@ struct OpCtx {
 
 // per-process counters of how op buffers were handed to the peers (pcclxIpcStats): [0] direct inputs, [1] direct
 // outputs, [2] staged inputs, [3] staged outputs
-static std::atomic<uint64_t> g_buf_stats[4];
+// [0..3] direct_in, direct_out, staged_in, staged_out; [4] comm buffers quarantined after an abort; [5] drains that
+// waited for a dead peer's threads to finish tearing down its address space
+static std::atomic<uint64_t> g_buf_stats[6];
 
 // per-process bookkeeping
 static std::mutex g_ctx_mtx;
@@ -368,7 +371,15 @@ IpcArena::CommBuf *IpcArena::acquire_buffer(size_t bytes, int device) {
 void IpcArena::release_buffer(CommBuf *b) {
     if (!b) return;
     std::lock_guard l(mtx_);
-    b->busy = false;
+    if (!b->quarantined) b->busy = false;
+}
+
+void IpcArena::quarantine_buffer(CommBuf *b) {
+    if (!b) return;
+    std::lock_guard l(mtx_);
+    if (!b->quarantined) ++g_buf_stats[4];
+    b->quarantined = true;
+    b->busy = true;
 }
 
 void *IpcArena::pin_mapping(int peer, const uint8_t *handle, int my_device, MapKey &key) {
@@ -437,23 +448,59 @@ void IpcArena::set_phase(uint64_t seq, uint32_t phase) {
         ->phase.store(((seq + 1) << 8) | phase, std::memory_order_release);
 }
 
-// A crashed peer stays a zombie until its parent reaps it, and kill(pid, 0) succeeds on zombies: also check the
-// process state in /proc so that survivors abort promptly instead of waiting for the barrier timeout.
-static bool pid_alive(int pid) {
-    if (kill(pid, 0) != 0 && errno != EPERM) return false;
-    char path[64];
-    std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+// One-character state of /proc/<pid>/task/<tid>/stat (or /proc/<pid>/stat with tid < 0); 0 if unreadable.
+static char proc_state(int pid, int tid) {
+    char path[96];
+    if (tid < 0) std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+    else std::snprintf(path, sizeof(path), "/proc/%d/task/%d/stat", pid, tid);
     FILE *f = std::fopen(path, "r");
-    if (!f) return true; // no procfs view of it (other namespace): trust kill()
+    if (!f) return 0;
     char buf[512];
     const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
     std::fclose(f);
     buf[n] = 0;
     const char *rp = std::strrchr(buf, ')'); // "pid (comm) state ..."; comm may contain spaces or parentheses
-    if (!rp || rp[1] == 0 || rp[2] == 0) return true;
-    const char state = rp[2];
+    if (!rp || rp[1] == 0 || rp[2] == 0) return 0;
+    return rp[2];
+}
+
+// A crashed peer stays a zombie until its parent reaps it, and kill(pid, 0) succeeds on zombies: also check the
+// process state in /proc so that survivors abort promptly instead of waiting for the barrier timeout. "Not alive"
+// only means the peer will make no more protocol progress - NOT that its GPU work has stopped (see pid_quiesced).
+static bool pid_alive(int pid) {
+    if (kill(pid, 0) != 0 && errno != EPERM) return false;
+    const char state = proc_state(pid, -1);
+    if (state == 0) return true; // no procfs view of it (other namespace): trust kill()
     return state != 'Z' && state != 'X' && state != 'x';
 }
+
+// Whether a dead peer can no longer touch GPU memory. Its kernels and copy queues live until its address space is
+// torn down: KFD evicts the process's queues from the mm teardown (exit_mmap of the last thread holding the mm).
+// A SIGKILLed multi-threaded process shows its group leader as a zombie while other threads are still running
+// do_exit, so a zombie leader alone proves nothing. Every thread runs exit_mm (which drops the mm and, for the last
+// user, tears it down synchronously) before it turns zombie or is released, hence: quiesced once the process is
+// gone, or once every thread listed under /proc/<pid>/task is a zombie / dead.
+static bool pid_quiesced(int pid) {
+    if (kill(pid, 0) != 0 && errno == ESRCH) return true; // reaped: nothing of it is left
+    char path[64];
+    std::snprintf(path, sizeof(path), "/proc/%d/task", pid);
+    DIR *d = ::opendir(path);
+    if (!d) return errno == ENOENT; // gone between the calls; no procfs view (other namespace): not provable
+    bool quiet = true;
+    while (dirent *e = ::readdir(d)) {
+        if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+        const char st = proc_state(pid, std::atoi(e->d_name));
+        if (st != 0 && st != 'Z' && st != 'X' && st != 'x') {
+            quiet = false;
+            break;
+        }
+    }
+    ::closedir(d);
+    return quiet;
+}
+
+bool ipc_pid_quiesced_for_test(int pid) { return pid_quiesced(pid); }
+bool ipc_pid_alive_for_test(int pid) { return pid_alive(pid); }
 
 int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
     const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
@@ -534,6 +581,7 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
     const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
     const auto t0 = steady_clock::now();
     const auto timeout = milliseconds(env_size("PCCL_IPC_TIMEOUT_MS", 60000));
+    bool waited_zombie = false;
     for (size_t k = 0; k < ring_.size(); ++k) {
         if (k == rank_) continue;
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
@@ -542,7 +590,12 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
             const uint64_t vs = v >> 8;
             const uint32_t vp = static_cast<uint32_t>(v & 0xff);
             if (vs != seq + 1 || vp == PH_GATHERED || vp == PH_RELEASED || vp == PH_ABORTED) break;
-            if (!pid_alive(pids_[k])) break;
+            // a dead peer may still have kernels in flight until its address space is gone (pid_quiesced)
+            if (!pid_alive(pids_[k])) {
+                if (pid_quiesced(pids_[k])) break;
+                if (!waited_zombie) ++g_buf_stats[5];
+                waited_zombie = true;
+            }
             if (steady_clock::now() - t0 > timeout) {
                 LOG(WARN) << "IPC: peer " << k << " did not finish op seq " << seq << " before the restore";
                 break;
@@ -683,8 +736,8 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
                 be->stream_sync(stream.get());
         }
         unpin_mappings(pins);
-        release_buffer(inb);
-        release_buffer(outb);
+        quarantine_buffer(inb);
+        quarantine_buffer(outb);
         return code;
     };
     const int rc = barrier(c, tag, seq, PH_VOTED);
@@ -821,8 +874,13 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
             set_phase(seq, PH_RELEASED);
         }
         unpin_mappings(ctx.pins);
-        release_buffer(inb);
-        release_buffer(outb);
+        if (rc != 0) { // peers may have written into them for this op: never reissued (drain_peers is bounded)
+            quarantine_buffer(inb);
+            quarantine_buffer(outb);
+        } else {
+            release_buffer(inb);
+            release_buffer(outb);
+        }
         return {rc == 0, rc == 2};
     };
     if (!st) {
@@ -1001,4 +1059,11 @@ std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint6
 
 extern "C" __attribute__((visibility("default"))) void pcclxIpcStats(uint64_t *out4) {
     for (int k = 0; k < 4; ++k) out4[k] = pccl::client::g_buf_stats[k].load(std::memory_order_relaxed);
+}
+
+// All counters (see g_buf_stats); returns how many exist (writes at most n).
+extern "C" __attribute__((visibility("default"))) size_t pcclxIpcStatsEx(uint64_t *out, size_t n) {
+    constexpr size_t kN = sizeof(pccl::client::g_buf_stats) / sizeof(pccl::client::g_buf_stats[0]);
+    for (size_t k = 0; k < n && k < kN; ++k) out[k] = pccl::client::g_buf_stats[k].load(std::memory_order_relaxed);
+    return kN;
 }

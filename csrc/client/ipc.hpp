@@ -73,6 +73,11 @@ int ipc_unreachable_peer(const std::vector<uint64_t> &gpu_uids, size_t rank, int
                          const std::function<int(uint64_t)> &device_of_uid,
                          const std::function<bool(int, int)> &can_access_peer);
 
+// peer-process liveness as the IPC path sees it (exposed for the unit tests): alive = can still make protocol
+// progress; quiesced = can no longer touch GPU memory (every thread past its address-space teardown)
+bool ipc_pid_alive_for_test(int pid);
+bool ipc_pid_quiesced_for_test(int pid);
+
 class IpcArena {
 public:
     // kAbortedByMaster: the vote barrier consumed the master's abort packet for this op (exactly one is sent per op,
@@ -117,9 +122,13 @@ private:
         size_t cap = 0;
         int device = -1;
         bool busy = false;
+        bool quarantined = false; // written by an aborted op: never handed out again (freed with the arena)
     };
     CommBuf *acquire_buffer(size_t bytes, int device);
     void release_buffer(CommBuf *b);
+    // after an abort: the buffer stays busy for the rest of the arena's life, so a late write of a peer that the
+    // drain could not prove finished lands in memory no later op uses
+    void quarantine_buffer(CommBuf *b);
     struct Mapping {
         void *ptr = nullptr;
         bool vmm = false;  // imported VMM allocation (unmap) vs hipIpc mapping (close)

@@ -160,6 +160,7 @@ def _load() -> ctypes.CDLL:
         "pcclxShareableQuery": ([c_void_p, c_size_t, p(c_uint64), p(c_size_t)], c_int),
         "pcclxShareableLiveBytes": ([], c_size_t),
         "pcclxIpcStats": ([p(c_uint64)], None),
+        "pcclxIpcStatsEx": ([p(c_uint64), c_size_t], c_size_t),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

@@ -142,10 +142,13 @@ def live_bytes() -> int:
 
 def ipc_buffer_stats() -> dict:
     """How this process's xGMI/IPC ops handed their buffers to the peers since start: direct (zero-copy) vs staged
-    (copy-in / copy-out through VMM comm buffers), per input and output."""
-    out = (ctypes.c_uint64 * 4)()
-    _native.C.pcclxIpcStats(out)
-    return {"direct_in": out[0], "direct_out": out[1], "staged_in": out[2], "staged_out": out[3]}
+    (copy-in / copy-out through VMM comm buffers), per input and output; plus ``quarantined`` (staged comm buffers of
+    aborted ops, never reissued) and ``zombie_drains`` (abort drains that waited for a dead peer's threads to finish
+    tearing down its address space, i.e. its GPU queues)."""
+    out = (ctypes.c_uint64 * 8)()
+    n = int(_native.C.pcclxIpcStatsEx(out, 8))
+    keys = ("direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains")
+    return {k: int(out[i]) for i, k in enumerate(keys[:n])}
 
 
 def maybe_shareable(device) -> contextlib.AbstractContextManager:

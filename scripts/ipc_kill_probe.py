@@ -37,6 +37,9 @@ def main():
                                                             "running ring: new IPC arena with a fresh process)")
     ap.add_argument("--inject", default="", help="PCCL_FAULT_INJECT for the victim (e.g. ipc_kernel:200): it kills "
                                                  "itself at that protocol point instead of the parent's timed SIGKILL")
+    ap.add_argument("--victim-threads", type=int, default=0, help="extra busy threads in the victim process")
+    ap.add_argument("--verify-restore-ms", type=int, default=-1,
+                    help="survivors re-read an in-place buffer this long after an aborted op (must equal the input)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     from pccl_amd.utils import local_master
@@ -55,6 +58,10 @@ def main():
                 args.append("--inplace")
             if a.shareable:
                 args.append("--shareable")
+            if r == 0 and a.victim_threads:
+                args += ["--busy-threads", str(a.victim_threads)]
+            if r != 0 and a.verify_restore_ms >= 0:
+                args += ["--verify-restore-ms", str(a.verify_restore_ms)]
             penv = dict(env, PCCL_FAULT_INJECT=a.inject) if (r == 0 and a.inject) else env
             ps.append(subprocess.Popen(args, stdout=fo, stderr=fe, env=penv))
         # wait until the victim has completed a few ops, then kill it at an arbitrary point
@@ -130,13 +137,16 @@ def main():
                                "bad": sum(1 for x in oks if x.get("bad")),
                                "worlds": sorted({x["world"] for x in oks}),
                                "paths": sorted({x["path"] for x in oks}),
-                               "ipc_bufs": oks[-1].get("ipc_bufs") if oks else None}
+                               "ipc_bufs": oks[-1].get("ipc_bufs") if oks else None,
+                               "restore_checked": sum(1 for x in lines if "restore_bad" in x),
+                               "restore_bad": sum(1 for x in lines if x.get("restore_bad"))}
         with open(os.path.join(a.out, f"peer{r}.err")) as f:
             err = f.read()
         summary[f"peer{r}"]["fault_lines"] = [ln for ln in err.splitlines() if "fault" in ln.lower()][:5]
     summary["killed_after_start_s"] = round(killed_at - t0, 2)
     print(json.dumps(summary), flush=True)
-    ok = all(rc == 0 for rc in rcs) and all(summary[f"peer{r}"]["bad"] == 0 for r in range(1, len(ps)))
+    ok = all(rc == 0 for rc in rcs) and all(summary[f"peer{r}"]["bad"] == 0 and summary[f"peer{r}"]["restore_bad"] == 0
+                                            for r in range(1, len(ps)))
     sys.exit(0 if ok else 1)
 
 

@@ -18,7 +18,10 @@
 #include "client/ipc.hpp"
 #include "client/vmm_share.hpp"
 
+#include <signal.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -379,6 +382,44 @@ TEST(vmm_share_serves_fds_by_random_id_only) {
     EXPECT(client::VmmShare::fetch(::getpid(), svc.nonce(), id, 2000) < 0); // retracted
     svc.retract(id2);
     ::close(p[0]);
+}
+
+TEST(ipc_zombie_leader_with_live_threads_is_not_quiesced) {
+    // The case the IPC abort drain must not get wrong: the group leader of a peer is a zombie while other threads of
+    // the process still run (they still hold the address space, so its GPU queues may still be live).
+    int go[2];
+    EXPECT(::pipe(go) == 0);
+    const pid_t child = ::fork();
+    if (child == 0) {
+        for (int i = 0; i < 4; ++i)
+            std::thread([] {
+                while (true) std::this_thread::sleep_for(1ms);
+            }).detach();
+        if (::write(go[1], "r", 1) != 1) ::_exit(3);
+        ::syscall(SYS_exit, 0); // only the leader thread exits
+    }
+    char c;
+    EXPECT(::read(go[0], &c, 1) == 1);
+    bool zombie_leader = false;
+    for (int i = 0; i < 400 && !zombie_leader; ++i) { // leader turns zombie, its threads keep running
+        zombie_leader = !client::ipc_pid_alive_for_test(child);
+        if (!zombie_leader) std::this_thread::sleep_for(5ms);
+    }
+    EXPECT(zombie_leader);
+    EXPECT(!client::ipc_pid_quiesced_for_test(child));
+    ::kill(child, SIGKILL);
+    bool quiet = false;
+    for (int i = 0; i < 400 && !quiet; ++i) { // not reaped yet: quiesced once every thread is past do_exit
+        quiet = client::ipc_pid_quiesced_for_test(child);
+        if (!quiet) std::this_thread::sleep_for(5ms);
+    }
+    EXPECT(quiet);
+    EXPECT(client::ipc_pid_alive_for_test(::getpid()) && !client::ipc_pid_quiesced_for_test(::getpid()));
+    int st = 0;
+    ::waitpid(child, &st, 0);
+    EXPECT(client::ipc_pid_quiesced_for_test(child)); // reaped
+    ::close(go[0]);
+    ::close(go[1]);
 }
 
 TEST(mux_peer_close_is_detected) {

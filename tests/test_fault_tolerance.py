@@ -107,7 +107,7 @@ def test_gpu_peer_crash_survivors_continue(hip):
 @pytest.mark.parametrize("point,inplace,respawn,shareable", [
     ("ipc_kernel", False, False, False), ("ipc_kernel", True, False, False), ("ipc_vote", True, False, False),
     ("ipc_kernel", False, True, False), ("ipc_kernel", False, False, True), ("ipc_kernel", True, False, True)])
-def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn, shareable):
+def test_gpu_ipc_sigkill_mid_op(hip, tmp_path, point, inplace, respawn, shareable):
     """xGMI/IPC path, 3 processes on one GPU, 512 MiB bf16: peer 0 SIGKILLs itself at a fixed protocol point of op
     300 (PCCL_FAULT_INJECT) - right after launching its push kernel (every peer's kernel is then reading / writing the
     victim's exported HBM) or right after publishing its vote. Survivors must abort that op, re-form the ring and
@@ -115,14 +115,41 @@ def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn, shareable):
     joins the running ring afterwards (new arena, the BASELINE config 5 sequence). With `shareable` the peers' buffers
     live in fd-shareable memory (pccl_amd.memory): the kernels read / write the victim's own tensors (zero-copy), and
     those must survive its death just as the staged comm buffers do."""
+    summary = _ipc_kill(tmp_path, point, inplace, respawn, shareable)
+    for k in (1, 2):
+        s_k = summary[f"peer{k}"]
+        if shareable:  # the output (and, out of place, the input) went to the peers directly
+            b = s_k["ipc_bufs"]
+            assert b["direct_out"] > 300 and b["staged_out"] == 0, b
+            assert (b["direct_in"] > 300 and b["staged_in"] == 0) if not inplace else b["direct_in"] == 0, b
+
+
+@pytest.mark.gpu
+def test_gpu_ipc_sigkill_many_threads_restore_is_final(hip, tmp_path):
+    """Abort quiescence keyed to GPU state, not process state: the victim runs 48 extra busy threads, so when it is
+    SIGKILLed right after launching its push kernel its group leader turns zombie while the other threads still exit
+    (and still hold the address space whose teardown evicts its GPU queues). In-place ops in shareable memory: the
+    victim's kernel writes straight into the survivors' buffers. Each survivor waits for that teardown before it
+    restores its buffer, re-reads the buffer 200 ms after the failed op and requires the original input bit-exactly,
+    and the staged comm buffer of the aborted op is quarantined (never handed to a later op)."""
+    summary = _ipc_kill(tmp_path, "ipc_kernel", True, False, True, "--victim-threads", "48",
+                        "--verify-restore-ms", "200")
+    for k in (1, 2):
+        s_k = summary[f"peer{k}"]
+        assert s_k["restore_checked"] >= 1 and s_k["restore_bad"] == 0, s_k
+        assert s_k["ipc_bufs"]["quarantined"] >= 1, s_k
+
+
+def _ipc_kill(tmp_path, point, inplace, respawn, shareable, *extra):
+    """Runs scripts/ipc_kill_probe.py (victim = peer 0, killed at `point` of op 300) and checks the common outcome:
+    the victim died of SIGKILL, the survivors exited cleanly with exact results over both world sizes on the IPC path
+    and no GPU fault line. Returns the probe's JSON summary."""
     import sys
     probe = os.path.join(os.path.dirname(HERE), "scripts", "ipc_kill_probe.py")
-    out = os.path.join(os.path.dirname(HERE), "gpurun_out",
-                       f"pytest_ipc_kill_{point}_{int(inplace)}_{int(respawn)}_{int(shareable)}")
     args = [sys.executable, probe, "--inject", f"{point}:300", "--duration", "12" if respawn else "4", "--n",
-            str(1 << 28), "--out", out]
+            str(1 << 28), "--out", str(tmp_path / "ipc_kill")]
     args += (["--inplace"] if inplace else []) + (["--respawn"] if respawn else []) + \
-        (["--shareable"] if shareable else [])
+        (["--shareable"] if shareable else []) + list(extra)
     r = subprocess.run(args, capture_output=True, text=True, timeout=150)
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["victim_rc"] == -9, summary
@@ -134,10 +161,7 @@ def test_gpu_ipc_sigkill_mid_op(hip, point, inplace, respawn, shareable):
         s_k = summary[f"peer{k}"]
         assert s_k["bad"] == 0 and not s_k["fault_lines"], s_k
         assert 2 in s_k["worlds"] and 3 in s_k["worlds"] and s_k["ops_ok"] > 300 and s_k["paths"] == [3], s_k
-        if shareable:  # the output (and, out of place, the input) went to the peers directly
-            b = s_k["ipc_bufs"]
-            assert b["direct_out"] > 300 and b["staged_out"] == 0, b
-            assert (b["direct_in"] > 300 and b["staged_in"] == 0) if not inplace else b["direct_in"] == 0, b
+    return summary
 
 
 @pytest.mark.gpu

@@ -47,7 +47,22 @@ def main():
     ap.add_argument("--leave-when-alone", action="store_true",
                     help="exit 0 once every other peer has left after this one completed a step (a joiner whose "
                          "partners finished their run first cannot complete more steps)")
+    ap.add_argument("--busy-threads", type=int, default=0,
+                    help="extra threads that keep making syscalls (a SIGKILLed process with many live threads takes "
+                         "longer to tear down: its group leader is a zombie while the other threads still exit)")
+    ap.add_argument("--verify-restore-ms", type=int, default=-1,
+                    help="in-place: after a failed op wait this long, then require the buffer to be bit-exactly the "
+                         "input again (the abort restore must not be overwritten by a late peer write)")
     a = ap.parse_args()
+    if a.busy_threads:
+        import threading
+
+        def _busy():
+            while True:
+                os.stat("/")
+                time.sleep(0.002)
+        for _ in range(a.busy_threads):
+            threading.Thread(target=_busy, daemon=True).start()
     op = {"sum": pccl.ReduceOp.SUM, "avg": pccl.ReduceOp.AVG, "max": pccl.ReduceOp.MAX}[a.op]
     qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant == "u8" \
         else None
@@ -83,7 +98,13 @@ def main():
         try:
             info = comm.all_reduce(x, y, op=op, tag=0 if a.const else step, quantization_options=qopt)
         except pccl.PCCLError as e:
-            print(json.dumps({"rank": a.rank, "step": step, "error": e.result.name}), flush=True)
+            rec = {"rank": a.rank, "step": step, "error": e.result.name}
+            if a.verify_restore_ms >= 0 and a.inplace:
+                time.sleep(a.verify_restore_ms / 1e3)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+                rec["restore_bad"] = not bool((x == val).all())
+            print(json.dumps(rec), flush=True)
             failures += 1
             if failures > 50:
                 sys.exit(3)
