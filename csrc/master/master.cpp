@@ -19,8 +19,7 @@ Master::~Master() {
     interrupt();
     join();
     stopping_ = true;
-    for (auto &t : optimizer_threads_)
-        if (t.joinable()) t.join();
+    optimizer_pool_.stop();
 }
 
 bool Master::launch() {
@@ -604,15 +603,19 @@ void Master::run_topology_optimization(uint32_t group) {
         return;
     }
     // moonshot: asynchronous wider search; result applied at the next establishment round
+    // one moonshot per group at a time on the bounded pool (4 threads, 64 queued; reference master handler:13-14)
     BandwidthStore snapshot = gs.bw;
-    optimizer_threads_.emplace_back([this, group, ring, snapshot]() mutable {
+    const bool queued = optimizer_pool_.submit(group, [this, group, ring, snapshot]() mutable {
         if (stopping_) return;
         bool optimal = false, improved = false;
-        if (optimize_ring(snapshot, ring, true, optimal, improved) && improved) {
+        if (optimize_ring(snapshot, ring, true, optimal, improved, &stopping_) && improved && !stopping_) {
             std::lock_guard lock(pending_mtx_);
             pending_rings_[group] = {ring, optimal};
         }
     });
+    if (!queued) {
+        LOG(DEBUG) << "moonshot topology optimization of group " << group << " already running / queue full";
+    }
 }
 
 void Master::check_optimize_complete_consensus() {

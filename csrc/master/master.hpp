@@ -171,8 +171,11 @@ private:
     // async moonshot optimization
     std::mutex pending_mtx_;
     std::map<uint32_t, std::pair<std::vector<Uuid>, bool>> pending_rings_;
-    std::vector<std::thread> optimizer_threads_;
     std::atomic<bool> stopping_{false};
+    OptimizerPool optimizer_pool_{4, 64}; // declared last: stopped (joined) before the state its tasks touch
+
+public:
+    size_t optimizer_thread_count() { return optimizer_pool_.thread_count(); }
 };
 
 } // namespace pccl::master

@@ -2,7 +2,14 @@
 // reference: ccoip/src/cpp/bandwidth_store.cpp, ccoip/src/cpp/topolgy_optimizer.cpp:6-182).
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <map>
 #include <optional>
 #include <set>
@@ -40,16 +47,41 @@ struct AtspResult {
     bool ok = false;
 };
 
-// cost[i][j] < 0 means "no edge". Exact Held-Karp DP for n <= exact_limit, otherwise randomized
-// nearest-neighbour construction + Or-opt/2-opt/3-opt-segment-insertion local search with restarts until
-// `time_limit_ms`. Deterministic for a given seed.
+// cost[i][j] < 0 means "no edge". Exact Held-Karp DP for n <= exact_limit (at most 20), otherwise randomised
+// construction + iterated local search (Or-opt, or-3opt segment swap, 2-opt; double-bridge kicks) with `restarts`
+// restarts inside `time_limit_ms`. A set `cancel` ends the search early (best tour so far). Deterministic for a given
+// seed when the time budget does not bind.
 AtspResult solve_atsp(const std::vector<std::vector<double>> &cost, int exact_limit, int time_limit_ms,
-                      int restarts, uint64_t seed);
+                      int restarts, uint64_t seed, const std::atomic<bool> *cancel = nullptr);
 
 // Computes a ring order over `ring` using measured bandwidths (cost = 1000 / Mbit/s). `moonshot` widens the exact
 // bound and search budget (the reference's "ImproveTopologyMoonshot").
 bool optimize_ring(const BandwidthStore &store, std::vector<Uuid> &ring, bool moonshot, bool &is_optimal,
-                   bool &improved);
+                   bool &improved, const std::atomic<bool> *cancel = nullptr);
+
+// Bounded worker pool for the asynchronous (moonshot) optimizations, like the reference master's thread pool of 4
+// threads with a queue of 64 (ccoip_master_handler.cpp:13-14): at most `threads` workers, at most `queue` waiting
+// tasks (submit() returns false beyond that), one task per key (a group) queued or running at a time.
+class OptimizerPool {
+public:
+    OptimizerPool(size_t threads, size_t queue) : max_threads_(threads), max_queue_(queue) {}
+    ~OptimizerPool(); // cancels waiting tasks, joins the workers
+    bool submit(uint64_t key, std::function<void()> fn);
+    size_t thread_count();
+    size_t pending();
+    void stop();
+
+private:
+    void loop();
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::pair<uint64_t, std::function<void()>>> q_;
+    std::set<uint64_t> active_; // keys queued or running
+    std::vector<std::thread> threads_;
+    size_t idle_ = 0;
+    const size_t max_threads_, max_queue_;
+    bool stop_ = false;
+};
 
 double ring_cost(const BandwidthStore &store, const std::vector<Uuid> &ring);
 

@@ -204,6 +204,89 @@ TEST(atsp_exact_matches_brute_force) {
     }
 }
 
+TEST(atsp_heuristic_within_2pct_of_exact) {
+    // 50 random asymmetric instances, n = 12..16: the heuristic (exact search disabled) against Held-Karp
+    std::mt19937_64 rng(2024);
+    double worst = 0, sum = 0;
+    int optimal_hits = 0;
+    for (int inst = 0; inst < 50; ++inst) {
+        const int n = 12 + inst % 5;
+        std::uniform_real_distribution<double> d(1.0, 100.0);
+        std::vector<std::vector<double>> c(n, std::vector<double>(n, 0));
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) c[i][j] = i == j ? -1 : d(rng);
+        const auto exact = master::solve_atsp(c, 20, 1000, 1, 42);
+        const auto heur = master::solve_atsp(c, 0, 1000, 4, 42);
+        EXPECT(exact.ok && exact.optimal && heur.ok && !heur.optimal);
+        const double gap = heur.cost / exact.cost - 1.0;
+        EXPECT(gap >= -1e-9);
+        worst = std::max(worst, gap);
+        sum += gap;
+        optimal_hits += gap < 1e-9;
+    }
+    std::printf("    atsp heuristic vs Held-Karp: mean gap %.3f %%, worst %.3f %%, optimal %d / 50\n", 100 * sum / 50,
+                100 * worst, optimal_hits);
+    EXPECT(worst <= 0.02);
+}
+
+TEST(atsp_64_nodes_within_budget) {
+    std::mt19937_64 rng(5);
+    std::uniform_real_distribution<double> d(1.0, 100.0);
+    const int n = 64;
+    std::vector<std::vector<double>> c(n, std::vector<double>(n, 0));
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) c[i][j] = i == j ? -1 : d(rng);
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto r = master::solve_atsp(c, 8, 1000, 4, 42); // the reference's synchronous budget
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    EXPECT(r.ok && r.tour.size() == 64u && s < 1.5);
+    std::vector<int> seen = r.tour;
+    std::sort(seen.begin(), seen.end());
+    for (int i = 0; i < n; ++i) EXPECT(seen[i] == i);
+    // a greedy nearest-neighbour tour is a weak upper bound: the search must beat it
+    std::vector<int> nn = {0};
+    std::vector<bool> used(n, false);
+    used[0] = true;
+    for (int k = 1; k < n; ++k) {
+        int b = -1;
+        for (int j = 0; j < n; ++j)
+            if (!used[j] && (b < 0 || c[nn.back()][j] < c[nn.back()][b])) b = j;
+        used[b] = true;
+        nn.push_back(b);
+    }
+    double nn_cost = 0;
+    for (int i = 0; i < n; ++i) nn_cost += c[nn[i]][nn[(i + 1) % n]];
+    std::printf("    atsp n=64: %.3f s, cost %.1f (nearest neighbour %.1f)\n", s, r.cost, nn_cost);
+    EXPECT(r.cost < nn_cost);
+    // cancellation returns promptly with a valid tour
+    std::atomic<bool> cancel{true};
+    const auto t1 = std::chrono::steady_clock::now();
+    const auto rc = master::solve_atsp(c, 8, 30000, 16, 42, &cancel);
+    EXPECT(rc.ok && std::chrono::steady_clock::now() - t1 < std::chrono::seconds(2));
+}
+
+TEST(optimizer_pool_bounds_threads_and_queue) {
+    master::OptimizerPool pool(4, 64);
+    std::atomic<int> ran{0};
+    std::atomic<bool> release{false};
+    int accepted = 0;
+    for (uint64_t k = 0; k < 100; ++k) // 100 optimize rounds of 100 groups while the first ones block
+        accepted += pool.submit(k, [&] {
+            while (!release.load()) std::this_thread::sleep_for(1ms);
+            ++ran;
+        });
+    EXPECT(pool.thread_count() <= 4);
+    EXPECT(accepted <= 4 + 64 && accepted >= 64);
+    EXPECT(!pool.submit(0, [] {})); // key 0 still queued / running
+    release = true;
+    for (int i = 0; i < 500 && ran.load() < accepted; ++i) std::this_thread::sleep_for(10ms);
+    EXPECT(ran.load() == accepted);
+    for (int i = 0; i < 100 && pool.pending() > 0; ++i) std::this_thread::sleep_for(5ms);
+    for (int round = 0; round < 100; ++round) pool.submit(7, [&] { ++ran; }); // one group, 100 rounds
+    EXPECT(pool.thread_count() <= 4);
+    pool.stop();
+}
+
 TEST(atsp_heuristic_is_valid_tour) {
     const int n = 40;
     std::mt19937_64 rng(3);
