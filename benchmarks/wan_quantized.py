@@ -6,8 +6,11 @@
 Defaults model a transatlantic long fat pipe: 50 ms one way, ~1 Gbit/s per TCP flow (window-limited at 100 ms RTT),
 a 25 Gbit/s NIC per peer (the reference's transatlantic figure), 16 pooled connections per neighbour.
 
-Peer processes on one host with the built-in WAN emulation (PCCL_SIM_WAN, csrc/net/mux.hpp: one-way latency, a
-per-TCP-flow rate and a per-peer shared link rate -- tc-netem needs root, which the benchmark boxes do not grant).
+Peer processes on one host behind a WAN emulator -- tc-netem needs root, which the benchmark boxes do not grant:
+  * --emulator relay (default): pccl_wan_relay, a separate process outside the library (csrc/tools/wan_relay.cpp);
+    every peer advertises a relay port as its P2P address and the relay delays each byte by the one-way latency and
+    paces it per TCP connection and per link (token buckets). The library cannot influence this link.
+  * --emulator builtin: the in-library pacing model (PCCL_SIM_WAN, csrc/net/mux.hpp), for comparison.
 The xGMI IPC path is disabled (PCCL_DISABLE_IPC=1) so every byte crosses the emulated WAN through the TCP ring:
 device tensors are staged through pinned memory and (de)quantized by the HIP kernels.
 For each wire format (fp32 / uint8 min-max / int8 zero-point-scale / fp8 e4m3 min-max) an AVG all-reduce of --mib MiB
@@ -40,7 +43,8 @@ def peer(a):
     dev = torch.device(a.device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool)
+    ports = json.loads(a.ports) if a.ports else {}
+    comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool, **ports)
     comm.connect(n_attempts=60)
     wait_for_world(comm, a.peers, timeout=300)
     D, Q = pccl.DataType, pccl.QuantizationAlgorithm
@@ -97,21 +101,52 @@ def main():
     ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--formats", default=",".join(FORMATS))
+    ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
+    ap.add_argument("--ports", default="", help=argparse.SUPPRESS)  # internal: Communicator port kwargs (JSON)
     ap.add_argument("--rank", type=int, default=None)
     ap.add_argument("--master", default=None)
     a = ap.parse_args()
     if a.rank is not None:
         return peer(a)
-    from pccl_amd.utils import local_master, spawn_python
-    env = {"PCCL_SIM_WAN": f"{a.latency_ms}:{a.flow_mbit}:{a.link_mbit}", "PCCL_DISABLE_IPC": "1",
-           "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)}
+    from pccl_amd.utils import free_ports, local_master, spawn_python
+    env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)}
     args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
             "--concurrent", str(a.concurrent),
             "--formats", a.formats]
-    with local_master() as addr:
-        ps = [spawn_python([os.path.abspath(__file__), "--rank", str(r), "--master", addr, *args], env=env,
-                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(a.peers)]
-        outs = [p.communicate(timeout=1500) for p in ps]
+    relay = None
+    peer_ports = [{} for _ in range(a.peers)]
+    if a.emulator == "builtin":
+        env["PCCL_SIM_WAN"] = f"{a.latency_ms}:{a.flow_mbit}:{a.link_mbit}"
+    else:
+        fp = free_ports(4 * a.peers)
+        maps = []
+        for r in range(a.peers):
+            listen, adv, ss, bm = fp[4 * r:4 * r + 4]
+            peer_ports[r] = {"p2p_listen_port": listen, "advertised_p2p_port": adv, "shared_state_listen_port": ss,
+                             "benchmark_listen_port": bm}
+            maps += ["--map", f"{adv}:{listen}"]
+        exe = os.path.join(ROOT, "pccl_amd", "lib", "pccl_wan_relay")
+        relay = subprocess.Popen([exe, "--delay-ms", str(a.latency_ms), "--flow-mbit", str(a.flow_mbit),
+                                  "--link-mbit", str(a.link_mbit), *maps], stdout=subprocess.PIPE,
+                                 stderr=subprocess.DEVNULL, text=True)
+        relay.stdout.readline()  # {"relay": "ready"}
+    try:
+        with local_master() as addr:
+            ps = [spawn_python([os.path.abspath(__file__), "--rank", str(r), "--master", addr, "--ports",
+                                json.dumps(peer_ports[r]), *args], env=env,
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(a.peers)]
+            outs = [p.communicate(timeout=1500) for p in ps]
+    finally:
+        relayed = None
+        if relay is not None:
+            relay.terminate()
+            try:
+                line = relay.stdout.readline()
+                relayed = json.loads(line).get("relayed_bytes") if line.startswith("{") else None
+                relay.wait(timeout=10)
+            except (subprocess.TimeoutExpired, ValueError):
+                relay.kill()
+                relay.wait()
     res = []
     for p, (o, e) in zip(ps, outs):
         if p.returncode != 0:
@@ -131,8 +166,11 @@ def main():
     print(json.dumps({"metric": "quantized all-reduce over emulated WAN",
                       "config": "int8-quantized all-reduce over tc-netem 50 ms simulated WAN, 8 peers",
                       "peers": a.peers, "mib_per_peer": a.mib, "device": a.device,
-                      "wan": {"one_way_latency_ms": a.latency_ms, "flow_mbit": a.flow_mbit, "link_mbit": a.link_mbit,
-                              "pool": a.pool, "concurrent_ops": a.concurrent},
+                      "wan": {"emulator": "pccl_wan_relay (separate process)" if a.emulator == "relay"
+                              else "PCCL_SIM_WAN (inside the library)",
+                              "one_way_latency_ms": a.latency_ms, "flow_mbit": a.flow_mbit, "link_mbit": a.link_mbit,
+                              "pool": a.pool, "concurrent_ops": a.concurrent,
+                              "relayed_GB": round(relayed / 1e9, 3) if relayed is not None else None},
                       "reference_published_Gbit": {"transatlantic": 25, "collocated_eu": 45},
                       "formats": summary}), flush=True)
 

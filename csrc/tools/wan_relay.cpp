@@ -1,0 +1,250 @@
+// Userspace WAN emulator OUTSIDE libpccl (BASELINE config 3 without tc-netem, which needs root): a TCP relay that
+// delays every byte by a fixed one-way latency and paces it through token buckets, per TCP connection (a window-
+// limited long-fat-pipe flow) and per relayed link (the sending peer's NIC). Peers advertise a relay port as their
+// P2P address (Communicator(..., advertised_p2p_port=...)); the relay forwards each accepted connection to the real
+// listen port. Nothing inside the library is shaped, so the measurement is the library's behaviour over a link it
+// cannot influence.
+//
+//   pccl_wan_relay --delay-ms 50 --flow-mbit 1000 --link-mbit 25000 --map 40001:48149 [--map 40002:48152 ...]
+//
+// Model: one-way delay d in both directions; a connection's bytes leave the relay no earlier than arrival + d and no
+// faster than flow_mbit (per direction); all bytes relayed towards one map target share link_mbit (in a ring, all
+// of them come from the target's predecessor, so this is that peer's egress link). The relay reads at most
+// 2 x d x flow_rate bytes ahead per direction (the bandwidth-delay product of the flow: the window a real WAN TCP
+// connection would have in flight), so senders feel back-pressure as on a real long fat pipe.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
+void sleep_until_s(double t) {
+    const double d = t - now_s();
+    if (d > 0) std::this_thread::sleep_for(std::chrono::duration<double>(d));
+}
+
+struct Config {
+    double delay_s = 0.05, flow_Bps = 125e6, link_Bps = 0;
+};
+Config g_cfg;
+std::atomic<uint64_t> g_bytes{0};
+volatile sig_atomic_t g_stop = 0;
+
+// shared egress link of one map target (all connections relayed towards it)
+struct Link {
+    std::mutex m;
+    double next_free = 0;
+    // reserves n bytes on the link no earlier than t; returns when they have left
+    double reserve(size_t n, double t) {
+        if (g_cfg.link_Bps <= 0) return t;
+        std::lock_guard l(m);
+        const double start = std::max(t, next_free);
+        next_free = start + static_cast<double>(n) / g_cfg.link_Bps;
+        return next_free;
+    }
+};
+
+struct Chunk {
+    double arrival;
+    std::vector<char> data;
+};
+
+// one direction of one connection: reader thread -> delay queue -> paced writer thread
+class Pump {
+public:
+    Pump(int src, int dst, Link *link) : src_(src), dst_(dst), link_(link) {
+        window_ = std::max<size_t>(1 << 20, static_cast<size_t>(2 * g_cfg.delay_s * g_cfg.flow_Bps));
+    }
+    void run() {
+        std::thread r([this] { reader(); });
+        writer();
+        r.join();
+    }
+
+private:
+    void reader() {
+        while (true) {
+            std::vector<char> buf(256 << 10);
+            const ssize_t k = ::recv(src_, buf.data(), buf.size(), 0);
+            if (k <= 0) break;
+            buf.resize(static_cast<size_t>(k));
+            std::unique_lock l(m_);
+            cv_.wait(l, [&] { return queued_ < window_ || closed_; });
+            if (closed_) break;
+            queued_ += buf.size();
+            q_.push_back({now_s(), std::move(buf)});
+            cv_.notify_all();
+        }
+        std::lock_guard l(m_);
+        eof_ = true;
+        cv_.notify_all();
+    }
+    void writer() {
+        double flow_next = 0;
+        while (true) {
+            Chunk c;
+            {
+                std::unique_lock l(m_);
+                cv_.wait(l, [&] { return !q_.empty() || eof_; });
+                if (q_.empty()) break;
+                c = std::move(q_.front());
+                q_.pop_front();
+            }
+            const size_t n = c.data.size();
+            double t = std::max(c.arrival + g_cfg.delay_s, flow_next);
+            flow_next = t + static_cast<double>(n) / g_cfg.flow_Bps;
+            t = std::max(flow_next, link_ ? link_->reserve(n, t) : t);
+            sleep_until_s(t);
+            size_t off = 0;
+            bool ok = true;
+            while (off < n) {
+                const ssize_t k = ::send(dst_, c.data.data() + off, n - off, MSG_NOSIGNAL);
+                if (k <= 0) {
+                    ok = false;
+                    break;
+                }
+                off += static_cast<size_t>(k);
+            }
+            g_bytes += off;
+            {
+                std::lock_guard l(m_);
+                queued_ -= n;
+                cv_.notify_all();
+            }
+            if (!ok) break;
+        }
+        {
+            std::lock_guard l(m_);
+            closed_ = true;
+            cv_.notify_all();
+        }
+        ::shutdown(dst_, SHUT_WR);
+        ::shutdown(src_, SHUT_RD);
+    }
+    int src_, dst_;
+    Link *link_;
+    size_t window_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<Chunk> q_;
+    size_t queued_ = 0;
+    bool eof_ = false, closed_ = false;
+};
+
+void tune(int fd) {
+    int one = 1, buf = 32 << 20;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+int listen_on(uint16_t port) {
+    const int s = ::socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    setsockopt(s, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = htons(port);
+    if (::bind(s, reinterpret_cast<sockaddr *>(&a), sizeof(a)) != 0 || ::listen(s, 256) != 0) {
+        std::fprintf(stderr, "wan_relay: cannot listen on %u\n", port);
+        std::exit(2);
+    }
+    return s;
+}
+
+int connect_to(uint16_t port) {
+    const int s = ::socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = htons(port);
+    for (int attempt = 0; attempt < 50; ++attempt) {
+        if (::connect(s, reinterpret_cast<sockaddr *>(&a), sizeof(a)) == 0) return s;
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    ::close(s);
+    return -1;
+}
+
+void serve(uint16_t listen_port, uint16_t target) {
+    const int ls = listen_on(listen_port);
+    auto *link = new Link(); // lives as long as the process
+    while (true) {
+        const int c = ::accept(ls, nullptr, nullptr);
+        if (c < 0) continue;
+        std::thread([c, target, link] {
+            const int t = connect_to(target);
+            if (t < 0) {
+                ::close(c);
+                return;
+            }
+            tune(c);
+            tune(t);
+            Pump up(c, t, link), down(t, c, nullptr); // towards the target: the predecessor's egress link
+            std::thread d([&] { down.run(); });
+            up.run();
+            d.join();
+            ::close(c);
+            ::close(t);
+        }).detach();
+    }
+}
+
+} // namespace
+
+int main(int argc, char **argv) {
+    std::vector<std::pair<uint16_t, uint16_t>> maps;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        const std::string k = argv[i];
+        const char *v = argv[i + 1];
+        if (k == "--delay-ms") g_cfg.delay_s = std::atof(v) / 1e3;
+        else if (k == "--flow-mbit") g_cfg.flow_Bps = std::atof(v) * 1e6 / 8;
+        else if (k == "--link-mbit") g_cfg.link_Bps = std::atof(v) * 1e6 / 8;
+        else if (k == "--map") {
+            unsigned a = 0, b = 0;
+            if (std::sscanf(v, "%u:%u", &a, &b) != 2) return 2;
+            maps.emplace_back(static_cast<uint16_t>(a), static_cast<uint16_t>(b));
+        } else {
+            std::fprintf(stderr, "usage: %s --delay-ms D --flow-mbit F --link-mbit L --map LISTEN:TARGET ...\n", argv[0]);
+            return 2;
+        }
+    }
+    if (maps.empty()) return 2;
+    signal(SIGPIPE, SIG_IGN);
+    signal(SIGTERM, [](int) { g_stop = 1; });
+    for (auto [l, t] : maps) std::thread(serve, l, t).detach();
+    std::printf("{\"relay\": \"ready\", \"maps\": %zu}\n", maps.size());
+    std::fflush(stdout);
+    // until SIGTERM: relayed bytes once a second on stderr, the total as JSON on stdout at the end
+    uint64_t last = 0;
+    while (!g_stop) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        const uint64_t b = g_bytes.load();
+        if (b - last > (1ull << 30)) {
+            std::fprintf(stderr, "wan_relay: %.3f GB relayed\n", b / 1e9);
+            last = b;
+        }
+    }
+    std::printf("{\"relay\": \"done\", \"relayed_bytes\": %llu}\n", static_cast<unsigned long long>(g_bytes.load()));
+    std::fflush(stdout);
+    std::_Exit(0);
+}
