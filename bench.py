@@ -60,6 +60,7 @@ def _args():
     ap.add_argument("--quick", action="store_true", help="headline only (no IPC / sweep / latency extras)")
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     ap.add_argument("--no-peer-curve", action="store_true", help="skip the 2 / 4 peer points of the 1 GiB curve")
+    ap.add_argument("--no-quant-extra", action="store_true", help="skip the uint8-quantized device ring in extra")
     ap.add_argument("--extras-child", default="", help=argparse.SUPPRESS)  # internal: run only the extras, write JSON
     return ap.parse_args()
 
@@ -188,7 +189,7 @@ class Job:
         return out
 
 
-def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None):
+def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None, qopt=None):
     """warmup + `steps` timed all-reduces between job-wide barriers; returns (seconds, tx, rx, path, cpu seconds).
     `ops` (optional list) receives the wall time of every timed op as seen by this peer."""
     import pccl_amd as pccl
@@ -196,7 +197,7 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None):
     for s in range(warmup):
         for attempt in range(3):  # an aborted warmup op (e.g. xGMI vote fell back) is retried by all peers
             try:
-                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + s)
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + s, quantization_options=qopt)
                 break
             except pccl.PCCLError:
                 if attempt == 2:
@@ -209,7 +210,7 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None):
     tx = rx = 0
     for s in range(steps):
         ta = time.perf_counter()
-        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + warmup + s)
+        info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag0 + warmup + s, quantization_options=qopt)
         if ops is not None:
             ops.append(time.perf_counter() - ta)
         tx += info.tx_bytes
@@ -301,7 +302,7 @@ def _curve_point(nbytes, t, n):
     return {"ms": round(t * 1e3, 4), "bus_bw_per_peer_GBps": round(_bw(nbytes, t, n)[1], 3)}
 
 
-def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, windows=1):
+def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, windows=1, quant=False):
     """Runs one phase; returns {"t": s/op (max over the job), "tx", "rx", "path", "sweep": {bytes: s/op}, "ok",
     "windows": [s/op of each timed window (the first is "t")], "op_ms": per-op wall times of peer 0 in window 1}."""
     torch = job.torch
@@ -319,7 +320,8 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, 
             x = torch.randn(n, device=job.dev, dtype=torch.bfloat16, generator=g)
             y = torch.empty_like(x)
         ops = []
-        r = {"main": _timed(job, i, comm, x, y, steps, warmup, ops=ops), "ops": ops, "win": []}
+        qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if quant else None
+        r = {"main": _timed(job, i, comm, x, y, steps, warmup, ops=ops, qopt=qopt), "ops": ops, "win": []}
         tag = 5_000
         for _w in range(1, windows):  # further windows of the same ops (the first one is the reported value)
             r["win"].append(_timed(job, i, comm, x, y, steps, 0, tag0=tag)[0])
@@ -434,6 +436,8 @@ def run_extras(job, a, nbytes):
                                for b, t in ipc["sweep"].items()}
         sweep["DEVICE_IPC"][f"{a.mib}MiB"] = {"ms": round(ipc["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(ibus, 3)}
         extra["latency_1MiB_ipc_us"] = round(ipc["sweep"][1 << 20] * 1e6, 1)
+        # how this rank's IPC ops handed buffers over, incl. the cross-GPU pre-flight result (pccl_amd.memory)
+        extra["ipc_buffer_stats_rank0"] = pccl.memory.ipc_buffer_stats()
         if job.world == 1:
             two = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=2)
             talg, tbus = _bw(nbytes, two["t"], 2)
@@ -441,6 +445,14 @@ def run_extras(job, a, nbytes):
                                          "reduce_path": pccl.ReducePath(two["path"]).name}
             curve.setdefault("DEVICE_IPC", {})["2"] = _curve_point(nbytes, two["t"], 2)
             curve["DEVICE_IPC"][str(P)] = _curve_point(nbytes, ipc["t"], P)
+    if not a.no_quant_extra:
+        # the quantized wire format on the same device ring (uint8 min-max: bf16 -> u8 on the GPU, 2x fewer bytes on
+        # the wire; BASELINE config 3's format without the WAN)
+        qr = measure(job, ipc=False, nbytes=nbytes, steps=max(3, a.steps // 2), warmup=2, quant=True)
+        extra["ring_quant_u8_same_peers"] = {"ms_per_op": round(qr["t"] * 1e3, 3),
+                                             "bus_bw_per_peer_GBps": round(_bw(nbytes, qr["t"], P)[1], 3),
+                                             "wire_tx_bytes_per_op_rank0": qr["tx"],
+                                             "reduce_path": pccl.ReducePath(qr["path"]).name}
     if job.world == 1 and not a.no_peer_curve:
         # the metric's "2/4/8 peers": the same 1 GiB all-reduce at fewer peers (8 is the headline / ipc_same_peers)
         for p in (2, 4):
@@ -501,6 +513,8 @@ def extras_in_child(job, a):
         args.append("--no-ipc-extra")
     if a.no_peer_curve:
         args.append("--no-peer-curve")
+    if a.no_quant_extra:
+        args.append("--no-quant-extra")
     env = dict(os.environ)
     if job.world > 1:
         env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 11)

@@ -1327,12 +1327,31 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     auto quant_ready = [&](size_t end) { return end == 0 || event_wait_polling(be, ev((end - 1) / (piece_el * qs))); };
     auto always_ready = [](size_t) { return true; };
 
+    // No stream synchronisation per step: the reduce-scatter's next quantization reads its min / max after the
+    // previous step's de-quantize kernels in stream order (quantize_to_pinned syncs once for the meta packet), and an
+    // all-gather step's received bytes are de-quantized asynchronously while the next step forwards them. A pinned
+    // sink is refilled two steps later, so step s waits only for the kernels that read its sink at step s-2.
+    DevEvent sink_read[2] = {nullptr, nullptr};
+    struct SinkEvents { // back to the pool once the op's stream is drained
+        DeviceBackend *be;
+        DevStream s;
+        DevEvent e[2];
+        ~SinkEvents() {
+            be->stream_sync(s);
+            for (auto x : e) event_pool().put(x);
+        }
+    } sink_events{be, st, {event_pool().get(), event_pool().get()}};
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
                         uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx) -> int {
+        const int b = sink == rxbuf[0] ? 0 : 1;
+        if (sink_read[b]) event_wait_polling(be, sink_read[b]);
         const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs,
                                     piece_el * qs, consume, aborted, op.tx, op.rx, before_rx, piece_el * qs);
-        if (rc == 0) be->stream_sync(st); // everything consumed from `sink` has landed in HBM
+        if (rc == 0) {
+            sink_read[b] = sink_events.e[b]; // waited for above before it is recorded again
+            be->event_record(sink_read[b], st);
+        }
         return rc;
     };
     auto fail = [&](int code) -> std::pair<bool, bool> {

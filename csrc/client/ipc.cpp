@@ -33,7 +33,7 @@ constexpr uint32_t kClosed = 0x80000000u;
 constexpr uint32_t kSlots = 128; // ops in flight per ring (slot = seq % kSlots)
 constexpr uint32_t kMaxWorld = 16;
 
-constexpr uint32_t PH_VOTED = 1, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
+constexpr uint32_t PH_VOTED = 1, PH_PROBED = 2, PH_REDUCED = 3, PH_GATHERED = 4, PH_RELEASED = 5, PH_ABORTED = 0xEE;
 
 uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
     const auto *b = static_cast<const uint8_t *>(p);
@@ -110,8 +110,9 @@ struct OpCtx {
 // per-process counters of how op buffers were handed to the peers (pcclxIpcStats): [0] direct inputs, [1] direct
 // outputs, [2] staged inputs, [3] staged outputs
 // [0..3] direct_in, direct_out, staged_in, staged_out; [4] comm buffers quarantined after an abort; [5] drains that
-// waited for a dead peer's threads to finish tearing down its address space
-static std::atomic<uint64_t> g_buf_stats[6];
+// waited for a dead peer's threads to finish tearing down its address space; [6] / [7] cross-GPU pre-flight probes
+// failed / passed
+static std::atomic<uint64_t> g_buf_stats[8];
 
 // per-process bookkeeping
 static std::mutex g_ctx_mtx;
@@ -123,6 +124,24 @@ int ipc_grid_budget(const std::vector<uint64_t> &gpu_uids, size_t rank) {
     int sharing = 0;
     for (uint64_t u : gpu_uids) sharing += u == gpu_uids[rank] ? 1 : 0;
     return std::max(256, 512 / std::max(1, sharing));
+}
+
+bool ipc_needs_preflight(const std::vector<uint64_t> &gpu_uids, bool done, size_t bytes) {
+    // PCCL_IPC_PREFLIGHT: 0 off, 1 (default) rings spanning several GPUs, 2 every ring (rehearsal on one GPU)
+    static const size_t mode = env_size("PCCL_IPC_PREFLIGHT", 1);
+    if (done || mode == 0 || bytes < gpu_uids.size() * 256) return false;
+    if (mode >= 2) return true;
+    for (uint64_t u : gpu_uids)
+        if (u != gpu_uids[0]) return true;
+    return false;
+}
+
+int ipc_push_grid(const std::vector<uint64_t> &gpu_uids, size_t rank, int remote_grid) {
+    const int base = ipc_grid_budget(gpu_uids, rank);
+    if (remote_grid <= 0) return base;
+    for (uint64_t u : gpu_uids)
+        if (u != gpu_uids[rank]) return std::min(remote_grid, 4096);
+    return base;
 }
 
 int ipc_unreachable_peer(const std::vector<uint64_t> &gpu_uids, size_t rank, int my_device,
@@ -834,6 +853,42 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     return kUseIpc;
 }
 
+bool IpcArena::preflight(Client &c, uint64_t tag, uint64_t seq, OpCtx &ctx, int device, DevStream st) {
+    DeviceBackend *be = device_backend();
+    const size_t W = ring_.size();
+    constexpr size_t kSlot = 256;
+    std::vector<uint32_t> pat(kSlot / 4);
+    auto pattern = [&](size_t from) {
+        for (size_t i = 0; i < pat.size(); ++i)
+            pat[i] = 0x9e3779b9u * static_cast<uint32_t>(seq + 1) ^ static_cast<uint32_t>(from << 16 | i);
+    };
+    Lease src(device_pool(), kSlot, device);
+    if (!src.ok()) return false;
+    pattern(rank_);
+    bool ok = be->memcpy_async(src.data(), pat.data(), kSlot, st) && be->stream_sync(st);
+    for (size_t k = 0; k < W && ok; ++k) {
+        if (k == rank_) continue;
+        const void *s = src.data();
+        const size_t zero = 0, n = kSlot;
+        ok = be->multi_gather(ctx.out[k].at(rank_ * kSlot), &s, &zero, &n, 1, -1, DType::U8, st, true);
+    }
+    ok = ok && be->stream_sync(st);
+    if (!ok) return false;
+    set_phase(seq, PH_PROBED);
+    if (barrier(c, tag, seq, PH_PROBED) != 0) return false;
+    std::vector<uint32_t> got(W * kSlot / 4);
+    if (!be->memcpy_async(got.data(), ctx.out[rank_].at(0), W * kSlot, st) || !be->stream_sync(st)) return false;
+    for (size_t k = 0; k < W; ++k) {
+        if (k == rank_) continue;
+        pattern(k);
+        if (std::memcmp(got.data() + k * kSlot / 4, pat.data(), kSlot) != 0) {
+            LOG(ERR) << "IPC pre-flight: the probe of peer " << k << " did not arrive in my output buffer";
+            return false;
+        }
+    }
+    return true;
+}
+
 std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
                                     DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
                                     std::atomic<uint64_t> &rx, const InterHost *inter, size_t world) {
@@ -911,7 +966,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     // peers whose kernels run concurrently on this GPU, but not below 256 per kernel (fewer cannot saturate HBM)
     std::vector<uint64_t> uids(W);
     for (size_t k = 0; k < W; ++k) uids[k] = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->gpu_uid;
-    const int grid = ipc_grid_budget(uids, rank_);
+    static const int remote_grid = static_cast<int>(env_size("PCCL_IPC_REMOTE_GRID", 0));
+    const int grid = ipc_push_grid(uids, rank_, remote_grid);
     // system-scope release at kernel end when a destination lives on another GPU, or is a staged buffer that the
     // copy-out reads with a copy engine: without it whole 4 KiB workgroup tiles of the result were still zero in the
     // copy (measured: test_device_ipc_modes, 6144 stale floats in 6 tiles of a 12 MB op)
@@ -919,6 +975,23 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     for (size_t k = 0; k < W; ++k) {
         const OpPeerShm *p = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k));
         remote = remote || uids[k] != uids[rank_] || !(p->zero_copy & 2u);
+    }
+
+    // Pre-flight on the first cross-GPU op of this arena: every peer writes a 256-byte pattern into slot `rank` of
+    // every other peer's output through the same mappings the push kernels use (system-scope release), then reads
+    // its own slots back. A write that did not land (wrong access flags on an imported allocation, a broken peer
+    // mapping) fails this op and makes this peer vote for the TCP ring from now on, instead of every later op
+    // producing wrong results; the kernels below overwrite the slots.
+    if (ipc_needs_preflight(uids, preflight_done_, bytes)) {
+        preflight_done_ = true;
+        if (!preflight(c, tag, seq, ctx, device, st)) {
+            ++g_buf_stats[6];
+            map_failed_.store(true, std::memory_order_relaxed);
+            LOG(ERR) << "IPC: cross-GPU pre-flight failed on device " << device << "; using the TCP ring for later ops";
+            return finish(1);
+        }
+        ++g_buf_stats[7];
+        trace_mark("preflight");
     }
 
     if (inter) {

@@ -76,7 +76,15 @@ int ipc_unreachable_peer(const std::vector<uint64_t> &gpu_uids, size_t rank, int
 // peer-process liveness as the IPC path sees it (exposed for the unit tests): alive = can still make protocol
 // progress; quiesced = can no longer touch GPU memory (every thread past its address-space teardown)
 bool ipc_pid_alive_for_test(int pid);
+// Whether an op on this ring runs the cross-GPU pre-flight write probe (first op of an arena whose peers span more
+// than one GPU and that is large enough to hold one 256-byte probe slot per peer); identical on every peer.
+bool ipc_needs_preflight(const std::vector<uint64_t> &gpu_uids, bool done, size_t bytes);
+// Workgroup budget of this peer's push kernel: ipc_grid_budget, or `remote_grid` (> 0, PCCL_IPC_REMOTE_GRID) when a
+// destination lives on another GPU (remote xGMI writes and reads have more latency to cover).
+int ipc_push_grid(const std::vector<uint64_t> &gpu_uids, size_t rank, int remote_grid);
 bool ipc_pid_quiesced_for_test(int pid);
+
+struct OpCtx; // per-op mapping context (ipc.cpp)
 
 class IpcArena {
 public:
@@ -85,6 +93,7 @@ public:
     static constexpr int kUseIpc = 1, kUseRing = 0, kAborted = -1, kAbortedByMaster = -2;
     using MapKey = std::tuple<int, std::array<uint8_t, kIpcHandleBytes>, int>; // (peer, handle, my device)
     std::atomic<bool> map_failed_{false}; // a peer's IPC handle could not be opened: stop voting for xGMI
+    bool preflight_done_ = false;         // the cross-GPU write probe ran on this arena (first eligible op)
 
     static std::shared_ptr<IpcArena> create(Client &c, const std::vector<Uuid> &ring, uint16_t master_port,
                                             uint32_t group);
@@ -142,6 +151,8 @@ private:
     bool export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset);
     // waits until every peer reached `phase` for `seq`; 0 ok, 1 failure (peer dead/aborted/timeout), 2 master abort
     int barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase);
+    // cross-GPU write probe of one op (see run()); true if every peer's probe arrived in my output
+    bool preflight(Client &c, uint64_t tag, uint64_t seq, OpCtx &ctx, int device, DevStream st);
     void set_phase(uint64_t seq, uint32_t phase);
     bool wait_slot_free(Client &c, uint64_t seq);
     // waits until no live peer can still write into my receive buffer for `seq` (push algorithm, abort path)

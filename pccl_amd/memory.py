@@ -144,10 +144,12 @@ def ipc_buffer_stats() -> dict:
     """How this process's xGMI/IPC ops handed their buffers to the peers since start: direct (zero-copy) vs staged
     (copy-in / copy-out through VMM comm buffers), per input and output; plus ``quarantined`` (staged comm buffers of
     aborted ops, never reissued) and ``zombie_drains`` (abort drains that waited for a dead peer's threads to finish
-    tearing down its address space, i.e. its GPU queues)."""
+    tearing down its address space, i.e. its GPU queues), ``preflight_failed`` / ``preflight_passed`` (cross-GPU write
+    probes on the first op of an arena whose peers span several GPUs)."""
     out = (ctypes.c_uint64 * 8)()
     n = int(_native.C.pcclxIpcStatsEx(out, 8))
-    keys = ("direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains")
+    keys = ("direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains", "preflight_failed",
+            "preflight_passed")
     return {k: int(out[i]) for i, k in enumerate(keys[:n])}
 
 

@@ -584,6 +584,22 @@ TEST(crc32c_tiers_agree) {
 }
 
 // xGMI path on a multi-GPU node without the node: the workgroup budget and the peer-access precheck with fake GPU uids
+TEST(ipc_preflight_and_remote_grid_decisions) {
+    // fake GPU uids: which rings probe cross-GPU writes on their first op, and the push kernel's workgroup budget
+    using client::ipc_needs_preflight;
+    using client::ipc_push_grid;
+    const std::vector<uint64_t> one_gpu(8, 7), eight = {1, 2, 3, 4, 5, 6, 7, 8}, pairs = {1, 1, 2, 2};
+    EXPECT(!ipc_needs_preflight(one_gpu, false, 1 << 20));    // all peers on one GPU: nothing crosses xGMI
+    EXPECT(ipc_needs_preflight(eight, false, 1 << 20));       // first op across GPUs
+    EXPECT(!ipc_needs_preflight(eight, true, 1 << 20));       // once per arena
+    EXPECT(!ipc_needs_preflight(eight, false, 8 * 256 - 2));  // too small for a slot per peer: a later op probes
+    EXPECT(ipc_needs_preflight(pairs, false, 4 * 256));
+    EXPECT(ipc_push_grid(eight, 0, 0) == 512);                // default: the local budget
+    EXPECT(ipc_push_grid(eight, 3, 1024) == 1024);            // PCCL_IPC_REMOTE_GRID for remote destinations
+    EXPECT(ipc_push_grid(one_gpu, 3, 1024) == 256);           // no remote destination: knob ignored
+    EXPECT(ipc_push_grid(pairs, 1, 100000) == 4096);          // clamped
+}
+
 TEST(ipc_grid_budget_by_gpu_sharing) {
     using client::ipc_grid_budget;
     const std::vector<uint64_t> eight_gpus = {11, 12, 13, 14, 15, 16, 17, 18};

@@ -230,6 +230,30 @@ def test_two_process_ipc(hip, mode, ipc_mode):
             assert b["direct_in"] == 0 and b["direct_out"] == 0, b
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_preflight_rehearsal(hip, world):
+    """The cross-GPU pre-flight (first op of an arena whose peers span several GPUs: a 256-byte probe written into
+    every peer's output through the push kernels' mappings, read back after a barrier) forced on one GPU with
+    PCCL_IPC_PREFLIGHT=2: it passes once per process, and that first op and every later one stay exact on the IPC
+    path. This is the 1-GPU rehearsal of what an 8-GPU node runs first."""
+    with local_master() as addr:
+        procs = [spawn_python([os.path.join(HERE, "workers", "allreduce_peer.py"), addr, str(world), str(r), "--n",
+                               str((1 << 20) + 3), "--dtype", "bf16", "--device", "cuda:0", "--steps", "4"],
+                              env={"PCCL_IPC_PREFLIGHT": "2"}, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(world)]
+        outs = communicate_all(procs, 240, DIAG_SIGNALS)
+    tri = world * (world + 1) // 2
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
+        assert len(lines) == 4 and not any("error" in ln for ln in lines), lines
+        for ln in lines:
+            assert ln["lo"] == ln["hi"] == float(tri + world * ln["step"])
+            assert ln["path"] == pccl.ReducePath.DEVICE_IPC.value
+        b = lines[-1]["ipc_bufs"]
+        assert b["preflight_passed"] == 1 and b["preflight_failed"] == 0, b
+
+
 @pytest.mark.parametrize("gib", [1.25, 2.5])
 def test_two_process_ipc_large(hip, gib):
     """Ops whose staged comm buffers / user allocations exceed 1-2 GiB: staged buffers are built from 1 GiB segments
