@@ -378,6 +378,30 @@ def latency_cpu(job, n_ops=300):
     return {"median_us": round(statistics.median(ts) * 1e6, 1), "p99_us": round(ts[int(0.99 * (len(ts) - 1))] * 1e6, 1)}
 
 
+def latency_native(peers):
+    """Small-op latency of the xGMI/IPC path without Python in the loop: pccl_amd/lib/pccl_latency (the C API with
+    hipMalloc'd buffers, threaded peers on cuda:0, csrc/tools/latency_native.hip), 1 MiB bf16 at `peers` and 2 peers;
+    median / p90 of the per-op max over the peers. The Python sweep point (extra.latency_1MiB_ipc_us) adds the
+    interpreter: 8 peer threads serialise on the GIL around every op."""
+    import subprocess
+
+    from pccl_amd.utils import free_port
+    exe = os.path.join(ROOT, "pccl_amd", "lib", "pccl_latency")
+    if not os.path.exists(exe):
+        return {"error": "pccl_latency not built"}
+    out = {}
+    for p in sorted({peers, 2}):
+        try:
+            r = subprocess.run([exe, str(free_port()), str(p), str(1 << 20), "400", "50"], capture_output=True,
+                               text=True, timeout=120)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            out[f"{p}_peers_1MiB"] = json.loads(line[-1]) if r.returncode == 0 and line else \
+                {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+        except subprocess.TimeoutExpired:
+            out[f"{p}_peers_1MiB"] = {"error": "timeout"}
+    return out
+
+
 def rejoin_latency(job):
     """A new peer connects mid-run; seconds from its connect() until its first all-reduce completed (admission vote +
     P2P establishment + IPC rendezvous + first op). N == 1 only."""
@@ -466,6 +490,7 @@ def run_extras(job, a, nbytes):
     if curve:
         extra["peer_curve"] = curve
     if job.world == 1:
+        extra["latency_native"] = latency_native(P)
         extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
