@@ -392,6 +392,20 @@ pcclResult_t pcclCreateMaster(ccoip_socket_address_t listen_address, pcclMasterI
     return pcclSuccess;
 }
 
+// Extension: the master's bandwidth stores as text ("<group> <from> -> <to>: <Mbit/s> Mbit/s" per line). Writes at
+// most cap bytes (NUL-terminated when cap > 0); returns the full length.
+extern "C" __attribute__((visibility("default"))) size_t pcclxMasterBandwidthTable(pcclMasterInstance_t *m, char *buf,
+                                                                                  size_t cap) {
+    if (m == nullptr || m->master == nullptr) return 0;
+    const std::string t = m->master->bandwidth_table();
+    if (cap > 0) {
+        const size_t n = std::min(cap - 1, t.size());
+        std::memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return t.size();
+}
+
 pcclResult_t pcclRunMaster(pcclMasterInstance_t *m) {
     PCCL_REQUIRE(m != nullptr && m->master != nullptr, pcclInvalidArgument);
     if (!m->master->launch()) return pcclInvalidUsage;

@@ -67,6 +67,10 @@ static std::vector<std::pair<size_t, size_t>> chunk_bounds(size_t total, size_t 
     return b;
 }
 
+namespace {
+bool use_small_path(size_t bytes, size_t ws);
+} // namespace
+
 bool Client::abort_received(uint64_t tag) {
     auto p = master_.receive<M2CCollectiveCommsAbort>([tag](const M2CCollectiveCommsAbort &a) { return a.tag == tag; },
                                                        0ms);
@@ -182,12 +186,16 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
         init.data_type = op->req.dtype;
         init.op = op->req.op;
         if (rv && rv->hier && device) init.flags |= kCollFlagHierarchical;
+        if (rv && rv->ring.size() >= 2 && use_small_path(op->req.count * dtype_size(op->req.dtype), rv->ring.size()) &&
+            (op->req.qalgo == QuantAlgo::None || op->req.qtype == op->req.dtype))
+            init.flags |= kCollFlagSmallPath;
         if (master_.send(init)) {
             auto c = master_.receive<M2CCollectiveCommsCommence>(
                 [tag](const M2CCollectiveCommsCommence &p) { return p.tag == tag; });
             if (c) {
                 seq = c->seq_nr;
                 agreed = c->flags;
+                op->small_path = (agreed & kCollFlagSmallPath) != 0;
                 commenced = true;
                 trace_mark("commence");
             }
@@ -592,7 +600,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
     auto aborted = [&] { return abort_received(q.tag); };
 
-    if (!quant && use_small_path(bytes, ws)) {
+    if (!quant && op.small_path) {
         const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
                                               aborted, op.tx, op.rx);
         trace_mark("allgather_reduce");
@@ -941,7 +949,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     StreamLease stream(device);
     DevStream st = stream.get();
     if (!st) return {false, false};
-    if (use_small_path(bytes, ws)) { // latency-bound: one D2H, host all-gather + reduce, one H2D
+    if (op.small_path) { // latency-bound (agreed by every peer): one D2H, host all-gather + reduce, one H2D
         Lease hin(pinned_pool(), std::max<size_t>(bytes, 64)), hout(pinned_pool(), std::max<size_t>(bytes, 64));
         if (!hin.ok() || !hout.ok()) return {false, false};
         if (!be->memcpy_async(hin.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};

@@ -121,6 +121,9 @@ bool Client::connect() {
     C2MRequestSessionRegistration reg;
     reg.peer_group = cfg_.peer_group;
     reg.host_token = net::host_token();
+    // PCCL_XGMI_CAPABLE=0/1 overrides the advertised capability (tests on GPU-less hosts)
+    reg.xgmi_capable = std::getenv("PCCL_XGMI_CAPABLE") ? env_flag("PCCL_XGMI_CAPABLE", true)
+                                                       : !env_flag("PCCL_DISABLE_IPC", false) && device_backend_available();
     reg.use_explicit_addresses = cfg_.explicit_addresses;
     if (cfg_.explicit_addresses) {
         reg.advertised_p2p = cfg_.adv_p2p;

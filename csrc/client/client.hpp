@@ -158,6 +158,7 @@ private:
         uint64_t revision_at_start = 0;
         std::atomic<uint64_t> tx{0}, rx{0};
         uint32_t world = 0;
+        bool small_path = false; // every peer agreed on the small-message algorithm (kCollFlagSmallPath)
     };
 
     // Hierarchical layout (master's host_of extension): hosts x local ranks. The host-local peers share an IPC arena;

@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <functional>
+#include <future>
+#include <sstream>
 
 #include "../common/log.hpp"
 
@@ -343,6 +345,7 @@ void Master::handle_join(const SockAddr &addr, const C2MRequestSessionRegistrati
         c.addr = addr;
         c.group = p.peer_group;
         c.host_token = p.host_token;
+        c.xgmi = p.xgmi_capable;
         if (p.use_explicit_addresses) {
             c.p2p = p.advertised_p2p;
             c.ss = p.advertised_ss;
@@ -552,10 +555,11 @@ void Master::check_optimize_consensus() {
             if (un != unreachable_.end() && un->second.count(e.to)) continue;
             const ClientInfo *to = client_by_uuid(e.to);
             if (!to || to->phase != Phase::Accepted) continue;
-            if (same_host_mbps() > 0 && !c.host_token.empty() && c.host_token == to->host_token) {
-                // same host (boot id + hostname): the pair talks over loopback or xGMI, never over the NIC, so it
-                // is not benchmarked (reference benchmarks every pair for 10 s); a fixed, NIC-beating cost makes
-                // the ATSP keep co-located peers adjacent (PCCL_SAME_HOST_MBPS, 0 = measure as usual)
+            if (same_host_mbps() > 0 && !c.host_token.empty() && c.host_token == to->host_token && c.xgmi && to->xgmi) {
+                // same host (boot id + hostname) and both peers can take the xGMI path: the pair never talks over
+                // the NIC, so it is not benchmarked (reference benchmarks every pair for 10 s); a fixed, NIC-beating
+                // cost makes the ATSP keep co-located peers adjacent (PCCL_SAME_HOST_MBPS, 0 = measure as usual).
+                // Same-host pairs that use loopback TCP (PCCL_DISABLE_IPC, no GPU backend) are measured below.
                 groups_[c.group].bw.store(u, e.to, same_host_mbps());
                 continue;
             }
@@ -1059,6 +1063,21 @@ void Master::on_tick() {
     if (now - last_dump_ < std::chrono::seconds(every)) return;
     last_dump_ = now;
     LOG(WARN) << "Master state:\n" << dump_state();
+}
+
+std::string Master::bandwidth_table() {
+    auto done = std::make_shared<std::promise<std::string>>();
+    auto fut = done->get_future();
+    server_.post([this, done] {
+        std::string out;
+        for (const auto &[g, gs] : groups_) {
+            std::istringstream in(gs.bw.dump());
+            for (std::string ln; std::getline(in, ln);) out += std::to_string(g) + " " + ln + "\n";
+        }
+        done->set_value(out);
+    });
+    if (fut.wait_for(std::chrono::seconds(10)) != std::future_status::ready) return {};
+    return fut.get();
 }
 
 std::string Master::dump_state() const {

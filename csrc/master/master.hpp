@@ -67,6 +67,7 @@ struct ClientInfo {
     SockAddr p2p{}, ss{}, bm{};
     uint64_t ss_revision = 0; // revision announced in the current shared-state round
     std::string host_token;   // registration extension; empty for reference clients
+    bool xgmi = true;         // registration extension: may take the xGMI IPC path
 };
 
 struct GroupState {
@@ -106,6 +107,9 @@ private:
 
 public:
     std::string dump_state() const;
+    // "<group> <from uuid> <to uuid> <Mbit/s>" per measured (or same-host constant) edge of every group's bandwidth
+    // store; runs on the loop thread (must not be called from it)
+    std::string bandwidth_table();
 
 private:
     void kick(const SockAddr &addr);

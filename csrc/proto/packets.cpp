@@ -16,7 +16,10 @@ void C2MRequestSessionRegistration::encode(WBuf &w) const {
         w.u16(ss_port);
         w.u16(bm_port);
     }
-    if (!host_token.empty()) w.str(host_token);
+    if (!host_token.empty()) {
+        w.str(host_token);
+        w.boolean(xgmi_capable);
+    }
 }
 
 bool C2MRequestSessionRegistration::decode(RBuf &r) {
@@ -35,6 +38,8 @@ bool C2MRequestSessionRegistration::decode(RBuf &r) {
         bm_port = r.u16();
     }
     if (r.ok() && r.remaining() > 0) host_token = r.str(); // absent when the peer is a reference implementation
+    xgmi_capable = true;
+    if (r.ok() && r.remaining() > 0) xgmi_capable = r.boolean();
     return r.ok();
 }
 

@@ -71,6 +71,10 @@ struct C2MRequestSessionRegistration {
     // extension (appended, optional on decode): host identity (boot id + hostname) so the master can tell peers
     // that share a host -- and may use the xGMI IPC path -- even when the master is not on loopback
     std::string host_token;
+    // extension after host_token (optional, default true): this peer can take the xGMI IPC path (a GPU backend and
+    // no PCCL_DISABLE_IPC). Same-host pairs of which one cannot are benchmarked like remote pairs: their traffic
+    // crosses loopback TCP, so a fixed xGMI-class cost would mislead the ring optimiser.
+    bool xgmi_capable = true;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };
@@ -171,6 +175,10 @@ struct C2MCollectiveCommsInitiate {
 
 // the peer can run this op hierarchically (device buffers, host-local IPC arena, inter-host ring connections)
 constexpr uint8_t kCollFlagHierarchical = 1;
+// this peer's PCCL_SMALL_ALLREDUCE_BYTES selects the all-gather small-message algorithm for this op; ANDed by the
+// master like every capability bit, so a threshold that differs between peers cannot split the ring between the two
+// algorithms (the op then uses the reduce-scatter ring everywhere)
+constexpr uint8_t kCollFlagSmallPath = 2;
 
 struct C2MCollectiveCommsComplete {
     static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_COMPLETE;

@@ -587,6 +587,18 @@ class MasterNode:
     def interrupt(self):
         PCCLError.check(C.pcclInterruptMaster(self._master), "pcclInterruptMaster")
 
+    def bandwidth_table(self):
+        """The master's measured link bandwidths: [(peer group, from uuid, to uuid, Mbit/s)] (every entry of every
+        group's bandwidth store, including the fixed cost of same-host xGMI pairs)."""
+        n = int(C.pcclxMasterBandwidthTable(self._master, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        C.pcclxMasterBandwidthTable(self._master, buf, n + 1)
+        out = []
+        for ln in buf.value.decode().splitlines():
+            g, frm, _, to, mbps, _unit = ln.replace(":", "").split()
+            out.append((int(g), frm, to, float(mbps)))
+        return out
+
     def await_termination(self):
         if self._running:
             C.pcclMasterAwaitTermination(self._master)

@@ -323,3 +323,26 @@ def test_small_message_allgather_path(small_limit, world, dtype, inplace, monkey
                 assert torch.equal(y.double(), expect.double()), (op, y[:8], expect[:8])
             nbytes = n * inputs[0].element_size()
             assert tx == (nbytes * (world - 1) if small_limit else tx), tx  # all-gather sends W-1 whole vectors
+
+
+def test_small_message_threshold_mismatch_is_agreed():
+    """Peers whose PCCL_SMALL_ALLREDUCE_BYTES differ (one would take the all-gather small-message algorithm, the other
+    the reduce-scatter ring) must not split the ring between the two: the choice travels as a capability bit of the
+    collective initiate that the master ANDs, so both run the same algorithm and the results stay exact."""
+    import json
+    import os
+    import subprocess
+
+    from pccl_amd.utils import DIAG_SIGNALS, communicate_all, local_master, spawn_python
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "workers", "allreduce_peer.py")
+    with local_master() as addr:
+        ps = [spawn_python([worker, addr, "2", str(r), "--n", "1000", "--steps", "3"],
+                           env={"PCCL_SMALL_ALLREDUCE_BYTES": "0" if r == 0 else str(1 << 20)},
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+        outs = communicate_all(ps, 120, DIAG_SIGNALS)
+    for p, (o, e) in zip(ps, outs):
+        assert p.returncode == 0, e[-2000:]
+        lines = [json.loads(x) for x in o.splitlines() if x.startswith("{")]
+        assert len(lines) == 3 and all("error" not in ln for ln in lines), lines
+        for ln in lines:
+            assert ln["lo"] == ln["hi"] == float(3 + 2 * ln["step"])

@@ -36,16 +36,65 @@ def test_optimize_topology_same_host_pairs_not_benchmarked(monkeypatch):
     import time
     monkeypatch.delenv("PCCL_BENCHMARK_MILLIS", raising=False)
     monkeypatch.delenv("PCCL_SAME_HOST_MBPS", raising=False)
+    monkeypatch.setenv("PCCL_XGMI_CAPABLE", "1")  # peers that would take the xGMI path (this host may lack a GPU)
+    from pccl_amd.utils import free_port
+    port = free_port()
+    master = pccl.MasterNode(f"127.0.0.1:{port}")
+    master.run()
+
+    tables = []
 
     def fn(rank, comm):
         t0 = time.perf_counter()
         comm.optimize_topology()
         dt = time.perf_counter() - t0
+        if rank == 0:  # while every peer is still registered (leaving peers drop their edges)
+            tables.append(master.bandwidth_table())
         x = torch.full((1000,), float(rank + 1))
         comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)
         return dt, float(x[0])
 
-    with local_master() as addr:
-        res = run_threaded_peers(3, fn, address=addr, timeout=120)
+    try:
+        res = run_threaded_peers(3, fn, address=f"127.0.0.1:{port}", timeout=120)
+    finally:
+        master.interrupt()
+        master.await_termination()
+    table = tables[0]
     assert all(r[1] == 6.0 for r in res)
     assert max(r[0] for r in res) < 8.0, res
+    assert len(table) == 6 and all(t[3] == 1e6 for t in table), table
+
+
+def test_optimize_topology_same_host_tcp_pairs_are_measured(monkeypatch):
+    """Same-host peers that cannot use xGMI (PCCL_DISABLE_IPC=1: their ring runs over loopback TCP) are benchmarked
+    like remote pairs, so the bandwidth store holds measured values rather than the fixed xGMI-class constant
+    (reference ccoip_client_handler.cpp:640-736 measures every ordered pair)."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_BENCHMARK_MILLIS", "150")
+    monkeypatch.setenv("PCCL_NUM_BENCHMARK_CONNECTIONS", "2")
+    monkeypatch.delenv("PCCL_SAME_HOST_MBPS", raising=False)
+    monkeypatch.delenv("PCCL_XGMI_CAPABLE", raising=False)
+    from pccl_amd.utils import free_port
+    port = free_port()
+    master = pccl.MasterNode(f"127.0.0.1:{port}")
+    master.run()
+
+    tables = []
+
+    def fn(rank, comm):
+        comm.optimize_topology()
+        if rank == 0:
+            tables.append(master.bandwidth_table())
+        x = torch.full((1000,), float(rank + 1))
+        comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)
+        return float(x[0])
+
+    try:
+        res = run_threaded_peers(3, fn, address=f"127.0.0.1:{port}", timeout=120)
+    finally:
+        master.interrupt()
+        master.await_termination()
+    table = tables[0]
+    assert all(r == 6.0 for r in res)
+    assert len(table) == 6, table  # every ordered pair
+    assert all(0 < t[3] < 1e6 for t in table), table  # measured loopback throughput, not the constant
