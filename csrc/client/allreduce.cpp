@@ -931,6 +931,315 @@ private:
 
 } // namespace
 
+namespace {
+
+// Start signal between the lanes of one device-ring op (lane k+1 starts once lane k reached its all-gather).
+struct LaneGate {
+    std::mutex m;
+    std::condition_variable cv;
+    bool open = false;
+    void signal() {
+        {
+            std::lock_guard l(m);
+            open = true;
+        }
+        cv.notify_all();
+    }
+};
+
+// One lane of the device ring: a complete pipelined ring all-reduce of `n` elements at `region` (HBM, already holding
+// the input) whose step-0 payload is staged from `src`, on its own compute stream, tag and staging rings.
+struct Lane {
+    // inputs
+    const std::vector<std::shared_ptr<net::MuxConn>> *txs, *rxs; // the ring's connections to next / from prev
+    size_t ws, rank;                                              // ring size, my position
+    uint64_t tag, seq;
+    DeviceBackend *be;
+    PcieQueues pq;
+    DevStream st;       // this lane's compute stream (waits for `ready` first)
+    DevEvent ready;     // the op-level input copy / backup (recorded on the op stream), or nullptr
+    const uint8_t *src; // step-0 source of this lane's elements
+    uint8_t *dst;       // this lane's elements in the op's destination
+    size_t count, es, piece;
+    DType dtype;
+    ReduceOp rop;
+    int device;
+    bool ahead, step0_on_op_stream;
+    LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
+    std::function<bool()> aborted;
+    std::atomic<uint64_t> *tx, *rx;
+    bool main_lane = false; // trace marks and fault points
+    // output
+    int rc = 0; // 0 ok, 1 io failure, 2 abort
+};
+
+void run_lane(Lane &L) {
+    const auto &txs = *L.txs;
+    const auto &rxs = *L.rxs;
+    DeviceBackend *be = L.be;
+    const PcieQueues pq = L.pq;
+    DevStream st = L.st;
+    const size_t ws = L.ws, rank = L.rank, es = L.es, piece = L.piece;
+    const uint64_t tag = L.tag, seq = L.seq;
+    auto fail = [&](int code) {
+        L.rc = code;
+        if (L.open_gate) L.open_gate->signal(); // never leave a waiting lane behind
+    };
+    if (L.wait_gate) {
+        std::unique_lock l(L.wait_gate->m);
+        L.wait_gate->cv.wait(l, [&] { return L.wait_gate->open; });
+    }
+    if (L.ready) be->stream_wait_event(st, L.ready);
+
+    // events of this lane (returned to the pool once everything they guard has completed)
+    std::vector<DevEvent> owned;
+    DevEvent last_h2d = nullptr, last_d2h = nullptr;
+    auto record = [&](DevStream s) {
+        DevEvent e = event_pool().get();
+        owned.push_back(e);
+        be->event_record(e, s);
+        return e;
+    };
+    const auto bounds = chunk_bounds(L.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t stage_bytes = max_chunk * es + 64;
+    // Staging rings of kNb buffers: step g receives into rxbuf[g % kNb] (HBM twin rxdev[g % kNb] for the reduce) and
+    // its reduce writes the next payload into txbuf[(g + 1) % kNb]. Three deep, because step g+1's sinks are posted
+    // while step g still receives and step g+1's sends run while step g's do: a buffer is refilled only after the
+    // step two back finished with it.
+    constexpr size_t kNb = 3;
+    Lease txl[kNb], rxl[kNb], dvl[kNb];
+    uint8_t *txbuf[kNb], *rxbuf[kNb], *rxdev[kNb];
+    for (size_t i = 0; i < kNb; ++i) {
+        txl[i] = Lease(pinned_pool(), stage_bytes);
+        rxl[i] = Lease(pinned_pool(), stage_bytes);
+        dvl[i] = Lease(device_pool(), stage_bytes, L.device);
+        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return fail(1);
+        txbuf[i] = txl[i].data();
+        rxbuf[i] = rxl[i].data();
+        rxdev[i] = dvl[i].data();
+    }
+    // declared after every staging lease: destroyed first, so nothing of this lane still reads or writes them when
+    // they go back to the pools (also on the early returns below)
+    struct Drain {
+        DeviceBackend *be;
+        DevStream st;
+        DevEvent *h2d, *d2h;
+        std::vector<DevEvent> *ev;
+        ~Drain() {
+            if (*h2d) be->event_sync(*h2d);
+            if (*d2h) be->event_sync(*d2h);
+            be->stream_sync(st);
+            for (auto e : *ev) event_pool().put(e);
+        }
+    } drain{be, st, &last_h2d, &last_d2h, &owned};
+
+    ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
+    size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
+    DevEvent h2d_done[kNb] = {nullptr, nullptr, nullptr}; // last H2D copy reading rxbuf[i] / writing rxdev[i]
+    DevEvent red_done[kNb] = {nullptr, nullptr, nullptr}; // last reduce kernel reading rxdev[i]
+
+    const size_t nsteps = 2 * (ws - 1);
+    auto is_rs = [&](size_t g) { return g + 1 < ws; };
+    auto chunk_tx = [&](size_t g) { // chunk index this peer sends at global step g
+        return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
+    };
+    auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
+    auto region_of = [&](size_t g) { return L.dst + bounds[chunk_rx(g)].first * es; };
+    size_t max_stripes = 1;
+    for (size_t g = 0; g < nsteps; ++g) {
+        const auto [ts, te] = bounds[chunk_tx(g)];
+        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, txs.size()).off.size());
+    }
+    // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
+    OpSenders senders(txs, tag, seq, piece, nsteps, max_stripes, be, *L.tx);
+    auto publish = [&](size_t g) {
+        if (senders.published(g)) return;
+        const auto [ts, te] = bounds[chunk_tx(g)];
+        const bool staged = g < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
+        OpSenders::Step stp;
+        stp.payload = staged ? txbuf[g % kNb] + txshift[g % kNb] : rxbuf[(g - 1) % kNb];
+        stp.bytes = (te - ts) * es;
+        stp.ready = staged ? &txready[g % kNb] : &rxready[(g - 1) % kNb];
+        senders.publish(g, stp);
+    };
+    auto fail_all = [&](int code) {
+        senders.cancel();
+        fail(code);
+    };
+
+    // ---- receive side: one set of sinks per step, posted up to one step early
+    struct StepRx {
+        StripePlan rp;
+        std::vector<net::MuxConn::SinkRef> sinks;
+        std::vector<size_t> done; // elements consumed per stripe
+        size_t remaining = 0;
+        bool posted = false;
+    };
+    std::vector<StepRx> srx(nsteps);
+    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
+    // rxbuf[g % kNb] may take step g's bytes once the step that used it before (g - kNb) is finished with it: its H2D
+    // copies and reduce kernels completed and (all-gather) the step after it has forwarded its bytes
+    auto can_post = [&](size_t g) {
+        if (g < kNb) return true;
+        const size_t b = g % kNb, prev = g - kNb;
+        if (h2d_done[b] && be->event_query(h2d_done[b]) == 0) return false;
+        if (red_done[b] && be->event_query(red_done[b]) == 0) return false;
+        if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
+        return true;
+    };
+    auto post = [&](size_t g) {
+        StepRx &r = srx[g];
+        const size_t b = g % kNb;
+        h2d_done[b] = red_done[b] = nullptr;
+        if (!is_rs(g)) rxready[b].clear();
+        const auto [rs0, re0] = bounds[chunk_rx(g)];
+        r.rp = plan_stripes((re0 - rs0) * es, rxs.size());
+        r.sinks.resize(r.rp.off.size());
+        r.done.assign(r.rp.off.size(), 0);
+        r.remaining = 0;
+        for (size_t k = 0; k < r.rp.off.size(); ++k) {
+            if (r.rp.len[k] == 0) continue;
+            r.sinks[k] = rx_conn(k)->post_sink(tag, seq, rxbuf[b] + r.rp.off[k], r.rp.len[k]);
+            ++r.remaining;
+        }
+        r.posted = true;
+    };
+    auto unpost = [&](size_t g) {
+        StepRx &r = srx[g];
+        if (!r.posted) return;
+        for (size_t k = 0; k < r.sinks.size(); ++k)
+            if (r.sinks[k]) rx_conn(k)->remove_sink(tag, r.sinks[k]);
+        r.sinks.clear();
+        r.posted = false;
+    };
+    struct Unposter { // sinks must never outlive their buffers (also on failure)
+        std::function<void()> fn;
+        ~Unposter() { fn(); }
+    } unposter{[&] {
+        for (size_t g = 0; g < nsteps; ++g) unpost(g);
+    }};
+
+    for (size_t g = 0; g < nsteps; ++g) {
+        const size_t b = g % kNb, nb = (g + 1) % kNb;
+        const bool rs = is_rs(g);
+        if (!L.ahead && g > 0 && !senders.wait(g - 1)) return fail_all(1);
+        // 1. step g's sinks (normally posted during step g-1)
+        while (!srx[g].posted) {
+            if (can_post(g)) {
+                post(g);
+                break;
+            }
+            if (senders.failed()) return fail_all(1);
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
+        uint8_t *region = region_of(g);
+        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
+        if (rs) {
+            if (g >= 2 && !senders.wait(g - 2)) return fail_all(1);
+            txready[nb].clear();
+            txshift[nb] = shift;
+        }
+        // 3. own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+        if (g == 0) {
+            const auto [ts, te] = bounds[chunk_tx(0)];
+            txready[0].clear();
+            txshift[0] = 0;
+            DevStream q0 = L.step0_on_op_stream ? st : pq.d2h;
+            for (size_t off = 0; off < (te - ts) * es; off += piece) {
+                const size_t n = std::min(piece, (te - ts) * es - off);
+                be->memcpy_async(txbuf[0] + off, L.src + ts * es + off, n, q0);
+                DevEvent e = record(q0);
+                if (!L.step0_on_op_stream) last_d2h = e;
+                txready[0].add(off, off + n, e);
+            }
+        }
+        publish(g);
+        if (L.ahead && g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
+        if (g + 1 == ws - 1 && L.open_gate) L.open_gate->signal(); // next step is this lane's all-gather
+        // 4. receive + consume step g
+        StepRx &r = srx[g];
+        uint8_t *sink = rxbuf[b];
+        DevEvent last_red = nullptr;
+        std::function<void(size_t, size_t)> consume;
+        if (rs) {
+            // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
+            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
+            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
+                const size_t off = a * es, n = (e - a) * es;
+                be->memcpy_async(stage + off, sink + off, n, pq.h2d);
+                last_h2d = record(pq.h2d);
+                be->stream_wait_event(st, last_h2d);
+                be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, st);
+                last_red = record(st);
+                txready[nb].add(off, off + n, last_red);
+            };
+        } else {
+            consume = [&, sink, region, b](size_t a, size_t e) {
+                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d);
+                last_h2d = record(pq.h2d);
+                rxready[b].add(a * es, e * es, nullptr); // in host memory: forwardable at once
+            };
+        }
+        const size_t gran_el = std::max<size_t>(1, piece / es);
+        int rc = 0;
+        size_t idle = 0, rr = 0;
+        while (r.remaining > 0) {
+            bool progress = false;
+            for (size_t k = 0; k < r.sinks.size(); ++k) {
+                if (!r.sinks[k]) continue;
+                const size_t want = r.rp.len[k] / es;
+                if (r.done[k] >= want) continue;
+                const size_t have = net::MuxConn::sink_progress(r.sinks[k]) / es;
+                if (have > r.done[k] && (have - r.done[k] >= gran_el || have >= want)) {
+                    const size_t e0 = r.rp.off[k] / es;
+                    consume(e0 + r.done[k], e0 + have);
+                    r.done[k] = have;
+                    progress = true;
+                    if (r.done[k] >= want) --r.remaining;
+                }
+            }
+            // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
+            if (L.ahead && g + 1 < nsteps && !srx[g + 1].posted && can_post(g + 1)) post(g + 1);
+            if (r.remaining == 0 || progress) {
+                idle = 0;
+                continue;
+            }
+            size_t k = rr++ % r.sinks.size();
+            while (!r.sinks[k] || r.done[k] >= r.rp.len[k] / es) k = rr++ % r.sinks.size();
+            net::MuxConn *c = rx_conn(k);
+            c->wait_sink(r.sinks[k], std::min(r.rp.len[k], (r.done[k] + gran_el) * es), 5ms);
+            if (!c->is_open() || senders.failed()) {
+                rc = 1;
+                break;
+            }
+            if (++idle % 8 == 0 && L.aborted()) {
+                rc = 2;
+                break;
+            }
+        }
+        h2d_done[b] = last_h2d;
+        red_done[b] = last_red;
+        if (rc) return fail_all(rc);
+        *L.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
+        unpost(g);
+        if (!L.ahead && !senders.wait(g)) return fail_all(1); // classic schedule: a step ends when its sends are done
+        if (L.main_lane) {
+            step_mark(rs, rs ? g : g - (ws - 1));
+            if (g == 0) fault_point("ring_step", seq);
+            if (g + 2 == ws) trace_mark("reduce_scatter");
+        }
+    }
+    if (!senders.wait(nsteps - 1)) return fail_all(1);
+    if (L.open_gate) L.open_gate->signal();
+    // the lane is complete once its last received bytes landed in HBM (the Drain waits for them)
+}
+
+} // namespace
+
 std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
     const ReduceRequest &q = op.req;
     if (q.qalgo != QuantAlgo::None && q.qtype != q.dtype) return ring_reduce_device_quant(op, rv, seq, device);
@@ -970,55 +1279,8 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     }
     if (!pq.h2d || !pq.d2h) return {false, false};
 
-    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
-    (void) io;
-    auto aborted = [&] { return abort_received(q.tag); };
-
-    // events of this op (returned to the pool once everything they guard has completed)
-    std::vector<DevEvent> owned;
-    DevEvent last_h2d = nullptr, last_d2h = nullptr;
-    auto record = [&](DevStream s) {
-        DevEvent e = event_pool().get();
-        owned.push_back(e);
-        be->event_record(e, s);
-        return e;
-    };
-
-    const auto bounds = chunk_bounds(q.count, ws);
-    size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
-    const size_t stage_bytes = max_chunk * es + 64;
-    // Staging rings of kNb buffers: step g receives into rxbuf[g % kNb] (HBM twin rxdev[g % kNb] for the reduce) and
-    // its reduce writes the next payload into txbuf[(g + 1) % kNb]. Three deep, because step g+1's sinks are posted
-    // while step g still receives and step g+1's sends run while step g's do: a buffer is refilled only after the
-    // step two back finished with it.
-    constexpr size_t kNb = 3;
-    Lease txl[kNb], rxl[kNb], dvl[kNb];
-    uint8_t *txbuf[kNb], *rxbuf[kNb], *rxdev[kNb];
-    for (size_t i = 0; i < kNb; ++i) {
-        txl[i] = Lease(pinned_pool(), stage_bytes);
-        rxl[i] = Lease(pinned_pool(), stage_bytes);
-        dvl[i] = Lease(device_pool(), stage_bytes, device);
-        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return {false, false};
-        txbuf[i] = txl[i].data();
-        rxbuf[i] = rxl[i].data();
-        rxdev[i] = dvl[i].data();
-    }
+    // the caller's input -> dst (out of place) or a backup of it (in place, restored on abort), on the op stream
     Lease backup;
-    // declared after every staging lease: destroyed first, so nothing of this op still reads or writes them when
-    // they go back to the pools (also on the early returns below)
-    struct Drain { // runs on every exit: nothing of this op may still touch its staging buffers / dst afterwards
-        DeviceBackend *be;
-        DevStream st;
-        DevEvent *h2d, *d2h;
-        std::vector<DevEvent> *ev;
-        ~Drain() {
-            if (*h2d) be->event_sync(*h2d);
-            if (*d2h) be->event_sync(*d2h);
-            be->stream_sync(st);
-            for (auto e : *ev) event_pool().put(e);
-        }
-    } drain{be, st, &last_h2d, &last_d2h, &owned};
     if (q.src == q.dst && !q.scratch) {
         backup = Lease(device_pool(), bytes, device);
         if (!backup.ok()) return {false, false};
@@ -1026,227 +1288,88 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     } else if (q.src != q.dst) {
         be->memcpy_async(dst, q.src, bytes, st);
     }
-    auto restore = [&] {
-        if (last_h2d) be->event_sync(last_h2d);
-        if (last_d2h) be->event_sync(last_d2h);
+    DevEvent ready = event_pool().get();
+    struct EvBack { // the op stream drains before the event returns to the pool (every exit)
+        DeviceBackend *be;
+        DevStream st;
+        DevEvent e;
+        ~EvBack() {
+            be->stream_sync(st);
+            event_pool().put(e);
+        }
+    } ev_back{be, st, ready};
+    be->event_record(ready, st);
+
+    // Lanes: the buffer is split into PCCL_RING_LANES contiguous parts, each a complete ring all-reduce with its own
+    // tag (the op's tag with the lane number in bits 60-63), stream and staging rings; lane k+1 starts when lane k
+    // reaches its all-gather. The all-gather moves bytes host -> device only while a reduce-scatter moves them both
+    // ways, so overlapping lane k's all-gather with lane k+1's reduce-scatter keeps both PCIe directions busy.
+    const size_t lanes_req = std::max<size_t>(1, std::min<size_t>(4, env_size("PCCL_RING_LANES", 1)));
+    const size_t align_el = std::max<size_t>(1, 4096 / es);
+    size_t nl = lanes_req;
+    while (nl > 1 && q.count / nl < ws * piece / es) --nl; // every lane keeps >= one piece per chunk
+    std::vector<size_t> lo(nl + 1, 0);
+    for (size_t k = 1; k < nl; ++k) lo[k] = std::min(q.count, (q.count * k / nl) / align_el * align_el);
+    lo[nl] = q.count;
+    std::vector<LaneGate> gates(nl);
+    std::vector<std::unique_ptr<StreamLease>> lane_streams;
+    std::vector<Lane> lanes(nl);
+    for (size_t k = 0; k < nl; ++k) {
+        lane_streams.push_back(std::make_unique<StreamLease>(device));
+        if (!lane_streams.back()->get()) return {false, false};
+        Lane &L = lanes[k];
+        L.txs = &rv.tx;
+        L.rxs = &rv.rx;
+        L.ws = ws;
+        L.rank = rank;
+        L.tag = q.tag ^ (static_cast<uint64_t>(k) << 60);
+        L.seq = seq;
+        L.be = be;
+        L.pq = pq;
+        L.st = lane_streams.back()->get();
+        L.ready = ready;
+        L.src = static_cast<const uint8_t *>(q.src) + lo[k] * es;
+        L.dst = dst + lo[k] * es;
+        L.count = lo[k + 1] - lo[k];
+        L.es = es;
+        L.piece = piece;
+        L.dtype = q.dtype;
+        L.rop = q.op;
+        L.device = device;
+        L.ahead = env_size("PCCL_RING_SEND_AHEAD", 1) != 0;
+        // step-0 payload (own input chunk -> pinned): on the process-wide D2H copy queue (default; FIFO across the
+        // peers of this process) or on the lane's stream (PCCL_RING_STEP0_OP_STREAM=1: blit kernels, per-peer copies
+        // run concurrently). 8 peers x 1 GiB, 32 MiB pieces, 3 runs each: queue 358 / 337 / 341 ms, op stream 331 /
+        // 429 / 388 ms (profiles/r3/ring_ab/summary.txt).
+        L.step0_on_op_stream = env_size("PCCL_RING_STEP0_OP_STREAM", 0) != 0;
+        L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
+        L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
+        L.aborted = [this, t = q.tag] { return abort_received(t); };
+        L.tx = &op.tx;
+        L.rx = &op.rx;
+        L.main_lane = k == 0;
+    }
+    if (nl == 1) {
+        run_lane(lanes[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < nl; ++k) th.emplace_back([&, k] {
+            name_thread("pccl-ring-lane");
+            run_lane(lanes[k]);
+        });
+        run_lane(lanes[0]);
+        for (auto &t : th) t.join();
+    }
+    int rc = 0;
+    for (const auto &L : lanes) rc = std::max(rc, L.rc); // abort (2) outranks an io failure (1)
+    if (rc != 0) {
         be->stream_sync(st);
-        if (q.src == q.dst && !q.scratch) {
+        if (q.src == q.dst && !q.scratch) { // every lane drained: restore the caller's buffer
             be->memcpy_async(dst, backup.data(), bytes, st);
             be->stream_sync(st);
         }
-    };
-    auto fail = [&](int code) -> std::pair<bool, bool> {
-        restore();
-        return {code == 2, code == 2};
-    };
-
-    ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
-    ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
-    size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
-    DevEvent h2d_done[kNb] = {nullptr, nullptr, nullptr}; // last H2D copy reading rxbuf[i] / writing rxdev[i]
-    DevEvent red_done[kNb] = {nullptr, nullptr, nullptr}; // last reduce kernel reading rxdev[i]
-
-    // Steps g = 0 .. 2(W-1)-1: reduce-scatter, then all-gather, run as one continuous pipeline (send-ahead): step
-    // g+1's sinks are posted and its sends published while step g still receives, so every connection streams the
-    // steps back to back and each piece of the next payload leaves the moment it has been reduced (or, all-gather,
-    // received). PCCL_RING_SEND_AHEAD=0 restores the step-synchronous schedule (A/B).
-    const bool ahead = env_size("PCCL_RING_SEND_AHEAD", 1) != 0;
-    // step-0 payload (own input chunk -> pinned): on the process-wide D2H copy queue (default; FIFO across the peers
-    // of this process) or on the op's stream (PCCL_RING_STEP0_OP_STREAM=1: blit kernels, per-peer copies run
-    // concurrently). 8 peers x 1 GiB, 32 MiB pieces, 3 runs each: queue 358 / 337 / 341 ms, op stream 331 / 429 /
-    // 388 ms (profiles/r3/ring_ab/summary.txt).
-    const bool step0_on_op_stream = env_size("PCCL_RING_STEP0_OP_STREAM", 0) != 0;
-    const size_t nsteps = 2 * (ws - 1);
-    auto is_rs = [&](size_t g) { return g + 1 < ws; };
-    auto chunk_tx = [&](size_t g) { // chunk index this peer sends at global step g
-        return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
-    };
-    auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
-    auto region_of = [&](size_t g) { return dst + bounds[chunk_rx(g)].first * es; };
-    size_t max_stripes = 1;
-    for (size_t g = 0; g < nsteps; ++g) {
-        const auto [ts, te] = bounds[chunk_tx(g)];
-        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, rv.tx.size()).off.size());
+        return {rc == 2, rc == 2};
     }
-    // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
-    OpSenders senders(rv.tx, q.tag, seq, piece, nsteps, max_stripes, be, op.tx);
-    auto publish = [&](size_t g) {
-        if (senders.published(g)) return;
-        const auto [ts, te] = bounds[chunk_tx(g)];
-        const bool staged = g < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
-        OpSenders::Step stp;
-        stp.payload = staged ? txbuf[g % kNb] + txshift[g % kNb] : rxbuf[(g - 1) % kNb];
-        stp.bytes = (te - ts) * es;
-        stp.ready = staged ? &txready[g % kNb] : &rxready[(g - 1) % kNb];
-        senders.publish(g, stp);
-    };
-    auto fail_all = [&](int code) {
-        senders.cancel();
-        return fail(code);
-    };
-
-    // ---- receive side: one set of sinks per step, posted up to one step early
-    struct StepRx {
-        StripePlan rp;
-        std::vector<net::MuxConn::SinkRef> sinks;
-        std::vector<size_t> done; // elements consumed per stripe
-        size_t remaining = 0;
-        bool posted = false;
-    };
-    std::vector<StepRx> srx(nsteps);
-    auto rx_conn = [&](size_t k) { return rv.rx[(seq + k) % rv.rx.size()].get(); };
-    // rxbuf[g % kNb] may take step g's bytes once the step that used it before (g - kNb) is finished with it: its H2D
-    // copies and reduce kernels completed and (all-gather) the step after it has forwarded its bytes
-    auto can_post = [&](size_t g) {
-        if (g < kNb) return true;
-        const size_t b = g % kNb, prev = g - kNb;
-        if (h2d_done[b] && be->event_query(h2d_done[b]) == 0) return false;
-        if (red_done[b] && be->event_query(red_done[b]) == 0) return false;
-        if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
-        return true;
-    };
-    auto post = [&](size_t g) {
-        StepRx &r = srx[g];
-        const size_t b = g % kNb;
-        h2d_done[b] = red_done[b] = nullptr;
-        if (!is_rs(g)) rxready[b].clear();
-        const auto [rs0, re0] = bounds[chunk_rx(g)];
-        r.rp = plan_stripes((re0 - rs0) * es, rv.rx.size());
-        r.sinks.resize(r.rp.off.size());
-        r.done.assign(r.rp.off.size(), 0);
-        r.remaining = 0;
-        for (size_t k = 0; k < r.rp.off.size(); ++k) {
-            if (r.rp.len[k] == 0) continue;
-            r.sinks[k] = rx_conn(k)->post_sink(q.tag, seq, rxbuf[b] + r.rp.off[k], r.rp.len[k]);
-            ++r.remaining;
-        }
-        r.posted = true;
-    };
-    auto unpost = [&](size_t g) {
-        StepRx &r = srx[g];
-        if (!r.posted) return;
-        for (size_t k = 0; k < r.sinks.size(); ++k)
-            if (r.sinks[k]) rx_conn(k)->remove_sink(q.tag, r.sinks[k]);
-        r.sinks.clear();
-        r.posted = false;
-    };
-    struct Unposter { // sinks must never outlive their buffers (also on failure)
-        std::function<void()> fn;
-        ~Unposter() { fn(); }
-    } unposter{[&] {
-        for (size_t g = 0; g < nsteps; ++g) unpost(g);
-    }};
-
-    for (size_t g = 0; g < nsteps; ++g) {
-        const size_t b = g % kNb, nb = (g + 1) % kNb;
-        const bool rs = is_rs(g);
-        if (!ahead && g > 0 && !senders.wait(g - 1)) return fail_all(1);
-        // 1. step g's sinks (normally posted during step g-1)
-        while (!srx[g].posted) {
-            if (can_post(g)) {
-                post(g);
-                break;
-            }
-            if (senders.failed()) return fail_all(1);
-            std::this_thread::sleep_for(std::chrono::microseconds(20));
-        }
-        // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
-        uint8_t *region = region_of(g);
-        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
-        if (rs) {
-            if (g >= 2 && !senders.wait(g - 2)) return fail_all(1);
-            txready[nb].clear();
-            txshift[nb] = shift;
-        }
-        // 3. own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
-        if (g == 0) {
-            const auto [ts, te] = bounds[chunk_tx(0)];
-            txready[0].clear();
-            txshift[0] = 0;
-            DevStream q0 = step0_on_op_stream ? st : pq.d2h;
-            for (size_t off = 0; off < (te - ts) * es; off += piece) {
-                const size_t n = std::min(piece, (te - ts) * es - off);
-                be->memcpy_async(txbuf[0] + off, static_cast<const uint8_t *>(q.src) + ts * es + off, n, q0);
-                DevEvent e = record(q0);
-                if (!step0_on_op_stream) last_d2h = e;
-                txready[0].add(off, off + n, e);
-            }
-        }
-        publish(g);
-        if (ahead && g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
-        // 4. receive + consume step g
-        StepRx &r = srx[g];
-        uint8_t *sink = rxbuf[b];
-        DevEvent last_red = nullptr;
-        std::function<void(size_t, size_t)> consume;
-        if (rs) {
-            // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
-            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
-            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
-                const size_t off = a * es, n = (e - a) * es;
-                be->memcpy_async(stage + off, sink + off, n, pq.h2d);
-                last_h2d = record(pq.h2d);
-                be->stream_wait_event(st, last_h2d);
-                be->reduce_copy(region + off, stage + off, out + off, e - a, q.dtype, q.op, st);
-                last_red = record(st);
-                txready[nb].add(off, off + n, last_red);
-            };
-        } else {
-            consume = [&, sink, region, b](size_t a, size_t e) {
-                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d);
-                last_h2d = record(pq.h2d);
-                rxready[b].add(a * es, e * es, nullptr); // in host memory: forwardable at once
-            };
-        }
-        const size_t gran_el = std::max<size_t>(1, piece / es);
-        int rc = 0;
-        size_t idle = 0, rr = 0;
-        while (r.remaining > 0) {
-            bool progress = false;
-            for (size_t k = 0; k < r.sinks.size(); ++k) {
-                if (!r.sinks[k]) continue;
-                const size_t want = r.rp.len[k] / es;
-                if (r.done[k] >= want) continue;
-                const size_t have = net::MuxConn::sink_progress(r.sinks[k]) / es;
-                if (have > r.done[k] && (have - r.done[k] >= gran_el || have >= want)) {
-                    const size_t e0 = r.rp.off[k] / es;
-                    consume(e0 + r.done[k], e0 + have);
-                    r.done[k] = have;
-                    progress = true;
-                    if (r.done[k] >= want) --r.remaining;
-                }
-            }
-            // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
-            if (ahead && g + 1 < nsteps && !srx[g + 1].posted && can_post(g + 1)) post(g + 1);
-            if (r.remaining == 0 || progress) {
-                idle = 0;
-                continue;
-            }
-            size_t k = rr++ % r.sinks.size();
-            while (!r.sinks[k] || r.done[k] >= r.rp.len[k] / es) k = rr++ % r.sinks.size();
-            net::MuxConn *c = rx_conn(k);
-            c->wait_sink(r.sinks[k], std::min(r.rp.len[k], (r.done[k] + gran_el) * es), 5ms);
-            if (!c->is_open() || senders.failed()) {
-                rc = 1;
-                break;
-            }
-            if (++idle % 8 == 0 && aborted()) {
-                rc = 2;
-                break;
-            }
-        }
-        h2d_done[b] = last_h2d;
-        red_done[b] = last_red;
-        if (rc) return fail_all(rc);
-        op.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
-        unpost(g);
-        if (!ahead && !senders.wait(g)) return fail_all(1); // classic schedule: a step ends when its sends are done
-        step_mark(rs, rs ? g : g - (ws - 1));
-        if (g == 0) fault_point("ring_step", seq);
-        if (g + 2 == ws) trace_mark("reduce_scatter");
-    }
-    if (!senders.wait(nsteps - 1)) return fail_all(1);
-    if (last_h2d) be->stream_wait_event(st, last_h2d);
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
     if (!be->stream_sync(st)) return {false, false};
     return {true, false};
