@@ -594,7 +594,41 @@ def _numa_bind():
         return {"numa_bind_error": repr(e)[:200]}
 
 
+def _cpu_spread():
+    """PCCL_BENCH_CPU_SPREAD=k (default 3 on one GPU, 0 = off; off by default with several ranks): restrict the
+    process to the first k CPUs of every L3 domain (CCD) in its affinity mask, before any thread exists. The
+    loopback-TCP ring moves ~15 GB through socket copies per op on a 16-CPU quota; with all 256 CPUs of the host in the
+    mask its ~40 threads migrate over every CCD and both sockets and burst past the quota (the cgroup then throttles
+    the whole process, GPU feeding included), while k cores per CCD keep the memory bandwidth of every CCD at hand.
+    Measured, 8 peers x 1 GiB, 3 runs each (profiles/r3/cpu_spread/): all 256 CPUs 374 / 355 / 389 ms, 2 per CCD
+    337 / 349 / 342, 3 per CCD 330 / 344 / 328, 4 per CCD 329 / 331 / 359. Returns a description for extra."""
+    default = "3" if int(os.environ.get("WORLD_SIZE", "1")) == 1 else "0"
+    k = int(os.environ.get("PCCL_BENCH_CPU_SPREAD", default))
+    if k <= 0:
+        return None
+    try:
+        allowed = os.sched_getaffinity(0)
+        domains = {}
+        for c in sorted(allowed):
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                    key = f.read().strip()
+            except OSError:
+                key = "?"
+            domains.setdefault(key, []).append(c)
+        pick = set()
+        for cpus in domains.values():
+            pick.update(cpus[:k])
+        if len(pick) < min(16, len(allowed)):  # unknown topology: leave the mask alone
+            return {"cpu_spread": "skipped", "l3_domains": len(domains)}
+        os.sched_setaffinity(0, pick)
+        return {"cpus": len(pick), "per_l3": k, "l3_domains": len(domains)}
+    except (OSError, ValueError) as e:
+        return {"cpu_spread_error": repr(e)[:200]}
+
+
 def main():
+    spread = _cpu_spread()
     numa = _numa_bind()
     a = _args()
     # stdout carries exactly one line, the result JSON: everything else any library, child process or the gloo
@@ -650,6 +684,7 @@ def main():
     extra["sweep"] = sweep
     if numa is not None:
         extra["numa_bind"] = numa
+    extra["cpu_affinity"] = spread or {"cpus": len(os.sched_getaffinity(0)), "per_l3": "all"}
 
     cfg_model = (f"{P}-peer ring all-reduce (SUM), {a.mib} MiB bf16 HIP device buffer per peer, "
                  f"{'loopback TCP device ring' if path_name == 'DEVICE_RING' else path_name}")
