@@ -339,7 +339,7 @@ def test_threaded_peers_skip_staging(hip):
     for lo, hi, xlo, xhi in _run(2, fn):
         assert lo == hi == 3.0 and xlo == xhi == 3.0
     s1 = pccl.memory.ipc_buffer_stats()
-    d = {k: s1[k] - s0[k] for k in s0}
+    d = {k: s1[k] - s0[k] for k in ("direct_in", "direct_out", "staged_in", "staged_out")}
     assert d == {"direct_in": 2, "direct_out": 4, "staged_in": 2, "staged_out": 0}, d
 
 
