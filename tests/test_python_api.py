@@ -145,7 +145,8 @@ def test_shareable_memory_api_on_cpu():
     assert not pccl.memory.is_shareable(torch.empty(16))
     assert isinstance(pccl.memory.maybe_shareable("cpu"), contextlib.nullcontext)
     st = pccl.memory.ipc_buffer_stats()
-    assert set(st) == {"direct_in", "direct_out", "staged_in", "staged_out"} and all(v >= 0 for v in st.values())
+    assert set(st) == {"direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains",
+                       "preflight_failed", "preflight_passed"} and all(v >= 0 for v in st.values())
     assert pccl.memory.live_bytes() >= 0
     if not torch.cuda.is_available():
         assert not pccl.memory.available()
