@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <tuple>
 
@@ -584,6 +585,10 @@ bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
     return true;
 }
 
+bool IpcArena::all_local_peers() const {
+    return std::all_of(pids_.begin(), pids_.end(), [&](int p) { return p == pids_[rank_]; });
+}
+
 bool IpcArena::push_algorithm() {
     static const bool two_shot = [] {
         const char *v = std::getenv("PCCL_IPC_ALGO");
@@ -682,7 +687,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
         // An in-place op always stages its input: peers read the staged copy while results land in the caller's
         // buffer, and the copy is the abort backup (reference reduce.cpp:551-580 keeps a backup for src == dst too).
         const bool allow_direct = !env_flag("PCCL_IPC_NO_ZERO_COPY", false);
-        const bool all_local = std::all_of(pids_.begin(), pids_.end(), [&](int p) { return p == pids_[rank_]; });
+        const bool all_local = all_local_peers();
         auto direct = [&](const void *p, uint8_t *handle, uint64_t &off) {
             if (!allow_direct) return false;
             if (all_local) {
@@ -846,6 +851,16 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     ctx.pins = std::move(pins);
     ++g_buf_stats[in_direct ? 0 : 2];
     ++g_buf_stats[out_direct ? 1 : 3];
+    // ordinary (non-shareable) tensors between processes: both directions staged, two extra full copies per op
+    // (8 peers x 1 GiB: 12.7 vs 3.7 ms with shareable buffers, docs/PERFORMANCE.md); say so once per process
+    if (!in_direct && !out_direct && src != dst && !all_local_peers()) {
+        static std::once_flag warned;
+        std::call_once(warned, [&] {
+            LOG(WARN) << "IPC: all-reduce of " << bytes << " bytes between processes stages both input and output "
+                      << "(the tensors are not in shareable memory); allocate them inside pccl_amd.memory."
+                      << "shareable_memory() for zero-copy xGMI ops";
+        });
+    }
     {
         std::lock_guard l(g_ctx_mtx);
         g_ctx[{this, seq}] = std::move(ctx);

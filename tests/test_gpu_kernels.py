@@ -85,9 +85,10 @@ def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
 
 
 @pytest.mark.parametrize("n", [1, 1000, (1 << 22) + 3, 300_000_001])
-def test_device_minmax_single_launch_repeated(hip, n):
-    """min/max is one launch with a last-workgroup fold and a re-armed ticket: repeated calls on the same stream
-    (all-negative data, then shifted data, tails, > 1024 workgroups of tiles) must equal the host."""
+def test_device_minmax_repeated(hip, n):
+    """min/max is two launches (k_minmax_partial writes one partial per workgroup, k_minmax_final folds them,
+    csrc/hip/kernels.hpp): repeated calls on the same stream (all-negative data, then shifted data, tails, > 1024
+    workgroups of tiles) must equal the host."""
     for shift in (-50.0, 3.0, 0.0):
         if n < (1 << 23):
             xd = (_rand(n, torch.float32, 7 + int(shift)) * 4 - 10.0 + shift).bfloat16().to(hip)
