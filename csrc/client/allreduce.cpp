@@ -12,6 +12,7 @@
 //    each piece is sent as soon as its event completes; received bytes land in pinned memory and HIP kernels reduce /
 //    de-quantize them straight from pinned memory into HBM (zero-copy over PCIe), overlapped with the socket.
 #include <algorithm>
+#include <array>
 #include <map>
 #include <condition_variable>
 #include <functional>
@@ -730,7 +731,10 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
 namespace {
 
 struct PcieQueues {
-    DevStream h2d = nullptr, d2h = nullptr;
+    static constexpr size_t kMaxH2d = 4;
+    std::array<DevStream, kMaxH2d> h2d{}; // received pieces -> HBM, round robin over nh2d queues
+    size_t nh2d = 1;
+    DevStream d2h = nullptr;
 };
 
 // process-wide copy queues of `device` (never destroyed: they may outlive static destruction order)
@@ -739,10 +743,13 @@ PcieQueues shared_pcie_queues(DeviceBackend *be, int device) {
     static auto *q = new std::map<int, PcieQueues>();
     std::lock_guard l(m);
     PcieQueues &e = (*q)[device];
-    if (!e.h2d) {
+    if (!e.h2d[0]) {
         const int cur = be->current_device();
         be->set_device(device);
-        e.h2d = be->create_stream();
+        // PCCL_H2D_QUEUES (1..4, default 1): one host->device stream runs ~46 GB/s on MI355X, several together
+        // ~57 GB/s one way (profiles/r2/sysprobe.json)
+        e.nh2d = std::max<size_t>(1, std::min(PcieQueues::kMaxH2d, env_size("PCCL_H2D_QUEUES", 1)));
+        for (size_t k = 0; k < e.nh2d; ++k) e.h2d[k] = be->create_stream();
         e.d2h = be->create_stream();
         if (cur >= 0) be->set_device(cur);
     }
@@ -993,7 +1000,9 @@ void run_lane(Lane &L) {
 
     // events of this lane (returned to the pool once everything they guard has completed)
     std::vector<DevEvent> owned;
-    DevEvent last_h2d = nullptr, last_d2h = nullptr;
+    DevEvent last_d2h = nullptr;
+    std::array<DevEvent, PcieQueues::kMaxH2d> last_h2d{}; // last copy issued on each H2D queue
+    size_t h2d_rr = 0;
     auto record = [&](DevStream s) {
         DevEvent e = event_pool().get();
         owned.push_back(e);
@@ -1025,10 +1034,12 @@ void run_lane(Lane &L) {
     struct Drain {
         DeviceBackend *be;
         DevStream st;
-        DevEvent *h2d, *d2h;
+        std::array<DevEvent, PcieQueues::kMaxH2d> *h2d;
+        DevEvent *d2h;
         std::vector<DevEvent> *ev;
         ~Drain() {
-            if (*h2d) be->event_sync(*h2d);
+            for (DevEvent e : *h2d)
+                if (e) be->event_sync(e);
             if (*d2h) be->event_sync(*d2h);
             be->stream_sync(st);
             for (auto e : *ev) event_pool().put(e);
@@ -1038,7 +1049,8 @@ void run_lane(Lane &L) {
     ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
     ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
     size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
-    DevEvent h2d_done[kNb] = {nullptr, nullptr, nullptr}; // last H2D copy reading rxbuf[i] / writing rxdev[i]
+    // last H2D copies (one per queue) reading rxbuf[i] / writing rxdev[i]
+    std::array<DevEvent, PcieQueues::kMaxH2d> h2d_done[kNb] = {};
     DevEvent red_done[kNb] = {nullptr, nullptr, nullptr}; // last reduce kernel reading rxdev[i]
 
     const size_t nsteps = 2 * (ws - 1);
@@ -1085,7 +1097,8 @@ void run_lane(Lane &L) {
     auto can_post = [&](size_t g) {
         if (g < kNb) return true;
         const size_t b = g % kNb, prev = g - kNb;
-        if (h2d_done[b] && be->event_query(h2d_done[b]) == 0) return false;
+        for (DevEvent e : h2d_done[b])
+            if (e && be->event_query(e) == 0) return false;
         if (red_done[b] && be->event_query(red_done[b]) == 0) return false;
         if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
         return true;
@@ -1093,7 +1106,8 @@ void run_lane(Lane &L) {
     auto post = [&](size_t g) {
         StepRx &r = srx[g];
         const size_t b = g % kNb;
-        h2d_done[b] = red_done[b] = nullptr;
+        h2d_done[b] = {};
+        red_done[b] = nullptr;
         if (!is_rs(g)) rxready[b].clear();
         const auto [rs0, re0] = bounds[chunk_rx(g)];
         r.rp = plan_stripes((re0 - rs0) * es, rxs.size());
@@ -1164,23 +1178,28 @@ void run_lane(Lane &L) {
         StepRx &r = srx[g];
         uint8_t *sink = rxbuf[b];
         DevEvent last_red = nullptr;
+        std::array<DevEvent, PcieQueues::kMaxH2d> step_h2d{}; // this step's last copy per queue
+        auto h2d_queue = [&] { return h2d_rr++ % pq.nh2d; };
         std::function<void(size_t, size_t)> consume;
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
             uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
             consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
                 const size_t off = a * es, n = (e - a) * es;
-                be->memcpy_async(stage + off, sink + off, n, pq.h2d);
-                last_h2d = record(pq.h2d);
-                be->stream_wait_event(st, last_h2d);
+                const size_t qi = h2d_queue();
+                be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
+                DevEvent ce = record(pq.h2d[qi]);
+                last_h2d[qi] = step_h2d[qi] = ce;
+                be->stream_wait_event(st, ce);
                 be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, st);
                 last_red = record(st);
                 txready[nb].add(off, off + n, last_red);
             };
         } else {
             consume = [&, sink, region, b](size_t a, size_t e) {
-                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d);
-                last_h2d = record(pq.h2d);
+                const size_t qi = h2d_queue();
+                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d[qi]);
+                last_h2d[qi] = step_h2d[qi] = record(pq.h2d[qi]);
                 rxready[b].add(a * es, e * es, nullptr); // in host memory: forwardable at once
             };
         }
@@ -1221,7 +1240,7 @@ void run_lane(Lane &L) {
                 break;
             }
         }
-        h2d_done[b] = last_h2d;
+        h2d_done[b] = step_h2d;
         red_done[b] = last_red;
         if (rc) return fail_all(rc);
         *L.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
@@ -1274,10 +1293,11 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     if (env_size("PCCL_SHARED_COPY_QUEUES", 1) != 0) {
         pq = shared_pcie_queues(be, device);
     } else { // A/B switch: per-op copy streams
-        pq.h2d = own_h2d.get();
+        pq.h2d[0] = own_h2d.get();
+        pq.nh2d = 1;
         pq.d2h = own_d2h.get();
     }
-    if (!pq.h2d || !pq.d2h) return {false, false};
+    if (!pq.h2d[0] || !pq.d2h) return {false, false};
 
     // the caller's input -> dst (out of place) or a backup of it (in place, restored on abort), on the op stream
     Lease backup;
