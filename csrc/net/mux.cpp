@@ -156,7 +156,9 @@ bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n)
     iovec iov[2] = {{hdr, 24}, {const_cast<void *>(data), n}};
     std::lock_guard lock(tx_mtx_);
     if (wan_sim().enabled) wan_shape(n + 24, sim_next_free_, sim_last_send_);
-    if (!sendv_all(fd_, iov, n ? 2 : 1)) {
+    // bulk frames from pinned staging buffers may go out as MSG_ZEROCOPY (socket.cpp: sendv_all_zerocopy)
+    const bool zc = zerocopy_send_enabled() && n >= (256u << 10);
+    if (!(zc ? sendv_all_zerocopy(fd_, iov, n ? 2 : 1, zc_next_id_) : sendv_all(fd_, iov, n ? 2 : 1))) {
         open_.store(false, std::memory_order_release);
         return false;
     }

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <fcntl.h>
 #include <ifaddrs.h>
+#include <linux/errqueue.h>
 #include <fstream>
 #include <mutex>
 #include <netinet/in.h>
@@ -72,7 +73,19 @@ void tune_socket(int fd, bool bulk) {
         int sz = 8 << 20;
         setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
         setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+        // like the reference's data sockets (tinysockets/src/multiplexed_socket.cpp:51-59): immediate ACKs, and busy
+        // polling of the device queue on NICs that support it (best effort: a value above net.core.busy_poll needs
+        // CAP_NET_ADMIN, and loopback has no NAPI queue to poll)
+        setsockopt(fd, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof(one));
+        int busy = static_cast<int>(env_size("PCCL_SO_BUSY_POLL_US", 50));
+        if (busy > 0) setsockopt(fd, SOL_SOCKET, SO_BUSY_POLL, &busy, sizeof(busy));
+        if (zerocopy_send_enabled()) setsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one));
     }
+}
+
+bool zerocopy_send_enabled() {
+    static const bool on = env_size("PCCL_ZEROCOPY_SEND", 0) != 0;
+    return on;
 }
 
 int connect_tcp(const SockAddr &addr, int timeout_ms) {
@@ -179,6 +192,77 @@ bool sendv_all(int fd, iovec *iov, int iovcnt) {
         while (iovcnt > 0 && iov->iov_len == 0) {
             ++iov;
             --iovcnt;
+        }
+    }
+    return true;
+}
+
+// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1, the socket has SO_ZEROCOPY): the kernel pins the user pages instead of
+// copying them into socket buffers and reports completion on the socket's error queue; the call returns once every
+// byte it sent is released, so the caller may reuse the buffer as after a plain send. On loopback the kernel copies
+// the pages anyway when it delivers them to the receiving socket ("deferred copy", reported as
+// SO_EE_CODE_ZEROCOPY_COPIED), so only a real NIC saves the copy. Returns false on error.
+bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id) {
+    uint32_t first = next_id;
+    bool sent_any = false;
+    while (iovcnt > 0) {
+        msghdr msg{};
+        msg.msg_iov = iov;
+        msg.msg_iovlen = static_cast<size_t>(iovcnt);
+        ssize_t k = ::sendmsg(fd, &msg, MSG_NOSIGNAL | MSG_ZEROCOPY);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            if (errno == ENOBUFS) { // optmem exhausted by pinned pages in flight: fall back for this piece
+                k = ::sendmsg(fd, &msg, MSG_NOSIGNAL);
+                if (k < 0) return false;
+            } else {
+                return false;
+            }
+        } else {
+            ++next_id; // every successful MSG_ZEROCOPY call takes one notification id
+            sent_any = true;
+        }
+        while (k > 0 && iovcnt > 0) {
+            if (static_cast<size_t>(k) >= iov->iov_len) {
+                k -= static_cast<ssize_t>(iov->iov_len);
+                ++iov;
+                --iovcnt;
+            } else {
+                iov->iov_base = static_cast<uint8_t *>(iov->iov_base) + k;
+                iov->iov_len -= static_cast<size_t>(k);
+                k = 0;
+            }
+        }
+        while (iovcnt > 0 && iov->iov_len == 0) {
+            ++iov;
+            --iovcnt;
+        }
+    }
+    if (!sent_any) return true;
+    // wait for the notifications of ids [first, next_id)
+    uint32_t done_to = first; // completed below this id
+    while (static_cast<int32_t>(next_id - done_to) > 0) {
+        pollfd pfd{fd, 0, 0}; // POLLERR is always reported
+        if (::poll(&pfd, 1, 1000) < 0 && errno != EINTR) return false;
+        while (true) {
+            char ctrl[128];
+            msghdr msg{};
+            msg.msg_control = ctrl;
+            msg.msg_controllen = sizeof(ctrl);
+            if (::recvmsg(fd, &msg, MSG_ERRQUEUE | MSG_DONTWAIT) < 0) {
+                if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
+                return false;
+            }
+            for (cmsghdr *cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
+                if (!((cm->cmsg_level == SOL_IP && cm->cmsg_type == IP_RECVERR) ||
+                      (cm->cmsg_level == SOL_IPV6 && cm->cmsg_type == IPV6_RECVERR)))
+                    continue;
+                sock_extended_err se{};
+                std::memcpy(&se, CMSG_DATA(cm), sizeof(se));
+                if (se.ee_origin != SO_EE_ORIGIN_ZEROCOPY) continue;
+                // [ee_info, ee_data] completed; notifications arrive in order on one socket
+                if (static_cast<int32_t>(se.ee_data + 1 - done_to) > 0) done_to = se.ee_data + 1;
+            }
         }
     }
     return true;

@@ -31,6 +31,9 @@ int listen_tcp(ccoip_inet_protocol_t proto, uint16_t port, bool bump, uint16_t &
 // Full send / receive. Return false on error or EOF. recv_all honours an optional abort flag polled every 100 ms.
 bool send_all(int fd, const void *data, size_t n);
 bool sendv_all(int fd, struct iovec *iov, int iovcnt);
+// MSG_ZEROCOPY variant (PCCL_ZEROCOPY_SEND=1); `next_id` = the socket's notification counter (starts at 0)
+bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id);
+bool zerocopy_send_enabled();
 bool recv_all(int fd, void *data, size_t n);
 
 // Waits until `fd` is readable. Returns 1 readable, 0 timeout, -1 error/hup.
