@@ -86,7 +86,9 @@ static void wan_shape(size_t n, double &flow_next_free, double &last_send) {
     last_send = now_s();
 }
 
-MuxConn::MuxConn(int fd, Mode mode, const SockAddr &peer_addr) : fd_(fd), mode_(mode), peer_addr_(peer_addr) {}
+MuxConn::MuxConn(int fd, Mode mode, const SockAddr &peer_addr)
+    : fd_(fd), mode_(mode), peer_addr_(peer_addr),
+      zerocopy_(mode == Mode::Tx && fd >= 0 && zerocopy_send_enabled() && socket_zerocopy_on(fd)) {}
 
 MuxConn::~MuxConn() {
     interrupt();
@@ -157,7 +159,7 @@ bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n)
     std::lock_guard lock(tx_mtx_);
     if (wan_sim().enabled) wan_shape(n + 24, sim_next_free_, sim_last_send_);
     // bulk frames from pinned staging buffers may go out as MSG_ZEROCOPY (socket.cpp: sendv_all_zerocopy)
-    const bool zc = zerocopy_send_enabled() && n >= (256u << 10);
+    const bool zc = zerocopy_ && n >= (256u << 10);
     if (!(zc ? sendv_all_zerocopy(fd_, iov, n ? 2 : 1, zc_next_id_) : sendv_all(fd_, iov, n ? 2 : 1))) {
         open_.store(false, std::memory_order_release);
         return false;

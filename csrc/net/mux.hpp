@@ -119,6 +119,7 @@ private:
     bool jobs_stop_ = false;
     double sim_next_free_ = 0; // WAN emulation: time (s, steady clock) at which this flow's link is free again
     double sim_last_send_ = -1e9;
+    const bool zerocopy_;     // bulk frames as MSG_ZEROCOPY (enabled and SO_ZEROCOPY set on this socket)
     uint32_t zc_next_id_ = 0; // MSG_ZEROCOPY notification counter of this socket (guarded by tx_mtx_)
 
     std::mutex mtx_;

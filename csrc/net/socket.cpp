@@ -83,8 +83,14 @@ void tune_socket(int fd, bool bulk) {
     }
 }
 
+bool socket_zerocopy_on(int fd) {
+    int v = 0;
+    socklen_t l = sizeof(v);
+    return ::getsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &v, &l) == 0 && v != 0;
+}
+
 bool zerocopy_send_enabled() {
-    static const bool on = env_size("PCCL_ZEROCOPY_SEND", 0) != 0;
+    static const bool on = env_size("PCCL_ZEROCOPY_SEND", 1) != 0;
     return on;
 }
 
@@ -197,7 +203,7 @@ bool sendv_all(int fd, iovec *iov, int iovcnt) {
     return true;
 }
 
-// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1, the socket has SO_ZEROCOPY): the kernel pins the user pages instead of
+// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1 (default), the socket has SO_ZEROCOPY: socket_zerocopy_on): the kernel pins the user pages instead of
 // copying them into socket buffers and reports completion on the socket's error queue; the call returns once every
 // byte it sent is released, so the caller may reuse the buffer as after a plain send. On loopback the kernel copies
 // the pages anyway when it delivers them to the receiving socket ("deferred copy", reported as
@@ -241,9 +247,15 @@ bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id) {
     if (!sent_any) return true;
     // wait for the notifications of ids [first, next_id)
     uint32_t done_to = first; // completed below this id
+    int idle_polls = 0;
     while (static_cast<int32_t>(next_id - done_to) > 0) {
         pollfd pfd{fd, 0, 0}; // POLLERR is always reported
-        if (::poll(&pfd, 1, 1000) < 0 && errno != EINTR) return false;
+        const int pr = ::poll(&pfd, 1, 1000);
+        if (pr < 0 && errno != EINTR) return false;
+        if (pr == 0 && ++idle_polls >= 30) { // no completion for 30 s: the peer stopped reading
+            LOG(WARN) << "MSG_ZEROCOPY: no send completion for 30 s; closing the connection";
+            return false;
+        }
         while (true) {
             char ctrl[128];
             msghdr msg{};

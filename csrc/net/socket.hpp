@@ -34,6 +34,7 @@ bool sendv_all(int fd, struct iovec *iov, int iovcnt);
 // MSG_ZEROCOPY variant (PCCL_ZEROCOPY_SEND=1); `next_id` = the socket's notification counter (starts at 0)
 bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id);
 bool zerocopy_send_enabled();
+bool socket_zerocopy_on(int fd); // SO_ZEROCOPY is set (else MSG_ZEROCOPY would be ignored: no completions)
 bool recv_all(int fd, void *data, size_t n);
 
 // Waits until `fd` is readable. Returns 1 readable, 0 timeout, -1 error/hup.
