@@ -972,6 +972,7 @@ struct Lane {
     ReduceOp rop;
     int device;
     bool ahead, step0_on_op_stream;
+    double host_frac = 0; // share of every intermediate reduce-scatter chunk reduced by the CPU (see run_lane)
     LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
     std::atomic<uint64_t> *tx, *rx;
@@ -1060,6 +1061,35 @@ void run_lane(Lane &L) {
     };
     auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
     auto region_of = [&](size_t g) { return L.dst + bounds[chunk_rx(g)].first * es; };
+    // PCIe-balanced reduce placement (PCCL_RING_HOST_REDUCE = f): of every intermediate reduce-scatter chunk (steps
+    // whose result is only forwarded), the first f of the elements are reduced by the CPU from the received bytes and
+    // the peer's own input staged device -> host one step ahead, straight into the next payload. Those bytes then
+    // never cross PCIe host -> device, the link direction that bounds the device ring (every received byte otherwise
+    // goes up for the GPU reduce), while the device -> host volume is unchanged (the input piece instead of the
+    // reduced piece). The last reduce-scatter step (the owner's final chunk) always reduces on the GPU.
+    const bool host_red = L.host_frac > 0 && ws >= 3;
+    auto host_elems = [&](size_t g) -> size_t {
+        if (!host_red || g + 2 >= ws) return 0;
+        const auto [c0, c1] = bounds[chunk_rx(g)];
+        return static_cast<size_t>(static_cast<double>(c1 - c0) * std::min(1.0, L.host_frac)) / 64 * 64;
+    };
+    Lease locl[2];
+    uint8_t *locbuf[2] = {nullptr, nullptr};
+    DevEvent loc_ready[2] = {nullptr, nullptr};
+    if (host_red) {
+        for (int i = 0; i < 2; ++i) {
+            locl[i] = Lease(pinned_pool(), stage_bytes);
+            if (!locl[i].ok()) return fail(1);
+            locbuf[i] = locl[i].data();
+        }
+    }
+    auto stage_local = [&](size_t g) { // own input of step g's host part -> pinned (read once by step g's reduce)
+        const size_t hb = g < 2 * (ws - 1) ? host_elems(g) : 0;
+        if (hb == 0) return;
+        be->memcpy_async(locbuf[g % 2], L.src + bounds[chunk_rx(g)].first * es, hb * es, pq.d2h);
+        loc_ready[g % 2] = last_d2h = record(pq.d2h);
+    };
+
     size_t max_stripes = 1;
     for (size_t g = 0; g < nsteps; ++g) {
         const auto [ts, te] = bounds[chunk_tx(g)];
@@ -1157,6 +1187,11 @@ void run_lane(Lane &L) {
             txready[nb].clear();
             txshift[nb] = shift;
         }
+        // own input of the host-reduced part of steps g (first step only) and g+1, one step ahead
+        if (host_red) {
+            if (g == 0) stage_local(0);
+            stage_local(g + 1);
+        }
         // 3. own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
         if (g == 0) {
             const auto [ts, te] = bounds[chunk_tx(0)];
@@ -1184,7 +1219,21 @@ void run_lane(Lane &L) {
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
             uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
-            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
+            const size_t hb = host_elems(g);
+            bool loc_waited = false;
+            consume = [&, stage, out, sink, region, nb, hb, g](size_t a, size_t e) {
+                if (a < hb) { // CPU part: out = op(own input, received), straight into the next payload
+                    const size_t he = std::min(e, hb);
+                    if (!loc_waited) {
+                        event_wait_polling(be, loc_ready[g % 2]);
+                        loc_waited = true;
+                    }
+                    kernels::host_reduce3(out + a * es, locbuf[g % 2] + a * es, sink + a * es, he - a, L.dtype,
+                                          L.rop);
+                    txready[nb].add(a * es, he * es, nullptr);
+                    a = he;
+                    if (a >= e) return;
+                }
                 const size_t off = a * es, n = (e - a) * es;
                 const size_t qi = h2d_queue();
                 be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
@@ -1362,6 +1411,9 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         // run concurrently). 8 peers x 1 GiB, 32 MiB pieces, 3 runs each: queue 358 / 337 / 341 ms, op stream 331 /
         // 429 / 388 ms (profiles/r3/ring_ab/summary.txt).
         L.step0_on_op_stream = env_size("PCCL_RING_STEP0_OP_STREAM", 0) != 0;
+        // (the CPU produces the same bits as the kernel, so peers may differ in this setting)
+        const char *hr = std::getenv("PCCL_RING_HOST_REDUCE");
+        L.host_frac = hr ? std::max(0.0, std::min(1.0, std::atof(hr))) : 0.0;
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
         L.aborted = [this, t = q.tag] { return abort_received(t); };

@@ -61,6 +61,95 @@ bool host_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op)
     return false;
 }
 
+template<typename E, typename Op>
+static void reduce3_loop(void *out_v, const void *a_v, const void *b_v, size_t n) {
+    using S = typename E::S;
+    using C = typename E::C;
+    auto *__restrict out = static_cast<S *>(out_v);
+    const auto *__restrict a = static_cast<const S *>(a_v);
+    const auto *__restrict b = static_cast<const S *>(b_v);
+    for (size_t i = 0; i < n; ++i) out[i] = E::st(apply_op<Op, C>(E::ld(a[i]), E::ld(b[i])));
+}
+
+// bf16 sum, 16 lanes: widen to fp32 (<< 16), add, round to nearest even with NaN quieting exactly as
+// num::f32_to_bf16, narrow. Returns the number of elements done (a multiple of 16).
+__attribute__((target("avx512f,avx512bw"))) static size_t bf16_sum3_avx512(uint16_t *out, const uint16_t *a,
+                                                                           const uint16_t *b, size_t n) {
+    const __m512i abs_mask = _mm512_set1_epi32(0x7fffffff), inf = _mm512_set1_epi32(0x7f800000);
+    const __m512i bias = _mm512_set1_epi32(0x7fff), one = _mm512_set1_epi32(1), quiet = _mm512_set1_epi32(0x40);
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        const __m512i ai = _mm512_slli_epi32(_mm512_cvtepu16_epi32(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(a + i))), 16);
+        const __m512i bi = _mm512_slli_epi32(_mm512_cvtepu16_epi32(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(b + i))), 16);
+        const __m512i u = _mm512_castps_si512(_mm512_add_ps(_mm512_castsi512_ps(ai), _mm512_castsi512_ps(bi)));
+        const __mmask16 nan = _mm512_cmpgt_epu32_mask(_mm512_and_si512(u, abs_mask), inf);
+        const __m512i hi = _mm512_srli_epi32(u, 16);
+        const __m512i rne = _mm512_srli_epi32(_mm512_add_epi32(u, _mm512_add_epi32(bias, _mm512_and_si512(hi, one))), 16);
+        const __m512i r = _mm512_mask_blend_epi32(nan, rne, _mm512_or_si512(hi, quiet));
+        _mm256_storeu_si256(reinterpret_cast<__m256i *>(out + i), _mm512_cvtepi32_epi16(r));
+    }
+    return i;
+}
+
+__attribute__((target("avx512f"))) static size_t f32_sum3_avx512(float *out, const float *a, const float *b, size_t n) {
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) _mm512_storeu_ps(out + i, _mm512_add_ps(_mm512_loadu_ps(a + i), _mm512_loadu_ps(b + i)));
+    return i;
+}
+
+static bool cpu_has_avx512bw() {
+    static const bool v = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+    return v;
+}
+
+template<typename E>
+static bool reduce3_op(void *out, const void *a, const void *b, size_t n, ReduceOp op) {
+    switch (op) {
+        case ReduceOp::Set: std::memcpy(out, b, n * sizeof(typename E::S)); return true;
+        case ReduceOp::Sum:
+        case ReduceOp::Avg: reduce3_loop<E, OpSum>(out, a, b, n); return true;
+        case ReduceOp::Prod: reduce3_loop<E, OpProd>(out, a, b, n); return true;
+        case ReduceOp::Max: reduce3_loop<E, OpMax>(out, a, b, n); return true;
+        case ReduceOp::Min: reduce3_loop<E, OpMin>(out, a, b, n); return true;
+    }
+    return false;
+}
+
+bool host_reduce3(void *out, const void *a, const void *b, size_t count, DType t, ReduceOp op) {
+    const bool sum = op == ReduceOp::Sum || op == ReduceOp::Avg;
+    size_t done = 0;
+    if (sum && cpu_has_avx512bw()) {
+        if (t == DType::BF16)
+            done = bf16_sum3_avx512(static_cast<uint16_t *>(out), static_cast<const uint16_t *>(a),
+                                    static_cast<const uint16_t *>(b), count);
+        else if (t == DType::F32)
+            done = f32_sum3_avx512(static_cast<float *>(out), static_cast<const float *>(a),
+                                   static_cast<const float *>(b), count);
+    }
+    const size_t es = dtype_size(t);
+    out = static_cast<uint8_t *>(out) + done * es;
+    a = static_cast<const uint8_t *>(a) + done * es;
+    b = static_cast<const uint8_t *>(b) + done * es;
+    count -= done;
+    switch (t) {
+        case DType::F32: return reduce3_op<EF32>(out, a, b, count, op);
+        case DType::F64: return reduce3_op<EF64>(out, a, b, count, op);
+        case DType::BF16: return reduce3_op<EBF16>(out, a, b, count, op);
+        case DType::F16: return reduce3_op<EF16>(out, a, b, count, op);
+        case DType::U8: return reduce3_op<EInt<uint8_t>>(out, a, b, count, op);
+        case DType::I8: return reduce3_op<EInt<int8_t>>(out, a, b, count, op);
+        case DType::U16: return reduce3_op<EInt<uint16_t>>(out, a, b, count, op);
+        case DType::I16: return reduce3_op<EInt<int16_t>>(out, a, b, count, op);
+        case DType::U32: return reduce3_op<EInt<uint32_t>>(out, a, b, count, op);
+        case DType::I32: return reduce3_op<EInt<int32_t>>(out, a, b, count, op);
+        case DType::U64: return reduce3_op<EInt<uint64_t>>(out, a, b, count, op);
+        case DType::I64: return reduce3_op<EInt<int64_t>>(out, a, b, count, op);
+        default: break;
+    }
+    LOG(ERR) << "host_reduce3: unsupported dtype " << dtype_name(t);
+    return false;
+}
+
 // ------------------------------------------------------------------------------------------------------------------
 // min / max
 // ------------------------------------------------------------------------------------------------------------------

@@ -152,6 +152,56 @@ TEST(packet_extensions_backward_compatible) {
 }
 
 // CRC-32C split algebra used by the HIP kernel: raw(A || B) = shift(raw(A), |B|) ^ raw(B)
+TEST(host_reduce3_matches_host_reduce_bitwise) {
+    // the 3-operand host reduce (AVX-512 path for bf16 / fp32 sums) must equal copy + host_reduce bit for bit,
+    // NaN / inf / denormal / rounding-tie inputs included, at lengths that exercise the vector body and the tail
+    std::mt19937_64 rng(11);
+    for (size_t n : {size_t(1), size_t(15), size_t(16), size_t(17), size_t(1000), size_t(65537)}) {
+        std::vector<uint16_t> a(n), b(n), want(n), got(n);
+        for (size_t i = 0; i < n; ++i) {
+            a[i] = static_cast<uint16_t>(rng());
+            b[i] = static_cast<uint16_t>(rng());
+        }
+        if (n > 8) {
+            a[0] = 0x7fc0; b[1] = 0xff81; a[2] = 0x7f80; b[2] = 0xff80; a[3] = 0x0001; b[3] = 0x0001;
+            a[4] = 0x3f80; b[4] = 0x3380; // 1 + 2^-24-ish: a rounding tie
+        }
+        for (ReduceOp op : {ReduceOp::Sum, ReduceOp::Max}) {
+            want = a;
+            EXPECT(kernels::host_reduce(want.data(), b.data(), n, DType::BF16, op));
+            EXPECT(kernels::host_reduce3(got.data(), a.data(), b.data(), n, DType::BF16, op));
+            for (size_t i = 0; i < n; ++i) {
+                const bool both_nan = (want[i] & 0x7fff) > 0x7f80 && (got[i] & 0x7fff) > 0x7f80;
+                // an op on two NaNs may return either (quieted) payload: x86 returns the first source operand's,
+                // and which operand comes first is up to the compiler's / the intrinsics' operand order
+                if (want[i] != got[i] && !both_nan) {
+                    std::printf("    n %zu op %d i %zu a %04x b %04x want %04x got %04x\n", n, static_cast<int>(op), i, a[i], b[i], want[i], got[i]);
+                    EXPECT(want[i] == got[i]);
+                    break;
+                }
+            }
+        }
+        std::vector<float> fa(n), fb(n), fw(n), fg(n);
+        for (size_t i = 0; i < n; ++i) {
+            fa[i] = static_cast<float>(static_cast<int64_t>(rng() % 2000001) - 1000000) * 1e-3f;
+            fb[i] = static_cast<float>(static_cast<int64_t>(rng() % 2000001) - 1000000) * 1e-5f;
+        }
+        fw = fa;
+        EXPECT(kernels::host_reduce(fw.data(), fb.data(), n, DType::F32, ReduceOp::Sum));
+        EXPECT(kernels::host_reduce3(fg.data(), fa.data(), fb.data(), n, DType::F32, ReduceOp::Sum));
+        EXPECT(std::memcmp(fw.data(), fg.data(), n * 4) == 0);
+    }
+    // throughput of the bf16 path on this host (informational)
+    const size_t n = 16u << 20;
+    std::vector<uint16_t> a(n, 0x3f80), b(n, 0x4000), o(n);
+    kernels::host_reduce3(o.data(), a.data(), b.data(), n, DType::BF16, ReduceOp::Sum);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < 4; ++r) kernels::host_reduce3(o.data(), a.data(), b.data(), n, DType::BF16, ReduceOp::Sum);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 4;
+    std::printf("    host_reduce3 bf16 sum: %.1f GB/s of output (one thread)\n", n * 2 / s / 1e9);
+    EXPECT(o[0] == 0x4040); // 1 + 2 = 3
+}
+
 TEST(crc32c_split_combine) {
     std::vector<uint8_t> m(100003);
     uint64_t x = 88172645463325252ull;

@@ -80,9 +80,10 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
             assert torch.all(y == float(1 + 2 * j))
 
 
-@pytest.mark.parametrize("shared_queues,lanes", [("1", "1"), ("0", "1"), ("1", "2")])
+@pytest.mark.parametrize("shared_queues,lanes,host", [("1", "1", "0"), ("0", "1", "0"), ("1", "2", "0"),
+                                                      ("1", "1", "0.6")])
 @pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
-def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, monkeypatch):
+def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, host, monkeypatch):
     """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
     chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
@@ -90,6 +91,7 @@ def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lan
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_SHARED_COPY_QUEUES", shared_queues)
     monkeypatch.setenv("PCCL_RING_LANES", lanes)
+    monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)
     n = 9_000_011
     base = (torch.arange(n, dtype=torch.int64) % 31).float()  # every partial sum < 256: exact in bf16
     inputs = [(base + 7 * r).to(torch.bfloat16) for r in range(world)]
@@ -120,9 +122,10 @@ def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lan
         assert torch.equal(y, expect)
 
 
-@pytest.mark.parametrize("ahead,step0_op,lanes", [("1", "1", "1"), ("0", "1", "1"), ("1", "0", "1"), ("1", "0", "2"),
-                                                  ("1", "1", "3")])
-def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, monkeypatch):
+@pytest.mark.parametrize("ahead,step0_op,lanes,host", [("1", "1", "1", "0"), ("0", "1", "1", "0"), ("1", "0", "1", "0"),
+                                                       ("1", "0", "2", "0"), ("1", "1", "3", "0"),
+                                                       ("1", "0", "1", "0.5"), ("0", "0", "2", "1")])
+def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, host, monkeypatch):
     """Neighbours with different P2P connection pool sizes (1 / 3 / 2 stripes) and chunks that are no multiple of the
     staging piece: a TX stripe of the next step then spans several RX stripes of this one, and the send-ahead
     pipeline must send no byte before it has been received and reduced (advisor round 2, high)."""
@@ -132,6 +135,7 @@ def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, monkeypatch):
     monkeypatch.setenv("PCCL_RING_SEND_AHEAD", ahead)
     monkeypatch.setenv("PCCL_RING_STEP0_OP_STREAM", step0_op)
     monkeypatch.setenv("PCCL_RING_LANES", lanes)  # lanes > 1: parts of the buffer on their own tags, overlapped
+    monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)  # > 0: part of every intermediate chunk reduced by the CPU
     world, n = 3, 9_000_011
     pools = [1, 3, 2]
     base = (torch.arange(n, dtype=torch.int64) % 29).float()
