@@ -973,6 +973,7 @@ struct Lane {
     int device;
     bool ahead, step0_on_op_stream;
     double host_frac = 0; // share of every intermediate reduce-scatter chunk reduced by the CPU (see run_lane)
+    bool ag_on_lane_stream = false; // all-gather bytes -> HBM by blit kernels on the lane stream, not the H2D queue
     LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
     std::atomic<uint64_t> *tx, *rx;
@@ -1246,6 +1247,12 @@ void run_lane(Lane &L) {
             };
         } else {
             consume = [&, sink, region, b](size_t a, size_t e) {
+                if (L.ag_on_lane_stream) { // blit kernel reading pinned memory, on this lane's stream
+                    be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, st);
+                    last_h2d[0] = step_h2d[0] = record(st);
+                    rxready[b].add(a * es, e * es, nullptr);
+                    return;
+                }
                 const size_t qi = h2d_queue();
                 be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d[qi]);
                 last_h2d[qi] = step_h2d[qi] = record(pq.h2d[qi]);
@@ -1414,6 +1421,9 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         // (the CPU produces the same bits as the kernel, so peers may differ in this setting)
         const char *hr = std::getenv("PCCL_RING_HOST_REDUCE");
         L.host_frac = hr ? std::max(0.0, std::min(1.0, std::atof(hr))) : 0.0;
+        // PCCL_RING_AG_KERNEL_COPY=1: the all-gather's received chunks go to HBM as copies on the lane stream (ROCclr
+        // blit kernels reading pinned memory) instead of the shared copy-engine queue
+        L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 0) != 0;
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
         L.aborted = [this, t = q.tag] { return abort_received(t); };
