@@ -974,6 +974,8 @@ struct Lane {
     bool ahead, step0_on_op_stream;
     double host_frac = 0; // share of every intermediate reduce-scatter chunk reduced by the CPU (see run_lane)
     bool ag_on_lane_stream = false; // all-gather bytes -> HBM by blit kernels on the lane stream, not the H2D queue
+    int rs_h2d = 0; // reduce-scatter received bytes: 0 copy engine -> HBM staging, 1 blit copy on the lane stream,
+                    // 2 none (the fused reduce reads them from pinned memory)
     LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
     std::atomic<uint64_t> *tx, *rx;
@@ -1134,6 +1136,11 @@ void run_lane(Lane &L) {
         if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
         return true;
     };
+    // zero-copy reduce-scatter reads the received bytes in place: they share the 16-byte phase of the HBM chunk they
+    // are reduced into, so the fused kernel stays vectorised
+    auto sink_shift = [&](size_t g) -> size_t {
+        return L.rs_h2d == 2 && is_rs(g) ? reinterpret_cast<uintptr_t>(region_of(g)) % 16 : 0;
+    };
     auto post = [&](size_t g) {
         StepRx &r = srx[g];
         const size_t b = g % kNb;
@@ -1147,7 +1154,7 @@ void run_lane(Lane &L) {
         r.remaining = 0;
         for (size_t k = 0; k < r.rp.off.size(); ++k) {
             if (r.rp.len[k] == 0) continue;
-            r.sinks[k] = rx_conn(k)->post_sink(tag, seq, rxbuf[b] + r.rp.off[k], r.rp.len[k]);
+            r.sinks[k] = rx_conn(k)->post_sink(tag, seq, rxbuf[b] + sink_shift(g) + r.rp.off[k], r.rp.len[k]);
             ++r.remaining;
         }
         r.posted = true;
@@ -1212,7 +1219,7 @@ void run_lane(Lane &L) {
         if (g + 1 == ws - 1 && L.open_gate) L.open_gate->signal(); // next step is this lane's all-gather
         // 4. receive + consume step g
         StepRx &r = srx[g];
-        uint8_t *sink = rxbuf[b];
+        uint8_t *sink = rxbuf[b] + sink_shift(g);
         DevEvent last_red = nullptr;
         std::array<DevEvent, PcieQueues::kMaxH2d> step_h2d{}; // this step's last copy per queue
         auto h2d_queue = [&] { return h2d_rr++ % pq.nh2d; };
@@ -1236,12 +1243,20 @@ void run_lane(Lane &L) {
                     if (a >= e) return;
                 }
                 const size_t off = a * es, n = (e - a) * es;
-                const size_t qi = h2d_queue();
-                be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
-                DevEvent ce = record(pq.h2d[qi]);
-                last_h2d[qi] = step_h2d[qi] = ce;
-                be->stream_wait_event(st, ce);
-                be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, st);
+                if (L.rs_h2d == 2) { // the kernel reads the received piece straight from pinned memory
+                    be->reduce_copy(region + off, sink + off, out + off, e - a, L.dtype, L.rop, st);
+                } else {
+                    if (L.rs_h2d == 1) {
+                        be->memcpy_async(stage + off, sink + off, n, st);
+                    } else {
+                        const size_t qi = h2d_queue();
+                        be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
+                        DevEvent ce = record(pq.h2d[qi]);
+                        last_h2d[qi] = step_h2d[qi] = ce;
+                        be->stream_wait_event(st, ce);
+                    }
+                    be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, st);
+                }
                 last_red = record(st);
                 txready[nb].add(off, off + n, last_red);
             };
@@ -1424,6 +1439,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         // PCCL_RING_AG_KERNEL_COPY=1: the all-gather's received chunks go to HBM as copies on the lane stream (ROCclr
         // blit kernels reading pinned memory) instead of the shared copy-engine queue
         L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 0) != 0;
+        L.rs_h2d = static_cast<int>(std::min<size_t>(2, env_size("PCCL_RING_RS_H2D", 0)));
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
         L.aborted = [this, t = q.tag] { return abort_received(t); };
