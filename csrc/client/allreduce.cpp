@@ -1436,9 +1436,12 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         // (the CPU produces the same bits as the kernel, so peers may differ in this setting)
         const char *hr = std::getenv("PCCL_RING_HOST_REDUCE");
         L.host_frac = hr ? std::max(0.0, std::min(1.0, std::atof(hr))) : 0.0;
-        // PCCL_RING_AG_KERNEL_COPY=1: the all-gather's received chunks go to HBM as copies on the lane stream (ROCclr
-        // blit kernels reading pinned memory) instead of the shared copy-engine queue
-        L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 0) != 0;
+        // the all-gather's received chunks go to HBM as copies on the lane stream (ROCclr blit kernels reading pinned
+        // memory, one per peer in parallel) instead of the shared copy-engine queue, which one stream drives at
+        // ~47 GB/s: interleaved A/B, 8 peers x 1 GiB, median of 6-8 windows: 347 vs 376 ms and 337 vs 342 ms on two
+        // boxes (profiles/r3/h2d_modes/). The reduce-scatter keeps the copy engine (blit: 366 ms, zero-copy reduce
+        // from pinned: 347 ms, copy engine: 337 ms). PCCL_RING_AG_KERNEL_COPY=0 / PCCL_RING_RS_H2D=1|2 for A/B.
+        L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 1) != 0;
         L.rs_h2d = static_cast<int>(std::min<size_t>(2, env_size("PCCL_RING_RS_H2D", 0)));
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
