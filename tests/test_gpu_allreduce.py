@@ -158,6 +158,38 @@ def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, host, monkeyp
         assert torch.equal(y, expect)
 
 
+@pytest.mark.parametrize("ag_kernel,rs_h2d", [("0", "0"), ("1", "1"), ("1", "2")])
+def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, monkeypatch):
+    """The device ring's host->device variants (copy engine / blit kernel on the op stream for the all-gather; copy
+    engine, blit, or zero-copy reads by the fused reduce for the reduce-scatter) give the exact result, in place and
+    with chunk offsets that are no multiple of 16 bytes (odd element count: the zero-copy sinks take the chunk's
+    16-byte phase)."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
+    monkeypatch.setenv("PCCL_RING_AG_KERNEL_COPY", ag_kernel)
+    monkeypatch.setenv("PCCL_RING_RS_H2D", rs_h2d)
+    world, n = 4, 6_000_007
+    base = (torch.arange(n, dtype=torch.int64) % 23).float()
+    inputs = [(base + 3 * r).to(torch.bfloat16) for r in range(world)]
+    expect = torch.stack([x.float() for x in inputs]).sum(0).to(torch.bfloat16)
+
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        for tag in range(2):
+            if tag:
+                x.copy_(inputs[rank].to(hip))
+            comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=tag)
+        torch.cuda.synchronize()
+        return x.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, timeout=180, comm_kwargs={"p2p_connection_pool_size": 2})
+    for y, path in res:
+        assert path == pccl.ReducePath.DEVICE_RING.value
+        assert torch.equal(y, expect)
+
+
 @pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
 def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
