@@ -1488,7 +1488,9 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     const size_t qs = dtype_size(q.qtype);
     auto *dst = static_cast<uint8_t *>(q.dst);
     const size_t bytes = q.count * es;
-    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20)) / es * es;
+    // value bytes per quantize / de-quantize piece: PCCL_QUANT_PIECE_BYTES, else PCCL_DEVICE_PIECE_BYTES, else 8 MiB
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_QUANT_PIECE_BYTES",
+                                                            env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20))) / es * es;
     const size_t piece_el = piece / es; // quantized pieces hold the same elements
 
     be->set_device(device);

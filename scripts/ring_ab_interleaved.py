@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--pool", type=int, default=0)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--quant", action="store_true", help="uint8 min-max quantized ring instead of plain bf16")
     a = ap.parse_args()
     variants = []
     for v in a.variants.split(";"):
@@ -55,12 +56,14 @@ def main():
         return 0
     lock = threading.Lock()
 
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if a.quant else None
+
     def fn(i, comm):
         x = torch.randn(n, device=job.dev, dtype=torch.bfloat16)
         y = torch.empty_like(x)
         tag = 0
         for _ in range(a.warmup):
-            comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+            comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
             tag += 1
         for w in range(a.windows):
             for name, kv in (variants if w % 2 == 0 else variants[::-1]):
@@ -70,14 +73,14 @@ def main():
                         os.environ[k] = v
                 job.sync(i)
                 # a first op under the new settings (pooled buffers of the new shape), untimed
-                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
                 tag += 1
                 torch.cuda.synchronize()
                 job.sync(i)
                 th0, c0 = throttled_us(), time.process_time()
                 t0 = time.perf_counter()
                 for _ in range(a.ops):
-                    comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+                    comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
                     tag += 1
                 torch.cuda.synchronize()
                 job.sync(i)
