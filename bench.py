@@ -459,7 +459,8 @@ def run_extras(job, a, nbytes):
                                                       "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
                                for b, t in ipc["sweep"].items()}
         sweep["DEVICE_IPC"][f"{a.mib}MiB"] = {"ms": round(ipc["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(ibus, 3)}
-        extra["latency_1MiB_ipc_us"] = round(ipc["sweep"][1 << 20] * 1e6, 1)
+        # through this harness: 8 peer threads of one Python interpreter, serialised on the GIL around every op
+        extra["latency_1MiB_ipc_python_threads_us"] = round(ipc["sweep"][1 << 20] * 1e6, 1)
         # how this rank's IPC ops handed buffers over, incl. the cross-GPU pre-flight result (pccl_amd.memory)
         extra["ipc_buffer_stats_rank0"] = pccl.memory.ipc_buffer_stats()
         if job.world == 1:
@@ -491,6 +492,9 @@ def run_extras(job, a, nbytes):
         extra["peer_curve"] = curve
     if job.world == 1:
         extra["latency_native"] = latency_native(P)
+        nat = extra["latency_native"].get(f"{P}_peers_1MiB", {})
+        if "median_us" in nat:  # the library's latency: C API, threaded peers, no interpreter in the loop
+            extra["latency_1MiB_ipc_us"] = nat["median_us"]
         extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
