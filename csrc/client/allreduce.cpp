@@ -1033,6 +1033,16 @@ void run_lane(Lane &L) {
         rxbuf[i] = rxl[i].data();
         rxdev[i] = dvl[i].data();
     }
+    // own input staged for the host-reduced part of a step (PCCL_RING_HOST_REDUCE, see host_elems below)
+    Lease locl[2];
+    uint8_t *locbuf[2] = {nullptr, nullptr};
+    if (L.host_frac > 0 && ws >= 3) {
+        for (int i = 0; i < 2; ++i) {
+            locl[i] = Lease(pinned_pool(), stage_bytes);
+            if (!locl[i].ok()) return fail(1);
+            locbuf[i] = locl[i].data();
+        }
+    }
     // declared after every staging lease: destroyed first, so nothing of this lane still reads or writes them when
     // they go back to the pools (also on the early returns below)
     struct Drain {
@@ -1076,16 +1086,7 @@ void run_lane(Lane &L) {
         const auto [c0, c1] = bounds[chunk_rx(g)];
         return static_cast<size_t>(static_cast<double>(c1 - c0) * std::min(1.0, L.host_frac)) / 64 * 64;
     };
-    Lease locl[2];
-    uint8_t *locbuf[2] = {nullptr, nullptr};
     DevEvent loc_ready[2] = {nullptr, nullptr};
-    if (host_red) {
-        for (int i = 0; i < 2; ++i) {
-            locl[i] = Lease(pinned_pool(), stage_bytes);
-            if (!locl[i].ok()) return fail(1);
-            locbuf[i] = locl[i].data();
-        }
-    }
     auto stage_local = [&](size_t g) { // own input of step g's host part -> pinned (read once by step g's reduce)
         const size_t hb = g < 2 * (ws - 1) ? host_elems(g) : 0;
         if (hb == 0) return;
