@@ -1,6 +1,9 @@
 #include "ipc.hpp"
 
 #include <dirent.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <climits>
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/mman.h>
@@ -46,6 +49,17 @@ uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
 }
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Futex on the low 32 bits of a shared 64-bit phase word (little endian: they change with every phase store).
+// Shared (not FUTEX_PRIVATE): the word lives in a shm segment mapped by several processes.
+int futex_wait32(std::atomic<uint64_t> *word, uint32_t expect, long timeout_us) {
+    timespec ts{timeout_us / 1000000, (timeout_us % 1000000) * 1000};
+    return static_cast<int>(::syscall(SYS_futex, reinterpret_cast<uint32_t *>(word), FUTEX_WAIT, expect, &ts,
+                                      nullptr, 0));
+}
+void futex_wake_all(std::atomic<uint64_t> *word) {
+    ::syscall(SYS_futex, reinterpret_cast<uint32_t *>(word), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+}
 } // namespace
 
 struct alignas(64) PeerSlotShm {
@@ -83,7 +97,9 @@ struct ArenaShm {
     std::atomic<uint32_t> join;
     std::atomic<uint32_t> unlinked;
     uint32_t world;
-    uint32_t pad[11];
+    // threads of any ring member sleeping in futex_wait_phase on a phase word: set_phase wakes only when non-zero
+    std::atomic<uint32_t> sleepers;
+    uint32_t pad[10];
     PeerSlotShm *peers() { return reinterpret_cast<PeerSlotShm *>(reinterpret_cast<uint8_t *>(this) + 64); }
     OpPeerShm *op(uint32_t slot, uint32_t peer) {
         auto *base = reinterpret_cast<uint8_t *>(this) + 64 + sizeof(PeerSlotShm) * kMaxWorld;
@@ -464,8 +480,19 @@ bool IpcArena::export_user(void *p, int device, uint8_t handle[kIpcHandleBytes],
 }
 
 void IpcArena::set_phase(uint64_t seq, uint32_t phase) {
-    shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_))
-        ->phase.store(((seq + 1) << 8) | phase, std::memory_order_release);
+    OpPeerShm *p = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    p->phase.store(((seq + 1) << 8) | phase, std::memory_order_seq_cst);
+    // a waiter registers in `sleepers` before it checks the word inside FUTEX_WAIT, and the store above precedes
+    // this load: either it sees the new value and does not sleep, or this wake reaches it
+    if (shm_->sleepers.load(std::memory_order_seq_cst) != 0) futex_wake_all(&p->phase);
+}
+
+// Sleeps until the phase word changes from `seen` (or `timeout_us` passed), instead of a fixed sleep.
+void IpcArena::wait_phase_change(std::atomic<uint64_t> *word, uint64_t seen, long timeout_us) {
+    shm_->sleepers.fetch_add(1, std::memory_order_seq_cst);
+    if (word->load(std::memory_order_seq_cst) == seen)
+        futex_wait32(word, static_cast<uint32_t>(seen & 0xffffffffu), timeout_us);
+    shm_->sleepers.fetch_sub(1, std::memory_order_seq_cst);
 }
 
 // One-character state of /proc/<pid>/task/<tid>/stat (or /proc/<pid>/stat with tid < 0); 0 if unreadable.
@@ -549,7 +576,9 @@ int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
                 cpu_relax();
                 continue;
             }
-            std::this_thread::sleep_for(microseconds(spins < 20000 ? 5 : 50));
+            // spun for a while: sleep until the peer's phase word changes (futex; woken by its set_phase), at most
+            // 2 ms so the liveness / abort checks below keep running
+            wait_phase_change(&p->phase, v, 2000);
             const auto now = steady_clock::now();
             if (now - last_check > milliseconds(10)) {
                 last_check = now;
@@ -578,7 +607,7 @@ bool IpcArena::wait_slot_free(Client &c, uint64_t seq) {
             const uint64_t v = p->phase.load(std::memory_order_acquire);
             const uint32_t vp = static_cast<uint32_t>(v & 0xff);
             if (v == 0 || (v >> 8) >= seq + 1 || vp == PH_RELEASED || vp == PH_ABORTED) break;
-            std::this_thread::sleep_for(microseconds(20));
+            wait_phase_change(&p->phase, v, 2000);
             if (steady_clock::now() - t0 > seconds(30) || !pid_alive(pids_[k]) || !c.master_.is_open()) return false;
         }
     }

@@ -151,6 +151,7 @@ private:
     bool export_user(void *p, int device, uint8_t handle[kIpcHandleBytes], uint64_t &offset);
     // waits until every peer reached `phase` for `seq`; 0 ok, 1 failure (peer dead/aborted/timeout), 2 master abort
     int barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase);
+    void wait_phase_change(std::atomic<uint64_t> *word, uint64_t seen, long timeout_us);
     bool all_local_peers() const; // every ring member is a thread of this process
     // cross-GPU write probe of one op (see run()); true if every peer's probe arrived in my output
     bool preflight(Client &c, uint64_t tag, uint64_t seq, OpCtx &ctx, int device, DevStream st);
