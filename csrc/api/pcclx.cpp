@@ -113,6 +113,46 @@ PCCLX_EXPORT int pcclxDequantReduce(void *dst, const void *src_q, size_t count, 
                : -1;
 }
 
+// dequant_reduce on the device with the fused per-workgroup (min, max) of the stored results, split into `pieces`
+// launches (as the ring's receive ranges are) and folded: minmax_out = {min, max} of dst after the reduce
+PCCLX_EXPORT int pcclxDequantReduceMinmax(void *dst, const void *src_q, size_t count, int vtype, int qtype, int algo,
+                                          int op, const double *meta, int pieces, double *minmax_out) {
+    proto::QuantMeta m;
+    m.algo = static_cast<QuantAlgo>(algo);
+    m.value_type = static_cast<DType>(vtype);
+    m.min_value = meta[0];
+    m.max_value = meta[1];
+    m.zero_point = static_cast<int64_t>(meta[2]);
+    m.scale = static_cast<float>(meta[3]);
+    const auto vt = static_cast<DType>(vtype), qt = static_cast<DType>(qtype);
+    DeviceBackend *be = device_backend();
+    if (!be || pieces < 1) return -1;
+    constexpr int kSlots = 8192;
+    double *partials = static_cast<double *>(be->alloc_device(kSlots * 2 * sizeof(double)));
+    double *out = static_cast<double *>(be->alloc_pinned(16));
+    bool ok = partials && out;
+    int used = 0;
+    const size_t es = dtype_size(vt), qs = dtype_size(qt);
+    const auto params = kernels::make_params(m, qt);
+    for (int k = 0; ok && k < pieces; ++k) {
+        const size_t a = count * k / pieces, b = count * (k + 1) / pieces;
+        int blocks = 0;
+        ok = kSlots - used >= 1 &&
+             be->dequant_reduce_minmax(static_cast<uint8_t *>(dst) + a * es, static_cast<const uint8_t *>(src_q) + a * qs,
+                                       b - a, vt, qt, static_cast<ReduceOp>(op), params, partials + 2 * used,
+                                       kSlots - used, &blocks, nullptr);
+        used += blocks;
+    }
+    ok = ok && be->minmax_fold(partials, used, count, out, nullptr) && be->device_sync();
+    if (ok) {
+        minmax_out[0] = out[0];
+        minmax_out[1] = out[1];
+    }
+    if (partials) be->free_device(partials);
+    if (out) be->free_pinned(out);
+    return ok ? 0 : -1;
+}
+
 PCCLX_EXPORT int pcclxMultiReduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, int dtype,
                                   int op) {
     DeviceBackend *be = device_backend();

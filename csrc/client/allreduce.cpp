@@ -12,6 +12,7 @@
 //    each piece is sent as soon as its event completes; received bytes land in pinned memory and HIP kernels reduce /
 //    de-quantize them straight from pinned memory into HBM (zero-copy over PCIe), overlapped with the socket.
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <map>
 #include <condition_variable>
@@ -55,6 +56,9 @@ BufferPool &device_pool() {
     static BufferPool p(BufferPool::Kind::Device);
     return p;
 }
+
+// quantized device ring: min / max of a step's payload folded from the previous step's fused partials (pcclxQuantStats)
+static std::atomic<uint64_t> g_quant_minmax_folds{0}, g_quant_minmax_passes{0};
 
 static std::vector<std::pair<size_t, size_t>> chunk_bounds(size_t total, size_t ws) {
     std::vector<std::pair<size_t, size_t>> b(ws);
@@ -1543,11 +1547,47 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         }
     } eg{be, st, &events};
 
-    // min/max of `n` elements at device `src` (one host round trip: the meta packet carries them), then the quantize
-    // kernels of every piece into pinned txbuf, each followed by an event that releases the piece to the senders
-    auto quantize_to_pinned = [&](const uint8_t *src, size_t n) -> QuantMeta {
+    // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
+    // (dequant_reduce_minmax) into `mmp`: the chunk a step receives is the chunk the next step quantizes (and the last
+    // step's is the all-gather's first payload), so its min / max is one fold of those partials instead of a second
+    // pass over the chunk. PCCL_QUANT_FUSED_MINMAX=0 turns it off; a step whose launches do not fit the partials
+    // buffer falls back to the separate min / max pass.
+    const bool fuse_mm = env_size("PCCL_QUANT_FUSED_MINMAX", 1) != 0;
+    constexpr int kMmSlots = 16384, kMmMinRoom = 64;
+    Lease mmp;
+    if (fuse_mm) mmp = Lease(device_pool(), kMmSlots * 2 * sizeof(double), device);
+    auto *mm_partials = mmp.ok() ? reinterpret_cast<double *>(mmp.data()) : nullptr;
+    int mm_used = 0;
+    bool mm_complete = false; // the partials cover every element of the chunk consumed by the last step
+    auto dequant_consume = [&](uint8_t *dst_el, const uint8_t *src_q, size_t n, ReduceOp rop,
+                               const kernels::QuantParams &params) {
+        int blocks = 0;
+        if (mm_complete && mm_partials && kMmSlots - mm_used >= kMmMinRoom &&
+            be->dequant_reduce_minmax(dst_el, src_q, n, q.dtype, q.qtype, rop, params, mm_partials + 2 * mm_used,
+                                      kMmSlots - mm_used, &blocks, st)) {
+            mm_used += blocks;
+            return;
+        }
+        mm_complete = false;
+        be->dequant_reduce(dst_el, src_q, n, q.dtype, q.qtype, rop, params, st);
+    };
+
+    // min/max of `n` elements at device `src` (one host round trip: the meta packet carries them) - folded from the
+    // previous step's partials when `fused` and they are complete - then the quantize kernels of every piece into
+    // pinned txbuf, each followed by an event that releases the piece to the senders
+    auto quantize_to_pinned = [&](const uint8_t *src, size_t n, bool fused) -> QuantMeta {
+        const bool fold = fused && mm_complete && mm_partials;
+        const int folded = mm_used;
+        mm_used = 0;
+        mm_complete = mm_partials != nullptr; // the next step's consumes start collecting afresh
         if (n == 0) return kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
-        be->minmax(src, n, q.dtype, minmax_out, st);
+        if (fold) {
+            g_quant_minmax_folds.fetch_add(1, std::memory_order_relaxed);
+            be->minmax_fold(mm_partials, folded, n, minmax_out, st);
+        } else {
+            g_quant_minmax_passes.fetch_add(1, std::memory_order_relaxed);
+            be->minmax(src, n, q.dtype, minmax_out, st);
+        }
         be->stream_sync(st);
         QuantMeta m = kernels::make_meta(q.qalgo, q.dtype, q.qtype, minmax_out[0], minmax_out[1]);
         const auto params = kernels::make_params(m, q.qtype);
@@ -1610,10 +1650,11 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         uint8_t *sink = rxbuf[step % 2];
         QuantMeta theirs;
         kernels::QuantParams params{};
-        const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts);
+        // step > 0: this chunk was produced by the previous step's de-quantize-reduce (fused min / max partials)
+        const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts, step > 0);
         if (int m = send_meta(io, mine, op.tx)) return fail(m);
         const int rc = run_step(txbuf.data(), (te - ts) * qs, quant_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-            be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, q.op, params, st);
+            dequant_consume(rx_region + a * es, sink + a * qs, b - a, q.op, params);
         }, meta_then(theirs, params));
         if (rc) return fail(rc);
     }
@@ -1633,7 +1674,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         QuantMeta mine, theirs;
         std::function<bool(size_t)> ready = always_ready;
         if (step == 0) {
-            mine = quantize_to_pinned(dst + ts * es, te - ts);
+            mine = quantize_to_pinned(dst + ts * es, te - ts, true); // the reduce-scatter's last received chunk
             if (te > ts) // parity: own chunk := D(Q(x))
                 be->dequant_reduce(dst + ts * es, txbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set,
                                    kernels::make_params(mine, q.qtype), st);
@@ -1658,3 +1699,9 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
 }
 
 } // namespace pccl::client
+
+// [0] quantized-ring payloads whose min / max came from the fused de-quantize partials, [1] separate min / max passes
+extern "C" __attribute__((visibility("default"))) void pcclxQuantStats(uint64_t *out2) {
+    out2[0] = pccl::client::g_quant_minmax_folds.load(std::memory_order_relaxed);
+    out2[1] = pccl::client::g_quant_minmax_passes.load(std::memory_order_relaxed);
+}

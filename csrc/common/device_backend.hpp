@@ -80,10 +80,18 @@ public:
                              DevStream s) = 0;
     virtual bool dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                                 const kernels::QuantParams &p, DevStream s) = 0;
+    // dequant_reduce that also writes each workgroup's (min, max) of the stored results as two doubles to
+    // mm_partials[2 * k ...] (device memory), k < *blocks <= max_blocks: the min / max of a chunk produced by several
+    // such launches is minmax_fold over all their partials (no second pass over the chunk)
+    virtual bool dequant_reduce_minmax(void *dst, const void *src_q, size_t count, DType vtype, DType qtype,
+                                       ReduceOp op, const kernels::QuantParams &p, double *mm_partials, int max_blocks,
+                                       int *blocks, DevStream s) = 0;
     virtual bool quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
                           const kernels::QuantParams &p, DevStream s) = 0;
     // writes {min, max} as two doubles to `out2` (pinned host or device memory)
     virtual bool minmax(const void *src, size_t count, DType vtype, double *out2, DevStream s) = 0;
+    // folds n_partials (min, max) pairs (device memory) of `count` elements into `out2` (asynchronous)
+    virtual bool minmax_fold(const double *partials, int n_partials, size_t count, double *out2, DevStream s) = 0;
     virtual bool finalize_avg(void *dst, size_t count, DType t, size_t world_size, DevStream s) = 0;
 
     // Intra-node xGMI kernels. srcs[k] points to shard `count` elements in peer k's buffer (IPC-mapped);

@@ -278,6 +278,13 @@ public:
                         const kernels::QuantParams &p, DevStream s) override {
         return hipk::launch_dequant_reduce(dst, src_q, count, vtype, qtype, op, p, static_cast<hipStream_t>(s));
     }
+    bool dequant_reduce_minmax(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                               const kernels::QuantParams &p, double *mm, int max_blocks, int *blocks,
+                               DevStream s) override {
+        if (!mm || max_blocks < 1) return false;
+        return hipk::launch_dequant_reduce(dst, src_q, count, vtype, qtype, op, p, static_cast<hipStream_t>(s), mm,
+                                           max_blocks, blocks);
+    }
     bool quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, const kernels::QuantParams &p,
                   DevStream s) override {
         return hipk::launch_quantize(dst_q, src, count, vtype, qtype, p, static_cast<hipStream_t>(s));
@@ -289,6 +296,9 @@ public:
         std::lock_guard l(*sc.mtx);
         return hipk::launch_minmax(src, count, vtype, sc.dev, out2, static_cast<hipStream_t>(s)) &&
                hipStreamSynchronize(static_cast<hipStream_t>(s)) == hipSuccess;
+    }
+    bool minmax_fold(const double *partials, int n, size_t count, double *out2, DevStream s) override {
+        return hipk::launch_minmax_fold(partials, n, count, out2, static_cast<hipStream_t>(s));
     }
     bool finalize_avg(void *dst, size_t count, DType t, size_t ws, DevStream s) override {
         return hipk::launch_finalize_avg(dst, count, t, ws, static_cast<hipStream_t>(s));

@@ -7,8 +7,17 @@
 namespace pccl::hipk {
 
 bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
-                           const kernels::QuantParams &p, hipStream_t st) {
+                           const kernels::QuantParams &p, hipStream_t st, double *mm, int mm_max_blocks,
+                           int *mm_blocks) {
+    if (mm_blocks) *mm_blocks = 0;
     if (count == 0) return true;
+    // with `mm`, the grid is capped at mm_max_blocks workgroups (the tile loop strides over the rest), each writing
+    // its (min, max) partial of the stored results to mm[2 * blockIdx.x ...]
+    auto grid_of = [&](int g) {
+        if (mm) g = std::max(1, std::min(g, mm_max_blocks));
+        if (mm_blocks) *mm_blocks = mm ? g : 0;
+        return g;
+    };
     return with_float_elem(vtype, [&](auto e) {
         using E = decltype(e);
         using S = typename E::S;
@@ -17,29 +26,39 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
             using O = decltype(o);
             if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
                 const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src_q, 1}});
-                const int grid = grid_ew(count, pl, V);
+                const int grid = grid_of(grid_ew(count, pl, V));
                 auto *d = static_cast<S *>(dst);
                 auto *q = static_cast<const uint8_t *>(src_q);
                 return launch_ok([&] {
-                    if (qtype == DType::F8E4M3)
-                        k_dq_fp8<E, O, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
-                    else
-                        k_dq_fp8<E, O, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
+                    if (qtype == DType::F8E4M3) {
+                        if (mm) k_dq_fp8<E, O, true, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                        else k_dq_fp8<E, O, true, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                    } else {
+                        if (mm) k_dq_fp8<E, O, false, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                        else k_dq_fp8<E, O, false, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                    }
                 });
             }
             return with_qint(qtype, [&](auto qv) {
                 using Q = decltype(qv);
                 const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src_q, sizeof(Q)}});
-                const int grid = grid_for(count, pl.vec ? V : 1);
                 auto *d = static_cast<S *>(dst);
                 auto *q = static_cast<const Q *>(src_q);
-                if (p.algo == QuantAlgo::MinMax)
+                if (p.algo == QuantAlgo::MinMax) {
+                    const int grid = grid_of(grid_ew(count, pl, V));
                     return launch_ok([&] {
-                        k_dq_minmax<E, O, Q><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec);
+                        if (mm) k_dq_minmax<E, O, Q, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                        else k_dq_minmax<E, O, Q, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
                     });
+                }
                 if constexpr (sizeof(Q) <= 4) {
-                    if (p.algo == QuantAlgo::ZeroPointScale)
-                        return launch_ok([&] { k_dq_zps<E, O, Q><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec); });
+                    if (p.algo == QuantAlgo::ZeroPointScale) {
+                        const int grid = grid_of(grid_for(count, pl.vec ? V : 1));
+                        return launch_ok([&] {
+                            if (mm) k_dq_zps<E, O, Q, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                            else k_dq_zps<E, O, Q, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                        });
+                    }
                 }
                 return false;
             });
@@ -81,6 +100,10 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
             return false;
         });
     });
+}
+
+bool launch_minmax_fold(const double *partial, int nblocks, size_t count, double *out2, hipStream_t st) {
+    return launch_ok([&] { k_minmax_final<><<<1, kBlock, 0, st>>>(partial, nblocks, count, out2); });
 }
 
 bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, double *out2, hipStream_t st) {

@@ -161,6 +161,60 @@ inline int grid_ew(size_t n, const EwPlan &pl, int V) {
 }
 
 
+// ---------------------------------------------------------------- min / max helpers
+// Comparisons run in the codec's compute type (exact for every value of the storage type); partials are doubles.
+template<typename C>
+__device__ __forceinline__ void wave_minmax(C &lo, C &hi) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const C l2 = __shfl_xor(lo, off, 64);
+        const C h2 = __shfl_xor(hi, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+}
+
+template<typename C>
+__device__ __forceinline__ void block_minmax(C &lo, C &hi, C *s_lo, C *s_hi) {
+    wave_minmax(lo, hi);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            lo = s_lo[k] < lo ? s_lo[k] : lo;
+            hi = s_hi[k] > hi ? s_hi[k] : hi;
+        }
+    }
+}
+
+// Per-thread running (min, max) of the values a kernel stores, folded per workgroup into partial[2*blockIdx.x ...]
+// at the end (the quantized ring's de-quantize-reduce kernels emit the min / max the next step's quantization needs,
+// so no separate min / max pass over the chunk; folded by k_minmax_final). Off (no-op) when MM is false.
+template<typename C, bool MM>
+struct MinMaxAcc {
+    C lo = static_cast<C>(__builtin_inf()), hi = static_cast<C>(-__builtin_inf());
+    __device__ __forceinline__ void take(C v) {
+        if constexpr (MM) {
+            lo = v < lo ? v : lo;
+            hi = v > hi ? v : hi;
+        }
+    }
+    __device__ __forceinline__ void finish(double *partial) {
+        if constexpr (MM) {
+            __shared__ C s_lo[kBlock / 64], s_hi[kBlock / 64];
+            block_minmax(lo, hi, s_lo, s_hi);
+            if (threadIdx.x == 0) {
+                partial[2 * blockIdx.x] = static_cast<double>(lo);
+                partial[2 * blockIdx.x + 1] = static_cast<double>(hi);
+            }
+        }
+    }
+};
+
 // ---------------------------------------------------------------- elementwise reduce (ring path)
 template<typename E, typename Op>
 __global__ __launch_bounds__(kBlock) void k_reduce(typename E::S *__restrict__ dst, const typename E::S *__restrict__ src,
@@ -213,9 +267,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_copy(typename E::S *__restric
 }
 
 // ---------------------------------------------------------------- fused dequant + reduce
-template<typename E, typename Op, typename Q>
+// MM: also emit the workgroup's (min, max) of the stored results (MinMaxAcc) into `mm`
+template<typename E, typename Op, typename Q, bool MM>
 __global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
-                                                      QuantParams p, size_t head, int vec) {
+                                                      QuantParams p, size_t head, int vec, double *__restrict__ mm) {
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = vec_width<S>();
@@ -223,11 +278,14 @@ __global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict_
         Pack<S, V> d;
         Pack<Q, V> q;
     };
+    MinMaxAcc<C, MM> acc;
     ew_loop_ls<V, kEwUnroll>(
         n, head, vec,
         [&](size_t i) {
             const C v = static_cast<C>(dq_minmax_int(static_cast<double>(src[i]), p));
-            dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
+            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), v));
+            dst[i] = r;
+            acc.take(E::ld(r));
         },
         [&](size_t b) { return DQ{ldp_nt<S, V>(dst + b), ldp<Q, V>(src + b)}; },
         [&](size_t b, DQ x) {
@@ -235,14 +293,16 @@ __global__ __launch_bounds__(kBlock) void k_dq_minmax(typename E::S *__restrict_
             for (int e = 0; e < V; ++e) {
                 const C v = static_cast<C>(dq_minmax_int(static_cast<double>(x.q.v[e]), p));
                 x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), v));
+                acc.take(E::ld(x.d.v[e]));
             }
             stp_nt<S, V>(dst + b, x.d);
         });
+    acc.finish(mm);
 }
 
-template<typename E, typename Op, bool E4M3>
+template<typename E, typename Op, bool E4M3, bool MM>
 __global__ __launch_bounds__(kBlock) void k_dq_fp8(typename E::S *__restrict__ dst, const uint8_t *__restrict__ src, size_t n,
-                                                   QuantParams p, size_t head, int vec) {
+                                                   QuantParams p, size_t head, int vec, double *__restrict__ mm) {
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = vec_width<S>();
@@ -251,20 +311,29 @@ __global__ __launch_bounds__(kBlock) void k_dq_fp8(typename E::S *__restrict__ d
         Pack<S, V> d;
         Pack<uint8_t, V> q;
     };
+    MinMaxAcc<C, MM> acc;
     ew_loop_ls<V, kEwUnroll>(
-        n, head, vec, [&](size_t i) { dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(deq(src[i])))); },
+        n, head, vec,
+        [&](size_t i) {
+            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(deq(src[i]))));
+            dst[i] = r;
+            acc.take(E::ld(r));
+        },
         [&](size_t b) { return DQ{ldp_nt<S, V>(dst + b), ldp<uint8_t, V>(src + b)}; },
         [&](size_t b, DQ x) {
 #pragma unroll
-            for (int e = 0; e < V; ++e)
+            for (int e = 0; e < V; ++e) {
                 x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), static_cast<C>(deq(x.q.v[e]))));
+                acc.take(E::ld(x.d.v[e]));
+            }
             stp_nt<S, V>(dst + b, x.d);
         });
+    acc.finish(mm);
 }
 
-template<typename E, typename Op, typename Q>
+template<typename E, typename Op, typename Q, bool MM>
 __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ dst, const Q *__restrict__ src, size_t n,
-                                                   QuantParams p, size_t head, int vec) {
+                                                   QuantParams p, size_t head, int vec, double *__restrict__ mm) {
     using S = typename E::S;
     using C = typename E::C;
     constexpr int V = vec_width<S>();
@@ -272,18 +341,24 @@ __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ d
         Pack<S, V> d;
         Pack<Q, V> q;
     };
+    MinMaxAcc<C, MM> acc;
     ew_loop_ls<V, kEwUnroll>(
         n, head, vec,
         [&](size_t i) {
-            dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps(static_cast<int64_t>(src[i]), p))));
+            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps(static_cast<int64_t>(src[i]), p))));
+            dst[i] = r;
+            acc.take(E::ld(r));
         },
         [&](size_t b) { return DQ{ldp_nt<S, V>(dst + b), ldp<Q, V>(src + b)}; },
         [&](size_t b, DQ x) {
 #pragma unroll
-            for (int e = 0; e < V; ++e)
+            for (int e = 0; e < V; ++e) {
                 x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), static_cast<C>(dq_zps(static_cast<int64_t>(x.q.v[e]), p))));
+                acc.take(E::ld(x.d.v[e]));
+            }
             stp_nt<S, V>(dst + b, x.d);
         });
+    acc.finish(mm);
 }
 
 // ---------------------------------------------------------------- quantize
@@ -351,35 +426,6 @@ __global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typ
 }
 
 // ---------------------------------------------------------------- min / max (two pass, exact)
-// Comparisons run in the codec's compute type (exact for every value of the storage type); partials are doubles.
-template<typename C>
-__device__ __forceinline__ void wave_minmax(C &lo, C &hi) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const C l2 = __shfl_xor(lo, off, 64);
-        const C h2 = __shfl_xor(hi, off, 64);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-}
-
-template<typename C>
-__device__ __forceinline__ void block_minmax(C &lo, C &hi, C *s_lo, C *s_hi) {
-    wave_minmax(lo, hi);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        s_lo[w] = lo;
-        s_hi[w] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < kBlock / 64; ++k) {
-            lo = s_lo[k] < lo ? s_lo[k] : lo;
-            hi = s_hi[k] > hi ? s_hi[k] : hi;
-        }
-    }
-}
-
 // Pass 1: every workgroup reduces its tiles to a (min, max) partial. A single-launch variant (last workgroup folds
 // the partials behind a device-scope ticket) measured slower on MI355X - each workgroup's agent-scope release is an
 // L2 write-back (`buffer_wbl2`), 1024 of them cost more than the second launch (profiles/r2/kernels_polish.md).

@@ -20,10 +20,12 @@ bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_
 
 // hip_quant.hip
 bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
-                           const kernels::QuantParams &p, hipStream_t s);
+                           const kernels::QuantParams &p, hipStream_t s, double *mm = nullptr, int mm_max_blocks = 0,
+                           int *mm_blocks = nullptr);
 bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
                      const kernels::QuantParams &p, hipStream_t s);
 bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, double *out2, hipStream_t st);
+bool launch_minmax_fold(const double *partial, int nblocks, size_t count, double *out2, hipStream_t st);
 
 // hip_ipc.hip
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,

@@ -150,6 +150,9 @@ def _load() -> ctypes.CDLL:
         "pcclxFinalizeAvg": ([c_void_p, c_size_t, c_int, c_size_t, c_int], c_int),
         "pcclxQuantize": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double)], c_int),
         "pcclxDequantReduce": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double), c_int], c_int),
+        "pcclxDequantReduceMinmax": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double), c_int,
+                                      p(c_double)], c_int),
+        "pcclxQuantStats": ([p(c_uint64)], None),
         "pcclxMultiReduce": ([p(c_void_p), c_int, p(c_void_p), c_int, c_size_t, c_int, c_int], c_int),
         "pcclxMultiGather": ([c_void_p, p(c_void_p), p(c_size_t), p(c_size_t), c_int, c_int, c_int], c_int),
         "pcclxBenchKernel": ([c_int, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int], c_double),

@@ -97,6 +97,27 @@ def dequant_reduce(dst: torch.Tensor, q: torch.Tensor, meta: Sequence[float], al
     return dst
 
 
+def dequant_reduce_minmax(dst: torch.Tensor, q: torch.Tensor, meta: Sequence[float], algo: str = "min_max",
+                          op: str = "sum", pieces: int = 1) -> Tuple[torch.Tensor, List[float]]:
+    """``dequant_reduce`` on the GPU in ``pieces`` launches whose kernels also emit per-workgroup (min, max) partials
+    of the values they store, folded into [min, max] of the result (the quantized device ring's next-step min / max
+    without a second pass; GPU only)."""
+    m = (ctypes.c_double * 4)(*meta)
+    out = (ctypes.c_double * 2)()
+    _check(C.pcclxDequantReduceMinmax(dst.data_ptr(), q.data_ptr(), dst.numel(), WIRE_DTYPE[dst.dtype],
+                                      WIRE_DTYPE[q.dtype], ALGOS[algo], OPS[op], m, pieces, out),
+           "dequant_reduce_minmax")
+    return dst, [out[0], out[1]]
+
+
+def quant_minmax_stats() -> dict:
+    """Quantized device ring, this process since start: payloads whose min / max was folded from the previous step's
+    fused de-quantize partials (``folds``) vs separate min / max passes over the payload (``passes``)."""
+    out = (ctypes.c_uint64 * 2)()
+    C.pcclxQuantStats(out)
+    return {"folds": int(out[0]), "passes": int(out[1])}
+
+
 def multi_reduce(srcs: Sequence[torch.Tensor], op: str = "sum", out: Optional[torch.Tensor] = None,
                  out2: Optional[torch.Tensor] = None, outs: Sequence[torch.Tensor] = ()) -> torch.Tensor:
     """out = op(srcs[0], ..., srcs[n-1]) in fixed order, also stored to out2 and every tensor of ``outs`` (the xGMI

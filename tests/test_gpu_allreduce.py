@@ -219,6 +219,48 @@ def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
             assert (err <= mag * 0.15 + 0.05).all()
 
 
+@pytest.mark.parametrize("qdtype,algo", [(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX),
+                                         (pccl.DataType.INT8, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
+                                         (pccl.DataType.FLOAT8_E5M2, pccl.QuantizationAlgorithm.MIN_MAX)])
+def test_device_quantized_fused_minmax_same_wire(hip, qdtype, algo, monkeypatch):
+    """Quantized device ring with the reduce-scatter's min / max folded from the de-quantize kernels' partials
+    (default) vs a separate min / max pass per step (PCCL_QUANT_FUSED_MINMAX=0): identical results and wire bytes on
+    every peer, over several pieces per step and uneven chunks; the fused path folds every payload but the first
+    reduce-scatter step's."""
+    from pccl_amd.ops import kernels as K
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
+    world, n = 4, 3_000_017
+    inputs = [torch.randn(n, generator=torch.Generator().manual_seed(60 + r)).bfloat16() for r in range(world)]
+    qopt = pccl.QuantizationOptions(qdtype, algo)
+
+    def run(fused):
+        monkeypatch.setenv("PCCL_QUANT_FUSED_MINMAX", fused)
+
+        def fn(rank, comm):
+            x = inputs[rank].to(hip)
+            y = torch.empty_like(x)
+            infos = [comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=t, quantization_options=qopt) for t in range(2)]
+            torch.cuda.synchronize()
+            return y.cpu(), [(i.tx_bytes, i.rx_bytes) for i in infos]
+
+        before = K.quant_minmax_stats()
+        res = _run(world, fn)
+        after = K.quant_minmax_stats()
+        return res, {k: after[k] - before[k] for k in after}
+
+    fused, st_f = run("1")
+    plain, st_p = run("0")
+    for (yf, bf), (yp, bp) in zip(fused, plain):
+        assert torch.equal(yf, yp)
+        assert bf == bp
+        assert torch.equal(yf, fused[0][0])
+    ops = 2 * world
+    # per op and peer: world - 1 reduce-scatter payloads + 1 all-gather payload, the first of them without partials
+    assert st_f == {"folds": ops * (world - 1), "passes": ops}
+    assert st_p == {"folds": 0, "passes": ops * world}
+
+
 def test_device_shared_state(hip):
     n = (1 << 22) + 1
 

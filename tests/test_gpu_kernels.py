@@ -84,6 +84,28 @@ def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
     assert torch.equal(rd.cpu(), rh)
 
 
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("qdtype,algo", [(torch.uint8, "min_max"), (torch.int8, "zero_point_scale"),
+                                         (getattr(torch, "float8_e4m3fn", None), "min_max")])
+@pytest.mark.parametrize("op", ["sum", "max"])
+@pytest.mark.parametrize("n,pieces", [(1, 1), (5000, 3), ((1 << 22) + 7, 7), (3_000_011, 1)])
+def test_device_dequant_reduce_fused_minmax(hip, vdtype, qdtype, algo, op, n, pieces):
+    """The quantized device ring's de-quantize-reduce kernels also emit per-workgroup (min, max) partials of the
+    values they store (several launches per chunk, like the ring's receive ranges), folded by k_minmax_final: the
+    stored result equals the plain kernel's bit for bit, and the fold equals torch's min / max of that result."""
+    if qdtype is None:
+        pytest.skip("no fp8 dtype")
+    x = _rand(n, vdtype, 31)
+    q, meta = K.quantize(x.to(hip), qdtype, algo)
+    acc = _rand(n, vdtype, 32) * 3 - 1
+    plain = K.dequant_reduce(acc.to(hip), q, meta, algo, op)
+    fused, mm = K.dequant_reduce_minmax(acc.to(hip), q, meta, algo, op, pieces=pieces)
+    torch.cuda.synchronize()
+    assert torch.equal(fused.cpu(), plain.cpu())
+    ref = plain.float()
+    assert mm == [float(ref.min()), float(ref.max())]
+
+
 @pytest.mark.parametrize("n", [1, 1000, (1 << 22) + 3, 300_000_001])
 def test_device_minmax_repeated(hip, n):
     """min/max is two launches (k_minmax_partial writes one partial per workgroup, k_minmax_final folds them,
