@@ -378,6 +378,24 @@ def latency_cpu(job, n_ops=300):
     return {"median_us": round(statistics.median(ts) * 1e6, 1), "p99_us": round(ts[int(0.99 * (len(ts) - 1))] * 1e6, 1)}
 
 
+class _full_cpu_mask:
+    """Runs a block with the calling thread's CPU mask from before the bench's per-CCD spread (_cpu_spread), if any;
+    threads and processes started inside inherit it. For the latency measurements: the spread suits the
+    socket-copy-bound TCP ring, but it scatters a phase's threads over 16 L3 domains of both sockets, where every
+    wake-up of a waiting peer lands on a sleeping core of another CCD."""
+
+    def __enter__(self):
+        full = os.environ.get("PCCL_BENCH_FULL_CPUS")
+        self.own = os.sched_getaffinity(0)
+        if full:
+            os.sched_setaffinity(0, {int(c) for c in full.split(",")})
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.own)
+        return False
+
+
 def latency_native(peers):
     """Small-op latency of the xGMI/IPC path without Python in the loop: pccl_amd/lib/pccl_latency (the C API with
     hipMalloc'd buffers, threaded peers on cuda:0, csrc/tools/latency_native.hip), 1 MiB bf16 at `peers` and 2 peers;
@@ -389,11 +407,16 @@ def latency_native(peers):
     exe = os.path.join(ROOT, "pccl_amd", "lib", "pccl_latency")
     if not os.path.exists(exe):
         return {"error": "pccl_latency not built"}
-    out = {}
+    # the harness runs with the process's CPU mask from before the bench's per-CCD spread (_cpu_spread): the spread
+    # suits the socket-copy-bound TCP ring, but it scatters the peers' op threads over 16 L3 domains and both sockets,
+    # where every shared-memory barrier word bounces between CCDs - 8 peers x 1 MiB measured 445 us median with the
+    # 3-per-CCD mask vs 153-167 us with the full mask on the same box (profiles/r3/latency_futex/affinity.jsonl)
+    out = {"cpu_mask": "full" if os.environ.get("PCCL_BENCH_FULL_CPUS") else "inherited"}
     for p in sorted({peers, 2}):
         try:
-            r = subprocess.run([exe, str(free_port()), str(p), str(1 << 20), "400", "50"], capture_output=True,
-                               text=True, timeout=120)
+            with _full_cpu_mask():  # the child inherits this thread's mask
+                r = subprocess.run([exe, str(free_port()), str(p), str(1 << 20), "400", "50"], capture_output=True,
+                                   text=True, timeout=120)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             out[f"{p}_peers_1MiB"] = json.loads(line[-1]) if r.returncode == 0 and line else \
                 {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
@@ -495,8 +518,9 @@ def run_extras(job, a, nbytes):
         nat = extra["latency_native"].get(f"{P}_peers_1MiB", {})
         if "median_us" in nat:  # the library's latency: C API, threaded peers, no interpreter in the loop
             extra["latency_1MiB_ipc_us"] = nat["median_us"]
-        extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
-        r = rejoin_latency(job)
+        with _full_cpu_mask():
+            extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
+            r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
     elif job.n_gpus > 1 and os.environ.get("PCCL_BENCH_RCCL", "1") == "1":
         extra["rccl_reference"] = rccl_reference(job, a, nbytes)
@@ -625,6 +649,8 @@ def _cpu_spread():
             pick.update(cpus[:k])
         if len(pick) < min(16, len(allowed)):  # unknown topology: leave the mask alone
             return {"cpu_spread": "skipped", "l3_domains": len(domains)}
+        # the mask before the spread, for measurements that are not the loopback-TCP ring (latency_native)
+        os.environ.setdefault("PCCL_BENCH_FULL_CPUS", ",".join(map(str, sorted(allowed))))
         os.sched_setaffinity(0, pick)
         return {"cpus": len(pick), "per_l3": k, "l3_domains": len(domains)}
     except (OSError, ValueError) as e:

@@ -226,39 +226,53 @@ def test_device_quantized_fused_minmax_same_wire(hip, qdtype, algo, monkeypatch)
     """Quantized device ring with the reduce-scatter's min / max folded from the de-quantize kernels' partials
     (default) vs a separate min / max pass per step (PCCL_QUANT_FUSED_MINMAX=0): identical results and wire bytes on
     every peer, over several pieces per step and uneven chunks; the fused path folds every payload but the first
-    reduce-scatter step's."""
+    reduce-scatter step's. Both ops run in one session: a quantized ring's result depends on the ring order (the
+    partial sums that get quantized), which the master may choose differently per session."""
+    import threading
+
     from pccl_amd.ops import kernels as K
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
     world, n = 4, 3_000_017
     inputs = [torch.randn(n, generator=torch.Generator().manual_seed(60 + r)).bfloat16() for r in range(world)]
     qopt = pccl.QuantizationOptions(qdtype, algo)
+    bar = threading.Barrier(world)
+    stats = {}
 
-    def run(fused):
-        monkeypatch.setenv("PCCL_QUANT_FUSED_MINMAX", fused)
+    def switch(rank, mode, prev):
+        bar.wait()
+        if rank == 0:
+            now = K.quant_minmax_stats()
+            if prev is not None:
+                stats[prev] = {k: now[k] - stats["_snap"][k] for k in now}
+            stats["_snap"] = now
+            if mode is not None:
+                os.environ["PCCL_QUANT_FUSED_MINMAX"] = mode  # read by every peer at its op's start
+        bar.wait()
 
-        def fn(rank, comm):
-            x = inputs[rank].to(hip)
+    def fn(rank, comm):
+        x = inputs[rank].to(hip)
+        out = []
+        prev = None
+        for tag, mode in enumerate(("1", "0")):
+            switch(rank, mode, prev)
             y = torch.empty_like(x)
-            infos = [comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=t, quantization_options=qopt) for t in range(2)]
+            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
             torch.cuda.synchronize()
-            return y.cpu(), [(i.tx_bytes, i.rx_bytes) for i in infos]
+            out.append((y.cpu(), info.tx_bytes, info.rx_bytes))
+            prev = mode
+        switch(rank, None, prev)
+        return out
 
-        before = K.quant_minmax_stats()
-        res = _run(world, fn)
-        after = K.quant_minmax_stats()
-        return res, {k: after[k] - before[k] for k in after}
-
-    fused, st_f = run("1")
-    plain, st_p = run("0")
-    for (yf, bf), (yp, bp) in zip(fused, plain):
+    monkeypatch.setenv("PCCL_QUANT_FUSED_MINMAX", "1")
+    res = _run(world, fn)
+    for (yf, txf, rxf), (yp, txp, rxp) in res:
         assert torch.equal(yf, yp)
-        assert bf == bp
-        assert torch.equal(yf, fused[0][0])
-    ops = 2 * world
-    # per op and peer: world - 1 reduce-scatter payloads + 1 all-gather payload, the first of them without partials
-    assert st_f == {"folds": ops * (world - 1), "passes": ops}
-    assert st_p == {"folds": 0, "passes": ops * world}
+        assert (txf, rxf) == (txp, rxp)
+        assert torch.equal(yf, res[0][0][0])
+    # per peer: world - 1 reduce-scatter payloads + 1 all-gather payload, the first of them without partials
+    assert stats["1"] == {"folds": world * (world - 1), "passes": world}
+    assert stats["0"] == {"folds": 0, "passes": world * world}
 
 
 def test_device_shared_state(hip):
