@@ -153,8 +153,12 @@ class Job:
         pool = min(2, self.pool_for(local)) if ipc else self.pool_for(local)
         self.phase_pool = pool
 
+        groups = _peer_cpu_groups(local) if not ipc else None
+
         def body(i):
             try:
+                if groups:  # this peer's library threads (created from here on) inherit the mask
+                    os.sched_setaffinity(0, groups[i])
                 self.torch.cuda.set_device(self.dev)
                 c = pccl.Communicator(addr, 0, p2p_connection_pool_size=pool, **ports[i])
                 comms[i] = c
@@ -620,6 +624,26 @@ def _numa_bind():
         return {"numa_node": node, "cpus": len(cpus)}
     except (OSError, ValueError) as e:
         return {"numa_bind_error": repr(e)[:200]}
+
+
+def _peer_cpu_groups(local: int):
+    """PCCL_BENCH_PEER_CCD=1 (TCP-ring phases, several peers in this process): peer thread i gets its own share of the
+    L3 domains (CCDs) of the process's CPU mask, so the threads the library starts for that peer (op thread, receive
+    and sender threads) stay on a few CCDs instead of migrating over all of them. Returns one CPU set per peer, or
+    None when off or when there are fewer L3 domains than peers."""
+    if local < 2 or os.environ.get("PCCL_BENCH_PEER_CCD", "0") != "1":
+        return None
+    domains = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                domains.setdefault(f.read().strip(), []).append(c)
+        except OSError:
+            return None
+    doms = [d for _, d in sorted(domains.items(), key=lambda kv: kv[1][0])]
+    if len(doms) < local:
+        return None
+    return [set(c for d in doms[i * len(doms) // local:(i + 1) * len(doms) // local] for c in d) for i in range(local)]
 
 
 def _cpu_spread():
