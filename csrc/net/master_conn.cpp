@@ -1,5 +1,6 @@
 #include "master_conn.hpp"
 
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -47,8 +48,20 @@ void MasterConnection::join() {
     }
 }
 
+namespace {
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+int64_t rx_spin_ns() {
+    static const int64_t ns = static_cast<int64_t>(env_size("PCCL_MASTER_RX_SPIN_US", 200)) * 1000;
+    return ns;
+}
+} // namespace
+
 bool MasterConnection::send_raw(uint16_t id, const std::vector<uint8_t> &payload) {
     if (!open_) return false;
+    if (const int64_t w = rx_spin_ns(); w > 0) rx_hot_until_.store(steady_ns() + w, std::memory_order_relaxed);
     std::lock_guard lock(send_mtx_);
     if (!send_ltv(fd_, id, payload.data(), payload.size())) {
         LOG(WARN) << "Failed to send packet " << id << " to master";
@@ -59,6 +72,14 @@ bool MasterConnection::send_raw(uint16_t id, const std::vector<uint8_t> &payload
 
 void MasterConnection::rx_loop() {
     while (!interrupted_) {
+        // shortly after a request: poll the socket (non-blocking) until the reply is readable or the window closes
+        while (!interrupted_ && steady_ns() < rx_hot_until_.load(std::memory_order_relaxed)) {
+            pollfd pfd{fd_, POLLIN, 0};
+            if (::poll(&pfd, 1, 0) != 0) break;
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
         auto pkt = recv_ltv(fd_);
         if (!pkt) break;
         {
