@@ -97,10 +97,15 @@ class Job:
         self.auto_pool = a.pool <= 0
 
     def pool_for(self, local_peers: int) -> int:
-        """Connections per ring neighbour for a phase with `local_peers` peer threads in this process."""
+        """Connections per ring neighbour for a phase with `local_peers` peer threads in each of the job's processes:
+        the CPUs this process may use, shared by every peer of the node (torchrun's ranks run in one container, so the
+        cgroup quota is node-wide), in [1, 8]. One GPU, 16 CPUs: 8 peers x 2, 4 x 4, 2 x 8 stripes (measured fastest,
+        profiles/r3/ring_ab/); with one peer per GPU each peer owns its GPU's PCIe link, and its ring steps are bound
+        by the socket copies of its stripes."""
         if not self.auto_pool:
             return self.a.pool
-        return max(1, min(8 if self.world == 1 else 4, int(_cpu_quota()) // max(1, local_peers)))
+        share = int(_cpu_quota()) // max(1, local_peers * self.world)
+        return max(1, min(8, share))
 
     # -- cross-peer helpers (called from peer threads) --------------------------------------------------------------
     def sync(self, i: int):
