@@ -739,6 +739,10 @@ struct PcieQueues {
     std::array<DevStream, kMaxH2d> h2d{}; // received pieces -> HBM, round robin over nh2d queues
     size_t nh2d = 1;
     DevStream d2h = nullptr;
+    // one compute stream for the fused reduce-scatter kernels of every device-ring op of the process on this GPU
+    // (PCCL_RING_SHARED_REDUCE), with the lock that keeps each (H2D copy, reduce) pair in the same order on both queues
+    DevStream red = nullptr;
+    std::mutex *red_mtx = nullptr;
 };
 
 // process-wide copy queues of `device` (never destroyed: they may outlive static destruction order)
@@ -755,6 +759,8 @@ PcieQueues shared_pcie_queues(DeviceBackend *be, int device) {
         e.nh2d = std::max<size_t>(1, std::min(PcieQueues::kMaxH2d, env_size("PCCL_H2D_QUEUES", 1)));
         for (size_t k = 0; k < e.nh2d; ++k) e.h2d[k] = be->create_stream();
         e.d2h = be->create_stream();
+        e.red = be->create_stream();
+        e.red_mtx = new std::mutex();
         if (cur >= 0) be->set_device(cur);
     }
     return e;
@@ -980,6 +986,7 @@ struct Lane {
     bool ag_on_lane_stream = false; // all-gather bytes -> HBM by blit kernels on the lane stream, not the H2D queue
     int rs_h2d = 0; // reduce-scatter received bytes: 0 copy engine -> HBM staging, 1 blit copy on the lane stream,
                     // 2 none (the fused reduce reads them from pinned memory)
+    bool shared_reduce = false; // reduce-scatter kernels on the process-wide stream pq.red (see ring_reduce_device)
     LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
     std::atomic<uint64_t> *tx, *rx;
@@ -1005,10 +1012,17 @@ void run_lane(Lane &L) {
         L.wait_gate->cv.wait(l, [&] { return L.wait_gate->open; });
     }
     if (L.ready) be->stream_wait_event(st, L.ready);
+    const bool shared_red = L.shared_reduce && pq.red && pq.red_mtx;
+    DevStream rst = shared_red ? pq.red : st; // stream of this lane's reduce-scatter kernels
+    if (shared_red && L.ready) {
+        std::lock_guard l(*pq.red_mtx);
+        be->stream_wait_event(rst, L.ready); // the op's input copy into dst precedes the reduces into it
+    }
 
     // events of this lane (returned to the pool once everything they guard has completed)
     std::vector<DevEvent> owned;
     DevEvent last_d2h = nullptr;
+    DevEvent lane_last_red = nullptr; // last reduce-scatter kernel of this lane (on rst)
     std::array<DevEvent, PcieQueues::kMaxH2d> last_h2d{}; // last copy issued on each H2D queue
     size_t h2d_rr = 0;
     auto record = [&](DevStream s) {
@@ -1053,16 +1067,17 @@ void run_lane(Lane &L) {
         DeviceBackend *be;
         DevStream st;
         std::array<DevEvent, PcieQueues::kMaxH2d> *h2d;
-        DevEvent *d2h;
+        DevEvent *d2h, *red;
         std::vector<DevEvent> *ev;
         ~Drain() {
             for (DevEvent e : *h2d)
                 if (e) be->event_sync(e);
             if (*d2h) be->event_sync(*d2h);
+            if (*red) be->event_sync(*red);
             be->stream_sync(st);
             for (auto e : *ev) event_pool().put(e);
         }
-    } drain{be, st, &last_h2d, &last_d2h, &owned};
+    } drain{be, st, &last_h2d, &last_d2h, &lane_last_red, &owned};
 
     ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
     ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
@@ -1229,6 +1244,9 @@ void run_lane(Lane &L) {
         std::array<DevEvent, PcieQueues::kMaxH2d> step_h2d{}; // this step's last copy per queue
         auto h2d_queue = [&] { return h2d_rr++ % pq.nh2d; };
         std::function<void(size_t, size_t)> consume;
+        // the all-gather overwrites regions this lane's reduce-scatter kernels wrote: with those on the shared stream,
+        // the lane stream (which takes the all-gather copies) waits for the last of them first
+        if (!rs && g + 1 == ws && shared_red && lane_last_red) be->stream_wait_event(st, lane_last_red);
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
             uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
@@ -1248,6 +1266,18 @@ void run_lane(Lane &L) {
                     if (a >= e) return;
                 }
                 const size_t off = a * es, n = (e - a) * es;
+                if (shared_red) { // copy engine -> HBM staging, then the reduce on the process-wide stream
+                    std::lock_guard l(*pq.red_mtx);
+                    const size_t qi = h2d_queue();
+                    be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
+                    DevEvent ce = record(pq.h2d[qi]);
+                    last_h2d[qi] = step_h2d[qi] = ce;
+                    be->stream_wait_event(rst, ce);
+                    be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, rst);
+                    lane_last_red = last_red = record(rst);
+                    txready[nb].add(off, off + n, last_red);
+                    return;
+                }
                 if (L.rs_h2d == 2) { // the kernel reads the received piece straight from pinned memory
                     be->reduce_copy(region + off, sink + off, out + off, e - a, L.dtype, L.rop, st);
                 } else {
@@ -1448,6 +1478,11 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         // from pinned: 347 ms, copy engine: 337 ms). PCCL_RING_AG_KERNEL_COPY=0 / PCCL_RING_RS_H2D=1|2 for A/B.
         L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 1) != 0;
         L.rs_h2d = static_cast<int>(std::min<size_t>(2, env_size("PCCL_RING_RS_H2D", 0)));
+        // PCCL_RING_SHARED_REDUCE=1: the fused reduce-scatter kernels of all device-ring ops of this process on one
+        // stream per GPU (the kernels' pinned writes are the device->host traffic of the ring: one writer at a time
+        // instead of one per peer). Copy-engine reduce-scatter H2D with the all-gather on the lane stream only.
+        L.shared_reduce = env_size("PCCL_RING_SHARED_REDUCE", 0) != 0 && L.rs_h2d == 0 && L.host_frac == 0 &&
+                          L.ag_on_lane_stream;
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
         L.aborted = [this, t = q.tag] { return abort_received(t); };

@@ -80,18 +80,21 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
             assert torch.all(y == float(1 + 2 * j))
 
 
-@pytest.mark.parametrize("shared_queues,lanes,host", [("1", "1", "0"), ("0", "1", "0"), ("1", "2", "0"),
-                                                      ("1", "1", "0.6")])
+@pytest.mark.parametrize("shared_queues,lanes,host,shared_red", [("1", "1", "0", "0"), ("0", "1", "0", "0"),
+                                                                 ("1", "2", "0", "0"), ("1", "1", "0.6", "0"),
+                                                                 ("1", "1", "0", "1"), ("1", "2", "0", "1")])
 @pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
-def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, host, monkeypatch):
+def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, host, shared_red, monkeypatch):
     """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
-    chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results."""
+    chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results, also
+    with every peer's reduce-scatter kernels on the process-wide reduce stream (PCCL_RING_SHARED_REDUCE)."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_SHARED_COPY_QUEUES", shared_queues)
     monkeypatch.setenv("PCCL_RING_LANES", lanes)
     monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)
+    monkeypatch.setenv("PCCL_RING_SHARED_REDUCE", shared_red)
     n = 9_000_011
     base = (torch.arange(n, dtype=torch.int64) % 31).float()  # every partial sum < 256: exact in bf16
     inputs = [(base + 7 * r).to(torch.bfloat16) for r in range(world)]
