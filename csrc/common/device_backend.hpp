@@ -71,6 +71,8 @@ public:
     virtual bool stream_wait_event(DevStream s, DevEvent e) = 0;
     virtual bool memcpy_async(void *dst, const void *src, size_t n, DevStream s) = 0; // any direction
     virtual bool memcpy_sync(void *dst, const void *src, size_t n) = 0;
+    // copy as a kernel of at most max_grid workgroups (0 = one per tile); any memory the device can address
+    virtual bool copy_kernel(void *dst, const void *src, size_t n, int max_grid, DevStream s) = 0;
     virtual bool device_sync() = 0;
 
     // kernels

@@ -267,6 +267,9 @@ public:
         return HIP_OK(hipMemcpy(dst, src, n, hipMemcpyDefault));
     }
     bool device_sync() override { return HIP_OK(hipDeviceSynchronize()); }
+    bool copy_kernel(void *dst, const void *src, size_t n, int max_grid, DevStream s) override {
+        return hipk::launch_copy_bytes(dst, src, n, max_grid, static_cast<hipStream_t>(s));
+    }
 
     bool reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, DevStream s) override {
         return hipk::launch_reduce(dst, src, count, t, op, static_cast<hipStream_t>(s));

@@ -1,4 +1,6 @@
 // Ring-path elementwise reduce + AVG finalization kernels (launchers).
+#include <cstdlib>
+
 #include "dispatch.hpp"
 #include "launchers.hpp"
 
@@ -35,11 +37,30 @@ bool launch_reduce_copy(void *dst, const void *src, void *out, size_t count, DTy
             using S = typename E::S;
             constexpr int V = vec_width<S>();
             const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src, sizeof(S)}, {out, sizeof(S)}});
+            // PCCL_REDUCE_COPY_GRID caps the workgroups writing the pinned copy (the device->host bytes of the ring:
+            // PCIe carries more in both directions together with few concurrent writers, profiles/r2/pcie_probe.log);
+            // read per launch so that in-process A/B runs can switch it
+            int grid = grid_ew(count, pl, V);
+            if (const char *g = std::getenv("PCCL_REDUCE_COPY_GRID")) {
+                const int cap = std::atoi(g);
+                if (cap > 0) grid = std::min(grid, cap);
+            }
             return launch_ok([&] {
-                k_reduce_copy<E, O><<<grid_ew(count, pl, V), kBlock, 0, st>>>(
+                k_reduce_copy<E, O><<<grid, kBlock, 0, st>>>(
                     static_cast<S *>(dst), static_cast<const S *>(src), static_cast<S *>(out), count, pl.head, pl.vec);
             });
         });
+    });
+}
+
+bool launch_copy_bytes(void *dst, const void *src, size_t n, int max_grid, hipStream_t st) {
+    if (n == 0) return true;
+    const EwPlan pl = plan_ew<16>(n, {{dst, 1}, {src, 1}});
+    int grid = grid_ew(n, pl, 16);
+    if (max_grid > 0) grid = std::min(grid, max_grid);
+    return launch_ok([&] {
+        k_copy_bytes<><<<grid, kBlock, 0, st>>>(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n,
+                                              pl.head, pl.vec);
     });
 }
 

@@ -488,6 +488,18 @@ __global__ __launch_bounds__(kBlock) void k_avg(typename E::S *__restrict__ dst,
         });
 }
 
+// ---------------------------------------------------------------- byte copy (device ring all-gather H2D)
+// Plain copy of n bytes as 16-byte packs (scalar head / tail); the device ring's all-gather moves received chunks
+// pinned -> HBM with it when it wants to choose the number of workgroups reading over PCIe (PCCL_RING_AG_COPY_GRID)
+// instead of the runtime's blit kernel.
+template<int Unused = 0> // a template: this header is included by several translation units
+__global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                     size_t n, size_t head, int vec) {
+    ew_loop_ls<16, kEwUnroll>(
+        n, head, vec, [&](size_t i) { dst[i] = src[i]; }, [&](size_t b) { return ldp<uint8_t, 16>(src + b); },
+        [&](size_t b, const Pack<uint8_t, 16> &v) { stp_nt<uint8_t, 16>(dst + b, v); });
+}
+
 // ---------------------------------------------------------------- xGMI multi-source reduce
 struct SrcList {
     const void *p[kMaxSrc];

@@ -17,6 +17,7 @@ namespace pccl::hipk {
 bool launch_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op, hipStream_t s);
 bool launch_reduce_copy(void *dst, const void *src, void *out, size_t count, DType t, ReduceOp op, hipStream_t s);
 bool launch_finalize_avg(void *dst, size_t count, DType t, size_t ws, hipStream_t s);
+bool launch_copy_bytes(void *dst, const void *src, size_t n, int max_grid, hipStream_t s);
 
 // hip_quant.hip
 bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,

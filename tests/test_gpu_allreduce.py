@@ -161,8 +161,9 @@ def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, host, monkeyp
         assert torch.equal(y, expect)
 
 
-@pytest.mark.parametrize("ag_kernel,rs_h2d", [("0", "0"), ("1", "1"), ("1", "2")])
-def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, monkeypatch):
+@pytest.mark.parametrize("ag_kernel,rs_h2d,ag_grid,rc_grid", [("0", "0", "0", "0"), ("1", "1", "0", "0"),
+                                                               ("1", "2", "0", "0"), ("1", "0", "64", "48")])
+def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, ag_grid, rc_grid, monkeypatch):
     """The device ring's host->device variants (copy engine / blit kernel on the op stream for the all-gather; copy
     engine, blit, or zero-copy reads by the fused reduce for the reduce-scatter) give the exact result, in place and
     with chunk offsets that are no multiple of 16 bytes (odd element count: the zero-copy sinks take the chunk's
@@ -172,6 +173,8 @@ def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, monkeypatch):
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_RING_AG_KERNEL_COPY", ag_kernel)
     monkeypatch.setenv("PCCL_RING_RS_H2D", rs_h2d)
+    monkeypatch.setenv("PCCL_RING_AG_COPY_GRID", ag_grid)  # > 0: our copy kernel with this many workgroups
+    monkeypatch.setenv("PCCL_REDUCE_COPY_GRID", rc_grid)  # > 0: workgroup cap of the fused reduce-scatter kernel
     world, n = 4, 6_000_007
     base = (torch.arange(n, dtype=torch.int64) % 23).float()
     inputs = [(base + 3 * r).to(torch.bfloat16) for r in range(world)]
