@@ -1593,7 +1593,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     // pass over the chunk. PCCL_QUANT_FUSED_MINMAX=0 turns it off; a step whose launches do not fit the partials
     // buffer falls back to the separate min / max pass.
     const bool fuse_mm = env_size("PCCL_QUANT_FUSED_MINMAX", 1) != 0;
-    constexpr int kMmSlots = 16384, kMmMinRoom = 64;
+    constexpr int kMmSlots = 65536, kMmMinRoom = 64; // 1 MiB of partials: ~1 GiB bf16 chunks
     Lease mmp;
     if (fuse_mm) mmp = Lease(device_pool(), kMmSlots * 2 * sizeof(double), device);
     auto *mm_partials = mmp.ok() ? reinterpret_cast<double *>(mmp.data()) : nullptr;
