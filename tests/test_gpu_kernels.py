@@ -88,7 +88,7 @@ def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
 @pytest.mark.parametrize("qdtype,algo", [(torch.uint8, "min_max"), (torch.int8, "zero_point_scale"),
                                          (getattr(torch, "float8_e4m3fn", None), "min_max")])
 @pytest.mark.parametrize("op", ["sum", "max"])
-@pytest.mark.parametrize("n,pieces", [(1, 1), (5000, 3), ((1 << 22) + 7, 7), (3_000_011, 1)])
+@pytest.mark.parametrize("n,pieces", [(1, 1), (5000, 3), ((1 << 22) + 7, 7), (3_000_011, 1), ((1 << 25) + 5, 3)])
 def test_device_dequant_reduce_fused_minmax(hip, vdtype, qdtype, algo, op, n, pieces):
     """The quantized device ring's de-quantize-reduce kernels also emit per-workgroup (min, max) partials of the
     values they store (several launches per chunk, like the ring's receive ranges), folded by k_minmax_final: the
