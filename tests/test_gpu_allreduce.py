@@ -479,3 +479,33 @@ def test_device_ring_small_messages(hip, n, monkeypatch):
     for y, x, path in res:
         assert path == pccl.ReducePath.DEVICE_RING.value
         assert torch.equal(y, 3 * base + 3) and torch.equal(x, base + 2)
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 4097])
+@pytest.mark.parametrize("quant", [False, True])
+def test_device_ring_fewer_elements_than_peers(hip, n, quant, monkeypatch):
+    """The pipelined device ring (small-message path off) with chunks of zero or one element: empty reduce-scatter /
+    all-gather steps must neither hang nor touch memory outside the buffer; quantized and plain."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_SMALL_ALLREDUCE_BYTES", "0")
+    world = 4
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if quant else None
+
+    def fn(rank, comm):
+        x = (torch.arange(n, device=hip, dtype=torch.float32) % 5 + rank).bfloat16()
+        y = torch.full((n + 64,), -7.0, device=hip, dtype=torch.bfloat16)  # guard elements after the output
+        for tag in range(2):
+            comm.all_reduce(x, y[:n], op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
+        torch.cuda.synchronize()
+        return y.cpu()
+
+    res = _run(world, fn)
+    base = (torch.arange(n, dtype=torch.float32) % 5)
+    expect = (world * base + sum(range(world))).bfloat16()
+    for y in res:
+        assert torch.all(y[n:] == -7.0)
+        assert torch.equal(y[:n], res[0][:n])
+        if not quant:
+            assert torch.equal(y[:n], expect)
+        else:
+            assert (y[:n].float() - expect.float()).abs().max() <= 0.5
