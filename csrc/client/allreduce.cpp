@@ -988,6 +988,7 @@ struct Lane {
                     // 2 none (the fused reduce reads them from pinned memory)
     bool shared_reduce = false; // reduce-scatter kernels on the process-wide stream pq.red (see ring_reduce_device)
     int ag_copy_grid = 0; // > 0: all-gather copies as our copy kernel with this many workgroups (PCCL_RING_AG_COPY_GRID)
+    bool shared_ag = false; // with shared_reduce: the all-gather copies on the shared stream too (PCCL_RING_SHARED_AG)
     LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
     std::atomic<uint64_t> *tx, *rx;
@@ -1298,6 +1299,13 @@ void run_lane(Lane &L) {
             };
         } else {
             consume = [&, sink, region, b](size_t a, size_t e) {
+                if (shared_red && L.shared_ag) { // our copy kernel on the process-wide stream, after the reduces
+                    std::lock_guard l(*pq.red_mtx);
+                    be->copy_kernel(region + a * es, sink + a * es, (e - a) * es, L.ag_copy_grid, rst);
+                    lane_last_red = last_h2d[0] = step_h2d[0] = record(rst);
+                    rxready[b].add(a * es, e * es, nullptr);
+                    return;
+                }
                 if (L.ag_on_lane_stream) { // blit kernel reading pinned memory, on this lane's stream
                     if (L.ag_copy_grid > 0)
                         be->copy_kernel(region + a * es, sink + a * es, (e - a) * es, L.ag_copy_grid, st);
@@ -1488,6 +1496,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         L.shared_reduce = env_size("PCCL_RING_SHARED_REDUCE", 0) != 0 && L.rs_h2d == 0 && L.host_frac == 0 &&
                           L.ag_on_lane_stream;
         L.ag_copy_grid = static_cast<int>(std::min<size_t>(4096, env_size("PCCL_RING_AG_COPY_GRID", 0)));
+        L.shared_ag = L.shared_reduce && env_size("PCCL_RING_SHARED_AG", 0) != 0;
         L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
         L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
         L.aborted = [this, t = q.tag] { return abort_received(t); };

@@ -82,7 +82,8 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
 
 @pytest.mark.parametrize("shared_queues,lanes,host,shared_red", [("1", "1", "0", "0"), ("0", "1", "0", "0"),
                                                                  ("1", "2", "0", "0"), ("1", "1", "0.6", "0"),
-                                                                 ("1", "1", "0", "1"), ("1", "2", "0", "1")])
+                                                                 ("1", "1", "0", "1"), ("1", "2", "0", "1"),
+                                                                 ("1", "1", "0", "ag"), ("1", "2", "0", "ag")])
 @pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
 def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, host, shared_red, monkeypatch):
     """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
@@ -94,7 +95,9 @@ def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lan
     monkeypatch.setenv("PCCL_SHARED_COPY_QUEUES", shared_queues)
     monkeypatch.setenv("PCCL_RING_LANES", lanes)
     monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)
-    monkeypatch.setenv("PCCL_RING_SHARED_REDUCE", shared_red)
+    monkeypatch.setenv("PCCL_RING_SHARED_REDUCE", "0" if shared_red == "0" else "1")
+    monkeypatch.setenv("PCCL_RING_SHARED_AG", "1" if shared_red == "ag" else "0")  # all-gather copies there too
+    monkeypatch.setenv("PCCL_RING_AG_COPY_GRID", "64" if shared_red == "ag" else "0")
     n = 9_000_011
     base = (torch.arange(n, dtype=torch.int64) % 31).float()  # every partial sum < 256: exact in bf16
     inputs = [(base + 7 * r).to(torch.bfloat16) for r in range(world)]
