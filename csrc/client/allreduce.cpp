@@ -1586,15 +1586,43 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         while (events.size() <= i) events.push_back(event_pool().get());
         return events[i];
     };
+    // Received quantized pieces are copied to HBM on the process's shared copy-engine queue and the de-quantize kernels
+    // read them there (PCCL_QUANT_RX_STAGE=0: the kernels read pinned memory over PCIe themselves). Interleaved A/B,
+    // uint8, 8 peers x 1 GiB: 249 vs 256 ms (profiles/r3/quant_fused/ab_rx_stage.jsonl).
+    const bool rx_stage = env_size("PCCL_QUANT_RX_STAGE", 1) != 0;
+    Lease dva, dvb;
+    uint8_t *rxdev[2] = {nullptr, nullptr};
+    PcieQueues pq;
+    if (rx_stage) {
+        dva = Lease(device_pool(), stage_bytes, device);
+        dvb = Lease(device_pool(), stage_bytes, device);
+        pq = shared_pcie_queues(be, device);
+        if (!dva.ok() || !dvb.ok() || !pq.h2d[0]) return {false, false};
+        rxdev[0] = dva.data();
+        rxdev[1] = dvb.data();
+    }
+    std::vector<DevEvent> copy_events; // the staging copies (each waited for by the op stream before its kernel)
     struct EvGuard { // drains the op's stream before its events / staging buffers are recycled
         DeviceBackend *be;
         DevStream s;
-        std::vector<DevEvent> *e;
+        std::vector<DevEvent> *e, *c;
         ~EvGuard() {
             be->stream_sync(s);
             for (auto x : *e) event_pool().put(x);
+            for (auto x : *c) event_pool().put(x);
         }
-    } eg{be, st, &events};
+    } eg{be, st, &events, &copy_events};
+    // where the kernels read received quantized elements [a, b) of `sink` (after queueing their copy when staging)
+    auto rx_src = [&](uint8_t *sink, size_t a, size_t b) -> const uint8_t * {
+        if (!rx_stage) return sink + a * qs;
+        uint8_t *d = rxdev[sink == rxbuf[0] ? 0 : 1] + a * qs;
+        be->memcpy_async(d, sink + a * qs, (b - a) * qs, pq.h2d[0]);
+        DevEvent e = event_pool().get();
+        copy_events.push_back(e);
+        be->event_record(e, pq.h2d[0]);
+        be->stream_wait_event(st, e);
+        return d;
+    };
 
     // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
     // (dequant_reduce_minmax) into `mmp`: the chunk a step receives is the chunk the next step quantizes (and the last
@@ -1703,9 +1731,10 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts, step > 0);
         if (int m = send_meta(io, mine, op.tx)) return fail(m);
         const int rc = run_step(txbuf.data(), (te - ts) * qs, quant_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-            dequant_consume(rx_region + a * es, sink + a * qs, b - a, q.op, params);
+            dequant_consume(rx_region + a * es, rx_src(sink, a, b), b - a, q.op, params);
         }, meta_then(theirs, params));
         if (rc) return fail(rc);
+        step_mark(true, step);
     }
 
     trace_mark("reduce_scatter");
@@ -1736,10 +1765,12 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         if (int m = send_meta(io, mine, op.tx)) return fail(m);
         kernels::QuantParams params{};
         const int rc = run_step(payload, (te - ts) * qs, ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-            be->dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, params, st);
+            be->dequant_reduce(rx_region + a * es, rx_src(sink, a, b), b - a, q.dtype, q.qtype, ReduceOp::Set, params,
+                               st);
         }, meta_then(theirs, params));
         prev_meta = theirs;
         if (rc) return fail(rc);
+        step_mark(false, step);
         cur = inc;
     }
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);

@@ -199,9 +199,14 @@ def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, ag_grid, rc_grid, monkeyp
         assert torch.equal(y, expect)
 
 
+@pytest.mark.parametrize("stage", ["0", "1"])
 @pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
-def test_device_quantized_all_reduce(hip, qdtype, monkeypatch):
+def test_device_quantized_all_reduce(hip, qdtype, stage, monkeypatch):
+    """stage=1: received quantized pieces staged to HBM by the copy engine before the de-quantize kernels
+    (PCCL_QUANT_RX_STAGE); 0: the kernels read them from pinned memory."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
+    monkeypatch.setenv("PCCL_QUANT_RX_STAGE", stage)
+    monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
     n = (1 << 20) + 3
     inputs = [torch.randn(n, generator=torch.Generator().manual_seed(40 + r)) for r in range(3)]
 
