@@ -1587,8 +1587,9 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         return events[i];
     };
     // Received quantized pieces are copied to HBM on the process's shared copy-engine queue and the de-quantize kernels
-    // read them there (PCCL_QUANT_RX_STAGE=0: the kernels read pinned memory over PCIe themselves). Interleaved A/B,
-    // uint8, 8 peers x 1 GiB: 249 vs 256 ms (profiles/r3/quant_fused/ab_rx_stage.jsonl).
+    // read them there (PCCL_QUANT_RX_STAGE=0: the kernels read pinned memory over PCIe themselves), like the
+    // unquantized ring. Interleaved A/B, uint8, 8 peers x 1 GiB: 249 vs 256 ms and 245 vs 244 ms on two boxes
+    // (profiles/r3/quant_fused/ab_rx_stage*.jsonl): the same PCIe bytes either way.
     const bool rx_stage = env_size("PCCL_QUANT_RX_STAGE", 1) != 0;
     Lease dva, dvb;
     uint8_t *rxdev[2] = {nullptr, nullptr};
