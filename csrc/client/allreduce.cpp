@@ -759,8 +759,13 @@ PcieQueues shared_pcie_queues(DeviceBackend *be, int device) {
         e.nh2d = std::max<size_t>(1, std::min(PcieQueues::kMaxH2d, env_size("PCCL_H2D_QUEUES", 1)));
         for (size_t k = 0; k < e.nh2d; ++k) e.h2d[k] = be->create_stream();
         e.d2h = be->create_stream();
-        e.red = be->create_stream();
         e.red_mtx = new std::mutex();
+        if (cur >= 0) be->set_device(cur);
+    }
+    if (!e.red && env_size("PCCL_RING_SHARED_REDUCE", 0) != 0) { // only when asked for: streams share HW queues
+        const int cur = be->current_device();
+        be->set_device(device);
+        e.red = be->create_stream();
         if (cur >= 0) be->set_device(cur);
     }
     return e;
