@@ -447,7 +447,7 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
                  size_t rx_bytes, size_t elem, size_t frame, const std::function<void(size_t, size_t)> &consume,
                  const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr,
-                 const std::function<int()> &before_rx = {}, size_t gran = 0) {
+                 const std::function<int()> &before_rx = {}, size_t gran = 0, size_t early_from = SIZE_MAX) {
     const StripePlan tp = plan_stripes(tx_bytes, txs.size());
     const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
     auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
@@ -484,14 +484,21 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                     senders.done();
                 });
     }
+    // stripes >= early_from may take their sinks before before_rx runs: their connections carry only this op's data
+    // frames (the metadata packet travels on stripe 0's connection, where a sink posted too early would swallow it)
+    const size_t nst = rp.off.size();
+    const size_t early = before_rx ? std::min(std::max<size_t>(early_from, 1), nst) : nst; // [early, nst) go first
+    for (size_t k = early; k < nst; ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    sinks_posted = early < nst;
     if (before_rx) {
         if (const int brc = before_rx()) {
             send_rc.store(brc);
             senders.wait();
+            remove_sinks();
             return brc;
         }
     }
-    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    for (size_t k = 0; k < early; ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
     sinks_posted = true;
     if (inline_send)
         for (size_t k = 0; k < tp.off.size(); ++k)
@@ -1699,13 +1706,18 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
             for (auto x : e) event_pool().put(x);
         }
     } sink_events{be, st, {event_pool().get(), event_pool().get()}};
+    // the data stripes other than stripe 0 (whose connection carries the metadata packet) take their receive sinks
+    // before the step waits for the peer's metadata, so their frames land in place instead of being queued and copied
+    // (PCCL_QUANT_EARLY_SINKS, see striped_step)
+    const bool early_sinks = env_size("PCCL_QUANT_EARLY_SINKS", 1) != 0;
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
                         uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx) -> int {
         const int b = sink == rxbuf[0] ? 0 : 1;
         if (sink_read[b]) event_wait_polling(be, sink_read[b]);
         const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs,
-                                    piece_el * qs, consume, aborted, op.tx, op.rx, before_rx, piece_el * qs);
+                                    piece_el * qs, consume, aborted, op.tx, op.rx, before_rx, piece_el * qs,
+                                    early_sinks ? 1 : SIZE_MAX);
         if (rc == 0) {
             sink_read[b] = sink_events.e[b]; // waited for above before it is recorded again
             be->event_record(sink_read[b], st);
