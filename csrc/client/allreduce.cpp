@@ -1706,10 +1706,10 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
             for (auto x : e) event_pool().put(x);
         }
     } sink_events{be, st, {event_pool().get(), event_pool().get()}};
-    // the data stripes other than stripe 0 (whose connection carries the metadata packet) take their receive sinks
-    // before the step waits for the peer's metadata, so their frames land in place instead of being queued and copied
-    // (PCCL_QUANT_EARLY_SINKS, see striped_step)
-    const bool early_sinks = env_size("PCCL_QUANT_EARLY_SINKS", 1) != 0;
+    // PCCL_QUANT_EARLY_SINKS=1: the data stripes other than stripe 0 (whose connection carries the metadata packet)
+    // take their receive sinks before the step waits for the peer's metadata (see striped_step). Interleaved A/B,
+    // uint8, 8 peers x 1 GiB: 234.3 vs 233.1 ms (profiles/r3/quant_fused/ab_early_sinks.jsonl), so off by default.
+    const bool early_sinks = env_size("PCCL_QUANT_EARLY_SINKS", 0) != 0;
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
                         uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx) -> int {

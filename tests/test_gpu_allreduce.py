@@ -206,6 +206,7 @@ def test_device_quantized_all_reduce(hip, qdtype, stage, monkeypatch):
     (PCCL_QUANT_RX_STAGE); 0: the kernels read them from pinned memory."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
     monkeypatch.setenv("PCCL_QUANT_RX_STAGE", stage)
+    monkeypatch.setenv("PCCL_QUANT_EARLY_SINKS", stage)  # the non-default data path in one of the two cases
     monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
     n = (1 << 20) + 3
     inputs = [torch.randn(n, generator=torch.Generator().manual_seed(40 + r)) for r in range(3)]
