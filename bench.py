@@ -423,9 +423,11 @@ def latency_native(peers):
     out = {"cpu_mask": "full" if os.environ.get("PCCL_BENCH_FULL_CPUS") else "inherited"}
     for p in sorted({peers, 2}):
         try:
+            env = dict(os.environ)
+            env.pop("PCCL_DISABLE_IPC", None)  # set by the TCP-ring phases of this process; this is the xGMI path
             with _full_cpu_mask():  # the child inherits this thread's mask
                 r = subprocess.run([exe, str(free_port()), str(p), str(1 << 20), "400", "50"], capture_output=True,
-                                   text=True, timeout=120)
+                                   text=True, timeout=120, env=env)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             out[f"{p}_peers_1MiB"] = json.loads(line[-1]) if r.returncode == 0 and line else \
                 {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}

@@ -38,8 +38,10 @@ exe = os.path.join(ROOT, "pccl_amd", "lib", "pccl_latency")
 for rep in range(int(os.environ.get("REPS", "3"))):
     for name, m in masks.items():
         os.sched_setaffinity(0, m)
+        env = dict(os.environ)
+        env.pop("PCCL_DISABLE_IPC", None)  # latency_cpu's phases set it in this process
         r = subprocess.run([exe, str(free_port()), "8", str(1 << 20), "400", "50"], capture_output=True, text=True,
-                           timeout=120)
+                           timeout=120, env=env)
         line = [x for x in r.stdout.splitlines() if x.startswith("{")]
         nat = json.loads(line[-1]) if line else {"error": r.stderr[-200:]}
         cfg1 = bench.latency_cpu(job)
