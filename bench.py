@@ -391,13 +391,30 @@ class _full_cpu_mask:
     """Runs a block with the calling thread's CPU mask from before the bench's per-CCD spread (_cpu_spread), if any;
     threads and processes started inside inherit it. For the latency measurements: the spread suits the
     socket-copy-bound TCP ring, but it scatters a phase's threads over 16 L3 domains of both sockets, where every
-    wake-up of a waiting peer lands on a sleeping core of another CCD."""
+    wake-up of a waiting peer lands on a sleeping core of another CCD. ccd=True narrows the mask further to the L3
+    domain (CCD) of its first CPU: BASELINE config 1 (2 threaded peers, 4 elements) measured 32-37 us median there in
+    3 / 3 runs vs 41-94 us (bimodal) with the full mask on the same box (profiles/r3/latency_futex/cfg1_masks.jsonl)."""
+
+    def __init__(self, ccd: bool = False):
+        self.ccd = ccd
 
     def __enter__(self):
         full = os.environ.get("PCCL_BENCH_FULL_CPUS")
         self.own = os.sched_getaffinity(0)
-        if full:
-            os.sched_setaffinity(0, {int(c) for c in full.split(",")})
+        mask = {int(c) for c in full.split(",")} if full else set(self.own)
+        if self.ccd:
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{min(mask)}/cache/index3/shared_cpu_list") as f:
+                    ccd = set()
+                    for part in f.read().strip().split(","):
+                        lo, _, hi = part.partition("-")
+                        ccd.update(range(int(lo), int(hi or lo) + 1))
+                if len(ccd & mask) >= 4:
+                    mask &= ccd
+            except (OSError, ValueError):
+                pass
+        if mask != self.own:
+            os.sched_setaffinity(0, mask)
         return self
 
     def __exit__(self, *exc):
@@ -529,8 +546,9 @@ def run_extras(job, a, nbytes):
         nat = extra["latency_native"].get(f"{P}_peers_1MiB", {})
         if "median_us" in nat:  # the library's latency: C API, threaded peers, no interpreter in the loop
             extra["latency_1MiB_ipc_us"] = nat["median_us"]
-        with _full_cpu_mask():
+        with _full_cpu_mask(ccd=True):
             extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
+        with _full_cpu_mask():
             r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
     elif job.n_gpus > 1 and os.environ.get("PCCL_BENCH_RCCL", "1") == "1":

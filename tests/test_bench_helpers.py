@@ -56,3 +56,12 @@ def test_peer_cpu_groups_off_by_default_and_disjoint(monkeypatch):
         return
     assert len(groups) == 2 and all(groups) and not (groups[0] & groups[1])
     assert groups[0] | groups[1] <= os.sched_getaffinity(0)
+
+
+def test_full_cpu_mask_ccd_narrows_to_one_l3_domain(monkeypatch):
+    own = os.sched_getaffinity(0)
+    monkeypatch.delenv("PCCL_BENCH_FULL_CPUS", raising=False)
+    with bench._full_cpu_mask(ccd=True):
+        inside = os.sched_getaffinity(0)
+    assert os.sched_getaffinity(0) == own
+    assert inside <= own and min(own) in inside
