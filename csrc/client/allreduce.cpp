@@ -355,22 +355,66 @@ bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {
 // ------------------------------------------------------------------------------------------------------------------
 namespace {
 
+// Quantized ring protocol. The buffer is split into lanes (quant_lane_bounds), each a complete ring all-reduce over
+// a contiguous part with its own data tag (lane_tag) and its own metadata tag (meta_tag). Per ring step a peer sends
+// the step's dequantization metadata packet on the metadata tag (on connection seq % pool) and the quantized payload
+// striped on the data tag. Keeping the packets off the data tag lets a peer post every receive sink of a step (and
+// the next step's) before the packet arrives: the reference sends the packet on the data tag and waits for the peer's
+// before any data moves (reference reduce.cpp:154-192), one extra latency per ring step. Host and device rings speak
+// the same protocol, so CPU and GPU peers mix in one quantized ring.
+constexpr uint64_t kMetaTagBit = 1ull << 63;
+inline uint64_t lane_tag(uint64_t tag, size_t lane) { return tag ^ (static_cast<uint64_t>(lane) << 60); }
+inline uint64_t meta_tag(uint64_t data_tag) { return data_tag ^ kMetaTagBit; }
+
+// Lane split of a quantized all-reduce of `count` elements (wire element size `qs`) over `ws` peers: element offsets
+// lo[0] = 0 < lo[1] < ... < lo[nl] = count. A quantized reduce-scatter step must receive and reduce its whole chunk
+// before the next step's min / max, and so its metadata and payload, exist: a single ring leaves its links idle for
+// a step's fill and drain at every step, and further lanes fill each other's gaps. Depends only on values every peer
+// shares (element count, ring size, wire type, PCCL_QUANT_LANES, which must match on all peers).
+std::vector<size_t> quant_lane_bounds(size_t count, size_t ws, size_t qs) {
+    constexpr size_t kMinLaneChunk = 8u << 20; // wire bytes per ring chunk and lane
+    const size_t max_lanes = std::max<size_t>(1, std::min<size_t>(4, env_size("PCCL_QUANT_LANES", 2)));
+    const size_t nl = std::min(max_lanes, std::max<size_t>(1, count / std::max<size_t>(1, ws) * qs / kMinLaneChunk));
+    std::vector<size_t> lo(nl + 1, 0);
+    for (size_t k = 1; k < nl; ++k) lo[k] = count / nl * k / 4096 * 4096;
+    lo[nl] = count;
+    return lo;
+}
+
+// Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first
+// poll that sees it (Client::abort_received), so that poll records it here for every other thread of the op.
+class OpAbort {
+public:
+    explicit OpAbort(std::function<bool()> poll) : poll_(std::move(poll)) {}
+    bool operator()() {
+        if (seen_.load(std::memory_order_acquire)) return true;
+        std::lock_guard l(m_);
+        if (seen_.load(std::memory_order_acquire)) return true;
+        if (!poll_()) return false;
+        seen_.store(true, std::memory_order_release);
+        return true;
+    }
+
+private:
+    std::function<bool()> poll_;
+    std::mutex m_;
+    std::atomic<bool> seen_{false};
+};
+
+// the connections a quantized step's metadata packet travels on, and its tag
 struct StepIo {
     net::MuxConn *tx;
     net::MuxConn *rx;
-    uint64_t tag;
+    uint64_t tag; // metadata tag
     uint64_t seq;
 };
 
 constexpr size_t kMetaFrameOverhead = 24;
 
-// Dequantization metadata of one quantized step (reference reduce.cpp:154-192 sends its own and then waits for the
-// peer's before any data moves, which costs one extra network latency per ring step). Here the sender sends its meta
-// and immediately its data; the receiver waits for the peer's meta before posting its data sink (data frames that
-// arrive first are queued by the connection), so meta and data share one latency. Returns 0 ok, 1 io failure.
+// Returns 0 ok, 1 io failure.
 int send_meta(const StepIo &io, const QuantMeta &mine, std::atomic<uint64_t> &tx) {
     P2PDequantizationMeta pkt;
-    pkt.tag = io.tag;
+    pkt.tag = io.tag ^ kMetaTagBit; // the lane's data tag
     pkt.meta = mine;
     auto bytes = encode_with_id(pkt);
     if (!io.tx->send_frame(io.tag, io.seq, bytes.data(), bytes.size())) return 1;
@@ -378,8 +422,10 @@ int send_meta(const StepIo &io, const QuantMeta &mine, std::atomic<uint64_t> &tx
     return 0;
 }
 
-// Waits for the peer's metadata of this step. Returns 0 ok, 1 io failure, 2 abort.
-int recv_meta(const StepIo &io, QuantMeta &theirs, std::atomic<uint64_t> &rx, const std::function<bool()> &aborted) {
+// Waits for the peer's metadata of the next step (the packets of a lane arrive in step order). Returns 0 ok, 1 io
+// failure, 2 abort.
+int recv_meta(const StepIo &io, QuantMeta &theirs, std::atomic<uint64_t> &rx, const std::function<bool()> &aborted,
+              const std::function<bool()> &failed = {}) {
     while (true) {
         auto m = io.rx->recv_packet<P2PDequantizationMeta>(io.tag, io.seq, 20ms);
         if (m) {
@@ -387,7 +433,7 @@ int recv_meta(const StepIo &io, QuantMeta &theirs, std::atomic<uint64_t> &rx, co
             rx += encode_with_id(*m).size() + kMetaFrameOverhead;
             return 0;
         }
-        if (!io.rx->is_open()) return 1;
+        if (!io.rx->is_open() || (failed && failed())) return 1;
         if (aborted()) return 2;
     }
 }
@@ -422,8 +468,8 @@ StripePlan plan_stripes(size_t bytes, size_t conns) {
 // One full-duplex ring step over the striped connections. `tx_ready(end)` blocks until payload bytes [0, end) of the
 // calling stripe may be sent; `consume(a, b)` processes received elements [a, b) (called from this thread only, any
 // order across stripes, in order within a stripe, in batches of at least `gran` bytes unless a stripe ends).
-// `before_rx` (optional) runs after the senders started and before the receive sinks are posted (the quantized steps
-// receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
+// `before_rx` (optional) runs after the senders started and the receive sinks are posted, before anything is consumed
+// (the quantized steps receive the peer's metadata there). Returns 0 ok, 1 io failure, 2 abort.
 // Stripes are sent by each connection's persistent sender thread (MuxConn::post_send_job); steps of at most
 // kInlineSendBytes are sent on the calling thread after the sinks are posted.
 constexpr size_t kInlineSendBytes = 256 << 10;
@@ -447,7 +493,7 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready, uint8_t *sink,
                  size_t rx_bytes, size_t elem, size_t frame, const std::function<void(size_t, size_t)> &consume,
                  const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr, std::atomic<uint64_t> &rx_ctr,
-                 const std::function<int()> &before_rx = {}, size_t gran = 0, size_t early_from = SIZE_MAX) {
+                 const std::function<int()> &before_rx = {}, size_t gran = 0) {
     const StripePlan tp = plan_stripes(tx_bytes, txs.size());
     const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
     auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
@@ -484,12 +530,9 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                     senders.done();
                 });
     }
-    // stripes >= early_from may take their sinks before before_rx runs: their connections carry only this op's data
-    // frames (the metadata packet travels on stripe 0's connection, where a sink posted too early would swallow it)
-    const size_t nst = rp.off.size();
-    const size_t early = before_rx ? std::min(std::max<size_t>(early_from, 1), nst) : nst; // [early, nst) go first
-    for (size_t k = early; k < nst; ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
-    sinks_posted = early < nst;
+    // (a quantized step's metadata packet travels on its own tag: no sink of this step can swallow it)
+    for (size_t k = 0; k < rp.off.size(); ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
+    sinks_posted = true;
     if (before_rx) {
         if (const int brc = before_rx()) {
             send_rc.store(brc);
@@ -498,8 +541,6 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
             return brc;
         }
     }
-    for (size_t k = 0; k < early; ++k) rx_conn(k)->post_sink(tag, seq, sink + rp.off[k], rp.len[k]);
-    sinks_posted = true;
     if (inline_send)
         for (size_t k = 0; k < tp.off.size(); ++k)
             if (tp.len[k] > 0) send_stripe(k);
@@ -599,57 +640,37 @@ int small_allgather_reduce(const std::vector<std::shared_ptr<net::MuxConn>> &txs
 // ------------------------------------------------------------------------------------------------------------------
 // host ring
 // ------------------------------------------------------------------------------------------------------------------
-std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq) {
-    const ReduceRequest &q = op.req;
-    const size_t ws = rv.ring.size(), rank = rv.rank;
+namespace {
+
+// One ring all-reduce over host memory of `count` elements at `dst` (already holding the input) on data tag `tag`:
+// the plain host ring, or one lane of a quantized ring (`quant`; metadata on meta_tag(tag)). Returns 0 ok, 1 io
+// failure, 2 abort.
+int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::vector<std::shared_ptr<net::MuxConn>> &rxs,
+              size_t ws, size_t rank, uint64_t tag, uint64_t seq, uint8_t *dst, size_t count, const ReduceRequest &q,
+              bool quant, const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
+              std::atomic<uint64_t> &rx_ctr) {
     const size_t es = dtype_size(q.dtype);
-    const bool quant = q.qalgo != QuantAlgo::None && q.qtype != q.dtype;
     const size_t qs = quant ? dtype_size(q.qtype) : es;
-    auto *dst = static_cast<uint8_t *>(q.dst);
-    const size_t bytes = q.count * es;
     const size_t chunk = net::multiplex_chunk_size();
+    StepIo io{txs[seq % txs.size()].get(), rxs[seq % rxs.size()].get(), meta_tag(tag), seq};
 
-    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
-    auto aborted = [&] { return abort_received(q.tag); };
-
-    if (!quant && op.small_path) {
-        const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
-                                              aborted, op.tx, op.rx);
-        trace_mark("allgather_reduce");
-        return {rc == 0, rc == 2};
-    }
-
-    Lease backup;
-    if (q.src == q.dst) {
-        backup = Lease(host_pool(), bytes);
-        std::memcpy(backup.data(), q.src, bytes);
-    } else {
-        std::memcpy(dst, q.src, bytes);
-    }
-    auto restore = [&] {
-        if (q.src == q.dst) std::memcpy(dst, backup.data(), bytes);
-    };
-
-    const auto bounds = chunk_bounds(q.count, ws);
+    const auto bounds = chunk_bounds(count, ws);
     size_t max_chunk = 0;
     for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
     Lease rbuf(host_pool(), max_chunk * qs + 64);
     Lease qbuf;
     if (quant) qbuf = Lease(host_pool(), max_chunk * qs + 64);
+    if (!rbuf.ok() || (quant && !qbuf.ok())) return 1;
 
     // One full-duplex (striped) step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)`
     // for newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
     auto run_step = [&](const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
                         const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx = {}) -> int {
-        return striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes,
-                            qs, chunk, consume, aborted, op.tx, op.rx, before_rx);
+        return striped_step(txs, rxs, tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes, qs,
+                            chunk, consume, aborted, tx_ctr, rx_ctr, before_rx);
     };
-    auto await_meta = [&](QuantMeta &theirs) { return [&, pt = &theirs] { return recv_meta(io, *pt, op.rx, aborted); }; };
-    auto fail = [&](int code) -> std::pair<bool, bool> {
-        restore();
-        return {code == 2, code == 2};
-    };
+    auto await_meta = [&](QuantMeta &theirs) { return [&, pt = &theirs] { return recv_meta(io, *pt, rx_ctr, aborted); }; };
 
     // ---- reduce-scatter
     for (size_t step = 0; step + 1 < ws; ++step) {
@@ -662,7 +683,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
             if (te > ts) mine = kernels::host_quantize(qbuf.data(), dst + ts * es, te - ts, q.dtype, q.qtype, q.qalgo);
             else mine = kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
             payload = qbuf.data();
-            if (int rc = send_meta(io, mine, op.tx)) return fail(rc);
+            if (int rc = send_meta(io, mine, tx_ctr)) return rc;
         }
         uint8_t *rx_region = dst + rs * es;
         const int rc = run_step(payload, (te - ts) * qs, rbuf.data(), (re - rs) * qs, [&](size_t a, size_t b) {
@@ -671,7 +692,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
             else
                 kernels::host_reduce(rx_region + a * es, rbuf.data() + a * es, b - a, q.dtype, q.op);
         }, quant ? std::function<int()>(await_meta(theirs)) : std::function<int()>());
-        if (rc) return fail(rc);
+        if (rc) return rc;
     }
 
     trace_mark("reduce_scatter");
@@ -680,6 +701,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     if (quant) {
         ag[0] = Lease(host_pool(), max_chunk * qs + 64);
         ag[1] = Lease(host_pool(), max_chunk * qs + 64);
+        if (!ag[0].ok() || !ag[1].ok()) return 1;
     }
     QuantMeta prev_meta;
     size_t cur = (rank + 1) % ws;
@@ -705,7 +727,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
                 mine = prev_meta;
                 payload = ag[(step - 1) % 2].data();
             }
-            if (int m = send_meta(io, mine, op.tx)) return fail(m);
+            if (int m = send_meta(io, mine, tx_ctr)) return m;
             uint8_t *sink = ag[step % 2].data();
             rc = run_step(payload, (te - ts) * qs, sink, (re - rs) * qs, [&](size_t a, size_t b) {
                 kernels::host_dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, theirs);
@@ -714,8 +736,63 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
         } else {
             rc = run_step(dst + ts * es, (te - ts) * es, rx_region, (re - rs) * es, [](size_t, size_t) {});
         }
-        if (rc) return fail(rc);
+        if (rc) return rc;
         cur = inc;
+    }
+    return 0;
+}
+
+// Runs fn(lane, lo, hi) for every lane of `lo` (lane 0 on the calling thread); returns the worst lane result
+// (abort 2 outranks io failure 1).
+int run_lanes(const std::vector<size_t> &lo, const std::function<int(size_t, size_t, size_t)> &fn) {
+    const size_t nl = lo.size() - 1;
+    std::vector<int> rc(nl, 0);
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < nl; ++k) th.emplace_back([&, k] {
+        name_thread("pccl-ring-lane");
+        rc[k] = fn(k, lo[k], lo[k + 1]);
+    });
+    rc[0] = fn(0, lo[0], lo[1]);
+    for (auto &t : th) t.join();
+    return *std::max_element(rc.begin(), rc.end());
+}
+
+} // namespace
+
+std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq) {
+    const ReduceRequest &q = op.req;
+    const size_t ws = rv.ring.size(), rank = rv.rank;
+    const size_t es = dtype_size(q.dtype);
+    const bool quant = q.qalgo != QuantAlgo::None && q.qtype != q.dtype;
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    OpAbort aborted([this, t = q.tag] { return abort_received(t); });
+    auto abort_fn = [&] { return aborted(); };
+
+    if (!quant && op.small_path) {
+        const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
+                                              abort_fn, op.tx, op.rx);
+        trace_mark("allgather_reduce");
+        return {rc == 0, rc == 2};
+    }
+
+    Lease backup;
+    if (q.src == q.dst) {
+        backup = Lease(host_pool(), bytes);
+        if (!backup.ok()) return {false, false};
+        std::memcpy(backup.data(), q.src, bytes);
+    } else {
+        std::memcpy(dst, q.src, bytes);
+    }
+    const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
+                                         : std::vector<size_t>{0, q.count};
+    const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
+        return host_ring(rv.tx, rv.rx, ws, rank, lane_tag(q.tag, k), seq, dst + a * es, b - a, q, quant, abort_fn,
+                         op.tx, op.rx);
+    });
+    if (rc) {
+        if (q.src == q.dst) std::memcpy(dst, backup.data(), bytes); // every lane returned: nothing writes dst
+        return {rc == 2, rc == 2};
     }
     if (q.op == ReduceOp::Avg) kernels::host_finalize_avg(dst, q.count, q.dtype, ws);
     return {true, false};
@@ -733,23 +810,23 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
 //   * every staging copy of the process goes to ONE host->device and ONE device->host stream per GPU (shared by all
 //     ops and all peers of the process); nothing is queued behind a cross-stream wait there, so ROCclr keeps them on
 //     the copy engines;
-//   * received bytes are copied into HBM staging by the copy engine and reduced HBM->HBM on the op's compute stream
-//     (cross-stream event wait, no host round trip) by k_reduce_copy, which also streams the result into pinned
-//     memory as the NEXT step's payload: a ring step's sends start the moment the previous step's last piece lands,
-//     and the only device->host copies left are the step-0 pieces of the input.
+//   * reduce-scatter: received bytes are copied into HBM staging by the copy engine and reduced HBM->HBM on the op's
+//     stream (cross-stream event wait, no host round trip) by k_reduce_copy, which also streams the result into
+//     pinned memory as the NEXT step's payload: a ring step's sends start the moment the previous step's last piece
+//     lands, and the only device->host copies left are the step-0 pieces of the input;
+//   * all-gather: received chunks go to HBM as copies on the op's stream (blit kernels reading pinned memory, one per
+//     peer in parallel, next to the shared copy-engine queue that carries the reduce-scatter's bytes): interleaved
+//     A/B, 8 peers x 1 GiB: 347 vs 376 ms and 337 vs 342 ms (profiles/r3/h2d_modes/).
 // PCIe bytes per peer and 1 GiB: D2H 1 GiB (step-0 payload + reduced pieces), H2D 1.75 GiB (received pieces).
+// Round 3 measured the alternatives (several H2D queues, per-op queues, a process-wide reduce stream, CPU-reduced
+// parts, kernels reading received bytes from pinned memory, lanes, a step-synchronous schedule): none was faster, so
+// none is kept (profiles/r3/{ring_ab,h2d_modes,shared_reduce,host_reduce,grid_caps}/).
 
 namespace {
 
 struct PcieQueues {
-    static constexpr size_t kMaxH2d = 4;
-    std::array<DevStream, kMaxH2d> h2d{}; // received pieces -> HBM, round robin over nh2d queues
-    size_t nh2d = 1;
-    DevStream d2h = nullptr;
-    // one compute stream for the fused reduce-scatter kernels of every device-ring op of the process on this GPU
-    // (PCCL_RING_SHARED_REDUCE), with the lock that keeps each (H2D copy, reduce) pair in the same order on both queues
-    DevStream red = nullptr;
-    std::mutex *red_mtx = nullptr;
+    DevStream h2d = nullptr; // received pieces -> HBM staging
+    DevStream d2h = nullptr; // step-0 payload pieces -> pinned
 };
 
 // process-wide copy queues of `device` (never destroyed: they may outlive static destruction order)
@@ -758,21 +835,11 @@ PcieQueues shared_pcie_queues(DeviceBackend *be, int device) {
     static auto *q = new std::map<int, PcieQueues>();
     std::lock_guard l(m);
     PcieQueues &e = (*q)[device];
-    if (!e.h2d[0]) {
+    if (!e.h2d) {
         const int cur = be->current_device();
         be->set_device(device);
-        // PCCL_H2D_QUEUES (1..4, default 1): one host->device stream runs ~46 GB/s on MI355X, several together
-        // ~57 GB/s one way (profiles/r2/sysprobe.json)
-        e.nh2d = std::max<size_t>(1, std::min(PcieQueues::kMaxH2d, env_size("PCCL_H2D_QUEUES", 1)));
-        for (size_t k = 0; k < e.nh2d; ++k) e.h2d[k] = be->create_stream();
+        e.h2d = be->create_stream();
         e.d2h = be->create_stream();
-        e.red_mtx = new std::mutex();
-        if (cur >= 0) be->set_device(cur);
-    }
-    if (!e.red && env_size("PCCL_RING_SHARED_REDUCE", 0) != 0) { // only when asked for: streams share HW queues
-        const int cur = be->current_device();
-        be->set_device(device);
-        e.red = be->create_stream();
         if (cur >= 0) be->set_device(cur);
     }
     return e;
@@ -846,7 +913,7 @@ struct ReadyRanges {
     }
 };
 
-// The send side of one device-ring op: one thread per stripe for the whole op (not per step), each sending its
+// The send side of one pipelined ring op: one thread per stripe for the whole op (not per step), each sending its
 // stripe of every step in order over connection (seq + k) % pool. The op thread publishes step g (payload, bytes,
 // readiness) as soon as step g may start sending — with send-ahead while step g-1 still receives — and a stripe thread
 // streams each piece once it is readable. Per-op threads instead of the connections' shared sender threads: a stripe
@@ -907,7 +974,6 @@ public:
         cv_.notify_all();
     }
     bool failed() const { return rc_.load() != 0; }
-    const std::atomic<int> &rc() const { return rc_; }
 
 private:
     void run(size_t k) {
@@ -958,94 +1024,142 @@ private:
     std::vector<std::thread> th_;
 };
 
-} // namespace
-
-namespace {
-
-// Start signal between the lanes of one device-ring op (lane k+1 starts once lane k reached its all-gather).
-struct LaneGate {
-    std::mutex m;
-    std::condition_variable cv;
-    bool open = false;
-    void signal() {
-        {
-            std::lock_guard l(m);
-            open = true;
-        }
-        cv.notify_all();
+// The receive side of one pipelined ring op: per step one sink per stripe on the connections from the previous peer.
+// Sinks of a tag form a FIFO on each connection, so step g+1's sinks may be posted while step g still receives (the
+// previous peer streams both steps back to back on every connection). Sinks never outlive the op: the destructor
+// removes every posted one (declare a RingRx after the buffers its sinks point into).
+class RingRx {
+public:
+    RingRx(const std::vector<std::shared_ptr<net::MuxConn>> &rxs, uint64_t tag, uint64_t seq, size_t nsteps)
+        : rxs_(rxs), tag_(tag), seq_(seq), steps_(nsteps) {}
+    ~RingRx() {
+        for (size_t g = 0; g < steps_.size(); ++g) unpost(g);
     }
+    RingRx(const RingRx &) = delete;
+    RingRx &operator=(const RingRx &) = delete;
+
+    bool posted(size_t g) const { return steps_[g].posted; }
+    // step g receives `bytes` into `buf`
+    void post(size_t g, uint8_t *buf, size_t bytes) {
+        Step &r = steps_[g];
+        r.rp = plan_stripes(bytes, rxs_.size());
+        r.sinks.assign(r.rp.off.size(), nullptr);
+        r.done.assign(r.rp.off.size(), 0);
+        r.remaining = 0;
+        for (size_t k = 0; k < r.rp.off.size(); ++k) {
+            if (r.rp.len[k] == 0) continue;
+            r.sinks[k] = conn(k)->post_sink(tag_, seq_, buf + r.rp.off[k], r.rp.len[k]);
+            ++r.remaining;
+        }
+        r.posted = true;
+    }
+    void unpost(size_t g) {
+        Step &r = steps_[g];
+        if (!r.posted) return;
+        for (size_t k = 0; k < r.sinks.size(); ++k)
+            if (r.sinks[k]) conn(k)->remove_sink(tag_, r.sinks[k]);
+        r.sinks.clear();
+        r.posted = false;
+    }
+    // Receives step g: consume(a, b) for newly arrived bytes [a, b) of the step (multiples of `unit`, at least `gran`
+    // bytes per call unless a stripe ends; in order within a stripe, any order across stripes). `between` runs after
+    // every scan of the stripes (the caller posts the next step's sinks there). Returns 0 ok, 1 io failure (a
+    // connection closed or `failed()`), 2 abort.
+    int receive(size_t g, size_t unit, size_t gran, const std::function<void(size_t, size_t)> &consume,
+                const std::function<void()> &between, const std::function<bool()> &failed,
+                const std::function<bool()> &aborted) {
+        Step &r = steps_[g];
+        const size_t gb = std::max(unit, gran / unit * unit);
+        size_t idle = 0, rr = 0;
+        while (r.remaining > 0) {
+            bool progress = false;
+            for (size_t k = 0; k < r.sinks.size(); ++k) {
+                if (!r.sinks[k]) continue;
+                const size_t want = r.rp.len[k];
+                if (r.done[k] >= want) continue;
+                const size_t have = net::MuxConn::sink_progress(r.sinks[k]) / unit * unit;
+                if (have > r.done[k] && (have - r.done[k] >= gb || have >= want)) {
+                    consume(r.rp.off[k] + r.done[k], r.rp.off[k] + have);
+                    r.done[k] = have;
+                    progress = true;
+                    if (have >= want) --r.remaining;
+                }
+            }
+            if (between) between();
+            if (r.remaining == 0 || progress) {
+                idle = 0;
+                continue;
+            }
+            // block on one unfinished stripe (round robin) until its next batch is complete or a short timeout
+            size_t k = rr++ % r.sinks.size();
+            while (!r.sinks[k] || r.done[k] >= r.rp.len[k]) k = rr++ % r.sinks.size();
+            net::MuxConn *c = conn(k);
+            c->wait_sink(r.sinks[k], std::min(r.rp.len[k], r.done[k] + gb), 5ms);
+            if (!c->is_open() || (failed && failed())) return 1;
+            if (++idle % 8 == 0 && aborted()) return 2;
+        }
+        return 0;
+    }
+
+private:
+    struct Step {
+        StripePlan rp;
+        std::vector<net::MuxConn::SinkRef> sinks;
+        std::vector<size_t> done; // bytes consumed per stripe
+        size_t remaining = 0;     // stripes not yet fully consumed
+        bool posted = false;
+    };
+    net::MuxConn *conn(size_t k) const { return rxs_[(seq_ + k) % rxs_.size()].get(); }
+    const std::vector<std::shared_ptr<net::MuxConn>> &rxs_;
+    const uint64_t tag_, seq_;
+    std::vector<Step> steps_;
 };
 
-// One lane of the device ring: a complete pipelined ring all-reduce of `n` elements at `region` (HBM, already holding
-// the input) whose step-0 payload is staged from `src`, on its own compute stream, tag and staging rings.
-struct Lane {
-    // inputs
-    const std::vector<std::shared_ptr<net::MuxConn>> *txs, *rxs; // the ring's connections to next / from prev
-    size_t ws, rank;                                              // ring size, my position
+// chunk index a peer sends / receives at global ring step g (reduce-scatter steps 0 .. ws-2, then all-gather)
+size_t ring_chunk_tx(size_t g, size_t rank, size_t ws) {
+    return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
+}
+size_t ring_chunk_rx(size_t g, size_t rank, size_t ws) { return (ring_chunk_tx(g, rank, ws) + ws - 1) % ws; }
+
+// inputs of one device-ring op
+struct DevRing {
+    const std::vector<std::shared_ptr<net::MuxConn>> &txs, &rxs; // the ring's connections to next / from prev
+    size_t ws, rank;
     uint64_t tag, seq;
     DeviceBackend *be;
     PcieQueues pq;
-    DevStream st;       // this lane's compute stream (waits for `ready` first)
-    DevEvent ready;     // the op-level input copy / backup (recorded on the op stream), or nullptr
-    const uint8_t *src; // step-0 source of this lane's elements
-    uint8_t *dst;       // this lane's elements in the op's destination
+    DevStream st;       // the op's stream (input copy / backup before any of the ring's work)
+    const uint8_t *src; // step-0 payload source: the caller's input (ready at call time, never written by the op
+                        // before its step-0 copies completed)
+    uint8_t *dst;       // the output, holding the input once `st` reaches the ring's first kernel
     size_t count, es, piece;
     DType dtype;
     ReduceOp rop;
     int device;
-    bool ahead, step0_on_op_stream;
-    double host_frac = 0; // share of every intermediate reduce-scatter chunk reduced by the CPU (see run_lane)
-    bool ag_on_lane_stream = false; // all-gather bytes -> HBM by blit kernels on the lane stream, not the H2D queue
-    int rs_h2d = 0; // reduce-scatter received bytes: 0 copy engine -> HBM staging, 1 blit copy on the lane stream,
-                    // 2 none (the fused reduce reads them from pinned memory)
-    bool shared_reduce = false; // reduce-scatter kernels on the process-wide stream pq.red (see ring_reduce_device)
-    int ag_copy_grid = 0; // > 0: all-gather copies as our copy kernel with this many workgroups (PCCL_RING_AG_COPY_GRID)
-    bool shared_ag = false; // with shared_reduce: the all-gather copies on the shared stream too (PCCL_RING_SHARED_AG)
-    LaneGate *wait_gate = nullptr, *open_gate = nullptr; // start after / signal when reaching the all-gather
     std::function<bool()> aborted;
-    std::atomic<uint64_t> *tx, *rx;
-    bool main_lane = false; // trace marks and fault points
-    // output
-    int rc = 0; // 0 ok, 1 io failure, 2 abort
+    std::atomic<uint64_t> &tx, &rx;
 };
 
-void run_lane(Lane &L) {
-    const auto &txs = *L.txs;
-    const auto &rxs = *L.rxs;
-    DeviceBackend *be = L.be;
-    const PcieQueues pq = L.pq;
-    DevStream st = L.st;
-    const size_t ws = L.ws, rank = L.rank, es = L.es, piece = L.piece;
-    const uint64_t tag = L.tag, seq = L.seq;
-    auto fail = [&](int code) {
-        L.rc = code;
-        if (L.open_gate) L.open_gate->signal(); // never leave a waiting lane behind
-    };
-    if (L.wait_gate) {
-        std::unique_lock l(L.wait_gate->m);
-        L.wait_gate->cv.wait(l, [&] { return L.wait_gate->open; });
-    }
-    if (L.ready) be->stream_wait_event(st, L.ready);
-    const bool shared_red = L.shared_reduce && pq.red && pq.red_mtx;
-    DevStream rst = shared_red ? pq.red : st; // stream of this lane's reduce-scatter kernels
-    if (shared_red && L.ready) {
-        std::lock_guard l(*pq.red_mtx);
-        be->stream_wait_event(rst, L.ready); // the op's input copy into dst precedes the reduces into it
-    }
+// The device ring as one pipeline over all 2(W-1) steps: step g+1's payload is produced (reduced into pinned
+// memory) and sent while step g still receives, and step g+1's sinks are posted as soon as their staging buffer is
+// free. Returns 0 ok, 1 io failure, 2 abort; on return no GPU work or socket write of the op touches any of its
+// buffers any more (the caller may restore the input).
+int device_ring_pipeline(DevRing &R) {
+    DeviceBackend *be = R.be;
+    const PcieQueues pq = R.pq;
+    DevStream st = R.st;
+    const size_t ws = R.ws, rank = R.rank, es = R.es, piece = R.piece;
+    const uint64_t seq = R.seq;
 
-    // events of this lane (returned to the pool once everything they guard has completed)
-    std::vector<DevEvent> owned;
+    std::vector<DevEvent> owned; // events of this op (back to the pool once everything they guard has completed)
     DevEvent last_d2h = nullptr;
-    DevEvent lane_last_red = nullptr; // last reduce-scatter kernel of this lane (on rst)
-    std::array<DevEvent, PcieQueues::kMaxH2d> last_h2d{}; // last copy issued on each H2D queue
-    size_t h2d_rr = 0;
     auto record = [&](DevStream s) {
         DevEvent e = event_pool().get();
         owned.push_back(e);
         be->event_record(e, s);
         return e;
     };
-    const auto bounds = chunk_bounds(L.count, ws);
+    const auto bounds = chunk_bounds(R.count, ws);
     size_t max_chunk = 0;
     for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
     const size_t stage_bytes = max_chunk * es + 64;
@@ -1059,81 +1173,45 @@ void run_lane(Lane &L) {
     for (size_t i = 0; i < kNb; ++i) {
         txl[i] = Lease(pinned_pool(), stage_bytes);
         rxl[i] = Lease(pinned_pool(), stage_bytes);
-        dvl[i] = Lease(device_pool(), stage_bytes, L.device);
-        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return fail(1);
+        dvl[i] = Lease(device_pool(), stage_bytes, R.device);
+        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return 1;
         txbuf[i] = txl[i].data();
         rxbuf[i] = rxl[i].data();
         rxdev[i] = dvl[i].data();
     }
-    // own input staged for the host-reduced part of a step (PCCL_RING_HOST_REDUCE, see host_elems below)
-    Lease locl[2];
-    uint8_t *locbuf[2] = {nullptr, nullptr};
-    if (L.host_frac > 0 && ws >= 3) {
-        for (int i = 0; i < 2; ++i) {
-            locl[i] = Lease(pinned_pool(), stage_bytes);
-            if (!locl[i].ok()) return fail(1);
-            locbuf[i] = locl[i].data();
-        }
-    }
-    // declared after every staging lease: destroyed first, so nothing of this lane still reads or writes them when
-    // they go back to the pools (also on the early returns below)
+    // declared after every staging lease: destroyed first, so nothing of this op still reads or writes them when
+    // they go back to the pools (also on the early returns below). The op stream waited for every H2D copy it
+    // issued; the step-0 device->host copies are not behind it.
     struct Drain {
         DeviceBackend *be;
         DevStream st;
-        std::array<DevEvent, PcieQueues::kMaxH2d> *h2d;
-        DevEvent *d2h, *red;
+        DevEvent *d2h;
         std::vector<DevEvent> *ev;
         ~Drain() {
-            for (DevEvent e : *h2d)
-                if (e) be->event_sync(e);
             if (*d2h) be->event_sync(*d2h);
-            if (*red) be->event_sync(*red);
             be->stream_sync(st);
             for (auto e : *ev) event_pool().put(e);
         }
-    } drain{be, st, &last_h2d, &last_d2h, &lane_last_red, &owned};
+    } drain{be, st, &last_d2h, &owned};
 
-    ReadyRanges txready[kNb];     // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
-    ReadyRanges rxready[kNb];     // received ranges of rxbuf[i] (the next all-gather step forwards them)
+    ReadyRanges txready[kNb];        // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    ReadyRanges rxready[kNb];        // received ranges of rxbuf[i] (the next all-gather step forwards them)
     size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
-    // last H2D copies (one per queue) reading rxbuf[i] / writing rxdev[i]
-    std::array<DevEvent, PcieQueues::kMaxH2d> h2d_done[kNb] = {};
-    DevEvent red_done[kNb] = {nullptr, nullptr, nullptr}; // last reduce kernel reading rxdev[i]
+    DevEvent buf_free[kNb] = {nullptr, nullptr, nullptr}; // last GPU work reading rxbuf[i] / rxdev[i]
 
     const size_t nsteps = 2 * (ws - 1);
     auto is_rs = [&](size_t g) { return g + 1 < ws; };
-    auto chunk_tx = [&](size_t g) { // chunk index this peer sends at global step g
-        return g + 1 < ws ? (rank + ws - g) % ws : (rank + 1 + ws - (g - (ws - 1)) % ws) % ws;
-    };
-    auto chunk_rx = [&](size_t g) { return (chunk_tx(g) + ws - 1) % ws; };
-    auto region_of = [&](size_t g) { return L.dst + bounds[chunk_rx(g)].first * es; };
-    // PCIe-balanced reduce placement (PCCL_RING_HOST_REDUCE = f): of every intermediate reduce-scatter chunk (steps
-    // whose result is only forwarded), the first f of the elements are reduced by the CPU from the received bytes and
-    // the peer's own input staged device -> host one step ahead, straight into the next payload. Those bytes then
-    // never cross PCIe host -> device, the link direction that bounds the device ring (every received byte otherwise
-    // goes up for the GPU reduce), while the device -> host volume is unchanged (the input piece instead of the
-    // reduced piece). The last reduce-scatter step (the owner's final chunk) always reduces on the GPU.
-    const bool host_red = L.host_frac > 0 && ws >= 3;
-    auto host_elems = [&](size_t g) -> size_t {
-        if (!host_red || g + 2 >= ws) return 0;
-        const auto [c0, c1] = bounds[chunk_rx(g)];
-        return static_cast<size_t>(static_cast<double>(c1 - c0) * std::min(1.0, L.host_frac)) / 64 * 64;
-    };
-    DevEvent loc_ready[2] = {nullptr, nullptr};
-    auto stage_local = [&](size_t g) { // own input of step g's host part -> pinned (read once by step g's reduce)
-        const size_t hb = g < 2 * (ws - 1) ? host_elems(g) : 0;
-        if (hb == 0) return;
-        be->memcpy_async(locbuf[g % 2], L.src + bounds[chunk_rx(g)].first * es, hb * es, pq.d2h);
-        loc_ready[g % 2] = last_d2h = record(pq.d2h);
-    };
+    auto chunk_tx = [&](size_t g) { return ring_chunk_tx(g, rank, ws); };
+    auto chunk_rx = [&](size_t g) { return ring_chunk_rx(g, rank, ws); };
+    auto region_of = [&](size_t g) { return R.dst + bounds[chunk_rx(g)].first * es; };
 
     size_t max_stripes = 1;
     for (size_t g = 0; g < nsteps; ++g) {
         const auto [ts, te] = bounds[chunk_tx(g)];
-        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, txs.size()).off.size());
+        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, R.txs.size()).off.size());
     }
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
-    OpSenders senders(txs, tag, seq, piece, nsteps, max_stripes, be, *L.tx);
+    OpSenders senders(R.txs, R.tag, seq, piece, nsteps, max_stripes, be, R.tx);
     auto publish = [&](size_t g) {
         if (senders.published(g)) return;
         const auto [ts, te] = bounds[chunk_tx(g)];
@@ -1144,247 +1222,113 @@ void run_lane(Lane &L) {
         stp.ready = staged ? &txready[g % kNb] : &rxready[(g - 1) % kNb];
         senders.publish(g, stp);
     };
-    auto fail_all = [&](int code) {
-        senders.cancel();
-        fail(code);
-    };
 
-    // ---- receive side: one set of sinks per step, posted up to one step early
-    struct StepRx {
-        StripePlan rp;
-        std::vector<net::MuxConn::SinkRef> sinks;
-        std::vector<size_t> done; // elements consumed per stripe
-        size_t remaining = 0;
-        bool posted = false;
-    };
-    std::vector<StepRx> srx(nsteps);
-    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
-    // rxbuf[g % kNb] may take step g's bytes once the step that used it before (g - kNb) is finished with it: its H2D
-    // copies and reduce kernels completed and (all-gather) the step after it has forwarded its bytes
+    RingRx rx(R.rxs, R.tag, seq, nsteps); // after the buffers its sinks point into
+    // rxbuf[g % kNb] may take step g's bytes once the step that used it before (g - kNb) is finished with it: its
+    // GPU work completed and (all-gather) the step after it has forwarded its bytes
     auto can_post = [&](size_t g) {
         if (g < kNb) return true;
         const size_t b = g % kNb, prev = g - kNb;
-        for (DevEvent e : h2d_done[b])
-            if (e && be->event_query(e) == 0) return false;
-        if (red_done[b] && be->event_query(red_done[b]) == 0) return false;
+        if (buf_free[b] && be->event_query(buf_free[b]) == 0) return false;
         if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
         return true;
     };
-    // zero-copy reduce-scatter reads the received bytes in place: they share the 16-byte phase of the HBM chunk they
-    // are reduced into, so the fused kernel stays vectorised
-    auto sink_shift = [&](size_t g) -> size_t {
-        return L.rs_h2d == 2 && is_rs(g) ? reinterpret_cast<uintptr_t>(region_of(g)) % 16 : 0;
-    };
     auto post = [&](size_t g) {
-        StepRx &r = srx[g];
         const size_t b = g % kNb;
-        h2d_done[b] = {};
-        red_done[b] = nullptr;
+        buf_free[b] = nullptr;
         if (!is_rs(g)) rxready[b].clear();
-        const auto [rs0, re0] = bounds[chunk_rx(g)];
-        r.rp = plan_stripes((re0 - rs0) * es, rxs.size());
-        r.sinks.resize(r.rp.off.size());
-        r.done.assign(r.rp.off.size(), 0);
-        r.remaining = 0;
-        for (size_t k = 0; k < r.rp.off.size(); ++k) {
-            if (r.rp.len[k] == 0) continue;
-            r.sinks[k] = rx_conn(k)->post_sink(tag, seq, rxbuf[b] + sink_shift(g) + r.rp.off[k], r.rp.len[k]);
-            ++r.remaining;
-        }
-        r.posted = true;
+        const auto [c0, c1] = bounds[chunk_rx(g)];
+        rx.post(g, rxbuf[b], (c1 - c0) * es);
     };
-    auto unpost = [&](size_t g) {
-        StepRx &r = srx[g];
-        if (!r.posted) return;
-        for (size_t k = 0; k < r.sinks.size(); ++k)
-            if (r.sinks[k]) rx_conn(k)->remove_sink(tag, r.sinks[k]);
-        r.sinks.clear();
-        r.posted = false;
+    auto fail = [&](int code) {
+        senders.cancel();
+        return code;
     };
-    struct Unposter { // sinks must never outlive their buffers (also on failure)
-        std::function<void()> fn;
-        ~Unposter() { fn(); }
-    } unposter{[&] {
-        for (size_t g = 0; g < nsteps; ++g) unpost(g);
-    }};
 
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb, nb = (g + 1) % kNb;
         const bool rs = is_rs(g);
-        if (!L.ahead && g > 0 && !senders.wait(g - 1)) return fail_all(1);
         // 1. step g's sinks (normally posted during step g-1)
-        while (!srx[g].posted) {
+        while (!rx.posted(g)) {
             if (can_post(g)) {
                 post(g);
                 break;
             }
-            if (senders.failed()) return fail_all(1);
+            if (senders.failed()) return fail(1);
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
         // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
         uint8_t *region = region_of(g);
         const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
         if (rs) {
-            if (g >= 2 && !senders.wait(g - 2)) return fail_all(1);
+            if (g >= 2 && !senders.wait(g - 2)) return fail(1);
             txready[nb].clear();
             txshift[nb] = shift;
         }
-        // own input of the host-reduced part of steps g (first step only) and g+1, one step ahead
-        if (host_red) {
-            if (g == 0) stage_local(0);
-            stage_local(g + 1);
-        }
-        // 3. own input chunk -> pinned, in pieces (from src: ready at call time, never written here)
+        // 3. own input chunk -> pinned, in pieces (from src: ready at call time)
         if (g == 0) {
             const auto [ts, te] = bounds[chunk_tx(0)];
             txready[0].clear();
             txshift[0] = 0;
-            DevStream q0 = L.step0_on_op_stream ? st : pq.d2h;
             for (size_t off = 0; off < (te - ts) * es; off += piece) {
                 const size_t n = std::min(piece, (te - ts) * es - off);
-                be->memcpy_async(txbuf[0] + off, L.src + ts * es + off, n, q0);
-                DevEvent e = record(q0);
-                if (!L.step0_on_op_stream) last_d2h = e;
-                txready[0].add(off, off + n, e);
+                be->memcpy_async(txbuf[0] + off, R.src + ts * es + off, n, pq.d2h);
+                last_d2h = record(pq.d2h);
+                txready[0].add(off, off + n, last_d2h);
             }
         }
         publish(g);
-        if (L.ahead && g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
-        if (g + 1 == ws - 1 && L.open_gate) L.open_gate->signal(); // next step is this lane's all-gather
+        if (g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
+        fault_point("ring", seq, g, "publish");
         // 4. receive + consume step g
-        StepRx &r = srx[g];
-        uint8_t *sink = rxbuf[b] + sink_shift(g);
-        DevEvent last_red = nullptr;
-        std::array<DevEvent, PcieQueues::kMaxH2d> step_h2d{}; // this step's last copy per queue
-        auto h2d_queue = [&] { return h2d_rr++ % pq.nh2d; };
+        DevEvent step_last = nullptr;
         std::function<void(size_t, size_t)> consume;
-        // the all-gather overwrites regions this lane's reduce-scatter kernels wrote: with those on the shared stream,
-        // the lane stream (which takes the all-gather copies) waits for the last of them first
-        if (!rs && g + 1 == ws && shared_red && lane_last_red) be->stream_wait_event(st, lane_last_red);
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
-            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift;
-            const size_t hb = host_elems(g);
-            bool loc_waited = false;
-            consume = [&, stage, out, sink, region, nb, hb, g](size_t a, size_t e) {
-                if (a < hb) { // CPU part: out = op(own input, received), straight into the next payload
-                    const size_t he = std::min(e, hb);
-                    if (!loc_waited) {
-                        event_wait_polling(be, loc_ready[g % 2]);
-                        loc_waited = true;
-                    }
-                    kernels::host_reduce3(out + a * es, locbuf[g % 2] + a * es, sink + a * es, he - a, L.dtype,
-                                          L.rop);
-                    txready[nb].add(a * es, he * es, nullptr);
-                    a = he;
-                    if (a >= e) return;
-                }
-                const size_t off = a * es, n = (e - a) * es;
-                if (shared_red) { // copy engine -> HBM staging, then the reduce on the process-wide stream
-                    std::lock_guard l(*pq.red_mtx);
-                    const size_t qi = h2d_queue();
-                    be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
-                    DevEvent ce = record(pq.h2d[qi]);
-                    last_h2d[qi] = step_h2d[qi] = ce;
-                    be->stream_wait_event(rst, ce);
-                    be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, rst);
-                    lane_last_red = last_red = record(rst);
-                    txready[nb].add(off, off + n, last_red);
-                    return;
-                }
-                if (L.rs_h2d == 2) { // the kernel reads the received piece straight from pinned memory
-                    be->reduce_copy(region + off, sink + off, out + off, e - a, L.dtype, L.rop, st);
-                } else {
-                    if (L.rs_h2d == 1) {
-                        be->memcpy_async(stage + off, sink + off, n, st);
-                    } else {
-                        const size_t qi = h2d_queue();
-                        be->memcpy_async(stage + off, sink + off, n, pq.h2d[qi]);
-                        DevEvent ce = record(pq.h2d[qi]);
-                        last_h2d[qi] = step_h2d[qi] = ce;
-                        be->stream_wait_event(st, ce);
-                    }
-                    be->reduce_copy(region + off, stage + off, out + off, e - a, L.dtype, L.rop, st);
-                }
-                last_red = record(st);
-                txready[nb].add(off, off + n, last_red);
+            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift, *sink = rxbuf[b];
+            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
+                be->memcpy_async(stage + a, sink + a, e - a, pq.h2d);
+                DevEvent ce = record(pq.h2d);
+                be->stream_wait_event(st, ce);
+                be->reduce_copy(region + a, stage + a, out + a, (e - a) / es, R.dtype, R.rop, st);
+                step_last = record(st);
+                txready[nb].add(a, e, step_last);
             };
         } else {
+            uint8_t *sink = rxbuf[b];
             consume = [&, sink, region, b](size_t a, size_t e) {
-                if (shared_red && L.shared_ag) { // our copy kernel on the process-wide stream, after the reduces
-                    std::lock_guard l(*pq.red_mtx);
-                    be->copy_kernel(region + a * es, sink + a * es, (e - a) * es, L.ag_copy_grid, rst);
-                    lane_last_red = last_h2d[0] = step_h2d[0] = record(rst);
-                    rxready[b].add(a * es, e * es, nullptr);
-                    return;
-                }
-                if (L.ag_on_lane_stream) { // blit kernel reading pinned memory, on this lane's stream
-                    if (L.ag_copy_grid > 0)
-                        be->copy_kernel(region + a * es, sink + a * es, (e - a) * es, L.ag_copy_grid, st);
-                    else
-                        be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, st);
-                    last_h2d[0] = step_h2d[0] = record(st);
-                    rxready[b].add(a * es, e * es, nullptr);
-                    return;
-                }
-                const size_t qi = h2d_queue();
-                be->memcpy_async(region + a * es, sink + a * es, (e - a) * es, pq.h2d[qi]);
-                last_h2d[qi] = step_h2d[qi] = record(pq.h2d[qi]);
-                rxready[b].add(a * es, e * es, nullptr); // in host memory: forwardable at once
+                be->memcpy_async(region + a, sink + a, e - a, st);
+                step_last = record(st);
+                rxready[b].add(a, e, nullptr); // in host memory: forwardable at once
             };
         }
-        const size_t gran_el = std::max<size_t>(1, piece / es);
-        int rc = 0;
-        size_t idle = 0, rr = 0;
-        while (r.remaining > 0) {
-            bool progress = false;
-            for (size_t k = 0; k < r.sinks.size(); ++k) {
-                if (!r.sinks[k]) continue;
-                const size_t want = r.rp.len[k] / es;
-                if (r.done[k] >= want) continue;
-                const size_t have = net::MuxConn::sink_progress(r.sinks[k]) / es;
-                if (have > r.done[k] && (have - r.done[k] >= gran_el || have >= want)) {
-                    const size_t e0 = r.rp.off[k] / es;
-                    consume(e0 + r.done[k], e0 + have);
-                    r.done[k] = have;
-                    progress = true;
-                    if (r.done[k] >= want) --r.remaining;
+        bool first = true;
+        const int rc = rx.receive(
+            g, es, piece,
+            [&](size_t a, size_t e) {
+                consume(a, e);
+                if (first) {
+                    first = false;
+                    fault_point("ring", seq, g, "rx"); // kernels / copies of this step in flight
                 }
-            }
-            // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
-            if (L.ahead && g + 1 < nsteps && !srx[g + 1].posted && can_post(g + 1)) post(g + 1);
-            if (r.remaining == 0 || progress) {
-                idle = 0;
-                continue;
-            }
-            size_t k = rr++ % r.sinks.size();
-            while (!r.sinks[k] || r.done[k] >= r.rp.len[k] / es) k = rr++ % r.sinks.size();
-            net::MuxConn *c = rx_conn(k);
-            c->wait_sink(r.sinks[k], std::min(r.rp.len[k], (r.done[k] + gran_el) * es), 5ms);
-            if (!c->is_open() || senders.failed()) {
-                rc = 1;
-                break;
-            }
-            if (++idle % 8 == 0 && L.aborted()) {
-                rc = 2;
-                break;
-            }
-        }
-        h2d_done[b] = step_h2d;
-        red_done[b] = last_red;
-        if (rc) return fail_all(rc);
-        *L.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
-        unpost(g);
-        if (!L.ahead && !senders.wait(g)) return fail_all(1); // classic schedule: a step ends when its sends are done
-        if (L.main_lane) {
-            step_mark(rs, rs ? g : g - (ws - 1));
-            if (g == 0) fault_point("ring_step", seq);
-            if (g + 2 == ws) trace_mark("reduce_scatter");
-        }
+            },
+            [&] { // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
+                if (g + 1 < nsteps && !rx.posted(g + 1) && can_post(g + 1)) {
+                    post(g + 1);
+                    fault_point("ring", seq, g, "ahead");
+                }
+            },
+            [&] { return senders.failed(); }, R.aborted);
+        buf_free[b] = step_last;
+        if (rc) return fail(rc);
+        R.rx += (bounds[chunk_rx(g)].second - bounds[chunk_rx(g)].first) * es;
+        rx.unpost(g);
+        step_mark(rs, rs ? g : g - (ws - 1));
+        if (g + 2 == ws) trace_mark("reduce_scatter");
+        fault_point("ring", seq, g, "end");
     }
-    if (!senders.wait(nsteps - 1)) return fail_all(1);
-    if (L.open_gate) L.open_gate->signal();
-    // the lane is complete once its last received bytes landed in HBM (the Drain waits for them)
+    if (!senders.wait(nsteps - 1)) return fail(1);
+    return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
 }
 
 } // namespace
@@ -1418,20 +1362,296 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         trace_mark("allgather_reduce");
         return {true, false};
     }
-    PcieQueues pq;
-    StreamLease own_h2d(device), own_d2h(device);
-    if (env_size("PCCL_SHARED_COPY_QUEUES", 1) != 0) {
-        pq = shared_pcie_queues(be, device);
-    } else { // A/B switch: per-op copy streams
-        pq.h2d[0] = own_h2d.get();
-        pq.nh2d = 1;
-        pq.d2h = own_d2h.get();
-    }
-    if (!pq.h2d[0] || !pq.d2h) return {false, false};
+    const PcieQueues pq = shared_pcie_queues(be, device);
+    if (!pq.h2d || !pq.d2h) return {false, false};
 
     // the caller's input -> dst (out of place) or a backup of it (in place, restored on abort), on the op stream
     Lease backup;
-    if (q.src == q.dst && !q.scratch) {
+    const bool keep_backup = q.src == q.dst && !q.scratch;
+    if (keep_backup) {
+        backup = Lease(device_pool(), bytes, device);
+        if (!backup.ok()) return {false, false};
+        be->memcpy_async(backup.data(), q.src, bytes, st);
+    } else if (q.src != q.dst) {
+        be->memcpy_async(dst, q.src, bytes, st);
+    }
+    OpAbort aborted([this, t = q.tag] { return abort_received(t); });
+    DevRing R{rv.tx, rv.rx, ws, rank, q.tag, seq, be, pq, st, static_cast<const uint8_t *>(q.src), dst, q.count, es,
+              piece, q.dtype, q.op, device, [&] { return aborted(); }, op.tx, op.rx};
+    const int rc = device_ring_pipeline(R);
+    if (rc != 0) {
+        // the pipeline drained every copy and kernel of the op and no sink of it is posted any more: restore
+        be->stream_sync(st);
+        if (keep_backup) {
+            be->memcpy_async(dst, backup.data(), bytes, st);
+            be->stream_sync(st);
+        }
+        return {rc == 2, rc == 2};
+    }
+    if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
+    if (!be->stream_sync(st)) return {false, false};
+    return {true, false};
+}
+
+// Quantized device ring (protocol: quant_lane_bounds / meta_tag). Each lane is one pipeline over its 2(W-1) steps on
+// its own thread and stream, built like the plain device ring (OpSenders, RingRx, sinks posted a step early):
+//   * reduce-scatter step g: the payload is the chunk step g-1 reduced, so its min / max (folded from the partials
+//     that step's de-quantize-reduce kernels emitted, one host round trip for the metadata packet) exists only once
+//     step g-1 has received everything; the quantize kernels then write it into pinned memory piece by piece (two
+//     payload buffers: step g quantizes while step g-1's sends drain) and each piece leaves once its kernel is done;
+//     received pieces go to HBM on the shared copy-engine queue and de-quantize-reduce there;
+//   * all-gather: the owner quantizes its finished chunk once and overwrites its own copy with D(Q(x)) (every peer
+//     ends bit-identical); received quantized chunks are forwarded cut-through (the next step's metadata and sends
+//     start when this step's metadata arrives; every piece leaves as it lands) and de-quantized by kernels reading
+//     pinned memory.
+// The per-step serialisation of the reduce-scatter is inherent to the protocol; lanes overlap it (one lane's fill and
+// drain runs while another lane's data moves).
+namespace {
+
+struct QLane {
+    const std::vector<std::shared_ptr<net::MuxConn>> *txs, *rxs;
+    size_t ws, rank;
+    uint64_t tag, seq; // the lane's data tag (metadata on meta_tag(tag))
+    DeviceBackend *be;
+    PcieQueues pq;
+    DevStream st;   // the lane's stream
+    DevEvent ready; // the op's input copy / backup into dst (recorded on the op stream)
+    uint8_t *dst;   // the lane's elements (hold the input once `ready` completed)
+    size_t count, es, qs, piece_el;
+    DType dtype, qtype;
+    QuantAlgo qalgo;
+    ReduceOp rop;
+    int device;
+    std::function<bool()> aborted;
+    std::atomic<uint64_t> *tx, *rx;
+    std::atomic<bool> *op_failed; // set by a lane that failed: its sibling lanes stop too
+};
+
+// Returns 0 ok, 1 io failure, 2 abort; on return no GPU work or socket write of the lane touches its buffers.
+int device_quant_lane(QLane &L) {
+    DeviceBackend *be = L.be;
+    DevStream st = L.st;
+    const size_t ws = L.ws, rank = L.rank, es = L.es, qs = L.qs, piece_el = L.piece_el;
+    const uint64_t seq = L.seq;
+    be->stream_wait_event(st, L.ready);
+
+    std::vector<DevEvent> owned;
+    auto record = [&](DevStream s) {
+        DevEvent e = event_pool().get();
+        owned.push_back(e);
+        be->event_record(e, s);
+        return e;
+    };
+    const auto bounds = chunk_bounds(L.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t qbytes = max_chunk * qs + 64;
+    constexpr size_t kNb = 3;
+    // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
+    // into `mm_partials`: the chunk a step receives is the chunk the next step quantizes (and the last step's is the
+    // all-gather's first payload), so its min / max is one fold of those partials instead of a second pass. A step
+    // whose launches do not fit the partials buffer falls back to a separate min / max pass.
+    constexpr int kMmSlots = 65536, kMmMinRoom = 64; // 1 MiB of partials: ~1 GiB bf16 chunks
+    Lease txl[2], rxl[kNb], dvl[kNb], mml, mmp;
+    uint8_t *txq[2], *rxbuf[kNb], *rxdev[kNb];
+    for (size_t i = 0; i < kNb; ++i) {
+        if (i < 2) {
+            txl[i] = Lease(pinned_pool(), qbytes);
+            if (!txl[i].ok()) return 1;
+            txq[i] = txl[i].data();
+        }
+        rxl[i] = Lease(pinned_pool(), qbytes);
+        dvl[i] = Lease(device_pool(), qbytes, L.device);
+        if (!rxl[i].ok() || !dvl[i].ok()) return 1;
+        rxbuf[i] = rxl[i].data();
+        rxdev[i] = dvl[i].data();
+    }
+    mml = Lease(pinned_pool(), 64);
+    mmp = Lease(device_pool(), kMmSlots * 2 * sizeof(double), L.device);
+    if (!mml.ok()) return 1;
+    auto *minmax_out = reinterpret_cast<double *>(mml.data());
+    auto *mm_partials = mmp.ok() ? reinterpret_cast<double *>(mmp.data()) : nullptr;
+    // declared after every lease: the lane's stream drains (every copy it waited for included) before they go back
+    struct Drain {
+        DeviceBackend *be;
+        DevStream st;
+        std::vector<DevEvent> *ev;
+        ~Drain() {
+            be->stream_sync(st);
+            for (auto e : *ev) event_pool().put(e);
+        }
+    } drain{be, st, &owned};
+
+    ReadyRanges txready[2], rxready[kNb];
+    DevEvent buf_free[kNb] = {nullptr, nullptr, nullptr}; // last GPU work reading rxbuf[i] / rxdev[i]
+    const size_t nsteps = 2 * (ws - 1);
+    auto is_rs = [&](size_t g) { return g + 1 < ws; };
+    auto chunk_tx = [&](size_t g) { return ring_chunk_tx(g, rank, ws); };
+    auto chunk_rx = [&](size_t g) { return ring_chunk_rx(g, rank, ws); };
+    auto nel = [&](size_t c) { return bounds[c].second - bounds[c].first; };
+
+    size_t max_stripes = 1;
+    for (size_t g = 0; g < nsteps; ++g)
+        max_stripes = std::max(max_stripes, plan_stripes(nel(chunk_tx(g)) * qs, L.txs->size()).off.size());
+    OpSenders senders(*L.txs, L.tag, seq, piece_el * qs, nsteps, max_stripes, be, *L.tx);
+    RingRx rx(*L.rxs, L.tag, seq, nsteps);
+    const StepIo io{(*L.txs)[seq % L.txs->size()].get(), (*L.rxs)[seq % L.rxs->size()].get(), meta_tag(L.tag), seq};
+
+    auto can_post = [&](size_t g) {
+        if (g < kNb) return true;
+        const size_t b = g % kNb, prev = g - kNb;
+        if (buf_free[b] && be->event_query(buf_free[b]) == 0) return false;
+        if (!is_rs(prev) && prev + 1 < nsteps && !senders.sent(prev + 1)) return false;
+        return true;
+    };
+    auto post = [&](size_t g) {
+        const size_t b = g % kNb;
+        buf_free[b] = nullptr;
+        if (!is_rs(g)) rxready[b].clear();
+        rx.post(g, rxbuf[b], nel(chunk_rx(g)) * qs);
+    };
+    auto fail = [&](int code) {
+        senders.cancel();
+        L.op_failed->store(true);
+        return code;
+    };
+    auto failed = [&] { return senders.failed() || L.op_failed->load(); };
+
+    int mm_used = 0;
+    bool mm_complete = false; // the partials cover every element of the chunk consumed by the last step
+    // metadata of `n` elements at device `src` (min / max folded from the previous step's partials when `fused` and
+    // they are complete, else a separate pass; one host round trip)
+    auto make_step_meta = [&](const uint8_t *src, size_t n, bool fused) -> QuantMeta {
+        const bool fold = fused && mm_complete && mm_partials;
+        const int folded = mm_used;
+        mm_used = 0;
+        mm_complete = mm_partials != nullptr; // the next step's consumes start collecting afresh
+        if (n == 0) return kernels::make_meta(L.qalgo, L.dtype, L.qtype, 0, 0);
+        if (fold) {
+            g_quant_minmax_folds.fetch_add(1, std::memory_order_relaxed);
+            be->minmax_fold(mm_partials, folded, n, minmax_out, st);
+        } else {
+            g_quant_minmax_passes.fetch_add(1, std::memory_order_relaxed);
+            be->minmax(src, n, L.dtype, minmax_out, st);
+        }
+        be->stream_sync(st);
+        return kernels::make_meta(L.qalgo, L.dtype, L.qtype, minmax_out[0], minmax_out[1]);
+    };
+    auto dequant_consume = [&](uint8_t *dst_el, const uint8_t *src_q, size_t n, const kernels::QuantParams &params) {
+        int blocks = 0;
+        if (mm_complete && mm_partials && kMmSlots - mm_used >= kMmMinRoom &&
+            be->dequant_reduce_minmax(dst_el, src_q, n, L.dtype, L.qtype, L.rop, params, mm_partials + 2 * mm_used,
+                                      kMmSlots - mm_used, &blocks, st)) {
+            mm_used += blocks;
+            return;
+        }
+        mm_complete = false;
+        be->dequant_reduce(dst_el, src_q, n, L.dtype, L.qtype, L.rop, params, st);
+    };
+    auto publish = [&](size_t g, const uint8_t *payload, ReadyRanges *ready) {
+        OpSenders::Step stp;
+        stp.payload = payload;
+        stp.bytes = nel(chunk_tx(g)) * qs;
+        stp.ready = ready;
+        senders.publish(g, stp);
+    };
+
+    QuantMeta theirs;
+    for (size_t g = 0; g < nsteps; ++g) {
+        const size_t b = g % kNb;
+        const bool rs = is_rs(g);
+        while (!rx.posted(g)) {
+            if (can_post(g)) {
+                post(g);
+                break;
+            }
+            if (failed()) return fail(1);
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        if (g < ws) { // own payload: reduce-scatter steps and the all-gather's first step
+            const size_t slot = g % 2, c = chunk_tx(g);
+            uint8_t *src = L.dst + bounds[c].first * es;
+            const size_t n = nel(c);
+            if (g >= 2 && !senders.wait(g - 2)) return fail(1); // txq[slot] was step g-2's payload
+            const QuantMeta mine = make_step_meta(src, n, g > 0);
+            const auto params = kernels::make_params(mine, L.qtype);
+            txready[slot].clear();
+            for (size_t off = 0; off < n; off += piece_el) {
+                const size_t k = std::min(piece_el, n - off);
+                be->quantize(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
+                txready[slot].add(off * qs, (off + k) * qs, record(st));
+            }
+            if (g + 1 == ws && n > 0) // parity: own chunk := D(Q(x)), what every other peer de-quantizes
+                be->dequant_reduce(src, txq[slot], n, L.dtype, L.qtype, ReduceOp::Set, params, st);
+            if (int m = send_meta(io, mine, *L.tx)) return fail(m);
+            publish(g, txq[slot], &txready[slot]);
+        } // else: forwarded chunk, published with its metadata when step g-1's metadata arrived
+        fault_point("qring", seq, g, "meta");
+        if (int m = recv_meta(io, theirs, *L.rx, L.aborted, failed)) return fail(m);
+        const auto params = kernels::make_params(theirs, L.qtype);
+        if (!rs && g + 1 < nsteps) { // cut-through all-gather: the next step forwards this chunk as it lands
+            if (int m = send_meta(io, theirs, *L.tx)) return fail(m);
+            publish(g + 1, rxbuf[b], &rxready[b]);
+        }
+        uint8_t *region = L.dst + bounds[chunk_rx(g)].first * es;
+        DevEvent step_last = nullptr;
+        bool first = true;
+        const int rc = rx.receive(
+            g, qs, piece_el * qs,
+            [&](size_t a, size_t e) {
+                const size_t n = (e - a) / qs;
+                if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM
+                    be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, L.pq.h2d);
+                    be->stream_wait_event(st, record(L.pq.h2d));
+                    dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
+                } else { // forwardable at once; de-quantized straight from pinned memory
+                    rxready[b].add(a, e, nullptr);
+                    be->dequant_reduce(region + a / qs * es, rxbuf[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
+                                       st);
+                }
+                step_last = record(st);
+                if (first) {
+                    first = false;
+                    fault_point("qring", seq, g, "rx");
+                }
+            },
+            [&] {
+                if (g + 1 < nsteps && !rx.posted(g + 1) && can_post(g + 1)) post(g + 1);
+            },
+            failed, L.aborted);
+        buf_free[b] = step_last;
+        if (rc) return fail(rc);
+        *L.rx += nel(chunk_rx(g)) * qs;
+        rx.unpost(g);
+        step_mark(rs, rs ? g : g - (ws - 1));
+        fault_point("qring", seq, g, "end");
+    }
+    if (!senders.wait(nsteps - 1)) return fail(1);
+    return 0;
+}
+
+} // namespace
+
+std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    DeviceBackend *be = device_backend();
+    const ReduceRequest &q = op.req;
+    const size_t ws = rv.ring.size();
+    const size_t es = dtype_size(q.dtype), qs = dtype_size(q.qtype);
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    // value bytes per quantize / de-quantize piece (and frame): PCCL_QUANT_PIECE_BYTES, default 8 MiB
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_QUANT_PIECE_BYTES", 8u << 20)) / es * es;
+
+    be->set_device(device);
+    StreamLease stream(device);
+    DevStream st = stream.get();
+    if (!st) return {false, false};
+    const PcieQueues pq = shared_pcie_queues(be, device);
+    if (!pq.h2d) return {false, false};
+
+    Lease backup;
+    const bool keep_backup = q.src == q.dst && !q.scratch;
+    if (keep_backup) {
         backup = Lease(device_pool(), bytes, device);
         if (!backup.ok()) return {false, false};
         be->memcpy_async(backup.data(), q.src, bytes, st);
@@ -1450,347 +1670,30 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     } ev_back{be, st, ready};
     be->event_record(ready, st);
 
-    // Lanes: the buffer is split into PCCL_RING_LANES contiguous parts, each a complete ring all-reduce with its own
-    // tag (the op's tag with the lane number in bits 60-63), stream and staging rings; lane k+1 starts when lane k
-    // reaches its all-gather. The all-gather moves bytes host -> device only while a reduce-scatter moves them both
-    // ways, so overlapping lane k's all-gather with lane k+1's reduce-scatter keeps both PCIe directions busy.
-    const size_t lanes_req = std::max<size_t>(1, std::min<size_t>(4, env_size("PCCL_RING_LANES", 1)));
-    const size_t align_el = std::max<size_t>(1, 4096 / es);
-    size_t nl = lanes_req;
-    while (nl > 1 && q.count / nl < ws * piece / es) --nl; // every lane keeps >= one piece per chunk
-    std::vector<size_t> lo(nl + 1, 0);
-    for (size_t k = 1; k < nl; ++k) lo[k] = std::min(q.count, (q.count * k / nl) / align_el * align_el);
-    lo[nl] = q.count;
-    std::vector<LaneGate> gates(nl);
+    const std::vector<size_t> lo = quant_lane_bounds(q.count, ws, qs);
+    const size_t nl = lo.size() - 1;
     std::vector<std::unique_ptr<StreamLease>> lane_streams;
-    std::vector<Lane> lanes(nl);
     for (size_t k = 0; k < nl; ++k) {
         lane_streams.push_back(std::make_unique<StreamLease>(device));
         if (!lane_streams.back()->get()) return {false, false};
-        Lane &L = lanes[k];
-        L.txs = &rv.tx;
-        L.rxs = &rv.rx;
-        L.ws = ws;
-        L.rank = rank;
-        L.tag = q.tag ^ (static_cast<uint64_t>(k) << 60);
-        L.seq = seq;
-        L.be = be;
-        L.pq = pq;
-        L.st = lane_streams.back()->get();
-        L.ready = ready;
-        L.src = static_cast<const uint8_t *>(q.src) + lo[k] * es;
-        L.dst = dst + lo[k] * es;
-        L.count = lo[k + 1] - lo[k];
-        L.es = es;
-        L.piece = piece;
-        L.dtype = q.dtype;
-        L.rop = q.op;
-        L.device = device;
-        L.ahead = env_size("PCCL_RING_SEND_AHEAD", 1) != 0;
-        // step-0 payload (own input chunk -> pinned): on the process-wide D2H copy queue (default; FIFO across the
-        // peers of this process) or on the lane's stream (PCCL_RING_STEP0_OP_STREAM=1: blit kernels, per-peer copies
-        // run concurrently). 8 peers x 1 GiB, 32 MiB pieces, 3 runs each: queue 358 / 337 / 341 ms, op stream 331 /
-        // 429 / 388 ms (profiles/r3/ring_ab/summary.txt).
-        L.step0_on_op_stream = env_size("PCCL_RING_STEP0_OP_STREAM", 0) != 0;
-        // (the CPU produces the same bits as the kernel, so peers may differ in this setting)
-        const char *hr = std::getenv("PCCL_RING_HOST_REDUCE");
-        L.host_frac = hr ? std::max(0.0, std::min(1.0, std::atof(hr))) : 0.0;
-        // the all-gather's received chunks go to HBM as copies on the lane stream (ROCclr blit kernels reading pinned
-        // memory, one per peer in parallel) instead of the shared copy-engine queue, which one stream drives at
-        // ~47 GB/s: interleaved A/B, 8 peers x 1 GiB, median of 6-8 windows: 347 vs 376 ms and 337 vs 342 ms on two
-        // boxes (profiles/r3/h2d_modes/). The reduce-scatter keeps the copy engine (blit: 366 ms, zero-copy reduce
-        // from pinned: 347 ms, copy engine: 337 ms). PCCL_RING_AG_KERNEL_COPY=0 / PCCL_RING_RS_H2D=1|2 for A/B.
-        L.ag_on_lane_stream = env_size("PCCL_RING_AG_KERNEL_COPY", 1) != 0;
-        L.rs_h2d = static_cast<int>(std::min<size_t>(2, env_size("PCCL_RING_RS_H2D", 0)));
-        // PCCL_RING_SHARED_REDUCE=1: the fused reduce-scatter kernels of all device-ring ops of this process on one
-        // stream per GPU (the kernels' pinned writes are the device->host traffic of the ring: one writer at a time
-        // instead of one per peer). Copy-engine reduce-scatter H2D with the all-gather on the lane stream only.
-        L.shared_reduce = env_size("PCCL_RING_SHARED_REDUCE", 0) != 0 && L.rs_h2d == 0 && L.host_frac == 0 &&
-                          L.ag_on_lane_stream;
-        L.ag_copy_grid = static_cast<int>(std::min<size_t>(4096, env_size("PCCL_RING_AG_COPY_GRID", 0)));
-        L.shared_ag = L.shared_reduce && env_size("PCCL_RING_SHARED_AG", 0) != 0;
-        L.wait_gate = k > 0 ? &gates[k - 1] : nullptr;
-        L.open_gate = k + 1 < nl ? &gates[k] : nullptr;
-        L.aborted = [this, t = q.tag] { return abort_received(t); };
-        L.tx = &op.tx;
-        L.rx = &op.rx;
-        L.main_lane = k == 0;
     }
-    if (nl == 1) {
-        run_lane(lanes[0]);
-    } else {
-        std::vector<std::thread> th;
-        for (size_t k = 1; k < nl; ++k) th.emplace_back([&, k] {
-            name_thread("pccl-ring-lane");
-            run_lane(lanes[k]);
-        });
-        run_lane(lanes[0]);
-        for (auto &t : th) t.join();
-    }
-    int rc = 0;
-    for (const auto &L : lanes) rc = std::max(rc, L.rc); // abort (2) outranks an io failure (1)
+    OpAbort aborted([this, t = q.tag] { return abort_received(t); });
+    std::atomic<bool> op_failed{false};
+    const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
+        QLane L{&rv.tx, &rv.rx, ws, rv.rank, lane_tag(q.tag, k), seq, be, pq, lane_streams[k]->get(), ready,
+                dst + a * es, b - a, es, qs, piece / es, q.dtype, q.qtype, q.qalgo, q.op, device,
+                [&] { return aborted(); }, &op.tx, &op.rx, &op_failed};
+        return device_quant_lane(L);
+    });
     if (rc != 0) {
-        be->stream_sync(st);
-        if (q.src == q.dst && !q.scratch) { // every lane drained: restore the caller's buffer
+        be->stream_sync(st); // every lane drained its own stream before returning
+        if (keep_backup) {
             be->memcpy_async(dst, backup.data(), bytes, st);
             be->stream_sync(st);
         }
         return {rc == 2, rc == 2};
     }
-    if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
-    if (!be->stream_sync(st)) return {false, false};
-    return {true, false};
-}
-
-// Quantized device ring: per ring step the owner reduces min/max of its outgoing chunk on the GPU (the metadata
-// packet needs them on the host), then quantizes the chunk piece by piece straight into pinned memory; each piece
-// is sent as soon as its quantize kernel has finished. The receiver de-quantizes + reduces from pinned memory (the
-// wire bytes are 2-4x smaller than the values, so PCIe is not the bound here; the network is).
-std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device) {
-    DeviceBackend *be = device_backend();
-    const ReduceRequest &q = op.req;
-    const size_t ws = rv.ring.size(), rank = rv.rank;
-    const size_t es = dtype_size(q.dtype);
-    const size_t qs = dtype_size(q.qtype);
-    auto *dst = static_cast<uint8_t *>(q.dst);
-    const size_t bytes = q.count * es;
-    // value bytes per quantize / de-quantize piece: PCCL_QUANT_PIECE_BYTES, else PCCL_DEVICE_PIECE_BYTES, else 8 MiB
-    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_QUANT_PIECE_BYTES",
-                                                            env_size("PCCL_DEVICE_PIECE_BYTES", 8u << 20))) / es * es;
-    const size_t piece_el = piece / es; // quantized pieces hold the same elements
-
-    be->set_device(device);
-    StreamLease stream(device);
-    DevStream st = stream.get();
-    if (!st) return {false, false};
-
-    StepIo io{rv.tx[seq % rv.tx.size()].get(), rv.rx[seq % rv.rx.size()].get(), q.tag, seq};
-    auto aborted = [&] { return abort_received(q.tag); };
-
-    Lease backup;
-    if (q.src == q.dst && !q.scratch) {
-        backup = Lease(device_pool(), bytes, device);
-        if (!backup.ok()) return {false, false};
-        be->memcpy_async(backup.data(), q.src, bytes, st);
-    } else if (q.src != q.dst) {
-        be->memcpy_async(dst, q.src, bytes, st);
-    }
-    auto restore = [&] {
-        be->stream_sync(st);
-        if (q.src == q.dst && !q.scratch) {
-            be->memcpy_async(dst, backup.data(), bytes, st);
-            be->stream_sync(st);
-        }
-    };
-
-    const auto bounds = chunk_bounds(q.count, ws);
-    size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
-    const size_t stage_bytes = max_chunk * qs + 64;
-    Lease txbuf(pinned_pool(), stage_bytes), rxa(pinned_pool(), stage_bytes), rxb(pinned_pool(), stage_bytes);
-    Lease mm(pinned_pool(), 64);
-    if (!txbuf.ok() || !rxa.ok() || !rxb.ok() || !mm.ok()) return {false, false};
-    uint8_t *rxbuf[2] = {rxa.data(), rxb.data()};
-    auto *minmax_out = reinterpret_cast<double *>(mm.data());
-
-    std::vector<DevEvent> events;
-    auto ev = [&](size_t i) {
-        while (events.size() <= i) events.push_back(event_pool().get());
-        return events[i];
-    };
-    // Received quantized pieces are copied to HBM on the process's shared copy-engine queue and the de-quantize kernels
-    // read them there (PCCL_QUANT_RX_STAGE=0: the kernels read pinned memory over PCIe themselves), like the
-    // unquantized ring. Interleaved A/B, uint8, 8 peers x 1 GiB: 249 vs 256 ms and 245 vs 244 ms on two boxes
-    // (profiles/r3/quant_fused/ab_rx_stage*.jsonl): the same PCIe bytes either way.
-    const bool rx_stage = env_size("PCCL_QUANT_RX_STAGE", 1) != 0;
-    Lease dva, dvb;
-    uint8_t *rxdev[2] = {nullptr, nullptr};
-    PcieQueues pq;
-    if (rx_stage) {
-        dva = Lease(device_pool(), stage_bytes, device);
-        dvb = Lease(device_pool(), stage_bytes, device);
-        pq = shared_pcie_queues(be, device);
-        if (!dva.ok() || !dvb.ok() || !pq.h2d[0]) return {false, false};
-        rxdev[0] = dva.data();
-        rxdev[1] = dvb.data();
-    }
-    std::vector<DevEvent> copy_events; // the staging copies (each waited for by the op stream before its kernel)
-    struct EvGuard { // drains the op's stream before its events / staging buffers are recycled
-        DeviceBackend *be;
-        DevStream s;
-        std::vector<DevEvent> *e, *c;
-        ~EvGuard() {
-            be->stream_sync(s);
-            for (auto x : *e) event_pool().put(x);
-            for (auto x : *c) event_pool().put(x);
-        }
-    } eg{be, st, &events, &copy_events};
-    // where the kernels read received quantized elements [a, b) of `sink` (after queueing their copy when staging)
-    auto rx_src = [&](uint8_t *sink, size_t a, size_t b) -> const uint8_t * {
-        if (!rx_stage) return sink + a * qs;
-        uint8_t *d = rxdev[sink == rxbuf[0] ? 0 : 1] + a * qs;
-        be->memcpy_async(d, sink + a * qs, (b - a) * qs, pq.h2d[0]);
-        DevEvent e = event_pool().get();
-        copy_events.push_back(e);
-        be->event_record(e, pq.h2d[0]);
-        be->stream_wait_event(st, e);
-        return d;
-    };
-
-    // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
-    // (dequant_reduce_minmax) into `mmp`: the chunk a step receives is the chunk the next step quantizes (and the last
-    // step's is the all-gather's first payload), so its min / max is one fold of those partials instead of a second
-    // pass over the chunk. PCCL_QUANT_FUSED_MINMAX=0 turns it off; a step whose launches do not fit the partials
-    // buffer falls back to the separate min / max pass.
-    const bool fuse_mm = env_size("PCCL_QUANT_FUSED_MINMAX", 1) != 0;
-    constexpr int kMmSlots = 65536, kMmMinRoom = 64; // 1 MiB of partials: ~1 GiB bf16 chunks
-    Lease mmp;
-    if (fuse_mm) mmp = Lease(device_pool(), kMmSlots * 2 * sizeof(double), device);
-    auto *mm_partials = mmp.ok() ? reinterpret_cast<double *>(mmp.data()) : nullptr;
-    int mm_used = 0;
-    bool mm_complete = false; // the partials cover every element of the chunk consumed by the last step
-    auto dequant_consume = [&](uint8_t *dst_el, const uint8_t *src_q, size_t n, ReduceOp rop,
-                               const kernels::QuantParams &params) {
-        int blocks = 0;
-        if (mm_complete && mm_partials && kMmSlots - mm_used >= kMmMinRoom &&
-            be->dequant_reduce_minmax(dst_el, src_q, n, q.dtype, q.qtype, rop, params, mm_partials + 2 * mm_used,
-                                      kMmSlots - mm_used, &blocks, st)) {
-            mm_used += blocks;
-            return;
-        }
-        mm_complete = false;
-        be->dequant_reduce(dst_el, src_q, n, q.dtype, q.qtype, rop, params, st);
-    };
-
-    // min/max of `n` elements at device `src` (one host round trip: the meta packet carries them) - folded from the
-    // previous step's partials when `fused` and they are complete - then the quantize kernels of every piece into
-    // pinned txbuf, each followed by an event that releases the piece to the senders
-    auto quantize_to_pinned = [&](const uint8_t *src, size_t n, bool fused) -> QuantMeta {
-        const bool fold = fused && mm_complete && mm_partials;
-        const int folded = mm_used;
-        mm_used = 0;
-        mm_complete = mm_partials != nullptr; // the next step's consumes start collecting afresh
-        if (n == 0) return kernels::make_meta(q.qalgo, q.dtype, q.qtype, 0, 0);
-        if (fold) {
-            g_quant_minmax_folds.fetch_add(1, std::memory_order_relaxed);
-            be->minmax_fold(mm_partials, folded, n, minmax_out, st);
-        } else {
-            g_quant_minmax_passes.fetch_add(1, std::memory_order_relaxed);
-            be->minmax(src, n, q.dtype, minmax_out, st);
-        }
-        be->stream_sync(st);
-        QuantMeta m = kernels::make_meta(q.qalgo, q.dtype, q.qtype, minmax_out[0], minmax_out[1]);
-        const auto params = kernels::make_params(m, q.qtype);
-        size_t k = 0;
-        for (size_t off = 0; off < n; off += piece_el, ++k) {
-            be->quantize(txbuf.data() + off * qs, src + off * es, std::min(piece_el, n - off), q.dtype, q.qtype, params,
-                         st);
-            be->event_record(ev(k), st);
-        }
-        return m;
-    };
-    auto quant_ready = [&](size_t end) { return end == 0 || event_wait_polling(be, ev((end - 1) / (piece_el * qs))); };
-    auto always_ready = [](size_t) { return true; };
-
-    // No stream synchronisation per step: the reduce-scatter's next quantization reads its min / max after the
-    // previous step's de-quantize kernels in stream order (quantize_to_pinned syncs once for the meta packet), and an
-    // all-gather step's received bytes are de-quantized asynchronously while the next step forwards them. A pinned
-    // sink is refilled two steps later, so step s waits only for the kernels that read its sink at step s-2.
-    DevEvent sink_read[2] = {nullptr, nullptr};
-    struct SinkEvents { // back to the pool once the op's stream is drained
-        DeviceBackend *be;
-        DevStream s;
-        DevEvent e[2];
-        ~SinkEvents() {
-            be->stream_sync(s);
-            for (auto x : e) event_pool().put(x);
-        }
-    } sink_events{be, st, {event_pool().get(), event_pool().get()}};
-    // PCCL_QUANT_EARLY_SINKS=1: the data stripes other than stripe 0 (whose connection carries the metadata packet)
-    // take their receive sinks before the step waits for the peer's metadata (see striped_step). Interleaved A/B,
-    // uint8, 8 peers x 1 GiB: 234.3 vs 233.1 ms (profiles/r3/quant_fused/ab_early_sinks.jsonl), so off by default.
-    const bool early_sinks = env_size("PCCL_QUANT_EARLY_SINKS", 0) != 0;
-    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, const std::function<bool(size_t)> &tx_ready,
-                        uint8_t *sink, size_t rx_bytes, const std::function<void(size_t, size_t)> &consume,
-                        const std::function<int()> &before_rx) -> int {
-        const int b = sink == rxbuf[0] ? 0 : 1;
-        if (sink_read[b]) event_wait_polling(be, sink_read[b]);
-        const int rc = striped_step(rv.tx, rv.rx, q.tag, seq, payload, tx_bytes, tx_ready, sink, rx_bytes, qs,
-                                    piece_el * qs, consume, aborted, op.tx, op.rx, before_rx, piece_el * qs,
-                                    early_sinks ? 1 : SIZE_MAX);
-        if (rc == 0) {
-            sink_read[b] = sink_events.e[b]; // waited for above before it is recorded again
-            be->event_record(sink_read[b], st);
-        }
-        return rc;
-    };
-    auto fail = [&](int code) -> std::pair<bool, bool> {
-        restore();
-        return {code == 2, code == 2};
-    };
-    auto meta_then = [&](QuantMeta &theirs, kernels::QuantParams &params) {
-        return [&, pt = &theirs, pp = &params] {
-            const int m = recv_meta(io, *pt, op.rx, aborted);
-            if (m == 0) *pp = kernels::make_params(*pt, q.qtype);
-            return m;
-        };
-    };
-
-    // ---- reduce-scatter
-    for (size_t step = 0; step + 1 < ws; ++step) {
-        const size_t tx_idx = (rank + ws - step) % ws, rx_idx = (rank + ws - step - 1) % ws;
-        const auto [ts, te] = bounds[tx_idx];
-        const auto [rs, re] = bounds[rx_idx];
-        uint8_t *rx_region = dst + rs * es;
-        uint8_t *sink = rxbuf[step % 2];
-        QuantMeta theirs;
-        kernels::QuantParams params{};
-        // step > 0: this chunk was produced by the previous step's de-quantize-reduce (fused min / max partials)
-        const QuantMeta mine = quantize_to_pinned(dst + ts * es, te - ts, step > 0);
-        if (int m = send_meta(io, mine, op.tx)) return fail(m);
-        const int rc = run_step(txbuf.data(), (te - ts) * qs, quant_ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-            dequant_consume(rx_region + a * es, rx_src(sink, a, b), b - a, q.op, params);
-        }, meta_then(theirs, params));
-        if (rc) return fail(rc);
-        step_mark(true, step);
-    }
-
-    trace_mark("reduce_scatter");
-    // ---- all-gather: the owner quantizes its finished chunk once and overwrites its own copy with D(Q(x)) (every
-    // peer ends bit-identical); received quantized chunks are forwarded verbatim
-    QuantMeta prev_meta;
-    size_t cur = (rank + 1) % ws;
-    for (size_t step = 0; step + 1 < ws; ++step) {
-        const size_t inc = (cur + ws - 1) % ws;
-        const auto [ts, te] = bounds[cur];
-        const auto [rs, re] = bounds[inc];
-        uint8_t *rx_region = dst + rs * es;
-        uint8_t *sink = rxbuf[step % 2];
-        const uint8_t *payload;
-        QuantMeta mine, theirs;
-        std::function<bool(size_t)> ready = always_ready;
-        if (step == 0) {
-            mine = quantize_to_pinned(dst + ts * es, te - ts, true); // the reduce-scatter's last received chunk
-            if (te > ts) // parity: own chunk := D(Q(x))
-                be->dequant_reduce(dst + ts * es, txbuf.data(), te - ts, q.dtype, q.qtype, ReduceOp::Set,
-                                   kernels::make_params(mine, q.qtype), st);
-            payload = txbuf.data();
-            ready = quant_ready;
-        } else {
-            mine = prev_meta;
-            payload = rxbuf[(step - 1) % 2];
-        }
-        if (int m = send_meta(io, mine, op.tx)) return fail(m);
-        kernels::QuantParams params{};
-        const int rc = run_step(payload, (te - ts) * qs, ready, sink, (re - rs) * qs, [&](size_t a, size_t b) {
-            be->dequant_reduce(rx_region + a * es, rx_src(sink, a, b), b - a, q.dtype, q.qtype, ReduceOp::Set, params,
-                               st);
-        }, meta_then(theirs, params));
-        prev_meta = theirs;
-        if (rc) return fail(rc);
-        step_mark(false, step);
-        cur = inc;
-    }
+    // the lanes' streams are drained (each lane's Drain): the result is complete in HBM
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
     if (!be->stream_sync(st)) return {false, false};
     return {true, false};

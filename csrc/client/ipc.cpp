@@ -128,8 +128,9 @@ struct OpCtx {
 // outputs, [2] staged inputs, [3] staged outputs
 // [0..3] direct_in, direct_out, staged_in, staged_out; [4] comm buffers quarantined after an abort; [5] drains that
 // waited for a dead peer's threads to finish tearing down its address space; [6] / [7] cross-GPU pre-flight probes
-// failed / passed
-static std::atomic<uint64_t> g_buf_stats[8];
+// failed / passed; [8] quarantined buffers reclaimed (no peer can still touch them); [9] quarantined VMM buffers
+// freed beyond the quarantine cap
+static std::atomic<uint64_t> g_buf_stats[10];
 
 // per-process bookkeeping
 static std::mutex g_ctx_mtx;
@@ -330,8 +331,12 @@ IpcArena::~IpcArena() {
     if (shm_) munmap(shm_, shm_bytes_);
 }
 
+static bool pid_alive(int pid);
+static bool pid_quiesced(int pid);
+
 IpcArena::CommBuf *IpcArena::acquire_buffer(size_t bytes, int device) {
     std::lock_guard l(mtx_);
+    reclaim_quarantined_locked();
     CommBuf *best = nullptr;
     for (auto &b : bufs_)
         if (!b->busy && b->device == device && b->cap >= bytes && (!best || b->cap < best->cap)) best = b.get();
@@ -410,12 +415,64 @@ void IpcArena::release_buffer(CommBuf *b) {
     if (!b->quarantined) b->busy = false;
 }
 
-void IpcArena::quarantine_buffer(CommBuf *b) {
+void IpcArena::quarantine_buffer(CommBuf *b, uint64_t seq) {
     if (!b) return;
     std::lock_guard l(mtx_);
     if (!b->quarantined) ++g_buf_stats[4];
     b->quarantined = true;
+    b->qseq = seq;
     b->busy = true;
+}
+
+bool IpcArena::op_quiet(uint64_t seq) const {
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        if (k == rank_) continue;
+        if (!pid_alive(pids_[k])) {
+            if (!pid_quiesced(pids_[k])) return false;
+            continue;
+        }
+        const uint64_t v = shm_->op(slot, static_cast<uint32_t>(k))->phase.load(std::memory_order_acquire);
+        const uint64_t vs = v >> 8;
+        const uint32_t vp = static_cast<uint32_t>(v & 0xff);
+        if (vs == seq + 1 && vp != PH_GATHERED && vp != PH_RELEASED && vp != PH_ABORTED) return false;
+    }
+    return true;
+}
+
+void IpcArena::reclaim_quarantined_locked() {
+    constexpr size_t kQuarantineCapBytes = size_t{8} << 30;
+    size_t held = 0;
+    for (auto &b : bufs_) {
+        if (!b->quarantined) continue;
+        if (op_quiet(b->qseq)) {
+            b->quarantined = false;
+            b->busy = false;
+            ++g_buf_stats[8];
+        } else {
+            held += b->cap;
+        }
+    }
+    if (held <= kQuarantineCapBytes) return;
+    DeviceBackend *be = device_backend();
+    const int cur = be->current_device();
+    for (auto it = bufs_.begin(); it != bufs_.end() && held > kQuarantineCapBytes;) {
+        CommBuf *b = it->get();
+        const bool vmm = std::all_of(b->share_ids.begin(), b->share_ids.end(), [](uint64_t id) { return id != 0; });
+        if (!b->quarantined || !vmm) {
+            ++it;
+            continue;
+        }
+        be->set_device(b->device);
+        for (size_t k = 0; k < b->segs.size(); ++k) {
+            VmmShare::instance().retract(b->share_ids[k]);
+            be->vmm_free(b->segs[k]);
+        }
+        held -= b->cap;
+        ++g_buf_stats[9];
+        it = bufs_.erase(it);
+    }
+    if (cur >= 0) be->set_device(cur);
 }
 
 void *IpcArena::pin_mapping(int peer, const uint8_t *handle, int my_device, MapKey &key) {
@@ -659,17 +716,8 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
 }
 
 namespace {
-// PCCL_IPC_COPY=memcpy: staged copies with hipMemcpyAsync instead of the copy kernel
-bool copy_with_memcpy() {
-    static const bool m = [] {
-        const char *v = std::getenv("PCCL_IPC_COPY");
-        return v && std::strcmp(v, "memcpy") == 0;
-    }();
-    return m;
-}
-
-// staged comm buffer segments <-> a contiguous device buffer (copies on `st`, not synchronised). By default the
-// copies run as a kernel (same-device kernel -> kernel ordering on one stream, no copy-engine path for VMM memory).
+// staged comm buffer segments <-> a contiguous device buffer (copies on `st`, not synchronised), as a kernel:
+// same-device kernel -> kernel ordering on one stream, no copy-engine path for VMM memory.
 bool copy_staged(DeviceBackend *be, const std::vector<void *> &segs, uint8_t *user, size_t bytes, bool to_user,
                  DevStream st) {
     for (size_t k = 0, off = 0; off < bytes; ++k, off += kIpcSegBytes) {
@@ -678,9 +726,7 @@ bool copy_staged(DeviceBackend *be, const std::vector<void *> &segs, uint8_t *us
         void *d = to_user ? static_cast<void *>(user + off) : static_cast<void *>(seg);
         const void *s = to_user ? static_cast<const void *>(seg) : static_cast<const void *>(user + off);
         const size_t zero = 0;
-        if (!(copy_with_memcpy() ? be->memcpy_async(d, s, n, st)
-                                 : be->multi_gather(d, &s, &zero, &n, 1, -1, DType::U8, st)))
-            return false;
+        if (!be->multi_gather(d, &s, &zero, &n, 1, -1, DType::U8, st)) return false;
     }
     return true;
 }
@@ -774,6 +820,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     mine->bytes = bytes;
     mine->dtype = static_cast<uint32_t>(dtype);
     mine->op = static_cast<uint32_t>(op);
+    fault_stall("ipc_vote", seq);
     set_phase(seq, PH_VOTED);
     fault_point("ipc_vote", seq);
 
@@ -789,8 +836,8 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
                 be->stream_sync(stream.get());
         }
         unpin_mappings(pins);
-        quarantine_buffer(inb);
-        quarantine_buffer(outb);
+        quarantine_buffer(inb, seq);
+        quarantine_buffer(outb, seq);
         return code;
     };
     const int rc = barrier(c, tag, seq, PH_VOTED);
@@ -974,8 +1021,8 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         }
         unpin_mappings(ctx.pins);
         if (rc != 0) { // peers may have written into them for this op: never reissued (drain_peers is bounded)
-            quarantine_buffer(inb);
-            quarantine_buffer(outb);
+            quarantine_buffer(inb, seq);
+            quarantine_buffer(outb, seq);
         } else {
             release_buffer(inb);
             release_buffer(outb);

@@ -131,13 +131,21 @@ private:
         size_t cap = 0;
         int device = -1;
         bool busy = false;
-        bool quarantined = false; // written by an aborted op: never handed out again (freed with the arena)
+        bool quarantined = false; // used by aborted op `qseq`: not handed out again until reclaimed
+        uint64_t qseq = 0;
     };
     CommBuf *acquire_buffer(size_t bytes, int device);
     void release_buffer(CommBuf *b);
-    // after an abort: the buffer stays busy for the rest of the arena's life, so a late write of a peer that the
-    // drain could not prove finished lands in memory no later op uses
-    void quarantine_buffer(CommBuf *b);
+    // After an abort: the buffer stays busy, so a late write of a peer that the abort drain could not prove finished
+    // lands in memory no later op uses. acquire_buffer reclaims it once no ring member can still touch it for that op
+    // (op_quiet), and frees quarantined VMM buffers beyond kQuarantineCapBytes (a VMM importer holds its own
+    // reference to the pages, so a late write lands in memory nobody reads).
+    void quarantine_buffer(CommBuf *b, uint64_t seq);
+    void reclaim_quarantined_locked();
+    // every other ring member is provably past op `seq`: its phase word shows a later op in that slot, or the op at
+    // PH_GATHERED / PH_RELEASED / PH_ABORTED, or no vote for it yet (it then sees my PH_ABORTED and never launches);
+    // a dead member's threads have all left its address space (pid_quiesced)
+    bool op_quiet(uint64_t seq) const;
     struct Mapping {
         void *ptr = nullptr;
         bool vmm = false;  // imported VMM allocation (unmap) vs hipIpc mapping (close)

@@ -60,8 +60,6 @@ DeviceBackend *device_backend() {
 bool device_backend_available() { return device_backend() != nullptr; }
 
 bool event_wait_polling(DeviceBackend *be, DevEvent e) {
-    static const bool poll = env_size("PCCL_EVENT_POLL", 1) != 0;
-    if (!poll) return be->event_sync(e);
     unsigned us = 2;
     while (true) {
         const int r = be->event_query(e);

@@ -132,7 +132,7 @@ public:
 // Waits for `e` by polling with short sleeps (2 us doubling to 100 us) instead of the runtime's synchronize, which
 // busy-waits: the device ring's sender / op threads wait on staging copies for milliseconds at a time, and the
 // loopback-TCP ring is CPU-bound (kernel socket copies on the box's CPU share, bench extra cpu_cores_busy_rank0), so
-// every spinning waiter takes a core from the socket copies. PCCL_EVENT_POLL=0 restores event_sync.
+// every spinning waiter takes a core from the socket copies.
 bool event_wait_polling(DeviceBackend *be, DevEvent e);
 
 // Returns the process-wide backend (nullptr if HIP is unavailable). Loaded lazily and thread-safely.

@@ -15,6 +15,7 @@
 #include <random>
 #include <string>
 #include <unistd.h>
+#include <vector>
 
 namespace pccl {
 
@@ -119,16 +120,51 @@ SockAddrKey SockAddrKey::of(const SockAddr &a) {
     return k;
 }
 
-void fault_point(const char *point, uint64_t seq) {
-    static const std::string spec = [] {
+namespace {
+struct FaultSpec {
+    std::string point, phase;
+    uint64_t seq = 0;
+    size_t step = SIZE_MAX; // SIZE_MAX: any
+    bool armed = false;
+};
+const FaultSpec &fault_spec() {
+    static const FaultSpec s = [] {
+        FaultSpec f;
         const char *e = std::getenv("PCCL_FAULT_INJECT");
-        return std::string(e ? e : "");
+        if (!e || !*e) return f;
+        std::vector<std::string> parts;
+        std::string cur;
+        for (const char *p = e;; ++p) {
+            if (*p == ':' || *p == 0) {
+                parts.push_back(cur);
+                cur.clear();
+                if (*p == 0) break;
+            } else {
+                cur += *p;
+            }
+        }
+        if (parts.size() < 2) return f;
+        f.point = parts[0];
+        f.seq = std::strtoull(parts[1].c_str(), nullptr, 10);
+        if (parts.size() > 2 && !parts[2].empty()) f.step = std::strtoull(parts[2].c_str(), nullptr, 10);
+        if (parts.size() > 3) f.phase = parts[3];
+        f.armed = true;
+        return f;
     }();
-    if (spec.empty()) return;
-    const size_t colon = spec.rfind(':');
-    if (colon == std::string::npos || spec.compare(0, colon, point) != 0) return;
-    if (std::strtoull(spec.c_str() + colon + 1, nullptr, 10) != seq) return;
-    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu\n", point, static_cast<unsigned long long>(seq));
+    return s;
+}
+} // namespace
+
+bool fault_injection_armed() { return fault_spec().armed; }
+
+void fault_point(const char *point, uint64_t seq, size_t step, const char *phase) {
+    const FaultSpec &f = fault_spec();
+    if (!f.armed || f.seq != seq || f.point != point) return;
+    if (f.step != SIZE_MAX && f.step != step) return;
+    if (!f.phase.empty() && (phase == nullptr || f.phase != phase)) return;
+    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu step %lld phase %s\n", point,
+                 static_cast<unsigned long long>(seq), step == SIZE_MAX ? -1ll : static_cast<long long>(step),
+                 phase ? phase : "-");
     std::fflush(stderr);
     if (const char *d = std::getenv("PCCL_FAULT_INJECT_DELAY_MS")) // die a little later (the point's work goes on)
         std::thread([ms = std::atol(d)] {
@@ -137,6 +173,17 @@ void fault_point(const char *point, uint64_t seq) {
         }).detach();
     else
         ::kill(::getpid(), SIGKILL);
+}
+
+void fault_stall(const char *point, uint64_t seq) {
+    static const char *spec = std::getenv("PCCL_FAULT_STALL");
+    if (!spec || !*spec) return;
+    const char *c1 = std::strchr(spec, ':');
+    if (!c1 || std::strncmp(spec, point, static_cast<size_t>(c1 - spec)) != 0 || point[c1 - spec] != 0) return;
+    char *end = nullptr;
+    const unsigned long long max_seq = std::strtoull(c1 + 1, &end, 10);
+    if (!end || *end != ':' || seq > max_seq) return;
+    ::usleep(static_cast<useconds_t>(std::atol(end + 1)) * 1000);
 }
 
 void fault_delay(uint64_t tag) {

@@ -92,10 +92,17 @@ struct SockAddrKeyHash {
 size_t env_size(const char *name, size_t dflt);
 bool env_flag(const char *name, bool dflt);
 
-// Fault injection for the crash tests: PCCL_FAULT_INJECT="<point>:<seq>" makes this process SIGKILL itself when it
-// reaches `point` in the op with master sequence number `seq` (points: ipc_vote, ipc_kernel, ring_step). Lets a test
-// kill a peer at an exact protocol position, e.g. while its xGMI push kernel and its peers' kernels are running.
-void fault_point(const char *point, uint64_t seq);
+// Fault injection for the crash tests: PCCL_FAULT_INJECT="<point>:<seq>[:<step>[:<phase>]]" makes this process
+// SIGKILL itself when it reaches `point` in the op with master sequence number `seq` (and, if given, at ring step
+// `step` (global step index 0 .. 2(W-1)-1, all-gather steps after the reduce-scatter's) in phase `phase`). Points:
+// ipc_vote, ipc_kernel, ss_serve; ring (device ring; phases publish / rx / ahead / end) and qring (quantized device
+// ring; phases meta / rx / end). Lets a test kill a peer at an exact protocol position, e.g. while its xGMI push kernel
+// and its peers' kernels are running or while the next ring step's receive sinks are already posted.
+void fault_point(const char *point, uint64_t seq, size_t step = SIZE_MAX, const char *phase = nullptr);
+bool fault_injection_armed();
+// PCCL_FAULT_STALL="<point>:<max_seq>:<ms>": ops with sequence number <= max_seq sleep `ms` at `point` (tests: a slow
+// peer makes its partners' barriers time out, so ops abort while the ring membership stays the same)
+void fault_stall(const char *point, uint64_t seq);
 // PCCL_FAULT_DELAY="<tag>:<ms>[,*:<ms>]": an op with that tag (or any tag, "*") sleeps before it initiates
 // (scheduler tests: a slow op among fast ones).
 void fault_delay(uint64_t tag);

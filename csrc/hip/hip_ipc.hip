@@ -41,17 +41,15 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
             bool ok = true;
             if (nvec > 0) {
                 // 512 workgroups (2 per CU) and 2 vectors per thread measured best on MI355X for one kernel per GPU
-                // (profiles/r1_ipc_grid_sweep.md); concurrent peers on one GPU pass a smaller budget. PCCL_IPC_GRID /
-                // PCCL_IPC_UNROLL (2 or 4) override both for tuning sweeps.
+                // (profiles/r1_ipc_grid_sweep.md); concurrent peers on one GPU pass a smaller budget. PCCL_IPC_GRID
+                // overrides the budget (8-GPU tuning).
                 // Single destination (two-shot / hierarchical host-local reduce) uses k_multi_reduce_tile (contiguous
                 // tile per workgroup, non-temporal loads, 4 vectors per thread): 8 srcs -> 1 dst 5000 -> 5586 GB/s.
                 // The multi-destination push keeps the strided kernel (2 -> 2: 5420 vs 5080 GB/s tiled);
-                // profiles/r1_ipc_tiled.md. PCCL_IPC_TILED=0/1 forces either kernel for tuning sweeps.
+                // profiles/r1_ipc_tiled.md.
                 static const int env_grid = env_int("PCCL_IPC_GRID", 0);
-                static const int env_tiled = env_int("PCCL_IPC_TILED", -1);
-                const bool tiled = env_tiled >= 0 ? env_tiled != 0 : ndst == 1;
-                static const int env_unroll = env_int("PCCL_IPC_UNROLL", 0);
-                const int unroll = env_unroll == 2 || env_unroll == 4 ? env_unroll : (tiled ? 4 : 2);
+                const bool tiled = ndst == 1;
+                const int unroll = tiled ? 4 : 2;
                 const int max_grid = env_grid > 0 ? env_grid : (max_grid_hint > 0 ? max_grid_hint : 512);
                 const int grid = std::max(1, std::min(grid_for(nvec, unroll), max_grid));
                 ok = launch_ok([&] {

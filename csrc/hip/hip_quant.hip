@@ -51,14 +51,12 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
                         else k_dq_minmax<E, O, Q, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
                     });
                 }
-                if constexpr (sizeof(Q) <= 4) {
-                    if (p.algo == QuantAlgo::ZeroPointScale) {
-                        const int grid = grid_of(grid_for(count, pl.vec ? V : 1));
-                        return launch_ok([&] {
-                            if (mm) k_dq_zps<E, O, Q, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
-                            else k_dq_zps<E, O, Q, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
-                        });
-                    }
+                if (p.algo == QuantAlgo::ZeroPointScale) {
+                    const int grid = grid_of(grid_for(count, pl.vec ? V : 1));
+                    return launch_ok([&] {
+                        if (mm) k_dq_zps<E, O, Q, true><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                        else k_dq_zps<E, O, Q, false><<<grid, kBlock, 0, st>>>(d, q, count, p, pl.head, pl.vec, mm);
+                    });
                 }
                 return false;
             });
@@ -93,10 +91,8 @@ bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DT
             if (p.algo == QuantAlgo::MinMax)
                 return launch_ok(
                     [&] { k_q_minmax<E, Q><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
-            if constexpr (sizeof(Q) <= 4) {
-                if (p.algo == QuantAlgo::ZeroPointScale)
-                    return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
-            }
+            if (p.algo == QuantAlgo::ZeroPointScale)
+                return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
             return false;
         });
     });

@@ -37,14 +37,7 @@ bool launch_reduce_copy(void *dst, const void *src, void *out, size_t count, DTy
             using S = typename E::S;
             constexpr int V = vec_width<S>();
             const EwPlan pl = plan_ew<V>(count, {{dst, sizeof(S)}, {src, sizeof(S)}, {out, sizeof(S)}});
-            // PCCL_REDUCE_COPY_GRID caps the workgroups writing the pinned copy (the device->host bytes of the ring:
-            // PCIe carries more in both directions together with few concurrent writers, profiles/r2/pcie_probe.log);
-            // read per launch so that in-process A/B runs can switch it
-            int grid = grid_ew(count, pl, V);
-            if (const char *g = std::getenv("PCCL_REDUCE_COPY_GRID")) {
-                const int cap = std::atoi(g);
-                if (cap > 0) grid = std::min(grid, cap);
-            }
+            const int grid = grid_ew(count, pl, V);
             return launch_ok([&] {
                 k_reduce_copy<E, O><<<grid, kBlock, 0, st>>>(
                     static_cast<S *>(dst), static_cast<const S *>(src), static_cast<S *>(out), count, pl.head, pl.vec);

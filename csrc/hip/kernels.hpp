@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ d
     ew_loop_ls<V, kEwUnroll>(
         n, head, vec,
         [&](size_t i) {
-            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps(static_cast<int64_t>(src[i]), p))));
+            const S r = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(dq_zps_as<Q>(src[i], p))));
             dst[i] = r;
             acc.take(E::ld(r));
         },
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kBlock) void k_dq_zps(typename E::S *__restrict__ d
         [&](size_t b, DQ x) {
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), static_cast<C>(dq_zps(static_cast<int64_t>(x.q.v[e]), p))));
+                x.d.v[e] = E::st(apply_op<Op, C>(E::ld(x.d.v[e]), static_cast<C>(dq_zps_as<Q>(x.q.v[e], p))));
                 acc.take(E::ld(x.d.v[e]));
             }
             stp_nt<S, V>(dst + b, x.d);
@@ -415,12 +415,12 @@ __global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typ
     using S = typename E::S;
     constexpr int V = vec_width<S>();
     ew_loop_ls<V, kEwUnroll>(
-        n, head, vec, [&](size_t i) { dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p)); },
+        n, head, vec, [&](size_t i) { dst[i] = q_zps_as<Q>(static_cast<float>(E::ld(src[i])), p); },
         [&](size_t b) { return ldp_nt<S, V>(src + b); },
         [&](size_t b, const Pack<S, V> &s) {
             Pack<Q, V> q;
 #pragma unroll
-            for (int e = 0; e < V; ++e) q.v[e] = static_cast<Q>(q_zps(static_cast<float>(E::ld(s.v[e])), p));
+            for (int e = 0; e < V; ++e) q.v[e] = q_zps_as<Q>(static_cast<float>(E::ld(s.v[e])), p);
             stp<Q, V>(dst + b, q);
         });
 }

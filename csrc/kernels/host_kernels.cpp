@@ -42,6 +42,9 @@ static bool reduce_op(void *dst, const void *src, size_t n, ReduceOp op) {
 }
 
 bool host_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op) {
+    // bf16 / fp32 sums take the AVX-512 body of host_reduce3 (element-wise: out may alias a)
+    if ((op == ReduceOp::Sum || op == ReduceOp::Avg) && (t == DType::BF16 || t == DType::F32))
+        return host_reduce3(dst, dst, src, count, t, op);
     switch (t) {
         case DType::F32: return reduce_op<EF32>(dst, src, count, op);
         case DType::F64: return reduce_op<EF64>(dst, src, count, op);
@@ -210,7 +213,7 @@ template<typename E, typename Q>
 static void quant_zps(void *dst_v, const void *src_v, size_t n, const QuantParams &p) {
     const auto *src = static_cast<const typename E::S *>(src_v);
     auto *dst = static_cast<Q *>(dst_v);
-    for (size_t i = 0; i < n; ++i) dst[i] = static_cast<Q>(q_zps(static_cast<float>(E::ld(src[i])), p));
+    for (size_t i = 0; i < n; ++i) dst[i] = q_zps_as<Q>(static_cast<float>(E::ld(src[i])), p);
 }
 
 template<typename E, typename Op, typename Q>
@@ -241,7 +244,7 @@ static void dq_zps_loop(void *dst_v, const void *src_v, size_t n, const QuantPar
     auto *dst = static_cast<typename E::S *>(dst_v);
     const auto *src = static_cast<const Q *>(src_v);
     for (size_t i = 0; i < n; ++i) {
-        const float f = dq_zps(static_cast<int64_t>(src[i]), p);
+        const float f = dq_zps_as<Q>(src[i], p);
         dst[i] = E::st(apply_op<Op, C>(E::ld(dst[i]), static_cast<C>(f)));
     }
 }
@@ -271,6 +274,8 @@ static bool quantize_v(void *dst_q, const void *src, size_t n, DType qtype, cons
             case DType::I16: quant_zps<E, int16_t>(dst_q, src, n, p); return true;
             case DType::U32: quant_zps<E, uint32_t>(dst_q, src, n, p); return true;
             case DType::I32: quant_zps<E, int32_t>(dst_q, src, n, p); return true;
+            case DType::U64: quant_zps<E, uint64_t>(dst_q, src, n, p); return true;
+            case DType::I64: quant_zps<E, int64_t>(dst_q, src, n, p); return true;
             default: return false;
         }
     }
@@ -321,6 +326,8 @@ static bool dequant_v(void *dst, const void *src_q, size_t n, DType qtype, const
             case DType::I16: dq_zps_loop<E, Op, int16_t>(dst, src_q, n, p); return true;
             case DType::U32: dq_zps_loop<E, Op, uint32_t>(dst, src_q, n, p); return true;
             case DType::I32: dq_zps_loop<E, Op, int32_t>(dst, src_q, n, p); return true;
+            case DType::U64: dq_zps_loop<E, Op, uint64_t>(dst, src_q, n, p); return true;
+            case DType::I64: dq_zps_loop<E, Op, int64_t>(dst, src_q, n, p); return true;
             default: return false;
         }
     }

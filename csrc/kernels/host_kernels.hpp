@@ -14,8 +14,8 @@ namespace pccl::kernels {
 
 // dst[i] = dst[i] (op) src[i] for `count` elements of `t`. op Set copies. Avg accumulates like Sum.
 bool host_reduce(void *dst, const void *src, size_t count, DType t, ReduceOp op);
-// out = op(a, b), element-wise (out may alias neither input); bit-identical to host_reduce and to the HIP kernels
-// (fp32 math for 16-bit floats, round to nearest even). AVX-512 path for bf16 / fp32 sums.
+// out = op(a, b), element-wise (out may be a, not b); bit-identical to the scalar definition and to the HIP kernels
+// (fp32 math for 16-bit floats, round to nearest even). AVX-512 path for bf16 / fp32 sums (host_reduce uses it).
 bool host_reduce3(void *out, const void *a, const void *b, size_t count, DType t, ReduceOp op);
 
 // dst[i] = dst[i] (op) dequant(src_q[i]) — fused de-quantization + accumulation (op Set = plain dequant).

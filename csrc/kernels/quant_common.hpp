@@ -12,7 +12,10 @@
 //        s = FP8_MAX / max(|min|, |max|).
 //  * ZERO_POINT_SCALE (integer wire types): scale = (max - min) / (qhi - qlo), zp = clamp(rint(qlo - min / scale)),
 //        q = clamp(rint(x * inv_scale) + zp, qlo, qhi), x' = (q - zp) * scale (float math). The reference delegates
-//        this to the absent piquant library; parity with piquant is unpinned.
+//        this to the absent piquant library; parity with piquant is unpinned. 64-bit wire types: the clamp and the
+//        de-quantize difference run in double (their ranges fit neither int64 nor float), and zp (an int64 on the
+//        wire, as in the reference's DeQuantizationMetaData) is additionally clamped to the int64 range.
+// The 64-bit ranges end at the largest doubles below 2^64 / 2^63, so every clamped value converts without overflow.
 #pragma once
 
 #include <cmath>
@@ -34,7 +37,8 @@ struct QuantParams {
     // zero-point-scale
     float zps_scale = 1.0f, zps_inv = 1.0f;
     int64_t zp = 0;
-    int64_t ilo = 0, ihi = 0;
+    int64_t ilo = 0, ihi = 0; // <= 32-bit wire types
+    double dlo = 0, dhi = 0;  // 64-bit wire types
 };
 
 inline void int_range(DType q, double &lo, double &hi) {
@@ -45,8 +49,8 @@ inline void int_range(DType q, double &lo, double &hi) {
         case DType::I16: lo = -32768; hi = 32767; break;
         case DType::U32: lo = 0; hi = 4294967295.0; break;
         case DType::I32: lo = -2147483648.0; hi = 2147483647.0; break;
-        case DType::U64: lo = 0; hi = 18446744073709551615.0; break;
-        case DType::I64: lo = -9223372036854775808.0; hi = 9223372036854775807.0; break;
+        case DType::U64: lo = 0; hi = 18446744073709549568.0; break;                    // 2^64 - 2048
+        case DType::I64: lo = -9223372036854775808.0; hi = 9223372036854774784.0; break; // 2^63 - 1024
         default: lo = 0; hi = 255; break;
     }
 }
@@ -58,7 +62,7 @@ inline bool quant_supported(DType vtype, DType qtype, QuantAlgo algo) {
     const bool vfloat = vtype == DType::F32 || vtype == DType::F64 || vtype == DType::BF16 || vtype == DType::F16;
     if (!vfloat) return false;
     if (algo == QuantAlgo::MinMax) return is_fp8(qtype) || (!dtype_is_float(qtype));
-    if (algo == QuantAlgo::ZeroPointScale) return !dtype_is_float(qtype) && dtype_size(qtype) <= 4;
+    if (algo == QuantAlgo::ZeroPointScale) return !dtype_is_float(qtype);
     return false;
 }
 
@@ -86,8 +90,12 @@ inline QuantParams make_params(const proto::QuantMeta &m, DType qtype) {
     } else if (m.algo == QuantAlgo::ZeroPointScale) {
         double lo, hi;
         int_range(qtype, lo, hi);
-        p.ilo = static_cast<int64_t>(lo);
-        p.ihi = static_cast<int64_t>(hi);
+        if (dtype_size(qtype) <= 4) {
+            p.ilo = static_cast<int64_t>(lo);
+            p.ihi = static_cast<int64_t>(hi);
+        }
+        p.dlo = lo;
+        p.dhi = hi;
         p.zps_scale = m.scale;
         p.zps_inv = m.scale != 0.0f ? 1.0f / m.scale : 1.0f;
         p.zp = m.zero_point;
@@ -107,9 +115,15 @@ inline proto::QuantMeta make_meta(QuantAlgo algo, DType vtype, DType qtype, doub
         int_range(qtype, lo, hi);
         float scale = static_cast<float>((mx - mn) / (hi - lo));
         if (!(scale > 0.0f) || !std::isfinite(scale)) scale = 1.0f;
+        // uint64 wire type: the zero point travels as an int64; data reaching far below zero would need a larger
+        // one, so the scale grows until it fits (the code then spans at least half of the uint64 range)
+        constexpr double kZpMax = 9223372036854774784.0; // largest double below 2^63
+        if (lo - mn / static_cast<double>(scale) > kZpMax)
+            scale = static_cast<float>(-mn / kZpMax * (1.0 + 1.0 / (1 << 20)));
         double zp = std::nearbyint(lo - mn / static_cast<double>(scale));
         if (zp < lo) zp = lo;
         if (zp > hi) zp = hi;
+        if (zp > kZpMax) zp = kZpMax;
         m.scale = scale;
         m.zero_point = static_cast<int64_t>(zp);
     }
@@ -138,5 +152,23 @@ PCCL_HD int64_t q_zps(float x, const QuantParams &p) {
     return q;
 }
 PCCL_HD float dq_zps(int64_t q, const QuantParams &p) { return static_cast<float>(q - p.zp) * p.zps_scale; }
+
+// wire element Q of zero-point-scale (64-bit types clamp and subtract in double)
+template<typename Q>
+PCCL_HD Q q_zps_as(float x, const QuantParams &p) {
+    if constexpr (sizeof(Q) <= 4) {
+        return static_cast<Q>(q_zps(x, p));
+    } else {
+        double r = static_cast<double>(__builtin_rintf(x * p.zps_inv)) + static_cast<double>(p.zp);
+        r = r < p.dlo ? p.dlo : r;
+        r = r > p.dhi ? p.dhi : r;
+        return static_cast<Q>(r);
+    }
+}
+template<typename Q>
+PCCL_HD float dq_zps_as(Q q, const QuantParams &p) {
+    if constexpr (sizeof(Q) <= 4) return dq_zps(static_cast<int64_t>(q), p);
+    else return static_cast<float>(static_cast<double>(q) - static_cast<double>(p.zp)) * p.zps_scale;
+}
 
 } // namespace pccl::kernels

@@ -61,6 +61,14 @@ SockAddr from_native(const sockaddr_storage &ss) {
     return a;
 }
 
+// the connected peer is this host (loopback or one of its own addresses)
+static bool peer_is_local(int fd) {
+    sockaddr_storage ss{};
+    socklen_t len = sizeof(ss);
+    if (::getpeername(fd, reinterpret_cast<sockaddr *>(&ss), &len) != 0) return false;
+    return is_local_address(from_native(ss));
+}
+
 void tune_socket(int fd, bool bulk) {
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
@@ -70,16 +78,24 @@ void tune_socket(int fd, bool bulk) {
     setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl));
     setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt));
     if (bulk) {
-        int sz = 8 << 20;
-        setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
-        setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+        // Same-host data sockets get fixed 8 MiB buffers and MSG_ZEROCOPY sends (loopback: the receiver copies at
+        // memory speed, and zero-copy saves the sender's copy, profiles/r3/zerocopy/). A socket to another host keeps
+        // the kernel's buffer autotuning, which grows the window to the path's bandwidth-delay product (a fixed
+        // 8 MiB caps a 100 ms-RTT connection at ~0.7 Gbit/s), and plain sends: a MSG_ZEROCOPY frame completes only
+        // once the peer acknowledged it, which turns every frame into one round trip on a long path (reference
+        // tinysockets/src/multiplexed_socket.cpp:19-61 leaves autotuning on as well).
+        if (peer_is_local(fd)) {
+            int sz = 8 << 20;
+            setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+            setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+            if (zerocopy_send_enabled()) setsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one));
+        }
         // like the reference's data sockets (tinysockets/src/multiplexed_socket.cpp:51-59): immediate ACKs, and busy
         // polling of the device queue on NICs that support it (best effort: a value above net.core.busy_poll needs
         // CAP_NET_ADMIN, and loopback has no NAPI queue to poll)
         setsockopt(fd, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof(one));
         int busy = static_cast<int>(env_size("PCCL_SO_BUSY_POLL_US", 50));
         if (busy > 0) setsockopt(fd, SOL_SOCKET, SO_BUSY_POLL, &busy, sizeof(busy));
-        if (zerocopy_send_enabled()) setsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one));
     }
 }
 
@@ -203,8 +219,8 @@ bool sendv_all(int fd, iovec *iov, int iovcnt) {
     return true;
 }
 
-// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1 (default), the socket has SO_ZEROCOPY: socket_zerocopy_on): the kernel pins the user pages instead of
-// copying them into socket buffers and reports completion on the socket's error queue; the call returns once every
+// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1 (default) and a same-host socket: socket_zerocopy_on): the kernel pins the
+// user pages instead of copying them into socket buffers and reports completion on the socket's error queue; the call returns once every
 // byte it sent is released, so the caller may reuse the buffer as after a plain send. On loopback the kernel copies
 // the pages anyway when it delivers them to the receiving socket ("deferred copy", reported as
 // SO_EE_CODE_ZEROCOPY_COPIED), so only a real NIC saves the copy. Returns false on error.

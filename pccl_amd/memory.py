@@ -145,11 +145,13 @@ def ipc_buffer_stats() -> dict:
     (copy-in / copy-out through VMM comm buffers), per input and output; plus ``quarantined`` (staged comm buffers of
     aborted ops, never reissued) and ``zombie_drains`` (abort drains that waited for a dead peer's threads to finish
     tearing down its address space, i.e. its GPU queues), ``preflight_failed`` / ``preflight_passed`` (cross-GPU write
-    probes on the first op of an arena whose peers span several GPUs)."""
-    out = (ctypes.c_uint64 * 8)()
-    n = int(_native.C.pcclxIpcStatsEx(out, 8))
+    probes on the first op of an arena whose peers span several GPUs), ``reclaimed`` (quarantined buffers handed out
+    again once no peer could still touch them for the aborted op) and ``quarantine_freed`` (quarantined VMM buffers
+    freed beyond the 8 GiB quarantine cap)."""
+    out = (ctypes.c_uint64 * 10)()
+    n = int(_native.C.pcclxIpcStatsEx(out, 10))
     keys = ("direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains", "preflight_failed",
-            "preflight_passed")
+            "preflight_passed", "reclaimed", "quarantine_freed")
     return {k: int(out[i]) for i, k in enumerate(keys[:n])}
 
 

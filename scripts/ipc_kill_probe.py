@@ -1,12 +1,15 @@
-"""SIGKILL a peer while xGMI/IPC all-reduce kernels are running (one GPU, separate processes).
+"""SIGKILL a peer while xGMI/IPC or device-ring all-reduce work is running (one GPU, separate processes).
 
     python scripts/ipc_kill_probe.py [--world 3] [--n 536870912] [--kill-after 3.0] [--duration 10] [--out DIR]
+                                     [--disable-ipc] [--quant u8] [--inject POINT:SEQ[:STEP[:PHASE]]]
 
 Spawns a master and WORLD peer processes on cuda:0 that run back-to-back bf16 all-reduces of `n` elements over the
 IPC path (x = 1 everywhere, result must equal the world size; checked every 16th op). After `kill-after` seconds the
 parent SIGKILLs peer 0 at an arbitrary point of its op loop (most of an op's time is kernel time at this size).
 Survivors must see the loss, re-form the ring and finish all their steps with exact results. Each peer's stdout /
 stderr (PCCL_LOG_LEVEL=DEBUG: the IPC mappings of every op) goes to DIR/peer<r>.{out,err}; a JSON summary is printed.
+--disable-ipc runs every peer on the loopback-TCP device ring instead (PCCL_DISABLE_IPC=1); --inject ring:SEQ:STEP:PHASE
+then kills the victim at a ring step (csrc/common/types.hpp).
 """
 from __future__ import annotations
 
@@ -38,6 +41,9 @@ def main():
     ap.add_argument("--inject", default="", help="PCCL_FAULT_INJECT for the victim (e.g. ipc_kernel:200): it kills "
                                                  "itself at that protocol point instead of the parent's timed SIGKILL")
     ap.add_argument("--victim-threads", type=int, default=0, help="extra busy threads in the victim process")
+    ap.add_argument("--disable-ipc", action="store_true", help="device TCP ring instead of the xGMI path")
+    ap.add_argument("--quant", default="none", choices=["none", "u8"], help="quantized all-reduce (device ring)")
+    ap.add_argument("--pool", type=int, default=0, help="P2P connection pool size of every peer (0: default)")
     ap.add_argument("--verify-restore-ms", type=int, default=-1,
                     help="survivors re-read an in-place buffer this long after an aborted op (must equal the input)")
     a = ap.parse_args()
@@ -45,6 +51,9 @@ def main():
     from pccl_amd.utils import local_master
     worker = os.path.join(ROOT, "tests", "workers", "allreduce_peer.py")
     env = dict(os.environ, PCCL_LOG_LEVEL=a.log_level, PCCL_DEBUG_BACKTRACE_SIGNAL="1")
+    if a.disable_ipc:
+        env["PCCL_DISABLE_IPC"] = "1"
+    common = ["--quant", a.quant] + (["--pool", str(a.pool)] if a.pool else [])
     summary = {"world": a.world, "n": a.n, "kill_after_s": a.kill_after}
     with local_master() as addr:
         ps, files = [], []
@@ -53,7 +62,7 @@ def main():
             fe = open(os.path.join(a.out, f"peer{r}.err"), "w")
             files += [fo, fe]
             args = [sys.executable, "-u", worker, addr, str(a.world), str(r), "--const", "--n", str(a.n), "--dtype",
-                    "bf16", "--duration", str(a.duration), "--device", "cuda:0", "--reuse", "--check-every", "16"]
+                    "bf16", "--duration", str(a.duration), "--device", "cuda:0", "--reuse", "--check-every", "16", *common]
             if a.inplace:
                 args.append("--inplace")
             if a.shareable:
@@ -107,7 +116,7 @@ def main():
             files += [fo, fe]
             args = [sys.executable, "-u", worker, addr, str(a.world), str(r), "--const", "--n", str(a.n), "--dtype",
                     "bf16", "--duration", str(max(2.0, a.duration / 2)), "--device", "cuda:0", "--reuse",
-                    "--check-every", "16", "--no-wait"] + (["--inplace"] if a.inplace else []) + \
+                    "--check-every", "16", "--no-wait", *common] + (["--inplace"] if a.inplace else []) + \
                 (["--shareable"] if a.shareable else [])
             ps.append(subprocess.Popen(args, stdout=fo, stderr=fe, env=env))
         rcs = []
@@ -136,6 +145,8 @@ def main():
         summary[f"peer{r}"] = {"ops_ok": len(oks), "errors": len(lines) - len(oks),
                                "bad": sum(1 for x in oks if x.get("bad")),
                                "worlds": sorted({x["world"] for x in oks}),
+                               "ops_ok_by_world": {str(w): sum(1 for x in oks if x["world"] == w)
+                                                   for w in sorted({x["world"] for x in oks})},
                                "paths": sorted({x["path"] for x in oks}),
                                "ipc_bufs": oks[-1].get("ipc_bufs") if oks else None,
                                "restore_checked": sum(1 for x in lines if "restore_bad" in x),

@@ -3,7 +3,7 @@ windows of K ops alternate between variants (env settings applied while every pe
 reads these knobs per op), so slow drifts of a noisy box hit every variant alike. Prints one JSON line per variant
 with the median / min ms per op over its windows.
 
-    python scripts/ring_ab_interleaved.py --variants "l1:PCCL_RING_LANES=1;l2:PCCL_RING_LANES=2" [--windows 6]
+    python scripts/ring_ab_interleaved.py --variants "s2:PCCL_RING_STRIPES=2;s4:PCCL_RING_STRIPES=4" [--windows 6]
                                           [--ops 4] [--peers 8] [--mib 1024] [--pool 0]
 """
 import argparse

@@ -152,9 +152,10 @@ TEST(packet_extensions_backward_compatible) {
 }
 
 // CRC-32C split algebra used by the HIP kernel: raw(A || B) = shift(raw(A), |B|) ^ raw(B)
-TEST(host_reduce3_matches_host_reduce_bitwise) {
-    // the 3-operand host reduce (AVX-512 path for bf16 / fp32 sums) must equal copy + host_reduce bit for bit,
-    // NaN / inf / denormal / rounding-tie inputs included, at lengths that exercise the vector body and the tail
+TEST(host_reduce3_matches_scalar_bitwise) {
+    // the 3-operand host reduce (AVX-512 path for bf16 / fp32 sums, also behind host_reduce) must equal the scalar
+    // definition (fp32 add, round to nearest even) bit for bit, NaN / inf / denormal / rounding-tie inputs included,
+    // at lengths that exercise the vector body and the tail
     std::mt19937_64 rng(11);
     for (size_t n : {size_t(1), size_t(15), size_t(16), size_t(17), size_t(1000), size_t(65537)}) {
         std::vector<uint16_t> a(n), b(n), want(n), got(n);
@@ -167,8 +168,13 @@ TEST(host_reduce3_matches_host_reduce_bitwise) {
             a[4] = 0x3f80; b[4] = 0x3380; // 1 + 2^-24-ish: a rounding tie
         }
         for (ReduceOp op : {ReduceOp::Sum, ReduceOp::Max}) {
-            want = a;
-            EXPECT(kernels::host_reduce(want.data(), b.data(), n, DType::BF16, op));
+            if (op == ReduceOp::Sum) {
+                for (size_t i = 0; i < n; ++i)
+                    want[i] = num::f32_to_bf16(num::bf16_to_f32(a[i]) + num::bf16_to_f32(b[i]));
+            } else { // max: the scalar element op of host_reduce is the definition
+                want = a;
+                EXPECT(kernels::host_reduce(want.data(), b.data(), n, DType::BF16, op));
+            }
             EXPECT(kernels::host_reduce3(got.data(), a.data(), b.data(), n, DType::BF16, op));
             for (size_t i = 0; i < n; ++i) {
                 const bool both_nan = (want[i] & 0x7fff) > 0x7f80 && (got[i] & 0x7fff) > 0x7f80;
@@ -186,8 +192,7 @@ TEST(host_reduce3_matches_host_reduce_bitwise) {
             fa[i] = static_cast<float>(static_cast<int64_t>(rng() % 2000001) - 1000000) * 1e-3f;
             fb[i] = static_cast<float>(static_cast<int64_t>(rng() % 2000001) - 1000000) * 1e-5f;
         }
-        fw = fa;
-        EXPECT(kernels::host_reduce(fw.data(), fb.data(), n, DType::F32, ReduceOp::Sum));
+        for (size_t i = 0; i < n; ++i) fw[i] = fa[i] + fb[i];
         EXPECT(kernels::host_reduce3(fg.data(), fa.data(), fb.data(), n, DType::F32, ReduceOp::Sum));
         EXPECT(std::memcmp(fw.data(), fg.data(), n * 4) == 0);
     }

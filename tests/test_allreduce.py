@@ -222,7 +222,10 @@ def test_all_reduce_multiple_sliding_window():
 @pytest.mark.parametrize("qdtype,algo", [(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX),
                                          (pccl.DataType.INT8, pccl.QuantizationAlgorithm.MIN_MAX),
                                          (pccl.DataType.UINT16, pccl.QuantizationAlgorithm.MIN_MAX),
-                                         (pccl.DataType.UINT8, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE)])
+                                         (pccl.DataType.UINT8, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
+                                         (pccl.DataType.INT32, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
+                                         (pccl.DataType.UINT64, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
+                                         (pccl.DataType.INT64, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE)])
 def test_quantized_all_reduce(qdtype, algo):
     world, n = 3, 20011
     inputs = [_peer_tensor(r, n, torch.float32) for r in range(world)]
@@ -244,7 +247,7 @@ def test_quantized_all_reduce(qdtype, algo):
     # the wire carries the quantized type: ~4x fewer bytes than fp32 for 8-bit
     tx = res[0][1].tx_bytes
     full = n * 4 * 2 * (world - 1) / world
-    if qdtype != pccl.DataType.UINT16:
+    if qdtype in (pccl.DataType.UINT8, pccl.DataType.INT8):
         assert tx < full / 2
 
 
@@ -282,6 +285,33 @@ def test_striped_large_all_reduce(world, pool, quant, monkeypatch):
     expect = _expected(inputs, pccl.ReduceOp.SUM).float()
     tol = 3 * world * max(float(t.max() - t.min()) for t in inputs) / 255 if quant else 1e-4
     assert (res[0] - expect).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("lanes,inplace", [("1", False), ("2", True), ("3", False)])
+def test_quantized_lanes(lanes, inplace, monkeypatch):
+    """Quantized all-reduce split into lanes (PCCL_QUANT_LANES, each >= 8 MiB of wire bytes per ring chunk): every
+    lane is its own ring on its own data / metadata tags; the result is within the quantization bound, identical on
+    every peer, and the wire bytes are the same for any lane count up to the per-step metadata packets."""
+    monkeypatch.setenv("PCCL_QUANT_LANES", lanes)
+    world, n = 2, (1 << 25) + 7
+    inputs = [_peer_tensor(r, n, torch.float32) for r in range(world)]
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX)
+
+    def fn(rank, comm):
+        x = inputs[rank].clone()
+        out = x if inplace else torch.empty(n)
+        info = comm.all_reduce(x, out, op=pccl.ReduceOp.SUM, tag=5, quantization_options=qopt)
+        return out, info.tx_bytes
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, comm_kwargs={"p2p_connection_pool_size": 2})
+    nl = int(lanes)
+    for out, tx in res:
+        assert torch.equal(out, res[0][0])
+        payload = n * 2 * (world - 1) // world  # uint8 bytes of the 2(W-1) steps
+        assert payload <= tx <= payload + 200 * 2 * (world - 1) * nl, tx  # + one metadata packet per step and lane
+    expect = _expected(inputs, pccl.ReduceOp.SUM).float()
+    assert (res[0][0] - expect).abs().max().item() <= 3 * world * max(float(t.max() - t.min()) for t in inputs) / 255
 
 
 @pytest.mark.parametrize("small_limit", [0, 1 << 18])

@@ -140,17 +140,19 @@ def test_gpu_ipc_sigkill_many_threads_restore_is_final(hip, tmp_path):
         assert s_k["ipc_bufs"]["quarantined"] >= 1, s_k
 
 
-def _ipc_kill(tmp_path, point, inplace, respawn, shareable, *extra):
-    """Runs scripts/ipc_kill_probe.py (victim = peer 0, killed at `point` of op 300) and checks the common outcome:
-    the victim died of SIGKILL, the survivors exited cleanly with exact results over both world sizes on the IPC path
-    and no GPU fault line. Returns the probe's JSON summary."""
+def _ipc_kill(tmp_path, point, inplace, respawn, shareable, *extra, inject=None, path=3, n=1 << 28, duration=None,
+              min_ops=300):
+    """Runs scripts/ipc_kill_probe.py (victim = peer 0, killed at `point` of op 300, or at `inject`) and checks the
+    common outcome: the victim died of SIGKILL, the survivors exited cleanly with exact results over both world sizes
+    on reduce path `path` (3 IPC, 2 device ring) and no GPU fault line. Returns the probe's JSON summary."""
     import sys
     probe = os.path.join(os.path.dirname(HERE), "scripts", "ipc_kill_probe.py")
-    args = [sys.executable, probe, "--inject", f"{point}:300", "--duration", "12" if respawn else "4", "--n",
-            str(1 << 28), "--out", str(tmp_path / "ipc_kill")]
+    dur = duration if duration is not None else ("12" if respawn else "4")
+    args = [sys.executable, probe, "--inject", inject or f"{point}:300", "--duration", str(dur), "--n", str(n),
+            "--out", str(tmp_path / "ipc_kill")]
     args += (["--inplace"] if inplace else []) + (["--respawn"] if respawn else []) + \
         (["--shareable"] if shareable else []) + list(extra)
-    r = subprocess.run(args, capture_output=True, text=True, timeout=150)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=240)
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["victim_rc"] == -9, summary
     assert summary["survivor_rcs"] == [0, 0] + ([0] if respawn else []), (summary, r.stderr[-2000:])
@@ -160,8 +162,36 @@ def _ipc_kill(tmp_path, point, inplace, respawn, shareable, *extra):
     for k in (1, 2):
         s_k = summary[f"peer{k}"]
         assert s_k["bad"] == 0 and not s_k["fault_lines"], s_k
-        assert 2 in s_k["worlds"] and 3 in s_k["worlds"] and s_k["ops_ok"] > 300 and s_k["paths"] == [3], s_k
+        assert 2 in s_k["worlds"] and 3 in s_k["worlds"] and s_k["ops_ok"] > min_ops and s_k["paths"] == [path], s_k
     return summary
+
+
+# Device TCP ring (PCCL_DISABLE_IPC=1), 3 processes on one GPU, 64 Mi bf16 elements: the victim SIGKILLs itself at a
+# global ring step (0-1 reduce-scatter, 2-3 all-gather) of op 12 in a given phase (csrc/common/types.hpp): `publish`
+# (its step's sends just handed to the stripe threads), `rx` (first received piece handed to the copy engine /
+# kernels), `ahead` (the next step's sinks posted while this step still receives), `end`; quantized ring: `meta`
+# (its metadata packet sent, waiting for the peer's), `rx`.
+RING_KILLS = [("ring", 0, "ahead", False), ("ring", 1, "rx", True), ("ring", 2, "rx", False),
+              ("ring", 3, "publish", True), ("ring", 1, "end", False), ("qring", 1, "meta", True),
+              ("qring", 2, "rx", False), ("qring", 0, "rx", True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("point,step,phase,inplace", RING_KILLS)
+def test_gpu_ring_sigkill_mid_op(hip, tmp_path, point, step, phase, inplace):
+    """Abort safety of the pipelined device ring (plain and quantized): survivors drain every copy / kernel of the
+    aborted op before their in-place buffer is restored (re-read 200 ms later, bit-exact), re-form the ring and keep
+    producing exact results for at least 20 more ops in the smaller world (reference reduce.cpp:551-580,657-660)."""
+    quant = point == "qring"
+    summary = _ipc_kill(tmp_path, point, inplace, False, False, "--disable-ipc", "--verify-restore-ms", "200",
+                        "--pool", "2", *(["--quant", "u8"] if quant else []), inject=f"{point}:12:{step}:{phase}",
+                        path=2, n=1 << 26, duration=12, min_ops=30)
+    for k in (1, 2):
+        s_k = summary[f"peer{k}"]
+        assert s_k["errors"] >= 1 and s_k["restore_bad"] == 0, s_k
+        if inplace:
+            assert s_k["restore_checked"] >= 1, s_k
+        assert s_k["ops_ok_by_world"].get("2", 0) >= 20, s_k
 
 
 @pytest.mark.gpu
@@ -211,3 +241,32 @@ def test_gpu_shared_state_many_tensors_packed_handoff(hip):
     sync = next(x for x in _lines(outs[2][0]) if x["phase"] == "sync")
     assert sync["lo"] == sync["hi"] == 7.0 and sync["extra_ok"] and sync["revision"] == 5, sync
     assert sync["sec"] < 5.0, sync
+
+
+@pytest.mark.gpu
+def test_gpu_ipc_quarantine_reclaimed_on_unchanged_ring(hip):
+    """50 aborted staged xGMI ops on a ring whose membership never changes (the arena is reused): peer 1 stalls
+    300 ms before publishing its vote for ops seq <= 49 (PCCL_FAULT_STALL) while peer 0's vote barrier gives up after
+    100 ms (PCCL_IPC_TIMEOUT_MS), so every such op aborts on both peers and quarantines its staged comm buffers. Each
+    later acquire reclaims them once no peer can still touch them for the aborted op: HBM use stays flat over the
+    aborts, the reclaim counter moves, and the ops after the stall succeed with exact results."""
+    n = 1 << 24  # 64 MiB fp32 per buffer
+    env = {"PCCL_IPC_TIMEOUT_MS": "100"}
+    with local_master() as addr:
+        ps = [spawn_python([WORKER, addr, "2", str(r), "--device", "cuda:0", "--const", "--inplace", "--n", str(n),
+                            "--steps", "10", "--max-failures", "60", "--report-mem"],
+                           env=dict(env, **({"PCCL_FAULT_STALL": "ipc_vote:49:300"} if r == 1 else {})),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+        outs = communicate_all(ps, 240, DIAG_SIGNALS)
+    for p, (o, e) in zip(ps, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = _lines(o)
+        errs = [x for x in lines if "error" in x]
+        oks = _check_ok(lines)
+        assert len(errs) >= 45 and len(oks) == 10, (len(errs), len(oks))
+        assert all(x["path"] == 3 and x["world"] == 2 for x in oks), oks[-1]
+        used = [x["hbm_used"] for x in errs]
+        # flat: no growth by a buffer per aborted op (64 MiB x 2 buffers x 2 peers each)
+        assert max(used[5:]) - used[5] < 3 * (n * 4), used
+        b = oks[-1]["ipc_bufs"]
+        assert b["quarantined"] >= 45 and b["reclaimed"] >= 40, b

@@ -80,24 +80,14 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
             assert torch.all(y == float(1 + 2 * j))
 
 
-@pytest.mark.parametrize("shared_queues,lanes,host,shared_red", [("1", "1", "0", "0"), ("0", "1", "0", "0"),
-                                                                 ("1", "2", "0", "0"), ("1", "1", "0.6", "0"),
-                                                                 ("1", "1", "0", "1"), ("1", "2", "0", "1"),
-                                                                 ("1", "1", "0", "ag"), ("1", "2", "0", "ag")])
 @pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
-def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lanes, host, shared_red, monkeypatch):
+def test_device_ring_pipelined_large(hip, world, inplace, op, monkeypatch):
     """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
-    chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results, also
-    with every peer's reduce-scatter kernels on the process-wide reduce stream (PCCL_RING_SHARED_REDUCE)."""
+    chunks): copy-engine staging, cross-stream waits and next-step payload staging must give exact results; the second
+    op reuses pooled staging buffers and events."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
-    monkeypatch.setenv("PCCL_SHARED_COPY_QUEUES", shared_queues)
-    monkeypatch.setenv("PCCL_RING_LANES", lanes)
-    monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)
-    monkeypatch.setenv("PCCL_RING_SHARED_REDUCE", "0" if shared_red == "0" else "1")
-    monkeypatch.setenv("PCCL_RING_SHARED_AG", "1" if shared_red == "ag" else "0")  # all-gather copies there too
-    monkeypatch.setenv("PCCL_RING_AG_COPY_GRID", "64" if shared_red == "ag" else "0")
     n = 9_000_011
     base = (torch.arange(n, dtype=torch.int64) % 31).float()  # every partial sum < 256: exact in bf16
     inputs = [(base + 7 * r).to(torch.bfloat16) for r in range(world)]
@@ -128,20 +118,13 @@ def test_device_ring_pipelined_large(hip, world, inplace, op, shared_queues, lan
         assert torch.equal(y, expect)
 
 
-@pytest.mark.parametrize("ahead,step0_op,lanes,host", [("1", "1", "1", "0"), ("0", "1", "1", "0"), ("1", "0", "1", "0"),
-                                                       ("1", "0", "2", "0"), ("1", "1", "3", "0"),
-                                                       ("1", "0", "1", "0.5"), ("0", "0", "2", "1")])
-def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, host, monkeypatch):
+def test_device_ring_mixed_pool_sizes(hip, monkeypatch):
     """Neighbours with different P2P connection pool sizes (1 / 3 / 2 stripes) and chunks that are no multiple of the
     staging piece: a TX stripe of the next step then spans several RX stripes of this one, and the send-ahead
     pipeline must send no byte before it has been received and reduced (advisor round 2, high)."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
-    monkeypatch.setenv("PCCL_RING_SEND_AHEAD", ahead)
-    monkeypatch.setenv("PCCL_RING_STEP0_OP_STREAM", step0_op)
-    monkeypatch.setenv("PCCL_RING_LANES", lanes)  # lanes > 1: parts of the buffer on their own tags, overlapped
-    monkeypatch.setenv("PCCL_RING_HOST_REDUCE", host)  # > 0: part of every intermediate chunk reduced by the CPU
     world, n = 3, 9_000_011
     pools = [1, 3, 2]
     base = (torch.arange(n, dtype=torch.int64) % 29).float()
@@ -164,51 +147,89 @@ def test_device_ring_mixed_pool_sizes(hip, ahead, step0_op, lanes, host, monkeyp
         assert torch.equal(y, expect)
 
 
-@pytest.mark.parametrize("ag_kernel,rs_h2d,ag_grid,rc_grid", [("0", "0", "0", "0"), ("1", "1", "0", "0"),
-                                                               ("1", "2", "0", "0"), ("1", "0", "64", "48")])
-def test_device_ring_h2d_modes(hip, ag_kernel, rs_h2d, ag_grid, rc_grid, monkeypatch):
-    """The device ring's host->device variants (copy engine / blit kernel on the op stream for the all-gather; copy
-    engine, blit, or zero-copy reads by the fused reduce for the reduce-scatter) give the exact result, in place and
-    with chunk offsets that are no multiple of 16 bytes (odd element count: the zero-copy sinks take the chunk's
-    16-byte phase)."""
+def _mixed_session(world, inputs, qopt, op=pccl.ReduceOp.SUM, pool=2):
+    """One session, three ops in one ring order: every peer on host memory (tag 0), peer 0 on host memory and the
+    others on HBM (tag 1), every peer on HBM (tag 2). Returns per rank [(result, tx, rx, path)] of the three ops."""
+    def fn(rank, comm):
+        out = []
+        for tag in range(3):
+            on_gpu = tag == 2 or (tag == 1 and rank != 0)
+            x = inputs[rank].to(hip_dev() if on_gpu else "cpu")
+            y = torch.empty_like(x)
+            info = comm.all_reduce(x, y, op=op, tag=tag, quantization_options=qopt)
+            if on_gpu:
+                torch.cuda.synchronize()
+            out.append((y.cpu(), info.tx_bytes, info.rx_bytes, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)))
+        return out
+
+    with local_master() as addr:
+        return run_threaded_peers(world, fn, address=addr, timeout=240, comm_kwargs={"p2p_connection_pool_size": pool})
+
+
+def hip_dev():
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_device_ring_random_bit_identical(hip, world, dtype, monkeypatch):
+    """Random data (rounding order matters) on the pipelined device ring at 4 and 8 peers: every peer ends with the
+    same bits, and those bits equal the host ring's (CPU tensors, same session and ring order) and a mixed ring's
+    where one peer holds CPU tensors and the others HBM tensors on the same wire protocol (SURVEY 7.4 #2)."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_DEVICE_PIECE_BYTES", str(1 << 20))
     monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(1 << 20))
-    monkeypatch.setenv("PCCL_RING_AG_KERNEL_COPY", ag_kernel)
-    monkeypatch.setenv("PCCL_RING_RS_H2D", rs_h2d)
-    monkeypatch.setenv("PCCL_RING_AG_COPY_GRID", ag_grid)  # > 0: our copy kernel with this many workgroups
-    monkeypatch.setenv("PCCL_REDUCE_COPY_GRID", rc_grid)  # > 0: workgroup cap of the fused reduce-scatter kernel
-    world, n = 4, 6_000_007
-    base = (torch.arange(n, dtype=torch.int64) % 23).float()
-    inputs = [(base + 3 * r).to(torch.bfloat16) for r in range(world)]
-    expect = torch.stack([x.float() for x in inputs]).sum(0).to(torch.bfloat16)
-
-    def fn(rank, comm):
-        x = inputs[rank].to(hip)
-        for tag in range(2):
-            if tag:
-                x.copy_(inputs[rank].to(hip))
-            comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=tag)
-        torch.cuda.synchronize()
-        return x.cpu(), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
-
-    with local_master() as addr:
-        res = run_threaded_peers(world, fn, address=addr, timeout=180, comm_kwargs={"p2p_connection_pool_size": 2})
-    for y, path in res:
-        assert path == pccl.ReducePath.DEVICE_RING.value
-        assert torch.equal(y, expect)
+    n = 3_000_017
+    inputs = [torch.randn(n, generator=torch.Generator().manual_seed(90 + r)).to(dtype) for r in range(world)]
+    res = _mixed_session(world, inputs, None, op=pccl.ReduceOp.AVG if dtype == torch.float32 else pccl.ReduceOp.SUM)
+    ref = res[0][0][0]
+    exact = torch.stack([x.double() for x in inputs]).sum(0)
+    if dtype == torch.float32:
+        exact = exact / world
+    tol = {torch.bfloat16: 0.05, torch.float16: 0.01, torch.float32: 1e-5}[dtype]
+    assert (ref.double() - exact).abs().max().item() <= tol * (1 + exact.abs().max().item())
+    host, dev = pccl.ReducePath.HOST_RING.value, pccl.ReducePath.DEVICE_RING.value
+    for rank, ops in enumerate(res):
+        assert [o[3] for o in ops] == [host, host if rank == 0 else dev, dev]
+        for y, *_ in ops:
+            assert torch.equal(y, ref)
 
 
-@pytest.mark.parametrize("stage", ["0", "1"])
-@pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
-def test_device_quantized_all_reduce(hip, qdtype, stage, monkeypatch):
-    """stage=1: received quantized pieces staged to HBM by the copy engine before the de-quantize kernels
-    (PCCL_QUANT_RX_STAGE); 0: the kernels read them from pinned memory."""
-    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
-    monkeypatch.setenv("PCCL_QUANT_RX_STAGE", stage)
-    monkeypatch.setenv("PCCL_QUANT_EARLY_SINKS", stage)  # the non-default data path in one of the two cases
+@pytest.mark.parametrize("qdtype,algo", [(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX),
+                                         (pccl.DataType.INT8, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
+                                         (pccl.DataType.FLOAT8_E5M2, pccl.QuantizationAlgorithm.MIN_MAX)])
+def test_device_quantized_matches_host_ring(hip, qdtype, algo, monkeypatch):
+    """Quantized ring, host memory vs mixed vs HBM in one session (one ring order: a quantized result depends on the
+    partial sums that get quantized): identical results and wire bytes on every peer and every op, over several
+    pieces per step and uneven chunks. The device ring folds every payload's min / max from the de-quantize kernels'
+    partials except the first reduce-scatter step's."""
+    from pccl_amd.ops import kernels as K
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
-    n = (1 << 20) + 3
+    world, n = 4, 3_000_017
+    inputs = [torch.randn(n, generator=torch.Generator().manual_seed(60 + r)).bfloat16() for r in range(world)]
+    s0 = K.quant_minmax_stats()
+    res = _mixed_session(world, inputs, pccl.QuantizationOptions(qdtype, algo))
+    s1 = K.quant_minmax_stats()
+    ref = res[0][0]
+    for ops in res:
+        for y, tx, rx, _ in ops:
+            assert torch.equal(y, ref[0])
+        assert len({(o[1], o[2]) for o in ops}) == 1, ops
+    # device peers: 3 in the mixed op, 4 in the all-HBM op; per peer and lane: world - 1 folded payloads + 1 pass
+    peers = (world - 1) + world
+    assert {k: s1[k] - s0[k] for k in s0} == {"folds": peers * (world - 1), "passes": peers}
+
+
+@pytest.mark.parametrize("lanes", ["1", "2", "3"])
+@pytest.mark.parametrize("qdtype", [pccl.DataType.UINT8, pccl.DataType.FLOAT8_E4M3])
+def test_device_quantized_all_reduce(hip, qdtype, lanes, monkeypatch):
+    """Quantized device ring, 1-3 lanes (PCCL_QUANT_LANES; a lane needs >= 8 MiB of wire bytes per chunk): result
+    within the quantization bound, identical on every peer, fewer wire bytes than fp32."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")  # quantization applies to the ring (wire) path
+    monkeypatch.setenv("PCCL_QUANT_LANES", lanes)
+    monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(4 << 20))
+    n = (3 << 24) + 3
     inputs = [torch.randn(n, generator=torch.Generator().manual_seed(40 + r)) for r in range(3)]
 
     def fn(rank, comm):
@@ -232,62 +253,6 @@ def test_device_quantized_all_reduce(hip, qdtype, stage, monkeypatch):
             # partial sums are re-quantized at every ring hop: error scales with sum(|x_r|), not |sum(x_r)|
             mag = inputs[0].abs() + inputs[1].abs() + inputs[2].abs()
             assert (err <= mag * 0.15 + 0.05).all()
-
-
-@pytest.mark.parametrize("qdtype,algo", [(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX),
-                                         (pccl.DataType.INT8, pccl.QuantizationAlgorithm.ZERO_POINT_SCALE),
-                                         (pccl.DataType.FLOAT8_E5M2, pccl.QuantizationAlgorithm.MIN_MAX)])
-def test_device_quantized_fused_minmax_same_wire(hip, qdtype, algo, monkeypatch):
-    """Quantized device ring with the reduce-scatter's min / max folded from the de-quantize kernels' partials
-    (default) vs a separate min / max pass per step (PCCL_QUANT_FUSED_MINMAX=0): identical results and wire bytes on
-    every peer, over several pieces per step and uneven chunks; the fused path folds every payload but the first
-    reduce-scatter step's. Both ops run in one session: a quantized ring's result depends on the ring order (the
-    partial sums that get quantized), which the master may choose differently per session."""
-    import threading
-
-    from pccl_amd.ops import kernels as K
-    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
-    monkeypatch.setenv("PCCL_QUANT_PIECE_BYTES", str(1 << 20))
-    world, n = 4, 3_000_017
-    inputs = [torch.randn(n, generator=torch.Generator().manual_seed(60 + r)).bfloat16() for r in range(world)]
-    qopt = pccl.QuantizationOptions(qdtype, algo)
-    bar = threading.Barrier(world)
-    stats = {}
-
-    def switch(rank, mode, prev):
-        bar.wait()
-        if rank == 0:
-            now = K.quant_minmax_stats()
-            if prev is not None:
-                stats[prev] = {k: now[k] - stats["_snap"][k] for k in now}
-            stats["_snap"] = now
-            if mode is not None:
-                os.environ["PCCL_QUANT_FUSED_MINMAX"] = mode  # read by every peer at its op's start
-        bar.wait()
-
-    def fn(rank, comm):
-        x = inputs[rank].to(hip)
-        out = []
-        prev = None
-        for tag, mode in enumerate(("1", "0")):
-            switch(rank, mode, prev)
-            y = torch.empty_like(x)
-            info = comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag, quantization_options=qopt)
-            torch.cuda.synchronize()
-            out.append((y.cpu(), info.tx_bytes, info.rx_bytes))
-            prev = mode
-        switch(rank, None, prev)
-        return out
-
-    monkeypatch.setenv("PCCL_QUANT_FUSED_MINMAX", "1")
-    res = _run(world, fn)
-    for (yf, txf, rxf), (yp, txp, rxp) in res:
-        assert torch.equal(yf, yp)
-        assert (txf, rxf) == (txp, rxp)
-        assert torch.equal(yf, res[0][0][0])
-    # per peer: world - 1 reduce-scatter payloads + 1 all-gather payload, the first of them without partials
-    assert stats["1"] == {"folds": world * (world - 1), "passes": world}
-    assert stats["0"] == {"folds": 0, "passes": world * world}
 
 
 def test_device_shared_state(hip):

@@ -63,14 +63,18 @@ def test_device_finalize_avg(hip, dtype):
 
 
 @pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("qdtype", [torch.uint8, torch.int8, torch.int16, getattr(torch, "float8_e4m3fn", None),
+@pytest.mark.parametrize("qdtype", [torch.uint8, torch.int8, torch.int16, torch.int32, torch.int64,
+                                    getattr(torch, "uint16", None), getattr(torch, "uint32", None),
+                                    getattr(torch, "uint64", None), getattr(torch, "float8_e4m3fn", None),
                                     getattr(torch, "float8_e5m2", None)])
 @pytest.mark.parametrize("algo", ["min_max", "zero_point_scale"])
 def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
+    """HIP quantize / de-quantize-reduce vs the host kernels, bit for bit, for every wire type of both algorithms
+    (zero-point-scale: 8- to 64-bit integers, like the reference's piquant map)."""
     if qdtype is None:
-        pytest.skip("no fp8 dtype")
-    if algo == "zero_point_scale" and qdtype not in (torch.uint8, torch.int8):
-        pytest.skip("zps is 8-bit integer only")
+        pytest.skip("dtype not in this torch build")
+    if algo == "zero_point_scale" and qdtype.is_floating_point:
+        pytest.skip("zero-point-scale needs an integer wire type")
     x = _rand((1 << 20) + 7, vdtype, 14)
     qh, mh = K.quantize(x, qdtype, algo)
     qd, md = K.quantize(x.to(hip), qdtype, algo)

@@ -101,9 +101,21 @@ def test_fp8_quant_roundtrip(qdtype):
     assert ((out - x).abs() <= x.abs() * rel + amax * 2 ** -9).all()
 
 
-def test_zero_point_scale_roundtrip():
-    x = _rand(4096, torch.float32, 8)
-    q, meta = K.quantize(x, torch.uint8, "zero_point_scale")
+@pytest.mark.parametrize("qdtype", ["uint8", "int8", "uint16", "int16", "uint32", "int32", "uint64", "int64"])
+@pytest.mark.parametrize("shift", [0.0, -5.0, 5.0])
+def test_zero_point_scale_roundtrip(qdtype, shift):
+    """Zero-point-scale to every integer wire type the reference's piquant map accepts (int8 .. uint64,
+    /root/reference/ccoip/internal/piquant_utils.hpp:13-38); mostly-negative / mostly-positive data moves the zero
+    point to the ends of the range. Wide types are limited by the float math of the formula (scale in float), not by
+    the wire range."""
+    qt = getattr(torch, qdtype, None)
+    if qt is None:
+        pytest.skip(f"no torch.{qdtype}")
+    x = _rand(4096, torch.float32, 8) + shift
+    q, meta = K.quantize(x, qt, "zero_point_scale")
+    assert q.dtype == qt
     out = K.dequant_reduce(torch.zeros_like(x), q, meta, "zero_point_scale", "set")
-    step = (x.max() - x.min()).item() / 255
-    assert (out - x).abs().max().item() <= step * 0.51 + 1e-6
+    bits = torch.iinfo(qt).bits
+    step = (x.max() - x.min()).item() / (2 ** bits - 1)
+    amax = x.abs().max().item()
+    assert (out - x).abs().max().item() <= step * 0.51 + amax * 2 ** -22 + 1e-6

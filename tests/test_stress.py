@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PEER = os.path.join(HERE, "workers", "stress_peer.py")
 
 
-def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
+def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None):
     rng = random.Random(1234)
     stop = tmp_path / "stop"
     procs, killed, signalled = [], 0, set()
@@ -29,7 +29,8 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False):
         def spawn():
             # stdout to a file: a long soak must never block a peer on a full pipe
             out = open(tmp_path / f"peer{len(procs)}.out", "w+")
-            procs.append((spawn_python([PEER, addr, str(stop)], env={"OMP_NUM_THREADS": "1", "STRESS_DEVICE": device},
+            procs.append((spawn_python([PEER, addr, str(stop)], env={"OMP_NUM_THREADS": "1", "STRESS_DEVICE": device,
+                                                                     **(env or {})},
                                        stdout=out, stderr=subprocess.STDOUT, text=True), out))
         for _ in range(target):
             spawn()
@@ -100,6 +101,19 @@ def test_random_kill_respawn_gpu_ipc(tmp_path, hip):
     kernels; no wrong result, survivors progress, everyone alive at the end exits cleanly."""
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
     killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60)
+    assert killed >= 3
+    assert summaries and all(s["bad"] == 0 for s in summaries), summaries
+    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+
+
+@pytest.mark.gpu
+def test_random_kill_respawn_gpu_ring(tmp_path, hip):
+    """The same random SIGKILL / respawn schedule on the loopback-TCP device ring (PCCL_DISABLE_IPC=1) with a 64 MiB
+    tensor per step next to the small ones, so kills land mid-pipeline (staging copies, fused reduce kernels and
+    send-ahead stripes in flight): no wrong result, survivors progress, everyone alive at the end exits cleanly."""
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
+    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60,
+                                    env={"PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "64"})
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
     assert sum(s["ok_ops"] for s in summaries) > 10, summaries

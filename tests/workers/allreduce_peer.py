@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--busy-threads", type=int, default=0,
                     help="extra threads that keep making syscalls (a SIGKILLed process with many live threads takes "
                          "longer to tear down: its group leader is a zombie while the other threads still exit)")
+    ap.add_argument("--pool", type=int, default=0, help="P2P connection pool size (0: library default)")
+    ap.add_argument("--max-failures", type=int, default=50, help="exit 3 after more failed ops than this")
+    ap.add_argument("--report-mem", action="store_true", help="add the GPU's used bytes (all processes) to every line")
     ap.add_argument("--verify-restore-ms", type=int, default=-1,
                     help="in-place: after a failed op wait this long, then require the buffer to be bit-exactly the "
                          "input again (the abort restore must not be overwritten by a late peer write)")
@@ -68,7 +71,7 @@ def main():
         else None
     dev = torch.device(a.device)
     t_start = time.perf_counter()
-    comm = pccl.Communicator(a.master, 0)
+    comm = pccl.Communicator(a.master, 0, **({"p2p_connection_pool_size": a.pool} if a.pool else {}))
     comm.connect(n_attempts=30)
     if not a.no_wait:
         wait_for_world(comm, a.world, timeout=120)
@@ -104,9 +107,13 @@ def main():
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
                 rec["restore_bad"] = not bool((x == val).all())
+            if a.report_mem and dev.type == "cuda":
+                free, total = torch.cuda.mem_get_info(dev)
+                rec["hbm_used"] = total - free
+                rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
             print(json.dumps(rec), flush=True)
             failures += 1
-            if failures > 50:
+            if failures > a.max_failures:
                 sys.exit(3)
             continue  # retry the step with the new world
         if dev.type == "cuda":
@@ -123,6 +130,9 @@ def main():
                "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
         if dev.type == "cuda":
             rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
+            if a.report_mem:
+                free, total = torch.cuda.mem_get_info(dev)
+                rec["hbm_used"] = total - free
         if a.const and not (lo == hi == float(info.local_world_size)):
             rec["bad"] = True
         print(json.dumps(rec), flush=True)

@@ -34,6 +34,9 @@ def main():
     weights = torch.zeros(4096, device=dev)
     state = pccl.SharedState([pccl.TensorInfo.from_torch(weights, "weights")])
     grads = [torch.ones(64 * 64 * (k + 1) * (64 if dev.type == "cuda" else 1), device=dev) for k in range(n_tensors)]
+    big_mib = int(os.environ.get("STRESS_BIG_MIB", "0"))  # one large tensor: kills land mid-pipeline
+    if big_mib:
+        grads.append(torch.ones(big_mib << 18, device=dev))
     bad, ok_ops, failed_ops, steps, syncs = 0, 0, 0, 0, 0
     reduce_thread = None
     result = {}
