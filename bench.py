@@ -551,32 +551,80 @@ def run_extras(job, a, nbytes):
         with _full_cpu_mask():
             r = rejoin_latency(job)
         extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
-    elif job.n_gpus > 1 and os.environ.get("PCCL_BENCH_RCCL", "1") == "1":
-        extra["rccl_reference"] = rccl_reference(job, a, nbytes)
+    else:
+        extra["multi_gpu_table"] = multi_gpu_table(job, a, nbytes)
     return extra, sweep
 
 
+SIZES_MIB = (1, 16, 256, 1024)
+
+
+def _size_row(job, P, ts):
+    return {f"{m}MiB": {"ms": round(t * 1e3, 4), "bus_bw_per_peer_GBps": round(_bw(m << 20, t, P)[1], 3)}
+            for m, t in ts.items()}
+
+
+def multi_gpu_table(job, a, nbytes):
+    """N > 1: the same sizes (1 / 16 / 256 / 1024 MiB) through RCCL (one rank per GPU, the vendor yardstick) and
+    through the xGMI path in each of its variants: one-shot push (default), two-shot (PCCL_IPC_ALGO=two_shot) and push
+    with a larger remote-aware workgroup budget (PCCL_IPC_REMOTE_GRID=1024), so the first cross-GPU run decides the
+    algorithm and the budget from data. Every variant is failure-isolated (an error is reported in its entry)."""
+    import pccl_amd as pccl
+    P = job.total
+    table = {"sizes_MiB": list(SIZES_MIB), "peers": P, "gpus": job.n_gpus}
+    if job.n_gpus > 1 and os.environ.get("PCCL_BENCH_RCCL", "1") == "1":
+        table["rccl"] = rccl_reference(job, a, nbytes)
+    else:
+        table["rccl"] = {"skipped": "peers share one GPU (RCCL needs one rank per GPU)"}
+    variants = [("ipc_push", {}), ("ipc_two_shot", {"PCCL_IPC_ALGO": "two_shot"}),
+                ("ipc_push_remote_grid_1024", {"PCCL_IPC_REMOTE_GRID": "1024"})]
+    for name, env in variants:
+        saved = {k: os.environ.get(k) for k in env}
+        try:
+            os.environ.update(env)  # read per op by the library; every rank switches at the same phase boundary
+            r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
+                        sweep=tuple(m << 20 for m in SIZES_MIB if (m << 20) < nbytes))
+            ts = {m: r["sweep"][m << 20] for m in SIZES_MIB if (m << 20) < nbytes}
+            ts[nbytes >> 20] = r["t"]
+            table[name] = {"sizes": _size_row(job, P, ts), "result_exact": r.get("ok"),
+                           "reduce_path": pccl.ReducePath(r["path"]).name}
+        except Exception as e:  # noqa: BLE001 - one variant's failure must not hide the others
+            table[name] = {"error": repr(e)[:300]}
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return table
+
+
 def rccl_reference(job, a, nbytes):
-    """RCCL (torch.distributed "nccl" backend) all-reduce of the same 1 GiB bf16 buffer, one rank per GPU: the
-    MI355X vendor collective as a yardstick for the xGMI path (RCCL has no elastic membership, so it is not an
-    alternative for PCCL's use case). N > 1 distinct GPUs only."""
+    """RCCL (torch.distributed "nccl" backend) all-reduce of bf16 buffers of SIZES_MIB, one rank per GPU: the MI355X
+    vendor collective as a yardstick for the xGMI path (RCCL has no elastic membership, so it is not an alternative for
+    PCCL's use case). N > 1 distinct GPUs only."""
     torch = job.torch
     dist = job.dist
     try:
         g = dist.new_group(backend="nccl")
         x = torch.randn(nbytes // 2, device=job.dev, dtype=torch.bfloat16)
-        for _ in range(max(2, a.warmup)):
-            dist.all_reduce(x, group=g)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            dist.all_reduce(x, group=g)
-        torch.cuda.synchronize()
-        dt = job.max_over_job([time.perf_counter() - t0]) / a.steps
-        dist.destroy_process_group(g)
         n = job.world
-        return {"ranks": n, "ms_per_op": round(dt * 1e3, 4), "bus_bw_per_rank_GBps": round(_bw(nbytes, dt, n)[1], 3)}
+        out = {"ranks": n}
+        for m in SIZES_MIB:
+            v = x[:min(x.numel(), (m << 20) // 2)]
+            reps = max(a.steps, min(200, int(4e9 // max(v.numel() * 2, 1))))
+            for _ in range(max(2, a.warmup)):
+                dist.all_reduce(v, group=g)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                dist.all_reduce(v, group=g)
+            torch.cuda.synchronize()
+            dt = job.max_over_job([time.perf_counter() - t0]) / reps
+            out[f"{m}MiB"] = {"ms": round(dt * 1e3, 4), "bus_bw_per_rank_GBps": round(_bw(v.numel() * 2, dt, n)[1], 3)}
+        dist.destroy_process_group(g)
+        return out
     except Exception as e:  # noqa: BLE001 - a yardstick: report, never fail the bench
         return {"error": repr(e)[:300]}
 

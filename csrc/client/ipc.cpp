@@ -83,7 +83,7 @@ struct alignas(64) OpPeerShm {
     uint32_t dtype;
     uint32_t op;
     uint32_t zero_copy; // bit 0: input is the caller's send buffer, bit 1: output is the caller's receive buffer
-    uint32_t pad;
+    uint32_t algo;      // 0 push, 1 two-shot (PCCL_IPC_ALGO at the vote; every peer must vote the same)
     uint64_t gpu_uid;   // physical GPU of this op's buffers (peers sharing a GPU split its CUs)
     uint32_t in_segs, out_segs;
     uint64_t in_off, out_off; // offset into the (single) exported allocation
@@ -675,12 +675,9 @@ bool IpcArena::all_local_peers() const {
     return std::all_of(pids_.begin(), pids_.end(), [&](int p) { return p == pids_[rank_]; });
 }
 
-bool IpcArena::push_algorithm() {
-    static const bool two_shot = [] {
-        const char *v = std::getenv("PCCL_IPC_ALGO");
-        return v && std::strcmp(v, "two_shot") == 0;
-    }();
-    return !two_shot;
+bool IpcArena::push_algorithm() { // read per op (the bench switches it between phases; the vote checks agreement)
+    const char *v = std::getenv("PCCL_IPC_ALGO");
+    return !(v && std::strcmp(v, "two_shot") == 0);
 }
 
 void IpcArena::drain_peers(Client &c, uint64_t seq) {
@@ -816,6 +813,7 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     mine->gpu_uid = device_ok ? be->device_uid(device) : 0;
     mine->vote = device_ok ? 1 : 0;
     mine->zero_copy = (in_direct ? 1u : 0u) | (out_direct ? 2u : 0u);
+    mine->algo = push_algorithm() ? 0u : 1u;
     mine->device = device;
     mine->bytes = bytes;
     mine->dtype = static_cast<uint32_t>(dtype);
@@ -849,7 +847,8 @@ int IpcArena::vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, i
     for (size_t k = 0; k < ring_.size(); ++k) {
         const OpPeerShm *p = shm_->op(slot, static_cast<uint32_t>(k));
         all = all && p->vote == 1 && p->bytes == bytes && p->dtype == static_cast<uint32_t>(dtype) &&
-              p->op == static_cast<uint32_t>(op) && p->in_segs >= 1 && p->in_segs <= kIpcMaxSegs &&
+              p->op == static_cast<uint32_t>(op) && p->algo == mine->algo && p->in_segs >= 1 &&
+              p->in_segs <= kIpcMaxSegs &&
               p->out_segs >= 1 && p->out_segs <= kIpcMaxSegs;
     }
     if (!all) {
@@ -1003,7 +1002,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
-    const bool push = inter != nullptr || push_algorithm();
+    const bool push = inter != nullptr || shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_))->algo == 0;
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
@@ -1057,7 +1056,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     // peers whose kernels run concurrently on this GPU, but not below 256 per kernel (fewer cannot saturate HBM)
     std::vector<uint64_t> uids(W);
     for (size_t k = 0; k < W; ++k) uids[k] = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->gpu_uid;
-    static const int remote_grid = static_cast<int>(env_size("PCCL_IPC_REMOTE_GRID", 0));
+    const int remote_grid = static_cast<int>(env_size("PCCL_IPC_REMOTE_GRID", 0)); // per op: bench phases switch it
     const int grid = ipc_push_grid(uids, rank_, remote_grid);
     // system-scope release at kernel end when a destination lives on another GPU, or is a staged buffer that the
     // copy-out reads with a copy engine: without it whole 4 KiB workgroup tiles of the result were still zero in the
