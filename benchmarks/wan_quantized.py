@@ -90,6 +90,14 @@ def peer(a):
     comm.destroy()
 
 
+def _proc_cpu_s(pid):
+    """user + sys CPU seconds of a process (the relay: its CPU use next to the bytes it moved)."""
+    with open(f"/proc/{pid}/stat") as f:
+        st = f.read()
+    fields = st[st.rindex(")") + 2:].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--peers", type=int, default=8)
@@ -99,6 +107,7 @@ def main():
     ap.add_argument("--link-mbit", type=float, default=25000)
     ap.add_argument("--pool", type=int, default=16)
     ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
+    ap.add_argument("--stripes", type=int, default=0, help="PCCL_RING_STRIPES (connections per ring step; 0 = default)")
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--formats", default=",".join(FORMATS))
     ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
@@ -110,6 +119,8 @@ def main():
         return peer(a)
     from pccl_amd.utils import free_ports, local_master, spawn_python
     env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)}
+    if a.stripes:
+        env["PCCL_RING_STRIPES"] = str(a.stripes)
     args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
             "--concurrent", str(a.concurrent),
             "--formats", a.formats]
@@ -130,6 +141,9 @@ def main():
                                   "--link-mbit", str(a.link_mbit), *maps], stdout=subprocess.PIPE,
                                  stderr=subprocess.DEVNULL, text=True)
         relay.stdout.readline()  # {"relay": "ready"}
+    t_run0 = time.perf_counter()
+    relay_cpu0 = _proc_cpu_s(relay.pid) if relay is not None else None
+    relay_cpu = None
     try:
         with local_master() as addr:
             ps = [spawn_python([os.path.abspath(__file__), "--rank", str(r), "--master", addr, "--ports",
@@ -138,6 +152,8 @@ def main():
             outs = [p.communicate(timeout=1500) for p in ps]
     finally:
         relayed = None
+        if relay is not None and relay.poll() is None:
+            relay_cpu = _proc_cpu_s(relay.pid) - relay_cpu0
         if relay is not None:
             relay.terminate()
             try:
@@ -169,8 +185,10 @@ def main():
                       "wan": {"emulator": "pccl_wan_relay (separate process)" if a.emulator == "relay"
                               else "PCCL_SIM_WAN (inside the library)",
                               "one_way_latency_ms": a.latency_ms, "flow_mbit": a.flow_mbit, "link_mbit": a.link_mbit,
-                              "pool": a.pool, "concurrent_ops": a.concurrent,
-                              "relayed_GB": round(relayed / 1e9, 3) if relayed is not None else None},
+                              "pool": a.pool, "concurrent_ops": a.concurrent, "stripes": a.stripes or 4,
+                              "relayed_GB": round(relayed / 1e9, 3) if relayed is not None else None,
+                              "relay_cpu_s": round(relay_cpu, 2) if relay_cpu is not None else None,
+                              "run_s": round(time.perf_counter() - t_run0, 2)},
                       "reference_published_Gbit": {"transatlantic": 25, "collocated_eu": 45},
                       "formats": summary}), flush=True)
 

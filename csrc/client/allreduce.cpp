@@ -363,7 +363,9 @@ namespace {
 // before any data moves (reference reduce.cpp:154-192), one extra latency per ring step. Host and device rings speak
 // the same protocol, so CPU and GPU peers mix in one quantized ring.
 constexpr uint64_t kMetaTagBit = 1ull << 63;
-inline uint64_t lane_tag(uint64_t tag, size_t lane) { return tag ^ (static_cast<uint64_t>(lane) << 60); }
+inline uint64_t lane_tag(uint64_t tag, size_t lane, size_t lanes) {
+    return tag ^ (static_cast<uint64_t>(lane) << 60) ^ (static_cast<uint64_t>(lanes - 1) << 58);
+}
 inline uint64_t meta_tag(uint64_t data_tag) { return data_tag ^ kMetaTagBit; }
 
 // Lane split of a quantized all-reduce of `count` elements (wire element size `qs`) over `ws` peers: element offsets
@@ -451,6 +453,16 @@ size_t ring_stripes() { return std::max<size_t>(1, std::min<size_t>(16, env_size
 size_t stripe_min_bytes() { return std::max<size_t>(1 << 20, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20)); }
 constexpr size_t kStripeAlign = 1 << 20; // multiple of every element size and of the device staging piece
 
+// Connection of stripe k of op `seq` (data tag `tag`) in a pool of `pool`: consecutive ops, and the lanes of one
+// quantized op (lane_tag: lane in bits 60-61, lane count - 1 in bits 58-59), start PCCL_RING_STRIPES connections
+// apart, so concurrent ops spread over the whole pool instead of piling onto its first connections (a long-fat-pipe
+// link is filled by many concurrent ops, reference src/pccl.cpp:345-523). Sender and receiver derive the same index.
+size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool) {
+    const uint64_t lanes = ((tag >> 58) & 3) + 1, lane = (tag >> 60) & 3;
+    const uint64_t base = (seq * lanes + lane) * ring_stripes();
+    return static_cast<size_t>((base + k) % pool);
+}
+
 StripePlan plan_stripes(size_t bytes, size_t conns) {
     StripePlan s;
     size_t p = std::min({ring_stripes(), std::max<size_t>(1, conns), std::max<size_t>(1, bytes / stripe_min_bytes())});
@@ -496,8 +508,8 @@ int striped_step(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
                  const std::function<int()> &before_rx = {}, size_t gran = 0) {
     const StripePlan tp = plan_stripes(tx_bytes, txs.size());
     const StripePlan rp = plan_stripes(rx_bytes, rxs.size());
-    auto rx_conn = [&](size_t k) { return rxs[(seq + k) % rxs.size()].get(); };
-    auto tx_conn = [&](size_t k) { return txs[(seq + k) % txs.size()].get(); };
+    auto rx_conn = [&](size_t k) { return rxs[stripe_conn(seq, tag, k, rxs.size())].get(); };
+    auto tx_conn = [&](size_t k) { return txs[stripe_conn(seq, tag, k, txs.size())].get(); };
     bool sinks_posted = false;
     auto remove_sinks = [&] {
         if (!sinks_posted) return;
@@ -652,7 +664,8 @@ int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::
     const size_t es = dtype_size(q.dtype);
     const size_t qs = quant ? dtype_size(q.qtype) : es;
     const size_t chunk = net::multiplex_chunk_size();
-    StepIo io{txs[seq % txs.size()].get(), rxs[seq % rxs.size()].get(), meta_tag(tag), seq};
+    StepIo io{txs[stripe_conn(seq, tag, 0, txs.size())].get(), rxs[stripe_conn(seq, tag, 0, rxs.size())].get(),
+              meta_tag(tag), seq};
 
     const auto bounds = chunk_bounds(count, ws);
     size_t max_chunk = 0;
@@ -787,7 +800,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
                                          : std::vector<size_t>{0, q.count};
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
-        return host_ring(rv.tx, rv.rx, ws, rank, lane_tag(q.tag, k), seq, dst + a * es, b - a, q, quant, abort_fn,
+        return host_ring(rv.tx, rv.rx, ws, rank, lane_tag(q.tag, k, lo.size() - 1), seq, dst + a * es, b - a, q, quant, abort_fn,
                          op.tx, op.rx);
     });
     if (rc) {
@@ -914,7 +927,7 @@ struct ReadyRanges {
 };
 
 // The send side of one pipelined ring op: one thread per stripe for the whole op (not per step), each sending its
-// stripe of every step in order over connection (seq + k) % pool. The op thread publishes step g (payload, bytes,
+// stripe of every step in order over connection stripe_conn(seq, tag, k). The op thread publishes step g (payload, bytes,
 // readiness) as soon as step g may start sending — with send-ahead while step g-1 still receives — and a stripe thread
 // streams each piece once it is readable. Per-op threads instead of the connections' shared sender threads: a stripe
 // thread may wait on its op's network progress (the previous peer's data), which must never hold up another op's
@@ -987,7 +1000,7 @@ private:
             }
             const StripePlan tp = plan_stripes(st.bytes, txs_.size());
             if (k >= tp.off.size() || tp.len[k] == 0) continue;
-            net::MuxConn *c = txs_[(seq_ + k) % txs_.size()].get();
+            net::MuxConn *c = txs_[stripe_conn(seq_, tag_, k, txs_.size())].get();
             const size_t base = tp.off[k], len = tp.len[k];
             for (size_t sent = 0; sent < len;) {
                 const size_t n = std::min(frame_, len - sent);
@@ -1109,7 +1122,7 @@ private:
         size_t remaining = 0;     // stripes not yet fully consumed
         bool posted = false;
     };
-    net::MuxConn *conn(size_t k) const { return rxs_[(seq_ + k) % rxs_.size()].get(); }
+    net::MuxConn *conn(size_t k) const { return rxs_[stripe_conn(seq_, tag_, k, rxs_.size())].get(); }
     const std::vector<std::shared_ptr<net::MuxConn>> &rxs_;
     const uint64_t tag_, seq_;
     std::vector<Step> steps_;
@@ -1495,7 +1508,8 @@ int device_quant_lane(QLane &L) {
         max_stripes = std::max(max_stripes, plan_stripes(nel(chunk_tx(g)) * qs, L.txs->size()).off.size());
     OpSenders senders(*L.txs, L.tag, seq, piece_el * qs, nsteps, max_stripes, be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, nsteps);
-    const StepIo io{(*L.txs)[seq % L.txs->size()].get(), (*L.rxs)[seq % L.rxs->size()].get(), meta_tag(L.tag), seq};
+    const StepIo io{(*L.txs)[stripe_conn(seq, L.tag, 0, L.txs->size())].get(),
+                    (*L.rxs)[stripe_conn(seq, L.tag, 0, L.rxs->size())].get(), meta_tag(L.tag), seq};
 
     auto can_post = [&](size_t g) {
         if (g < kNb) return true;
@@ -1680,7 +1694,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     OpAbort aborted([this, t = q.tag] { return abort_received(t); });
     std::atomic<bool> op_failed{false};
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
-        QLane L{&rv.tx, &rv.rx, ws, rv.rank, lane_tag(q.tag, k), seq, be, pq, lane_streams[k]->get(), ready,
+        QLane L{&rv.tx, &rv.rx, ws, rv.rank, lane_tag(q.tag, k, nl), seq, be, pq, lane_streams[k]->get(), ready,
                 dst + a * es, b - a, es, qs, piece / es, q.dtype, q.qtype, q.qalgo, q.op, device,
                 [&] { return aborted(); }, &op.tx, &op.rx, &op_failed};
         return device_quant_lane(L);

@@ -1,7 +1,7 @@
 #pragma once
 // Bounded busy-wait used before blocking on a condition variable in the latency-critical waits (master packets,
 // P2P sink progress): a futex wake-up of a sleeping thread costs 10-50 us on a loaded host, several times the
-// loopback round trip of a small collective. PCCL_SPIN_US (default 50, 0 disables) bounds the spin per wait.
+// loopback round trip of a small collective. 50 us bound the spin per wait.
 #include <sys/prctl.h>
 
 #include <chrono>
@@ -11,10 +11,7 @@
 
 namespace pccl {
 
-inline long spin_budget_us() {
-    static const long us = static_cast<long>(env_size("PCCL_SPIN_US", 50));
-    return us;
-}
+constexpr long spin_budget_us() { return 50; }
 
 /// The short sleeps of the op threads (IPC barriers: 5 us) would otherwise round up to the default 50 us timer
 /// slack; 1 us for the calling thread, once per thread.

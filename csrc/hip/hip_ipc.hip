@@ -8,11 +8,6 @@
 
 namespace pccl::hipk {
 
-static int env_int(const char *name, int dflt) {
-    const char *v = std::getenv(name);
-    return v && *v ? std::atoi(v) : dflt;
-}
-
 bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, int n, size_t count, DType t,
                          ReduceOp op, hipStream_t st, int max_grid_hint, bool release) {
     if (count == 0) return true;
@@ -41,16 +36,14 @@ bool launch_multi_reduce(void *const *dsts, int ndst, const void *const *srcs, i
             bool ok = true;
             if (nvec > 0) {
                 // 512 workgroups (2 per CU) and 2 vectors per thread measured best on MI355X for one kernel per GPU
-                // (profiles/r1_ipc_grid_sweep.md); concurrent peers on one GPU pass a smaller budget. PCCL_IPC_GRID
-                // overrides the budget (8-GPU tuning).
+                // (profiles/r1_ipc_grid_sweep.md); concurrent peers on one GPU pass a smaller budget.
                 // Single destination (two-shot / hierarchical host-local reduce) uses k_multi_reduce_tile (contiguous
                 // tile per workgroup, non-temporal loads, 4 vectors per thread): 8 srcs -> 1 dst 5000 -> 5586 GB/s.
                 // The multi-destination push keeps the strided kernel (2 -> 2: 5420 vs 5080 GB/s tiled);
                 // profiles/r1_ipc_tiled.md.
-                static const int env_grid = env_int("PCCL_IPC_GRID", 0);
                 const bool tiled = ndst == 1;
                 const int unroll = tiled ? 4 : 2;
-                const int max_grid = env_grid > 0 ? env_grid : (max_grid_hint > 0 ? max_grid_hint : 512);
+                const int max_grid = max_grid_hint > 0 ? max_grid_hint : 512;
                 const int grid = std::max(1, std::min(grid_for(nvec, unroll), max_grid));
                 ok = launch_ok([&] {
                     auto go = [&](auto avg_c, auto u_c) {

@@ -81,9 +81,8 @@ void EventServer::loop() {
     std::vector<epoll_event> events(256);
     // After a batch of events, poll without blocking for a short while before sleeping in epoll_wait: the peers'
     // packets of one consensus (8 collective initiates, 8 completes) arrive spread over tens of microseconds, and a
-    // sleeping loop thread pays a scheduler wake-up (10-30 us on a loaded host) for each. PCCL_MASTER_SPIN_US
-    // (default 100, 0 = always block) bounds the spin.
-    static const long spin_us = static_cast<long>(env_size("PCCL_MASTER_SPIN_US", 100));
+    // sleeping loop thread pays a scheduler wake-up (10-30 us on a loaded host) for each. 100 us bounds the spin.
+    constexpr long spin_us = 100;
     auto last_event = std::chrono::steady_clock::now() - std::chrono::hours(1);
     while (!stop_) {
         const bool spinning = spin_us > 0 && std::chrono::steady_clock::now() - last_event < std::chrono::microseconds(spin_us);

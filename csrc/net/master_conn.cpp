@@ -53,10 +53,7 @@ int64_t steady_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
 }
-int64_t rx_spin_ns() {
-    static const int64_t ns = static_cast<int64_t>(env_size("PCCL_MASTER_RX_SPIN_US", 200)) * 1000;
-    return ns;
-}
+constexpr int64_t rx_spin_ns() { return 200 * 1000; }
 } // namespace
 
 bool MasterConnection::send_raw(uint16_t id, const std::vector<uint8_t> &payload) {

@@ -76,7 +76,7 @@ private:
     std::atomic<uint64_t> gen_{0}; // bumped per queued packet (spinning waiters watch it without the lock)
     // steady-clock ns until which the RX thread polls the socket instead of sleeping in recv(): set by every send
     // (a request to the master is usually answered within tens of us, and waking a thread parked on an idle core
-    // costs about as much - PCCL_MASTER_RX_SPIN_US, default 200, 0 off)
+    // costs about as much: 200 us)
     std::atomic<int64_t> rx_hot_until_{0};
 };
 

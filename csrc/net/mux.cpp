@@ -88,7 +88,7 @@ static void wan_shape(size_t n, double &flow_next_free, double &last_send) {
 
 MuxConn::MuxConn(int fd, Mode mode, const SockAddr &peer_addr)
     : fd_(fd), mode_(mode), peer_addr_(peer_addr),
-      zerocopy_(mode == Mode::Tx && fd >= 0 && zerocopy_send_enabled() && socket_zerocopy_on(fd)) {}
+      zerocopy_(mode == Mode::Tx && fd >= 0 && socket_zerocopy_on(fd)) {}
 
 MuxConn::~MuxConn() {
     interrupt();

@@ -88,14 +88,14 @@ void tune_socket(int fd, bool bulk) {
             int sz = 8 << 20;
             setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
             setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
-            if (zerocopy_send_enabled()) setsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one));
+            setsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one)); // best effort (socket_zerocopy_on)
         }
         // like the reference's data sockets (tinysockets/src/multiplexed_socket.cpp:51-59): immediate ACKs, and busy
         // polling of the device queue on NICs that support it (best effort: a value above net.core.busy_poll needs
         // CAP_NET_ADMIN, and loopback has no NAPI queue to poll)
         setsockopt(fd, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof(one));
-        int busy = static_cast<int>(env_size("PCCL_SO_BUSY_POLL_US", 50));
-        if (busy > 0) setsockopt(fd, SOL_SOCKET, SO_BUSY_POLL, &busy, sizeof(busy));
+        int busy = 50;
+        setsockopt(fd, SOL_SOCKET, SO_BUSY_POLL, &busy, sizeof(busy));
     }
 }
 
@@ -105,10 +105,6 @@ bool socket_zerocopy_on(int fd) {
     return ::getsockopt(fd, SOL_SOCKET, SO_ZEROCOPY, &v, &l) == 0 && v != 0;
 }
 
-bool zerocopy_send_enabled() {
-    static const bool on = env_size("PCCL_ZEROCOPY_SEND", 1) != 0;
-    return on;
-}
 
 int connect_tcp(const SockAddr &addr, int timeout_ms) {
     sockaddr_storage ss{};
@@ -219,7 +215,7 @@ bool sendv_all(int fd, iovec *iov, int iovcnt) {
     return true;
 }
 
-// MSG_ZEROCOPY send (PCCL_ZEROCOPY_SEND=1 (default) and a same-host socket: socket_zerocopy_on): the kernel pins the
+// MSG_ZEROCOPY send (same-host sockets, socket_zerocopy_on): the kernel pins the
 // user pages instead of copying them into socket buffers and reports completion on the socket's error queue; the call returns once every
 // byte it sent is released, so the caller may reuse the buffer as after a plain send. On loopback the kernel copies
 // the pages anyway when it delivers them to the receiving socket ("deferred copy", reported as

@@ -31,9 +31,8 @@ int listen_tcp(ccoip_inet_protocol_t proto, uint16_t port, bool bump, uint16_t &
 // Full send / receive. Return false on error or EOF. recv_all honours an optional abort flag polled every 100 ms.
 bool send_all(int fd, const void *data, size_t n);
 bool sendv_all(int fd, struct iovec *iov, int iovcnt);
-// MSG_ZEROCOPY variant (PCCL_ZEROCOPY_SEND=1); `next_id` = the socket's notification counter (starts at 0)
+// MSG_ZEROCOPY variant (same-host sockets); `next_id` = the socket's notification counter (starts at 0)
 bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id);
-bool zerocopy_send_enabled();
 bool socket_zerocopy_on(int fd); // SO_ZEROCOPY is set (else MSG_ZEROCOPY would be ignored: no completions)
 bool recv_all(int fd, void *data, size_t n);
 

@@ -60,7 +60,10 @@ def main(d, bin_ms=20.0, skip_ms=0.0):
     for r in kernels:
         a, b = int(_col(r, "Start_Timestamp")), int(_col(r, "End_Timestamp"))
         name = _col(r, "Kernel_Name") or "?"
-        key = "blit" if "rocclr" in name.lower() else "k_reduce_copy" if "reduce_copy" in name else "kernel:other"
+        low = name.lower()
+        key = ("blit" if "rocclr" in low else "k_reduce_copy" if "reduce_copy" in name else
+               "k_dq" if "k_dq_" in name else "k_q" if "k_q_" in name else "k_minmax" if "minmax" in name else
+               "kernel:other")
         series[key].append((a, b))
     t0 = min(a for v in series.values() for a, _ in v) + int(skip_ms * 1e6)
     t1 = max(b for v in series.values() for _, b in v)
