@@ -2,6 +2,7 @@
 
     python benchmarks/wan_quantized.py [--peers 8] [--mib 2048] [--latency-ms 50] [--flow-mbit 1000]
                                         [--link-mbit 25000] [--device cuda:0|cpu] [--pool 16] [--concurrent 8]
+                                        [--concurrent-quant 32] [--stripes 4]
 
 Defaults model a transatlantic long fat pipe: 50 ms one way, ~1 Gbit/s per TCP flow (window-limited at 100 ms RTT),
 a 25 Gbit/s NIC per peer (the reference's transatlantic figure), 16 pooled connections per neighbour.
@@ -68,11 +69,14 @@ def peer(a):
         comm.all_reduce(x[:65536], y[:65536], op=pccl.ReduceOp.AVG, tag=tag, quantization_options=qopts[f])
         tag += 1
         # --concurrent all-reduces of equal slices in flight at once over the connection pool (the reference's
-        # recipe for long fat pipes: pcclAllReduceMultipleWithRetry, docs/md/01_Introduction.md:8)
+        # recipe for long fat pipes: pcclAllReduceMultipleWithRetry, docs/md/01_Introduction.md:8). A quantized
+        # op moves 4x fewer bytes per ring step while every step still pays the link latency (and a reduce-scatter
+        # step cannot start before the previous one's min / max exist): --concurrent-quant slices keep the link busy
+        conc = a.concurrent if qopts[f] is None else (a.concurrent_quant or a.concurrent)
         q = qopts[f] or pccl.QuantizationOptions(D.FLOAT, Q.NONE)
-        per = (n + a.concurrent - 1) // a.concurrent
+        per = (n + conc - 1) // conc
         descs = []
-        for k in range(a.concurrent):
+        for k in range(conc):
             lo, hi = k * per, min(n, (k + 1) * per)
             rd = pccl.ReduceDescriptor(hi - lo, pccl.ReduceOp.AVG, tag, pccl.ReduceOperandDescriptor(D.FLOAT), q)
             descs.append(pccl.ReduceOpDescriptor.from_torch(x[lo:hi], y[lo:hi], rd))
@@ -80,7 +84,7 @@ def peer(a):
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=a.concurrent)
+        info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -107,6 +111,7 @@ def main():
     ap.add_argument("--link-mbit", type=float, default=25000)
     ap.add_argument("--pool", type=int, default=16)
     ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
+    ap.add_argument("--concurrent-quant", type=int, default=32, help="the same for the quantized formats (0: --concurrent)")
     ap.add_argument("--stripes", type=int, default=0, help="PCCL_RING_STRIPES (connections per ring step; 0 = default)")
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--formats", default=",".join(FORMATS))
@@ -118,11 +123,12 @@ def main():
     if a.rank is not None:
         return peer(a)
     from pccl_amd.utils import free_ports, local_master, spawn_python
-    env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20)}
+    env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20),
+           "PCCL_MAX_CONCURRENT_COLLECTIVE_OPS": str(max(16, a.concurrent, a.concurrent_quant))}
     if a.stripes:
         env["PCCL_RING_STRIPES"] = str(a.stripes)
     args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
-            "--concurrent", str(a.concurrent),
+            "--concurrent", str(a.concurrent), "--concurrent-quant", str(a.concurrent_quant),
             "--formats", a.formats]
     relay = None
     peer_ports = [{} for _ in range(a.peers)]
@@ -185,7 +191,8 @@ def main():
                       "wan": {"emulator": "pccl_wan_relay (separate process)" if a.emulator == "relay"
                               else "PCCL_SIM_WAN (inside the library)",
                               "one_way_latency_ms": a.latency_ms, "flow_mbit": a.flow_mbit, "link_mbit": a.link_mbit,
-                              "pool": a.pool, "concurrent_ops": a.concurrent, "stripes": a.stripes or 4,
+                              "pool": a.pool, "concurrent_ops": a.concurrent,
+                              "concurrent_ops_quantized": a.concurrent_quant or a.concurrent, "stripes": a.stripes or 4,
                               "relayed_GB": round(relayed / 1e9, 3) if relayed is not None else None,
                               "relay_cpu_s": round(relay_cpu, 2) if relay_cpu is not None else None,
                               "run_s": round(time.perf_counter() - t_run0, 2)},

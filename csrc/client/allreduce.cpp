@@ -867,6 +867,16 @@ void step_mark(bool reduce_scatter, size_t step) {
     if (step < 16) trace_mark(reduce_scatter ? rs[step] : ag[step]);
 }
 
+// Waits until every piece of work queued on `s` so far has completed, sleeping between polls (hipStreamSynchronize
+// busy-waits: with 16 quantized lanes syncing once per ring step that took the process's CPU share from the socket
+// copies)
+bool stream_wait_polling(DeviceBackend *be, DevStream s) {
+    DevEvent e = event_pool().get();
+    const bool ok = be->event_record(e, s) && event_wait_polling(be, e);
+    event_pool().put(e);
+    return ok;
+}
+
 // payload bytes [a, b) of a pinned staging buffer become valid once `e` has completed (nullptr: already valid)
 struct Staged {
     size_t a, b;
@@ -1201,8 +1211,8 @@ int device_ring_pipeline(DevRing &R) {
         DevEvent *d2h;
         std::vector<DevEvent> *ev;
         ~Drain() {
-            if (*d2h) be->event_sync(*d2h);
-            be->stream_sync(st);
+            if (*d2h) event_wait_polling(be, *d2h);
+            stream_wait_polling(be, st);
             for (auto e : *ev) event_pool().put(e);
         }
     } drain{be, st, &last_d2h, &owned};
@@ -1402,7 +1412,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         return {rc == 2, rc == 2};
     }
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
-    if (!be->stream_sync(st)) return {false, false};
+    if (!stream_wait_polling(be, st)) return {false, false};
     return {true, false};
 }
 
@@ -1490,7 +1500,7 @@ int device_quant_lane(QLane &L) {
         DevStream st;
         std::vector<DevEvent> *ev;
         ~Drain() {
-            be->stream_sync(st);
+            stream_wait_polling(be, st);
             for (auto e : *ev) event_pool().put(e);
         }
     } drain{be, st, &owned};
@@ -1548,7 +1558,7 @@ int device_quant_lane(QLane &L) {
             g_quant_minmax_passes.fetch_add(1, std::memory_order_relaxed);
             be->minmax(src, n, L.dtype, minmax_out, st);
         }
-        be->stream_sync(st);
+        stream_wait_polling(be, st);
         return kernels::make_meta(L.qalgo, L.dtype, L.qtype, minmax_out[0], minmax_out[1]);
     };
     auto dequant_consume = [&](uint8_t *dst_el, const uint8_t *src_q, size_t n, const kernels::QuantParams &params) {
@@ -1653,8 +1663,10 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     const size_t es = dtype_size(q.dtype), qs = dtype_size(q.qtype);
     auto *dst = static_cast<uint8_t *>(q.dst);
     const size_t bytes = q.count * es;
-    // value bytes per quantize / de-quantize piece (and frame): PCCL_QUANT_PIECE_BYTES, default 8 MiB
-    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_QUANT_PIECE_BYTES", 8u << 20)) / es * es;
+    // value bytes per quantize / de-quantize piece (and frame): PCCL_QUANT_PIECE_BYTES, default 32 MiB (interleaved
+    // A/B, uint8, 8 peers x 1 GiB on one MI355X: 8 MiB 223 ms, 16 MiB 210, 32 MiB 201-206, 64 MiB 204-208;
+    // profiles/r4/ab2/): fewer kernels, copies, events and frames per byte
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_QUANT_PIECE_BYTES", 32u << 20)) / es * es;
 
     be->set_device(device);
     StreamLease stream(device);
@@ -1678,7 +1690,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
         DevStream st;
         DevEvent e;
         ~EvBack() {
-            be->stream_sync(st);
+            stream_wait_polling(be, st);
             event_pool().put(e);
         }
     } ev_back{be, st, ready};
@@ -1709,7 +1721,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     }
     // the lanes' streams are drained (each lane's Drain): the result is complete in HBM
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
-    if (!be->stream_sync(st)) return {false, false};
+    if (!stream_wait_polling(be, st)) return {false, false};
     return {true, false};
 }
 
