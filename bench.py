@@ -803,7 +803,12 @@ def main():
                              for b, t in ring["sweep"].items()}}
     sweep["DEVICE_RING"][f"{a.mib}MiB"] = {"ms": round(ring["t"] * 1e3, 3), "bus_bw_per_peer_GBps": round(bus, 3)}
     if not a.quick:
-        x_extra, x_sweep = extras_in_child(job, a)
+        # PCCL_BENCH_EXTRAS_INPROC=1: the extras in this process (rehearsals with many ranks on one GPU, where a child
+        # per rank would double the processes holding the GPU)
+        if os.environ.get("PCCL_BENCH_EXTRAS_INPROC") == "1":
+            x_extra, x_sweep = run_extras(job, a, nbytes)
+        else:
+            x_extra, x_sweep = extras_in_child(job, a)
         extra.update(x_extra)
         sweep.update(x_sweep)
         if "peer_curve" in extra:

@@ -5,7 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${OUTDIR:-r4_rehearsal}
 mkdir -p $OUT
-export HSA_ENABLE_IPC_MODE_LEGACY=0 PCCL_BENCH_SAME_GPU=1 GPU_MAX_HW_QUEUES=2 PCCL_BENCH_EXTRAS_TIMEOUT=500
+# extras in the ranks themselves: a child per rank would put 16 processes on the one GPU
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PCCL_BENCH_SAME_GPU=1 GPU_MAX_HW_QUEUES=2 PCCL_BENCH_EXTRAS_INPROC=1
 N=${NPROC:-8}
 echo "[$(date +%T)] torchrun $N" >> $OUT/steps.log
 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \

@@ -146,7 +146,8 @@ def test_shareable_memory_api_on_cpu():
     assert isinstance(pccl.memory.maybe_shareable("cpu"), contextlib.nullcontext)
     st = pccl.memory.ipc_buffer_stats()
     assert set(st) == {"direct_in", "direct_out", "staged_in", "staged_out", "quarantined", "zombie_drains",
-                       "preflight_failed", "preflight_passed"} and all(v >= 0 for v in st.values())
+                       "preflight_failed", "preflight_passed", "reclaimed", "quarantine_freed"} and \
+        all(v >= 0 for v in st.values())
     assert pccl.memory.live_bytes() >= 0
     if not torch.cuda.is_available():
         assert not pccl.memory.available()
