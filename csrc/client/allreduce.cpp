@@ -21,6 +21,7 @@
 #include <thread>
 #include <chrono>
 #include <cstring>
+#include <string>
 
 #include "../common/log.hpp"
 #include "../common/spin.hpp"
@@ -381,6 +382,19 @@ std::vector<size_t> quant_lane_bounds(size_t count, size_t ws, size_t qs) {
     for (size_t k = 1; k < nl; ++k) lo[k] = count / nl * k / 4096 * 4096;
     lo[nl] = count;
     return lo;
+}
+
+// finer per-step marks for PCCL_TRACE_OPS (global step g < 32): `kind` q = payload metadata known and its quantize
+// kernels queued, f = first received piece consumed
+void step_sub_mark(char kind, size_t g) {
+    if (g >= 32 || !current_trace()) return;
+    static const auto names = [] {
+        auto *v = new std::vector<std::string>();
+        for (char k : {'q', 'f'})
+            for (int i = 0; i < 32; ++i) v->push_back(std::string(1, k) + std::to_string(i));
+        return v;
+    }();
+    trace_mark((*names)[(kind == 'q' ? 0 : 32) + g].c_str());
 }
 
 // Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first
@@ -805,7 +819,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     }
     const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
                                          : std::vector<size_t>{0, q.count};
-    const int rc = quant ? run_lanes(lo, [&](size_t k, size_t a, size_t b) {
+    const int rc = (quant || std::getenv("PCCL_TMP_STEPWISE")) ? run_lanes(lo, [&](size_t k, size_t a, size_t b) {
         return host_ring(rv.tx, rv.rx, ws, rank, lane_tag(q.tag, k, lo.size() - 1), seq, dst + a * es, b - a, q, quant,
                          abort_fn, op.tx, op.rx);
     }) : host_ring_pipeline(rv.tx, rv.rx, ws, rank, q.tag, seq, dst, q.count, q.dtype, q.op, abort_fn, op.tx, op.rx);
@@ -896,25 +910,28 @@ struct Staged {
 // connection pool sizes), so a wait covers the whole byte range it sends.
 struct ReadyRanges {
     std::mutex m;
+    std::condition_variable cv; // signalled by add(): a waiting sender wakes when its range may be complete
     std::vector<Staged> v;
     void clear() {
         std::lock_guard l(m);
         v.clear();
     }
     void add(size_t a, size_t b, DevEvent e) {
-        std::lock_guard l(m);
-        v.push_back({a, b, e});
+        {
+            std::lock_guard l(m);
+            v.push_back({a, b, e});
+        }
+        cv.notify_all();
     }
     // blocks until every byte of [begin, end) is readable; false if `cancel` became non-zero first
     bool wait(size_t begin, size_t end, DeviceBackend *be, const std::atomic<int> &cancel) {
         if (end <= begin) return true;
-        unsigned us = 2;
         std::vector<std::pair<size_t, size_t>> iv;
         std::vector<DevEvent> evs;
         while (true) {
             bool covered = false;
             {
-                std::lock_guard l(m);
+                std::unique_lock l(m);
                 iv.clear();
                 evs.clear();
                 for (const auto &r : v)
@@ -929,15 +946,15 @@ struct ReadyRanges {
                     cur = std::max(cur, b);
                 }
                 covered = cur >= end;
+                if (!covered) {
+                    if (cancel.load(std::memory_order_relaxed) != 0) return false;
+                    cv.wait_for(l, std::chrono::milliseconds(1)); // (cancel is polled, not signalled)
+                    continue;
+                }
             }
-            if (covered) {
-                for (DevEvent e : evs)
-                    if (!event_wait_polling(be, e)) return false;
-                return true;
-            }
-            if (cancel.load(std::memory_order_relaxed) != 0) return false;
-            std::this_thread::sleep_for(std::chrono::microseconds(us));
-            us = std::min(us * 2, 200u);
+            for (DevEvent e : evs)
+                if (!event_wait_polling(be, e)) return false;
+            return true;
         }
     }
 };
@@ -1417,7 +1434,7 @@ int host_ring_pipeline(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
         uint8_t *reg = region(chunk_rx(g)), *buf = rb[g % 2].data();
         ReadyRanges *next = g + 1 < nsteps ? ready[g + 1].get() : nullptr;
         const int rc = rx.receive(
-            g, es, frame,
+            g, es, std::min<size_t>(frame, 1u << 20),
             [&](size_t a, size_t e) {
                 if (is_rs(g)) kernels::host_reduce(reg + a, buf + a, (e - a) / es, dtype, rop);
                 if (next) next->add(a, e, nullptr); // step g+1 sends this chunk: reduced (RS) / received (AG)
@@ -1736,6 +1753,7 @@ int device_quant_lane(QLane &L) {
                 be->dequant_reduce(src, txq[slot], n, L.dtype, L.qtype, ReduceOp::Set, params, st);
             if (int m = send_meta(io, mine, *L.tx)) return fail(m);
             publish(g, txq[slot], &txready[slot]);
+            step_sub_mark('q', g);
         } // else: forwarded chunk, published with its metadata when step g-1's metadata arrived
         fault_point("qring", seq, g, "meta");
         if (int m = recv_meta(io, theirs, *L.rx, L.aborted, failed)) return fail(m);
@@ -1763,6 +1781,7 @@ int device_quant_lane(QLane &L) {
                 step_last = record(st);
                 if (first) {
                     first = false;
+                    step_sub_mark('f', g);
                     fault_point("qring", seq, g, "rx");
                 }
             },
