@@ -769,12 +769,6 @@ int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::
     return 0;
 }
 
-int host_ring_pipeline(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
-                       const std::vector<std::shared_ptr<net::MuxConn>> &rxs, size_t ws, size_t rank, uint64_t tag,
-                       uint64_t seq, uint8_t *dst, size_t count, DType dtype, ReduceOp rop,
-                       const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
-                       std::atomic<uint64_t> &rx_ctr);
-
 // Runs fn(lane, lo, hi) for every lane of `lo` (lane 0 on the calling thread); returns the worst lane result
 // (abort 2 outranks io failure 1).
 int run_lanes(const std::vector<size_t> &lo, const std::function<int(size_t, size_t, size_t)> &fn) {
@@ -819,10 +813,10 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     }
     const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
                                          : std::vector<size_t>{0, q.count};
-    const int rc = (quant || std::getenv("PCCL_TMP_STEPWISE")) ? run_lanes(lo, [&](size_t k, size_t a, size_t b) {
+    const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
         return host_ring(rv.tx, rv.rx, ws, rank, lane_tag(q.tag, k, lo.size() - 1), seq, dst + a * es, b - a, q, quant,
                          abort_fn, op.tx, op.rx);
-    }) : host_ring_pipeline(rv.tx, rv.rx, ws, rank, q.tag, seq, dst, q.count, q.dtype, q.op, abort_fn, op.tx, op.rx);
+    });
     if (rc) {
         if (q.src == q.dst) std::memcpy(dst, backup.data(), bytes); // every lane returned: nothing writes dst
         return {rc == 2, rc == 2};
@@ -1375,85 +1369,6 @@ int device_ring_pipeline(DevRing &R) {
     }
     if (!senders.wait(nsteps - 1)) return fail(1);
     return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
-}
-
-} // namespace
-
-namespace {
-
-// The plain host ring as one pipeline over all 2(W-1) steps, like the device ring: step g+1's payload is the chunk
-// step g reduces in place in `dst` (already holding the input), and its frames leave as soon as their range is
-// reduced; all-gather chunks are received straight into `dst` and forwarded as they land; the next step's sinks are
-// posted while the current step still receives. A chunk's wire bytes and order are the step-synchronous ring's (and
-// the device ring's), so host and device peers mix in one ring. On a long-latency link a step costs its transfer
-// instead of a round trip plus its transfer. Returns 0 ok, 1 io failure, 2 abort; on return no sink or send of the op
-// touches `dst` any more.
-int host_ring_pipeline(const std::vector<std::shared_ptr<net::MuxConn>> &txs,
-                       const std::vector<std::shared_ptr<net::MuxConn>> &rxs, size_t ws, size_t rank, uint64_t tag,
-                       uint64_t seq, uint8_t *dst, size_t count, DType dtype, ReduceOp rop,
-                       const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
-                       std::atomic<uint64_t> &rx_ctr) {
-    const size_t es = dtype_size(dtype);
-    // frame (send) and consume granularity: pieces small enough that a step's first bytes move on quickly
-    const size_t frame = std::max<size_t>(es, std::min<size_t>(net::multiplex_chunk_size(), 4u << 20) / es * es);
-    const auto bounds = chunk_bounds(count, ws);
-    size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
-    const size_t nsteps = 2 * (ws - 1);
-    auto is_rs = [&](size_t g) { return g + 1 < ws; };
-    auto chunk_tx = [&](size_t g) { return ring_chunk_tx(g, rank, ws); };
-    auto chunk_rx = [&](size_t g) { return ring_chunk_rx(g, rank, ws); };
-    auto region = [&](size_t c) { return dst + bounds[c].first * es; };
-    auto nbytes = [&](size_t c) { return (bounds[c].second - bounds[c].first) * es; };
-    // reduce-scatter receive buffers: step g receives into rbuf[g % 2] (step g+1's sinks are posted during step g;
-    // step g-1, the previous user of rbuf[(g+1) % 2], has been reduced by then)
-    Lease rb[2];
-    for (auto &l : rb) {
-        l = Lease(host_pool(), max_chunk * es + 64);
-        if (!l.ok()) return 1;
-    }
-    // payload readiness per step: the input chunk at once, every other payload as the step before produces it
-    std::vector<std::unique_ptr<ReadyRanges>> ready(nsteps);
-    for (auto &r : ready) r = std::make_unique<ReadyRanges>();
-    ready[0]->add(0, nbytes(chunk_tx(0)), nullptr);
-    size_t max_stripes = 1;
-    for (size_t g = 0; g < nsteps; ++g)
-        max_stripes = std::max(max_stripes, plan_stripes(nbytes(chunk_tx(g)), txs.size()).off.size());
-    OpSenders senders(txs, tag, seq, frame, nsteps, max_stripes, nullptr, tx_ctr);
-    for (size_t g = 0; g < nsteps; ++g) { // every payload lives in dst: publish them all, readiness gates the bytes
-        OpSenders::Step stp;
-        stp.payload = region(chunk_tx(g));
-        stp.bytes = nbytes(chunk_tx(g));
-        stp.ready = ready[g].get();
-        senders.publish(g, stp);
-    }
-    RingRx rx(rxs, tag, seq, nsteps); // after the buffers its sinks point into
-    auto post = [&](size_t g) { rx.post(g, is_rs(g) ? rb[g % 2].data() : region(chunk_rx(g)), nbytes(chunk_rx(g))); };
-    for (size_t g = 0; g < nsteps; ++g) {
-        if (!rx.posted(g)) post(g);
-        uint8_t *reg = region(chunk_rx(g)), *buf = rb[g % 2].data();
-        ReadyRanges *next = g + 1 < nsteps ? ready[g + 1].get() : nullptr;
-        const int rc = rx.receive(
-            g, es, std::min<size_t>(frame, 1u << 20),
-            [&](size_t a, size_t e) {
-                if (is_rs(g)) kernels::host_reduce(reg + a, buf + a, (e - a) / es, dtype, rop);
-                if (next) next->add(a, e, nullptr); // step g+1 sends this chunk: reduced (RS) / received (AG)
-            },
-            [&] {
-                if (g + 1 < nsteps && !rx.posted(g + 1)) post(g + 1);
-            },
-            [&] { return senders.failed(); }, aborted);
-        if (rc) {
-            senders.cancel();
-            return rc;
-        }
-        rx_ctr += nbytes(chunk_rx(g));
-        rx.unpost(g);
-        step_mark(is_rs(g), is_rs(g) ? g : g - (ws - 1));
-        if (g + 2 == ws) trace_mark("reduce_scatter");
-    }
-    if (!senders.wait(nsteps - 1)) return 1;
-    return 0;
 }
 
 } // namespace
