@@ -1008,6 +1008,19 @@ public:
         cv_.wait(l, [&] { return rc_.load() != 0 || (published_ > g && done_[g] == 0); });
         return rc_.load() == 0;
     }
+    // blocks until every stripe of every step is sent (a stripe with no bytes in the last step may still be sending
+    // an earlier one); false on failure / cancel
+    bool wait_all() {
+        std::unique_lock l(m_);
+        cv_.wait(l, [&] {
+            if (rc_.load() != 0) return true;
+            if (published_ < steps_.size()) return false;
+            for (size_t d : done_)
+                if (d != 0) return false;
+            return true;
+        });
+        return rc_.load() == 0;
+    }
     void cancel() {
         rc_.store(1);
         std::lock_guard l(m_);
@@ -1367,7 +1380,7 @@ int device_ring_pipeline(DevRing &R) {
         if (g + 2 == ws) trace_mark("reduce_scatter");
         fault_point("ring", seq, g, "end");
     }
-    if (!senders.wait(nsteps - 1)) return fail(1);
+    if (!senders.wait_all()) return fail(1);
     return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
 }
 
@@ -1637,6 +1650,7 @@ int device_quant_lane(QLane &L) {
         L.open_gate->signal();
         gate_opened = true;
     };
+    const bool tmp_rs_pinned = env_size("PCCL_TMP_QRS_PINNED", 0) != 0;
     QuantMeta theirs;
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb;
@@ -1684,7 +1698,9 @@ int device_quant_lane(QLane &L) {
             g, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
-                if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM
+                if (rs && tmp_rs_pinned) { // A/B: the kernel reads the received piece from pinned memory
+                    dequant_consume(region + a / qs * es, rxbuf[b] + a, n, params);
+                } else if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM
                     be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, L.pq.h2d);
                     be->stream_wait_event(st, record(L.pq.h2d));
                     dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
@@ -1712,7 +1728,7 @@ int device_quant_lane(QLane &L) {
         step_mark(rs, rs ? g : g - (ws - 1));
         fault_point("qring", seq, g, "end");
     }
-    if (!senders.wait(nsteps - 1)) return fail(1);
+    if (!senders.wait_all()) return fail(1);
     return 0;
 }
 
