@@ -1650,7 +1650,6 @@ int device_quant_lane(QLane &L) {
         L.open_gate->signal();
         gate_opened = true;
     };
-    const bool tmp_rs_pinned = env_size("PCCL_TMP_QRS_PINNED", 0) != 0;
     QuantMeta theirs;
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb;
@@ -1698,9 +1697,8 @@ int device_quant_lane(QLane &L) {
             g, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
-                if (rs && tmp_rs_pinned) { // A/B: the kernel reads the received piece from pinned memory
-                    dequant_consume(region + a / qs * es, rxbuf[b] + a, n, params);
-                } else if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM
+                if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM (interleaved A/B against kernels
+                          // reading pinned memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
                     be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, L.pq.h2d);
                     be->stream_wait_event(st, record(L.pq.h2d));
                     dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
