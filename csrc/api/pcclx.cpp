@@ -94,6 +94,33 @@ PCCLX_EXPORT int pcclxQuantize(void *dst_q, const void *src, size_t count, int v
     return 0;
 }
 
+// Device only: quantizes `src` (min / max from the data, like pcclxQuantize) and overwrites it with D(Q(src)) in the
+// same kernel pass (the quantized device ring's owner parity step).
+PCCLX_EXPORT int pcclxQuantizeSetback(void *dst_q, void *src, size_t count, int vtype, int qtype, int algo,
+                                      double *meta_out) {
+    const auto vt = static_cast<DType>(vtype), qt = static_cast<DType>(qtype);
+    const auto al = static_cast<QuantAlgo>(algo);
+    if (!kernels::quant_supported(vt, qt, al)) return -2;
+    DeviceBackend *be = device_backend();
+    if (!be) return -1;
+    double *mm = static_cast<double *>(be->alloc_pinned(16));
+    if (!mm) return -1;
+    be->minmax(src, count, vt, mm, nullptr);
+    bool ok = be->device_sync();
+    const proto::QuantMeta m = kernels::make_meta(al, vt, qt, mm[0], mm[1]);
+    be->free_pinned(mm);
+    ok = ok && be->quantize_setback(dst_q, src, count, vt, qt, kernels::make_params(m, qt), nullptr) &&
+         be->device_sync();
+    if (!ok) return -1;
+    if (meta_out) {
+        meta_out[0] = m.min_value;
+        meta_out[1] = m.max_value;
+        meta_out[2] = static_cast<double>(m.zero_point);
+        meta_out[3] = m.scale;
+    }
+    return 0;
+}
+
 PCCLX_EXPORT int pcclxDequantReduce(void *dst, const void *src_q, size_t count, int vtype, int qtype, int algo, int op,
                                     const double *meta, int on_device) {
     proto::QuantMeta m;

@@ -1672,13 +1672,14 @@ int device_quant_lane(QLane &L) {
             txready[slot].clear();
             for (size_t off = 0; off < n; off += piece_el) {
                 const size_t k = std::min(piece_el, n - off);
-                be->quantize(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
+                if (g + 1 == ws) // the all-gather's payload; parity: own chunk := D(Q(x)), what the others de-quantize
+                    be->quantize_setback(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
+                else
+                    be->quantize(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
                 DevEvent e = record(st);
                 txready[slot].add(off * qs, (off + k) * qs, e);
                 if (g == 0) first_payload = e;
             }
-            if (g + 1 == ws && n > 0) // parity: own chunk := D(Q(x)), what every other peer de-quantizes
-                be->dequant_reduce(src, txq[slot], n, L.dtype, L.qtype, ReduceOp::Set, params, st);
             if (int m = send_meta(io, mine, *L.tx)) return fail(m);
             publish(g, txq[slot], &txready[slot]);
             step_sub_mark('q', g);

@@ -90,6 +90,10 @@ public:
                                        int *blocks, DevStream s) = 0;
     virtual bool quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
                           const kernels::QuantParams &p, DevStream s) = 0;
+    // quantize, and overwrite `src` with D(Q(src)) in the same pass (bit-identical to quantize followed by
+    // dequant_reduce(..., ReduceOp::Set, ...) of the quantized bytes)
+    virtual bool quantize_setback(void *dst_q, void *src, size_t count, DType vtype, DType qtype,
+                                  const kernels::QuantParams &p, DevStream s) = 0;
     // writes {min, max} as two doubles to `out2` (pinned host or device memory)
     virtual bool minmax(const void *src, size_t count, DType vtype, double *out2, DevStream s) = 0;
     // folds n_partials (min, max) pairs (device memory) of `count` elements into `out2` (asynchronous)

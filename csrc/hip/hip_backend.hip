@@ -292,6 +292,10 @@ public:
                   DevStream s) override {
         return hipk::launch_quantize(dst_q, src, count, vtype, qtype, p, static_cast<hipStream_t>(s));
     }
+    bool quantize_setback(void *dst_q, void *src, size_t count, DType vtype, DType qtype,
+                          const kernels::QuantParams &p, DevStream s) override {
+        return hipk::launch_quantize(dst_q, src, count, vtype, qtype, p, static_cast<hipStream_t>(s), true);
+    }
     bool minmax(const void *src, size_t count, DType vtype, double *out2, DevStream s) override {
         // the partials scratch is per stream; threads sharing a stream (e.g. the null stream) take turns until the
         // result has landed, so interleaved launches can never mix their partials

@@ -65,36 +65,42 @@ bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vty
 }
 
 bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
-                     const kernels::QuantParams &p, hipStream_t st) {
+                     const kernels::QuantParams &p, hipStream_t st, bool set_back) {
     if (count == 0) return true;
     return with_float_elem(vtype, [&](auto e) {
         using E = decltype(e);
         using S = typename E::S;
         constexpr int V = vec_width<S>();
-        auto *s = static_cast<const S *>(src);
-        if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
-            const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, 1}});
-            const int grid = grid_ew(count, pl, V);
-            auto *d = static_cast<uint8_t *>(dst_q);
-            return launch_ok([&] {
-                if (qtype == DType::F8E4M3)
-                    k_q_fp8<E, true><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
-                else
-                    k_q_fp8<E, false><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+        // (set_back: the kernels write D(Q(x)) back into src; otherwise src is only read)
+        auto *s = static_cast<S *>(const_cast<void *>(src));
+        auto go = [&](auto back_c) {
+            constexpr bool B = decltype(back_c)::value;
+            if (p.algo == QuantAlgo::MinMax && (qtype == DType::F8E4M3 || qtype == DType::F8E5M2)) {
+                const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, 1}});
+                const int grid = grid_ew(count, pl, V);
+                auto *d = static_cast<uint8_t *>(dst_q);
+                return launch_ok([&] {
+                    if (qtype == DType::F8E4M3)
+                        k_q_fp8<E, true, B><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+                    else
+                        k_q_fp8<E, false, B><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+                });
+            }
+            return with_qint(qtype, [&](auto qv) {
+                using Q = decltype(qv);
+                const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, sizeof(Q)}});
+                const int grid = grid_for(count, pl.vec ? V : 1);
+                auto *d = static_cast<Q *>(dst_q);
+                if (p.algo == QuantAlgo::MinMax)
+                    return launch_ok([&] {
+                        k_q_minmax<E, Q, B><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec);
+                    });
+                if (p.algo == QuantAlgo::ZeroPointScale)
+                    return launch_ok([&] { k_q_zps<E, Q, B><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
+                return false;
             });
-        }
-        return with_qint(qtype, [&](auto qv) {
-            using Q = decltype(qv);
-            const EwPlan pl = plan_ew<V>(count, {{src, sizeof(S)}, {dst_q, sizeof(Q)}});
-            const int grid = grid_for(count, pl.vec ? V : 1);
-            auto *d = static_cast<Q *>(dst_q);
-            if (p.algo == QuantAlgo::MinMax)
-                return launch_ok(
-                    [&] { k_q_minmax<E, Q><<<grid_ew(count, pl, V), kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
-            if (p.algo == QuantAlgo::ZeroPointScale)
-                return launch_ok([&] { k_q_zps<E, Q><<<grid, kBlock, 0, st>>>(d, s, count, p, pl.head, pl.vec); });
-            return false;
-        });
+        };
+        return set_back ? go(std::true_type{}) : go(std::false_type{});
     });
 }
 

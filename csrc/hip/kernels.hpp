@@ -373,55 +373,100 @@ __device__ __forceinline__ Q q_from_double(double q) {
     }
 }
 
-template<typename E, typename Q>
-__global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+// Quantize kernels. BACK: also overwrite the source with its de-quantized value, D(Q(x)), exactly as the
+// de-quantize kernels with ReduceOp::Set compute it (the owner's copy of a quantized all-gather payload must equal what
+// every other peer de-quantizes): one pass over the chunk instead of quantize + a de-quantize kernel that reads the
+// quantized bytes back from pinned host memory.
+template<typename E, typename Q, bool BACK>
+__global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, typename E::S *__restrict__ src, size_t n,
                                                      QuantParams p, size_t head, int vec) {
     using S = typename E::S;
+    using C = typename E::C;
     constexpr int V = vec_width<S>();
+    auto back = [&](Q q) { return E::st(static_cast<C>(dq_minmax_int(static_cast<double>(q), p))); };
     ew_loop_ls<V, kEwUnroll>(
-        n, head, vec, [&](size_t i) { dst[i] = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(src[i])), p)); },
+        n, head, vec,
+        [&](size_t i) {
+            const Q q = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(src[i])), p));
+            dst[i] = q;
+            if constexpr (BACK) src[i] = back(q);
+        },
         [&](size_t b) { return ldp_nt<S, V>(src + b); },
         [&](size_t b, const Pack<S, V> &s) {
             Pack<Q, V> q;
 #pragma unroll
             for (int e = 0; e < V; ++e) q.v[e] = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(s.v[e])), p));
             stp<Q, V>(dst + b, q);
+            if constexpr (BACK) {
+                Pack<S, V> d;
+#pragma unroll
+                for (int e = 0; e < V; ++e) d.v[e] = back(q.v[e]);
+                stp_nt<S, V>(src + b, d);
+            }
         });
 }
 
-template<typename E, bool E4M3>
-__global__ __launch_bounds__(kBlock) void k_q_fp8(uint8_t *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+template<typename E, bool E4M3, bool BACK>
+__global__ __launch_bounds__(kBlock) void k_q_fp8(uint8_t *__restrict__ dst, typename E::S *__restrict__ src, size_t n,
                                                   QuantParams p, size_t head, int vec) {
     using S = typename E::S;
+    using C = typename E::C;
     constexpr int V = vec_width<S>();
     auto qf = [&](S v) {
         const float x = static_cast<float>(E::ld(v)) * p.f8_scale;
         return E4M3 ? num::f32_to_fp8e4m3(x) : num::f32_to_fp8e5m2(x);
     };
+    auto back = [&](uint8_t q) {
+        return E::st(static_cast<C>((E4M3 ? num::fp8e4m3_to_f32(q) : num::fp8e5m2_to_f32(q)) * p.f8_inv));
+    };
     ew_loop_ls<V, kEwUnroll>(
-        n, head, vec, [&](size_t i) { dst[i] = qf(src[i]); },
+        n, head, vec,
+        [&](size_t i) {
+            const uint8_t q = qf(src[i]);
+            dst[i] = q;
+            if constexpr (BACK) src[i] = back(q);
+        },
         [&](size_t b) { return ldp_nt<S, V>(src + b); },
         [&](size_t b, const Pack<S, V> &s) {
             Pack<uint8_t, V> q;
 #pragma unroll
             for (int e = 0; e < V; ++e) q.v[e] = qf(s.v[e]);
             stp<uint8_t, V>(dst + b, q);
+            if constexpr (BACK) {
+                Pack<S, V> d;
+#pragma unroll
+                for (int e = 0; e < V; ++e) d.v[e] = back(q.v[e]);
+                stp_nt<S, V>(src + b, d);
+            }
         });
 }
 
-template<typename E, typename Q>
-__global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, const typename E::S *__restrict__ src, size_t n,
+template<typename E, typename Q, bool BACK>
+__global__ __launch_bounds__(kBlock) void k_q_zps(Q *__restrict__ dst, typename E::S *__restrict__ src, size_t n,
                                                   QuantParams p, size_t head, int vec) {
     using S = typename E::S;
+    using C = typename E::C;
     constexpr int V = vec_width<S>();
+    auto back = [&](Q q) { return E::st(static_cast<C>(dq_zps_as<Q>(q, p))); };
     ew_loop_ls<V, kEwUnroll>(
-        n, head, vec, [&](size_t i) { dst[i] = q_zps_as<Q>(static_cast<float>(E::ld(src[i])), p); },
+        n, head, vec,
+        [&](size_t i) {
+            const Q q = q_zps_as<Q>(static_cast<float>(E::ld(src[i])), p);
+            dst[i] = q;
+            if constexpr (BACK) src[i] = back(q);
+        },
         [&](size_t b) { return ldp_nt<S, V>(src + b); },
         [&](size_t b, const Pack<S, V> &s) {
             Pack<Q, V> q;
 #pragma unroll
             for (int e = 0; e < V; ++e) q.v[e] = q_zps_as<Q>(static_cast<float>(E::ld(s.v[e])), p);
             stp<Q, V>(dst + b, q);
+            if constexpr (BACK) {
+                Pack<S, V> d;
+#pragma unroll
+                for (int e = 0; e < V; ++e) d.v[e] = back(q.v[e]);
+                stp_nt<S, V>(src + b, d);
+            }
         });
 }
 

@@ -23,8 +23,9 @@ bool launch_copy_bytes(void *dst, const void *src, size_t n, int max_grid, hipSt
 bool launch_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                            const kernels::QuantParams &p, hipStream_t s, double *mm = nullptr, int mm_max_blocks = 0,
                            int *mm_blocks = nullptr);
+// set_back: also overwrite src with D(Q(src)) (src is written: the caller passes a mutable buffer)
 bool launch_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype,
-                     const kernels::QuantParams &p, hipStream_t s);
+                     const kernels::QuantParams &p, hipStream_t s, bool set_back = false);
 bool launch_minmax(const void *src, size_t count, DType vtype, double *partial, double *out2, hipStream_t st);
 bool launch_minmax_fold(const double *partial, int nblocks, size_t count, double *out2, hipStream_t st);
 

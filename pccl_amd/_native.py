@@ -149,6 +149,7 @@ def _load() -> ctypes.CDLL:
         "pcclxReduce": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int], c_int),
         "pcclxFinalizeAvg": ([c_void_p, c_size_t, c_int, c_size_t, c_int], c_int),
         "pcclxQuantize": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double)], c_int),
+        "pcclxQuantizeSetback": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, p(c_double)], c_int),
         "pcclxDequantReduce": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double), c_int], c_int),
         "pcclxDequantReduceMinmax": ([c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_int, p(c_double), c_int,
                                       p(c_double)], c_int),

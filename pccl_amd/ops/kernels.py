@@ -89,6 +89,16 @@ def quantize(src: torch.Tensor, qdtype: torch.dtype, algo: str = "min_max") -> T
     return out, list(meta)
 
 
+def quantize_setback(src: torch.Tensor, qdtype: torch.dtype, algo: str = "min_max") -> Tuple[torch.Tensor, List[float]]:
+    """GPU only: quantizes ``src`` and overwrites it with its de-quantized value D(Q(src)) in one kernel pass (the
+    quantized ring's owner parity step); returns (q, meta) like ``quantize``."""
+    out = torch.empty(src.shape, dtype=qdtype, device=src.device)
+    meta = (ctypes.c_double * 4)()
+    _check(C.pcclxQuantizeSetback(out.data_ptr(), src.data_ptr(), src.numel(), WIRE_DTYPE[src.dtype],
+                                  WIRE_DTYPE[qdtype], ALGOS[algo], meta), "quantize_setback")
+    return out, list(meta)
+
+
 def dequant_reduce(dst: torch.Tensor, q: torch.Tensor, meta: Sequence[float], algo: str = "min_max",
                    op: str = "sum") -> torch.Tensor:
     m = (ctypes.c_double * 4)(*meta)

@@ -88,6 +88,29 @@ def test_device_quant_bit_exact_with_host(hip, vdtype, qdtype, algo):
     assert torch.equal(rd.cpu(), rh)
 
 
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("qdtype,algo", [(torch.uint8, "min_max"), (torch.int8, "zero_point_scale"),
+                                         (torch.int16, "min_max"), (torch.int64, "zero_point_scale"),
+                                         (getattr(torch, "float8_e4m3fn", None), "min_max"),
+                                         (getattr(torch, "float8_e5m2", None), "min_max")])
+@pytest.mark.parametrize("n", [1, 1000, (1 << 21) + 7])
+def test_device_quantize_setback_matches_two_pass(hip, vdtype, qdtype, algo, n):
+    """The fused owner-parity kernel (quantize and overwrite the source with D(Q(x)) in one pass, used by the
+    quantized ring's all-gather payload) equals quantize followed by a de-quantize (Set) kernel, bit for bit, and its
+    quantized bytes equal the plain quantize's."""
+    if qdtype is None:
+        pytest.skip("no fp8 dtype")
+    x = _rand(n, vdtype, 41).to(hip)
+    q1, m1 = K.quantize(x, qdtype, algo)
+    two = K.dequant_reduce(torch.zeros_like(x), q1, m1, algo, "set")
+    y = x.clone()
+    q2, m2 = K.quantize_setback(y, qdtype, algo)
+    torch.cuda.synchronize()
+    assert m1 == m2
+    assert torch.equal(q2.cpu().view(torch.uint8), q1.cpu().view(torch.uint8))
+    assert torch.equal(y.cpu(), two.cpu())
+
+
 @pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("qdtype,algo", [(torch.uint8, "min_max"), (torch.int8, "zero_point_scale"),
                                          (getattr(torch, "float8_e4m3fn", None), "min_max")])

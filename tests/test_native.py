@@ -91,6 +91,7 @@ def test_sanitizer_build_unit_and_peers():
 
 
 @pytest.mark.skipif(os.environ.get("PCCL_TEST_SANITIZE") != "1", reason="set PCCL_TEST_SANITIZE=1 (slow build)")
+@pytest.mark.timeout(1800)
 def test_tsan_build_unit_and_peers(tmp_path):
     """ThreadSanitizer build (-DPCCL_SANITIZE_THREAD=ON, ROCm's clang: GCC 11's libtsan does not intercept
     pthread_cond_clockwait, so every condition-variable wait looks like a lost unlock): the unit tests and a 3-peer
