@@ -105,7 +105,7 @@ def test_tsan_build_unit_and_peers(tmp_path):
                    check=True, capture_output=True, env=env_cc)
     subprocess.run(["ninja", "-C", bdir, "-j", "8"], check=True, capture_output=True)
     logs = tmp_path / "tsan"
-    env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=0 report_signal_unsafe=0 log_path={logs}")
+    env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=0 report_signal_unsafe=0 die_after_fork=0 log_path={logs}")
     r = subprocess.run([os.path.join(bdir, "tests", "pccl_unit_tests")], capture_output=True, text=True, env=env,
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
