@@ -1,0 +1,125 @@
+"""Per-op latency of the Python API with one process per peer, the deployment shape (one process per GPU).
+
+    python benchmarks/py_latency.py [--peers 8] [--iters 200] [--sizes 65536,1048576,16777216] [--device cuda:0]
+
+bench.py's ``extra.latency_1MiB_ipc_python_threads_us`` runs its 8 peers as threads of ONE Python process, where every
+op's Python work (argument checks, descriptor, stream sync, ctypes call) of all 8 peers is serialised by the GIL. Here
+every peer is its own process, as under torchrun, so the number is what a DDP bucket of that size costs from Python.
+With every peer on one GPU the buffers are fd-shareable and the ops run the xGMI/IPC path; ``--device cpu`` measures
+the host ring.
+
+Per size: the median / p90 of the per-op wall time maximum over the peers (ops are matched by index: every peer runs
+the same sequence), and two call variants on the same buffers:
+  * ``all_reduce``: the public blocking call (synchronises the tensor's current stream first);
+  * ``ready``: ``_all_reduce_async_ready(...).wait()``, which skips that synchronisation (producers already waited
+    for), so the difference is the stream-sync cost.
+Prints one JSON object.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def peer(a):
+    import contextlib
+
+    import torch
+
+    import pccl_amd as pccl
+    from pccl_amd.utils import wait_for_world
+    dev = torch.device(a.device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    comm = pccl.Communicator(a.master, 0)
+    comm.connect(n_attempts=60)
+    wait_for_world(comm, a.peers, timeout=120)
+    out = {}
+    tag = 0
+    for b in [int(s) for s in a.sizes.split(",")]:
+        n = b // 2
+        with pccl.memory.maybe_shareable(dev) if dev.type == "cuda" else contextlib.nullcontext():
+            x = torch.full((n,), float(a.rank + 1), device=dev, dtype=torch.bfloat16)
+            y = torch.empty_like(x)
+        res = {}
+        for variant in ("all_reduce", "ready"):
+            ts = []
+            for i in range(a.iters + a.warmup):
+                t0 = time.perf_counter()
+                if variant == "all_reduce":
+                    comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+                else:
+                    ok, _, _ = comm._all_reduce_async_ready(x, y, op=pccl.ReduceOp.SUM, tag=tag).wait()
+                    assert ok
+                if i >= a.warmup:
+                    ts.append(time.perf_counter() - t0)
+                tag += 1
+            res[variant] = ts
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        want = a.peers * (a.peers + 1) / 2
+        assert float(y.min()) == float(y.max()) == want, (float(y.min()), float(y.max()), want)
+        res["path"] = comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+        out[b] = res
+    print(json.dumps(out), flush=True)
+    comm.destroy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--sizes", default="65536,1048576,16777216")
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--peer", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--master", default="")
+    ap.add_argument("--rank", type=int, default=0)
+    a = ap.parse_args()
+    if a.peer:
+        peer(a)
+        return
+    import pccl_amd as pccl
+    from pccl_amd.utils import DIAG_SIGNALS, communicate_all, free_port
+    port = free_port()
+    master = pccl.MasterNode(f"0.0.0.0:{port}")
+    master.run()
+    try:
+        procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--peer", "--master",
+                                   f"127.0.0.1:{port}", "--rank", str(r), "--peers", str(a.peers), "--iters",
+                                   str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                 for r in range(a.peers)]
+        outs = communicate_all(procs, 600, DIAG_SIGNALS)
+    finally:
+        master.interrupt()
+        master.await_termination()
+    res = []
+    for p, (o, e) in zip(procs, outs):
+        if p.returncode != 0:
+            raise SystemExit(f"peer failed rc={p.returncode}: {e[-3000:]}")
+        res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]))
+    names = {0: "none", 1: "host_ring", 2: "device_ring", 3: "ipc", 4: "hier"}
+    summary = {"peers": a.peers, "device": a.device, "iters": a.iters, "processes": "one per peer", "sizes": {}}
+    for b in res[0]:
+        row = {"path": names.get(res[0][b]["path"], "?")}
+        for v in ("all_reduce", "ready"):
+            per_op = [max(r[b][v][i] for r in res) for i in range(a.iters)]
+            q = statistics.quantiles(per_op, n=10)
+            row[v] = {"median_us": round(statistics.median(per_op) * 1e6, 1), "p90_us": round(q[-1] * 1e6, 1),
+                      "min_us": round(min(per_op) * 1e6, 1),
+                      "rank0_median_us": round(statistics.median(res[0][b][v]) * 1e6, 1)}
+        summary["sizes"][f"{int(b) >> 10}KiB"] = row
+    print(json.dumps(summary))
+
+
+if __name__ == "__main__":
+    main()

@@ -273,6 +273,10 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     if (!ok) {
         LOG(WARN) << "all-reduce tag " << tag << " failed/aborted";
     }
+    if (op->settle) {
+        op->settle(!ok);
+        op->settle = nullptr;
+    }
     if (current_trace()) {
         trace.mark("complete");
         static const char *names[] = {"none", "host_ring", "device_ring", "ipc", "hier", "?", "?", "?"};
@@ -689,13 +693,23 @@ int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::
     if (quant) qbuf = Lease(host_pool(), max_chunk * qs + 64);
     if (!rbuf.ok() || (quant && !qbuf.ok())) return 1;
 
-    // One full-duplex (striped) step: sends `payload`, receives `rx_bytes` into `sink`, calling `consume(from, to)`
-    // for newly complete received elements. Returns 0 ok, 1 io failure, 2 abort.
-    auto run_step = [&](const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
+    // One full-duplex (striped) step g (global: reduce-scatter 0 .. ws-2, then all-gather): sends `payload`,
+    // receives `rx_bytes` into `sink`, calling `consume(from, to)` for newly complete received elements. Returns 0 ok,
+    // 1 io failure, 2 abort. Fault points (tests): hring:<seq>:<g>:rx after the first consume, :end after the step.
+    auto run_step = [&](size_t g, const uint8_t *payload, size_t tx_bytes, uint8_t *sink, size_t rx_bytes,
                         const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx = {}) -> int {
-        return striped_step(txs, rxs, tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes, qs,
-                            chunk, consume, aborted, tx_ctr, rx_ctr, before_rx);
+        bool first = true;
+        const int rc = striped_step(txs, rxs, tag, seq, payload, tx_bytes, [](size_t) { return true; }, sink, rx_bytes,
+                                    qs, chunk, [&](size_t a, size_t b) {
+                                        consume(a, b);
+                                        if (first) {
+                                            first = false;
+                                            fault_point("hring", seq, g, "rx");
+                                        }
+                                    }, aborted, tx_ctr, rx_ctr, before_rx);
+        if (rc == 0) fault_point("hring", seq, g, "end");
+        return rc;
     };
     auto await_meta = [&](QuantMeta &theirs) { return [&, pt = &theirs] { return recv_meta(io, *pt, rx_ctr, aborted); }; };
 
@@ -713,7 +727,7 @@ int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::
             if (int rc = send_meta(io, mine, tx_ctr)) return rc;
         }
         uint8_t *rx_region = dst + rs * es;
-        const int rc = run_step(payload, (te - ts) * qs, rbuf.data(), (re - rs) * qs, [&](size_t a, size_t b) {
+        const int rc = run_step(step, payload, (te - ts) * qs, rbuf.data(), (re - rs) * qs, [&](size_t a, size_t b) {
             if (quant)
                 kernels::host_dequant_reduce(rx_region + a * es, rbuf.data() + a * qs, b - a, q.dtype, q.qtype, q.op, theirs);
             else
@@ -756,12 +770,12 @@ int host_ring(const std::vector<std::shared_ptr<net::MuxConn>> &txs, const std::
             }
             if (int m = send_meta(io, mine, tx_ctr)) return m;
             uint8_t *sink = ag[step % 2].data();
-            rc = run_step(payload, (te - ts) * qs, sink, (re - rs) * qs, [&](size_t a, size_t b) {
+            rc = run_step(ws - 1 + step, payload, (te - ts) * qs, sink, (re - rs) * qs, [&](size_t a, size_t b) {
                 kernels::host_dequant_reduce(rx_region + a * es, sink + a * qs, b - a, q.dtype, q.qtype, ReduceOp::Set, theirs);
             }, await_meta(theirs));
             prev_meta = theirs;
         } else {
-            rc = run_step(dst + ts * es, (te - ts) * es, rx_region, (re - rs) * es, [](size_t, size_t) {});
+            rc = run_step(ws - 1 + step, dst + ts * es, (te - ts) * es, rx_region, (re - rs) * es, [](size_t, size_t) {});
         }
         if (rc) return rc;
         cur = inc;
@@ -796,21 +810,27 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
     OpAbort aborted([this, t = q.tag] { return abort_received(t); });
     auto abort_fn = [&] { return aborted(); };
 
-    if (!quant && op.small_path) {
+    // in place: a backup of the input, restored if the ring fails or the master aborts the op afterwards (settle)
+    Lease backup;
+    if (q.src == q.dst && !q.scratch) {
+        backup = Lease(host_pool(), std::max<size_t>(bytes, 64));
+        if (!backup.ok()) return {false, false};
+        std::memcpy(backup.data(), q.src, bytes);
+    }
+    auto keep_backup = [&] {
+        if (!backup.ok()) return;
+        op.settle = [b = std::make_shared<Lease>(std::move(backup)), dst, bytes](bool restore) {
+            if (restore) std::memcpy(dst, b->data(), bytes);
+        };
+    };
+    if (!quant && op.small_path) { // writes dst only once every contribution arrived
         const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, q.src, dst, q.count, q.dtype, q.op, ws, rank,
                                               abort_fn, op.tx, op.rx);
         trace_mark("allgather_reduce");
+        if (rc == 0) keep_backup();
         return {rc == 0, rc == 2};
     }
-
-    Lease backup;
-    if (q.src == q.dst) {
-        backup = Lease(host_pool(), bytes);
-        if (!backup.ok()) return {false, false};
-        std::memcpy(backup.data(), q.src, bytes);
-    } else {
-        std::memcpy(dst, q.src, bytes);
-    }
+    if (q.src != q.dst) std::memcpy(dst, q.src, bytes);
     const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
                                          : std::vector<size_t>{0, q.count};
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
@@ -818,10 +838,11 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
                          abort_fn, op.tx, op.rx);
     });
     if (rc) {
-        if (q.src == q.dst) std::memcpy(dst, backup.data(), bytes); // every lane returned: nothing writes dst
+        if (backup.ok()) std::memcpy(dst, backup.data(), bytes); // every lane returned: nothing writes dst
         return {rc == 2, rc == 2};
     }
     if (q.op == ReduceOp::Avg) kernels::host_finalize_avg(dst, q.count, q.dtype, ws);
+    keep_backup();
     return {true, false};
 }
 
@@ -1384,6 +1405,19 @@ int device_ring_pipeline(DevRing &R) {
     return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
 }
 
+// An in-place device op finished its part: keep the input's backup (HBM or pinned) until the master's verdict and
+// copy it back into dst if the op failed anyway (OpState::settle).
+void settle_device_backup(std::function<void(bool)> &settle, DeviceBackend *be, int device, Lease &&backup,
+                          void *dst, size_t bytes) {
+    settle = [be, device, b = std::make_shared<Lease>(std::move(backup)), dst, bytes](bool restore) {
+        if (!restore) return;
+        be->set_device(device);
+        StreamLease s(device);
+        if (!s.get() || !be->memcpy_async(dst, b->data(), bytes, s.get()) || !be->stream_sync(s.get()))
+            LOG(ERR) << "all-reduce: could not restore the in-place input after a late abort";
+    };
+}
+
 } // namespace
 
 std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
@@ -1413,6 +1447,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         if (rc) return {false, rc == 2};
         if (!be->memcpy_async(dst, hout.data(), bytes, st) || !be->stream_sync(st)) return {false, false};
         trace_mark("allgather_reduce");
+        if (q.src == q.dst && !q.scratch) settle_device_backup(op.settle, be, device, std::move(hin), dst, bytes);
         return {true, false};
     }
     const PcieQueues pq = shared_pcie_queues(be, device);
@@ -1443,6 +1478,7 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     }
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
     if (!stream_wait_polling(be, st)) return {false, false};
+    if (keep_backup) settle_device_backup(op.settle, be, device, std::move(backup), dst, bytes);
     return {true, false};
 }
 
@@ -1801,6 +1837,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     // the lanes' streams are drained (each lane's Drain): the result is complete in HBM
     if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
     if (!stream_wait_polling(be, st)) return {false, false};
+    if (keep_backup) settle_device_backup(op.settle, be, device, std::move(backup), dst, bytes);
     return {true, false};
 }
 

@@ -159,6 +159,10 @@ private:
         std::atomic<uint64_t> tx{0}, rx{0};
         uint32_t world = 0;
         bool small_path = false; // every peer agreed on the small-message algorithm (kCollFlagSmallPath)
+        // Set by a data path that finished its part of an in-place op: holds the input's backup until the master's
+        // verdict. run_op calls it once with restore = true if the op failed anyway (a peer was lost after this
+        // peer's part was done), so a retry reduces the caller's input, not the result.
+        std::function<void(bool restore)> settle;
     };
 
     // Hierarchical layout (master's host_of extension): hosts x local ranks. The host-local peers share an IPC arena;

@@ -981,7 +981,8 @@ bool IpcArena::preflight(Client &c, uint64_t tag, uint64_t seq, OpCtx &ctx, int 
 
 std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
                                     DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
-                                    std::atomic<uint64_t> &rx, const InterHost *inter, size_t world) {
+                                    std::atomic<uint64_t> &rx, const InterHost *inter, size_t world,
+                                    std::function<void(bool)> *settle) {
     OpCtx ctx;
     {
         std::lock_guard l(g_ctx_mtx);
@@ -1022,6 +1023,19 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         if (rc != 0) { // peers may have written into them for this op: never reissued (drain_peers is bounded)
             quarantine_buffer(inb, seq);
             quarantine_buffer(outb, seq);
+        } else if (settle && src == dst && ctx.in_staged && inb) {
+            // in place: the staged original stays until the master's verdict (restored if the op fails anyway)
+            release_buffer(outb);
+            *settle = [this, be, device, inb, dst, bytes](bool restore) {
+                if (restore) {
+                    be->set_device(device);
+                    StreamLease s(device);
+                    if (!s.get() || !copy_staged(be, inb->segs, static_cast<uint8_t *>(dst), bytes, true, s.get()) ||
+                        !be->stream_sync(s.get()))
+                        LOG(ERR) << "IPC: could not restore the in-place input after a late abort";
+                }
+                release_buffer(inb);
+            };
         } else {
             release_buffer(inb);
             release_buffer(outb);
@@ -1182,7 +1196,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
 
 std::pair<bool, bool> Client::ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device) {
     return rv.arena->run(*this, op.req.tag, seq, op.req.src, op.req.dst, op.req.count, op.req.dtype, op.req.op, device,
-                         op.tx, op.rx);
+                         op.tx, op.rx, nullptr, 0, &op.settle);
 }
 
 // Hierarchical all-reduce (ring spans several hosts with L peers each): reduce-scatter inside each host over xGMI,
@@ -1215,7 +1229,7 @@ std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint6
         return r.first && !r.second ? 0 : (r.second ? 2 : 1);
     };
     return h.arena->run(*this, op.req.tag, seq, op.req.src, op.req.dst, op.req.count, op.req.dtype, op.req.op, device,
-                        op.tx, op.rx, &inter, rv.ring.size());
+                        op.tx, op.rx, &inter, rv.ring.size(), &op.settle);
 }
 
 } // namespace pccl::client

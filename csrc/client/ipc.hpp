@@ -115,7 +115,8 @@ public:
     // across hosts with `inter`, divide by `world` for AVG, then push it into every local peer's output.
     std::pair<bool, bool> run(Client &c, uint64_t tag, uint64_t seq, const void *src, void *dst, size_t count,
                               DType dtype, ReduceOp op, int device, std::atomic<uint64_t> &tx,
-                              std::atomic<uint64_t> &rx, const InterHost *inter = nullptr, size_t world = 0);
+                              std::atomic<uint64_t> &rx, const InterHost *inter = nullptr, size_t world = 0,
+                              std::function<void(bool)> *settle = nullptr);
 
     // internal (exposed for the vote template)
     int vote_impl(Client &c, uint64_t tag, uint64_t seq, bool device_ok, int device, size_t bytes, DType dtype,

@@ -95,8 +95,8 @@ bool env_flag(const char *name, bool dflt);
 // Fault injection for the crash tests: PCCL_FAULT_INJECT="<point>:<seq>[:<step>[:<phase>]]" makes this process
 // SIGKILL itself when it reaches `point` in the op with master sequence number `seq` (and, if given, at ring step
 // `step` (global step index 0 .. 2(W-1)-1, all-gather steps after the reduce-scatter's) in phase `phase`). Points:
-// ipc_vote, ipc_kernel, ss_serve; ring (device ring; phases publish / rx / ahead / end) and qring (quantized device
-// ring; phases meta / rx / end). Lets a test kill a peer at an exact protocol position, e.g. while its xGMI push kernel
+// ipc_vote, ipc_kernel, ss_serve; ring (device ring; phases publish / rx / ahead / end), qring (quantized device
+// ring; phases meta / rx / end) and hring (host ring; phases rx / end). Lets a test kill a peer at an exact protocol position, e.g. while its xGMI push kernel
 // and its peers' kernels are running or while the next ring step's receive sinks are already posted.
 void fault_point(const char *point, uint64_t seq, size_t step = SIZE_MAX, const char *phase = nullptr);
 bool fault_injection_armed();

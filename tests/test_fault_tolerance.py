@@ -173,7 +173,10 @@ def _ipc_kill(tmp_path, point, inplace, respawn, shareable, *extra, inject=None,
 # (its metadata packet sent, waiting for the peer's), `rx`.
 RING_KILLS = [("ring", 0, "ahead", False), ("ring", 1, "rx", True), ("ring", 2, "rx", False),
               ("ring", 3, "publish", True), ("ring", 1, "end", False), ("qring", 1, "meta", True),
-              ("qring", 2, "rx", False), ("qring", 0, "rx", True)]
+              ("qring", 2, "rx", False), ("qring", 0, "rx", True),
+              # the victim dies after its last step: survivors finish their part, the master aborts the op anyway and
+              # the in-place input comes back from the backup kept until the verdict (OpState::settle)
+              ("ring", 3, "end", True), ("qring", 3, "end", True)]
 
 
 @pytest.mark.gpu
@@ -270,3 +273,34 @@ def test_gpu_ipc_quarantine_reclaimed_on_unchanged_ring(hip):
         assert max(used[5:]) - used[5] < 3 * (n * 4), used
         b = oks[-1]["ipc_bufs"]
         assert b["quarantined"] >= 45 and b["reclaimed"] >= 40, b
+
+
+# Host ring (CPU tensors): the victim SIGKILLs itself in op 8 at a global ring step (0-1 reduce-scatter, 2-3
+# all-gather) after its first received bytes were reduced (`rx`) or after the step completed (`end`).
+HRING_KILLS = [(0, "rx", True, False), (1, "end", False, False), (2, "rx", True, False), (3, "rx", False, False),
+               (1, "rx", True, True), (2, "end", True, True), (3, "end", True, False), (3, "end", True, True)]
+
+
+@pytest.mark.parametrize("step,phase,inplace,quant", HRING_KILLS)
+def test_host_ring_sigkill_mid_op(step, phase, inplace, quant):
+    """Abort safety of the host ring (the reference's data path, reduce.cpp:551-580,657-660): survivors of a peer
+    killed mid-op get an error for that op, find their in-place buffer restored bit-exactly 100 ms later, re-form the
+    ring and finish every step with exact results in the smaller world."""
+    n = 1 << 22
+    extra = (["--inplace"] if inplace else []) + (["--quant", "u8"] if quant else [])
+    with local_master() as addr:
+        ps = [spawn_python([WORKER, addr, "3", str(r), "--device", "cpu", "--const", "--n", str(n), "--steps", "30",
+                            "--pool", "2", *extra, *(["--verify-restore-ms", "100"] if r else [])],
+                           env={"PCCL_FAULT_INJECT": f"hring:8:{step}:{phase}"} if r == 0 else None,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
+        outs = communicate_all(ps, 240, DIAG_SIGNALS)
+    assert ps[0].returncode == -9, outs[0][1][-2000:]
+    for r in (1, 2):
+        assert ps[r].returncode == 0, outs[r][1][-3000:]
+        lines = _lines(outs[r][0])
+        oks = _check_ok(lines)
+        errs = [x for x in lines if "error" in x]
+        assert len(oks) == 30 and oks[0]["world"] == 3 and oks[-1]["world"] == 2, (len(oks), oks[-1])
+        assert errs and not any(x.get("restore_bad") for x in errs), errs
+        if inplace:
+            assert any("restore_bad" in x for x in errs), errs
