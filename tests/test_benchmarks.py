@@ -74,3 +74,14 @@ def test_fault_tolerance(device):
     assert r["all_results_exact"] and not r["peer_errors"]
     assert r["recovery_ms"] is not None and r["rejoin_ms"] is not None
     assert r["topology_resolve_ok"]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_py_latency(device):
+    """One process per peer, both call variants, exact results (checked inside every peer)."""
+    r = _run("py_latency.py", "--peers", "3", "--iters", "20", "--warmup", "3", "--sizes", "4096,262144",
+             "--device", device)
+    assert r["processes"] == "one per peer" and set(r["sizes"]) == {"4KiB", "256KiB"}
+    for row in r["sizes"].values():
+        assert row["path"] == ("host_ring" if device == "cpu" else "ipc")
+        assert row["all_reduce"]["median_us"] > 0 and row["ready"]["median_us"] > 0
