@@ -156,15 +156,42 @@ bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
     if (inline_run) {
         run_op(op);
     } else {
+        if (!fault_delay_armed()) initiate_op(*op);
         workers_.submit([this, op] { run_op(op); });
     }
     return true;
 }
 
+// Snapshot of the ring, the buffers' location and the initiate packet. The ring cannot change while the op is
+// registered (re-establishment waits for running ops), so the view taken here is the one the op executes on.
+void Client::initiate_op(OpState &op) {
+    op.initiated = true;
+    op.rv = ring_view(0);
+    if (DeviceBackend *be = device_backend()) {
+        be->pointer_info(op.req.src, op.si);
+        be->pointer_info(op.req.dst, op.di);
+    }
+    op.device = op.si.is_device && op.di.is_device && op.si.device == op.di.device;
+    C2MCollectiveCommsInitiate init;
+    init.tag = op.req.tag;
+    init.count = op.req.count;
+    init.data_type = op.req.dtype;
+    init.op = op.req.op;
+    const auto &rv = op.rv;
+    if (rv && rv->hier && op.device) init.flags |= kCollFlagHierarchical;
+    if (rv && rv->ring.size() >= 2 && use_small_path(op.req.count * dtype_size(op.req.dtype), rv->ring.size()) &&
+        (op.req.qalgo == QuantAlgo::None || op.req.qtype == op.req.dtype))
+        init.flags |= kCollFlagSmallPath;
+    op.init_sent = master_.send(init);
+}
+
 void Client::run_op(const std::shared_ptr<OpState> &op) {
     const uint64_t tag = op->req.tag;
     low_timer_slack();
-    fault_delay(tag);
+    if (!op->initiated) {
+        fault_delay(tag);
+        initiate_op(*op);
+    }
     OpTrace trace;
     current_trace() = trace_ops_enabled() ? &trace : nullptr;
     char range_name[96];
@@ -175,36 +202,18 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     uint64_t seq = 0;
     bool commenced = false;
     uint8_t agreed = 0;
-    // the ring cannot change while this op runs (re-establishment waits for running ops), so the view taken here
-    // is the one the op executes on
-    auto rv = ring_view(0);
-    DevPtrInfo si{}, di{};
-    DeviceBackend *be = device_backend();
-    if (be) {
-        be->pointer_info(op->req.src, si);
-        be->pointer_info(op->req.dst, di);
-    }
-    const bool device = si.is_device && di.is_device && si.device == di.device;
-    {
-        C2MCollectiveCommsInitiate init;
-        init.tag = tag;
-        init.count = op->req.count;
-        init.data_type = op->req.dtype;
-        init.op = op->req.op;
-        if (rv && rv->hier && device) init.flags |= kCollFlagHierarchical;
-        if (rv && rv->ring.size() >= 2 && use_small_path(op->req.count * dtype_size(op->req.dtype), rv->ring.size()) &&
-            (op->req.qalgo == QuantAlgo::None || op->req.qtype == op->req.dtype))
-            init.flags |= kCollFlagSmallPath;
-        if (master_.send(init)) {
-            auto c = master_.receive<M2CCollectiveCommsCommence>(
-                [tag](const M2CCollectiveCommsCommence &p) { return p.tag == tag; });
-            if (c) {
-                seq = c->seq_nr;
-                agreed = c->flags;
-                op->small_path = (agreed & kCollFlagSmallPath) != 0;
-                commenced = true;
-                trace_mark("commence");
-            }
+    const auto &rv = op->rv;
+    const DevPtrInfo &si = op->si, &di = op->di;
+    const bool device = op->device;
+    if (op->init_sent) {
+        auto c = master_.receive<M2CCollectiveCommsCommence>(
+            [tag](const M2CCollectiveCommsCommence &p) { return p.tag == tag; });
+        if (c) {
+            seq = c->seq_nr;
+            agreed = c->flags;
+            op->small_path = (agreed & kCollFlagSmallPath) != 0;
+            commenced = true;
+            trace_mark("commence");
         }
     }
     if (commenced) {
@@ -287,6 +296,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
         current_trace() = nullptr;
     }
     op->success = ok;
+    op->rv.reset(); // the snapshot's connections must not outlive the op (a re-established ring closes them)
     op->finish();
     {
         std::lock_guard l(done_mtx_);

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../common/device_backend.hpp"
+#include "../common/spin.hpp"
 #include "../common/types.hpp"
 #include "../net/listener.hpp"
 #include "../net/master_conn.hpp"
@@ -134,6 +135,24 @@ private:
     friend class IpcArena;
     enum class EstablishResult { Success, Retry, Failed };
 
+    // Hierarchical layout (master's host_of extension): hosts x local ranks. The host-local peers share an IPC arena;
+    // the peers with my local rank on every host form the inter-host ring (extra TX / RX pools).
+    struct HierState {
+        size_t hosts = 0, local = 0;   // H, L
+        size_t host = 0, local_rank = 0;
+        std::vector<Uuid> host_ring;   // the member with my local rank on host 0 .. H-1
+        std::shared_ptr<IpcArena> arena; // over my host's members, in ring order
+    };
+    struct RingView { // immutable snapshot used by an op thread
+        std::vector<Uuid> ring;
+        size_t rank = 0;
+        std::vector<std::shared_ptr<net::MuxConn>> tx; // pool to next
+        std::vector<std::shared_ptr<net::MuxConn>> rx; // pool from prev
+        std::shared_ptr<IpcArena> arena;
+        std::shared_ptr<HierState> hier;                    // null unless the layout qualifies
+        std::vector<std::shared_ptr<net::MuxConn>> htx, hrx; // inter-host ring pools (to next / from previous host)
+    };
+
     struct OpState {
         ReduceRequest req;
         std::mutex m;
@@ -143,6 +162,8 @@ private:
         // a tag stays in running_collective_coms_ops_tags until joinAsyncCollectiveOp)
         std::atomic<bool> joined{false};
         void wait() {
+            // short ops finish within tens of us of the wait: spin before paying a futex wake-up
+            if (spin_until([this] { return done.load(std::memory_order_acquire); }, 200)) return;
             std::unique_lock l(m);
             cv.wait(l, [this] { return done.load(); });
         }
@@ -163,24 +184,11 @@ private:
         // verdict. run_op calls it once with restore = true if the op failed anyway (a peer was lost after this
         // peer's part was done), so a retry reduces the caller's input, not the result.
         std::function<void(bool restore)> settle;
-    };
-
-    // Hierarchical layout (master's host_of extension): hosts x local ranks. The host-local peers share an IPC arena;
-    // the peers with my local rank on every host form the inter-host ring (extra TX / RX pools).
-    struct HierState {
-        size_t hosts = 0, local = 0;   // H, L
-        size_t host = 0, local_rank = 0;
-        std::vector<Uuid> host_ring;   // the member with my local rank on host 0 .. H-1
-        std::shared_ptr<IpcArena> arena; // over my host's members, in ring order
-    };
-    struct RingView { // immutable snapshot used by an op thread
-        std::vector<Uuid> ring;
-        size_t rank = 0;
-        std::vector<std::shared_ptr<net::MuxConn>> tx; // pool to next
-        std::vector<std::shared_ptr<net::MuxConn>> rx; // pool from prev
-        std::shared_ptr<IpcArena> arena;
-        std::shared_ptr<HierState> hier;                    // null unless the layout qualifies
-        std::vector<std::shared_ptr<net::MuxConn>> htx, hrx; // inter-host ring pools (to next / from previous host)
+        // initiate_op's results: the ring snapshot, where the buffers live, whether the master got the initiate
+        // (async ops are initiated on the submitting thread, so a worker's wake-up overlaps the master round trip)
+        bool initiated = false, init_sent = false, device = false;
+        std::optional<RingView> rv;
+        DevPtrInfo si{}, di{};
     };
 
     // connection management
@@ -194,6 +202,7 @@ private:
     std::optional<RingView> ring_view(uint64_t seq);
 
     // collectives
+    void initiate_op(OpState &op);
     void run_op(const std::shared_ptr<OpState> &op);
     // returns {success, abort_received}
     std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);

@@ -24,9 +24,8 @@ inline void low_timer_slack() {
 /// the ring (bench.py extra.cpu_by_thread) groups the process's threads by these names.
 inline void name_thread(const char *name) { prctl(PR_SET_NAME, reinterpret_cast<unsigned long>(name), 0, 0, 0); }
 
-/// Spins until pred() is true or the budget is spent; returns pred()'s last value.
-template <class Pred> inline bool spin_until(Pred &&pred) {
-    const long budget = spin_budget_us();
+/// Spins until pred() is true or the budget (us) is spent; returns pred()'s last value.
+template <class Pred> inline bool spin_until(Pred &&pred, long budget = spin_budget_us()) {
     if (budget <= 0) return pred();
     const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(budget);
     for (unsigned i = 0;; ++i) {

@@ -186,11 +186,20 @@ void fault_stall(const char *point, uint64_t seq) {
     ::usleep(static_cast<useconds_t>(std::atol(end + 1)) * 1000);
 }
 
-void fault_delay(uint64_t tag) {
+namespace {
+const std::string &fault_delay_spec() {
     static const std::string spec = [] {
         const char *e = std::getenv("PCCL_FAULT_DELAY");
         return std::string(e ? e : "");
     }();
+    return spec;
+}
+} // namespace
+
+bool fault_delay_armed() { return !fault_delay_spec().empty(); }
+
+void fault_delay(uint64_t tag) {
+    const std::string &spec = fault_delay_spec();
     if (spec.empty()) return;
     long ms = -1, any_ms = -1;
     size_t pos = 0;

@@ -106,6 +106,7 @@ void fault_stall(const char *point, uint64_t seq);
 // PCCL_FAULT_DELAY="<tag>:<ms>[,*:<ms>]": an op with that tag (or any tag, "*") sleeps before it initiates
 // (scheduler tests: a slow op among fast ones).
 void fault_delay(uint64_t tag);
+bool fault_delay_armed(); // PCCL_FAULT_DELAY is set (ops then initiate on their worker, after the delay)
 
 // PCCL_DEBUG_BACKTRACE_SIGNAL=1 (debugging hangs on the GPU box, where debuggers may not attach): SIGUSR2 prints the
 // native backtrace of every thread of the process to stderr (each thread is signalled in turn).
