@@ -21,7 +21,8 @@ reference tests/basic_reduce_test/main.cpp:141-143).
 ``extra`` also carries, measured in the same run: the xGMI/IPC path at the same peers (the library's default for
 same-host peers), 2 peers over IPC (N == 1), a busBW-vs-size sweep for both paths, the 1 GiB busBW at 2 / 4 / 8
 peers for both paths (``extra.peer_curve``, N == 1), small-message latencies (2-peer 4-element CPU all-reduce =
-BASELINE config 1; 1 MiB over IPC) and the peer-rejoin latency.
+BASELINE config 1; 1 MiB over IPC from the C API, from Python with one process per peer, and from Python threads of
+one process) and the peer-rejoin latency.
 
 vs_baseline is null: the reference publishes only WAN throughputs (25 / 45 Gbit/s), which are not
 comparable with a single-host loopback/HBM measurement.
@@ -453,6 +454,28 @@ def latency_native(peers):
     return out
 
 
+def latency_python_processes(peers):
+    """The Python API's small-op latency in the deployment shape: one process per peer (benchmarks/py_latency.py),
+    `peers` processes on cuda:0 over the xGMI/IPC path, 1 MiB bf16; the blocking call and the async call awaited at
+    once. Unlike extra.latency_1MiB_ipc_python_threads_us no GIL is shared between the peers."""
+    import subprocess
+    env = dict(os.environ)
+    env.pop("PCCL_DISABLE_IPC", None)
+    try:
+        with _full_cpu_mask():
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "py_latency.py"), "--peers",
+                                str(peers), "--iters", "200", "--sizes", str(1 << 20)], capture_output=True, text=True,
+                               timeout=180, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    row = json.loads(line[-1])["sizes"]["1024KiB"]
+    return {"peers": peers, "path": row["path"], "blocking_median_us": row["all_reduce"]["median_us"],
+            "blocking_p90_us": row["all_reduce"]["p90_us"], "async_median_us": row["ready"]["median_us"]}
+
+
 def rejoin_latency(job):
     """A new peer connects mid-run; seconds from its connect() until its first all-reduce completed (admission vote +
     P2P establishment + IPC rendezvous + first op). N == 1 only."""
@@ -546,6 +569,8 @@ def run_extras(job, a, nbytes):
         nat = extra["latency_native"].get(f"{P}_peers_1MiB", {})
         if "median_us" in nat:  # the library's latency: C API, threaded peers, no interpreter in the loop
             extra["latency_1MiB_ipc_us"] = nat["median_us"]
+        if not a.no_ipc_extra:
+            extra["latency_1MiB_ipc_python_processes"] = latency_python_processes(P)
         with _full_cpu_mask(ccd=True):
             extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         with _full_cpu_mask():

@@ -162,8 +162,8 @@ private:
         // a tag stays in running_collective_coms_ops_tags until joinAsyncCollectiveOp)
         std::atomic<bool> joined{false};
         void wait() {
-            // short ops finish within tens of us of the wait: spin before paying a futex wake-up
-            if (spin_until([this] { return done.load(std::memory_order_acquire); }, 200)) return;
+            // short ops finish within tens of us of the wait: spin briefly before paying a futex wake-up
+            if (spin_until([this] { return done.load(std::memory_order_acquire); })) return;
             std::unique_lock l(m);
             cv.wait(l, [this] { return done.load(); });
         }
