@@ -1423,8 +1423,9 @@ void settle_device_backup(std::function<void(bool)> &settle, DeviceBackend *be, 
         if (!restore) return;
         be->set_device(device);
         StreamLease s(device);
-        if (!s.get() || !be->memcpy_async(dst, b->data(), bytes, s.get()) || !be->stream_sync(s.get()))
+        if (!s.get() || !be->memcpy_async(dst, b->data(), bytes, s.get()) || !be->stream_sync(s.get())) {
             LOG(ERR) << "all-reduce: could not restore the in-place input after a late abort";
+        }
     };
 }
 

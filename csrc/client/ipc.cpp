@@ -1031,8 +1031,9 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
                     be->set_device(device);
                     StreamLease s(device);
                     if (!s.get() || !copy_staged(be, inb->segs, static_cast<uint8_t *>(dst), bytes, true, s.get()) ||
-                        !be->stream_sync(s.get()))
+                        !be->stream_sync(s.get())) {
                         LOG(ERR) << "IPC: could not restore the in-place input after a late abort";
+                    }
                 }
                 release_buffer(inb);
             };
