@@ -203,7 +203,8 @@ static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr && descriptor != nullptr && handle_out != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
-    PCCL_REQUIRE(sendbuff != nullptr && recvbuff != nullptr, pcclInvalidArgument);
+    // a zero-length op is legal (every peer still runs the protocol; empty tensors have null data pointers)
+    PCCL_REQUIRE((sendbuff != nullptr && recvbuff != nullptr) || descriptor->count == 0, pcclInvalidArgument);
     auto dt = to_dtype(descriptor->src_descriptor.datatype);
     auto op = to_op(descriptor->op);
     auto qa = to_qalgo(descriptor->quantization_options.algorithm);

@@ -171,7 +171,8 @@ void Client::initiate_op(OpState &op) {
         be->pointer_info(op.req.src, op.si);
         be->pointer_info(op.req.dst, op.di);
     }
-    op.device = op.si.is_device && op.di.is_device && op.si.device == op.di.device;
+    // an empty op moves no data: the host ring runs its protocol without touching either buffer
+    op.device = op.req.count > 0 && op.si.is_device && op.di.is_device && op.si.device == op.di.device;
     C2MCollectiveCommsInitiate init;
     init.tag = op.req.tag;
     init.count = op.req.count;
@@ -243,7 +244,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
                 if (device) {
                     r = ring_reduce_device(*op, *rv, seq, di.device);
                     if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceRing);
-                } else if (!si.is_device && !di.is_device) {
+                } else if ((!si.is_device && !di.is_device) || op->req.count == 0) {
                     r = ring_reduce_host(*op, *rv, seq);
                     if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::HostRing);
                 } else {
@@ -822,8 +823,8 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
 
     // in place: a backup of the input, restored if the ring fails or the master aborts the op afterwards (settle)
     Lease backup;
-    if (q.src == q.dst && !q.scratch) {
-        backup = Lease(host_pool(), std::max<size_t>(bytes, 64));
+    if (q.src == q.dst && !q.scratch && bytes) {
+        backup = Lease(host_pool(), bytes);
         if (!backup.ok()) return {false, false};
         std::memcpy(backup.data(), q.src, bytes);
     }
@@ -840,7 +841,7 @@ std::pair<bool, bool> Client::ring_reduce_host(OpState &op, const RingView &rv, 
         if (rc == 0) keep_backup();
         return {rc == 0, rc == 2};
     }
-    if (q.src != q.dst) std::memcpy(dst, q.src, bytes);
+    if (q.src != q.dst && bytes) std::memcpy(dst, q.src, bytes);
     const std::vector<size_t> lo = quant ? quant_lane_bounds(q.count, ws, dtype_size(q.qtype))
                                          : std::vector<size_t>{0, q.count};
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {

@@ -376,3 +376,26 @@ def test_small_message_threshold_mismatch_is_agreed():
         assert len(lines) == 3 and all("error" not in ln for ln in lines), lines
         for ln in lines:
             assert ln["lo"] == ln["hi"] == float(3 + 2 * ln["step"])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("quant", [False, True])
+def test_zero_length(world, quant):
+    """An empty all-reduce is a legal no-op that still runs the protocol on every peer (the reference's ring tests
+    include zero-length inputs); the next op on the same communicators works."""
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if quant else None
+
+    def fn(rank, comm):
+        # null data pointers (torch.empty(0)) on rank 0, a non-null zero-length slice elsewhere
+        e = torch.empty(0) if rank == 0 else torch.ones(4)[:0]
+        info = comm.all_reduce(e, e, op=pccl.ReduceOp.SUM, tag=0, quantization_options=qopt)
+        x, out = torch.full((5,), float(rank + 1)), torch.empty(5)
+        comm.all_reduce(x, out, op=pccl.ReduceOp.SUM, tag=1)
+        return info, out
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr)
+    for info, out in res:
+        assert info.local_world_size == world
+        assert quant or info.tx_bytes == 0  # the quantized ring still exchanges its per-step metadata
+        assert out.tolist() == [world * (world + 1) / 2] * 5

@@ -80,6 +80,26 @@ def test_device_concurrent_tags(hip, disable_ipc, monkeypatch):
             assert torch.all(y == float(1 + 2 * j))
 
 
+@pytest.mark.parametrize("disable_ipc", [False, True])
+def test_device_zero_length(hip, disable_ipc, monkeypatch):
+    """Empty ops on HBM tensors: a null pointer (torch.empty(0)) on one peer, a non-null zero-length slice on the
+    others; every peer runs the protocol, no buffer is touched, and a real op follows on the same ring."""
+    if disable_ipc:
+        monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+
+    def fn(rank, comm):
+        base = torch.ones(16, device=hip)
+        x = torch.empty(0, device=hip) if rank == 0 else base[:0]
+        comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)
+        y = torch.empty_like(base)
+        comm.all_reduce(base, y, op=pccl.ReduceOp.SUM, tag=1)
+        torch.cuda.synchronize()
+        return base.cpu(), y.cpu()
+
+    for base, y in _run(3, fn):
+        assert base.tolist() == [1.0] * 16 and y.tolist() == [3.0] * 16
+
+
 @pytest.mark.parametrize("world,inplace,op", [(3, True, "sum"), (4, False, "avg"), (2, True, "max")])
 def test_device_ring_pipelined_large(hip, world, inplace, op, monkeypatch):
     """Device TCP ring with many pieces per stripe and several stripes per step (1 MiB copies, 4 stripes, uneven
