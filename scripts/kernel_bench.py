@@ -46,6 +46,11 @@ def main():
         n * 2 * 2 + n)
     row("dequant_reduce u8->bf16 sum (pccl)", timeit(lambda: K.dequant_reduce(x, q, meta, "min_max", "sum"), a.iters),
         n + 2 * n * 2)
+    ys = y.clone()
+    row("quantize_setback bf16->u8 + D(Q(x)) back (pccl, min/max pass + fused pass)",
+        timeit(lambda: K.quantize_setback(ys, torch.uint8, "min_max"), a.iters), n * 2 * 2 + n + n * 2)
+    row("dequant_reduce_minmax u8->bf16 sum + min/max partials (pccl)",
+        timeit(lambda: K.dequant_reduce_minmax(x, q, meta, "min_max", "sum"), a.iters), n + 2 * n * 2)
     qz, mz = K.quantize(y, torch.uint8, "zero_point_scale")
     row("quantize bf16->u8 zero-point-scale (pccl)",
         timeit(lambda: K.quantize(y, torch.uint8, "zero_point_scale"), a.iters), n * 2 * 2 + n)
