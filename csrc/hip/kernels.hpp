@@ -368,8 +368,25 @@ __device__ __forceinline__ Q q_from_double(double q) {
         return q >= 18446744073709551615.0 ? ~0ull : static_cast<uint64_t>(q);
     } else if constexpr (sizeof(Q) == 8) {
         return q >= 9223372036854775807.0 ? INT64_MAX : static_cast<int64_t>(q);
+    } else if constexpr (__is_signed(Q)) { // integral and inside Q's range: the native 32-bit conversions are exact
+        return static_cast<Q>(static_cast<int32_t>(q)); // (a 64-bit one is a ~6-instruction FP64 sequence)
     } else {
-        return static_cast<Q>(static_cast<int64_t>(q));
+        return static_cast<Q>(static_cast<uint32_t>(q));
+    }
+}
+
+// q_from_double(q_minmax_int(x, p)) without FP64 floor / add for wire types up to 32 bits: r is clamped to
+// [0, range] first, where truncation (the native conversion) equals floor, and adding qlo as an integer is exact -
+// the same integer for every input.
+template<typename Q>
+__device__ __forceinline__ Q q_minmax_as(double x, const QuantParams &p) {
+    if constexpr (sizeof(Q) == 8) {
+        return q_from_double<Q>(q_minmax_int(x, p));
+    } else {
+        double r = (x - p.min) * p.inv_dif * p.range + 0.5;
+        r = r < 0.0 ? 0.0 : r;
+        r = r > p.range ? p.range : r;
+        return static_cast<Q>(static_cast<int64_t>(static_cast<uint32_t>(r)) + static_cast<int64_t>(p.qlo));
     }
 }
 
@@ -387,7 +404,7 @@ __global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, typena
     ew_loop_ls<V, kEwUnroll>(
         n, head, vec,
         [&](size_t i) {
-            const Q q = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(src[i])), p));
+            const Q q = q_minmax_as<Q>(static_cast<double>(E::ld(src[i])), p);
             dst[i] = q;
             if constexpr (BACK) src[i] = back(q);
         },
@@ -395,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_q_minmax(Q *__restrict__ dst, typena
         [&](size_t b, const Pack<S, V> &s) {
             Pack<Q, V> q;
 #pragma unroll
-            for (int e = 0; e < V; ++e) q.v[e] = q_from_double<Q>(q_minmax_int(static_cast<double>(E::ld(s.v[e])), p));
+            for (int e = 0; e < V; ++e) q.v[e] = q_minmax_as<Q>(static_cast<double>(E::ld(s.v[e])), p);
             stp<Q, V>(dst + b, q);
             if constexpr (BACK) {
                 Pack<S, V> d;

@@ -156,7 +156,18 @@ PCCL_HD float dq_zps(int64_t q, const QuantParams &p) { return static_cast<float
 // wire element Q of zero-point-scale (64-bit types clamp and subtract in double)
 template<typename Q>
 PCCL_HD Q q_zps_as(float x, const QuantParams &p) {
-    if constexpr (sizeof(Q) <= 4) {
+    if constexpr (sizeof(Q) <= 2) { // same values as q_zps in 32-bit integers (|r|, |zp| < 2^17; no 64-bit emulation
+        float r = __builtin_rintf(x * p.zps_inv); // on the GPU)
+        const int32_t ilo = static_cast<int32_t>(p.ilo), ihi = static_cast<int32_t>(p.ihi);
+        const int32_t zp = static_cast<int32_t>(p.zp);
+        const float lo = static_cast<float>(ilo - zp), hi = static_cast<float>(ihi - zp);
+        r = r < lo ? lo : r;
+        r = r > hi ? hi : r;
+        int32_t q = static_cast<int32_t>(r) + zp;
+        q = q < ilo ? ilo : q;
+        q = q > ihi ? ihi : q;
+        return static_cast<Q>(q);
+    } else if constexpr (sizeof(Q) <= 4) {
         return static_cast<Q>(q_zps(x, p));
     } else {
         double r = static_cast<double>(__builtin_rintf(x * p.zps_inv)) + static_cast<double>(p.zp);
@@ -167,7 +178,8 @@ PCCL_HD Q q_zps_as(float x, const QuantParams &p) {
 }
 template<typename Q>
 PCCL_HD float dq_zps_as(Q q, const QuantParams &p) {
-    if constexpr (sizeof(Q) <= 4) return dq_zps(static_cast<int64_t>(q), p);
+    if constexpr (sizeof(Q) <= 2) return static_cast<float>(static_cast<int32_t>(q) - static_cast<int32_t>(p.zp)) * p.zps_scale;
+    else if constexpr (sizeof(Q) <= 4) return dq_zps(static_cast<int64_t>(q), p);
     else return static_cast<float>(static_cast<double>(q) - static_cast<double>(p.zp)) * p.zps_scale;
 }
 
