@@ -1539,8 +1539,7 @@ struct QLane {
     size_t ws, rank;
     uint64_t tag, seq; // the lane's data tag (metadata on meta_tag(tag))
     DeviceBackend *be;
-    PcieQueues pq;
-    DevStream st;   // the lane's stream
+    DevStream st;   // the lane's stream (its copies, kernels and events)
     DevEvent ready; // the op's input copy / backup into dst (recorded on the op stream)
     uint8_t *dst;   // the lane's elements (hold the input once `ready` completed)
     size_t count, es, qs, piece_el;
@@ -1699,6 +1698,7 @@ int device_quant_lane(QLane &L) {
         gate_opened = true;
     };
     QuantMeta theirs;
+    const bool ag_staged = env_flag("PCCL_QUANT_AG_STAGED", false); // temporary A/B
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb;
         const bool rs = is_rs(g);
@@ -1746,11 +1746,18 @@ int device_quant_lane(QLane &L) {
             g, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
-                if (rs) { // copy engine -> HBM, then de-quantize-reduce HBM -> HBM (interleaved A/B against kernels
-                          // reading pinned memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
-                    be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, L.pq.h2d);
-                    be->stream_wait_event(st, record(L.pq.h2d));
+                if (rs) { // host -> HBM on the lane's own stream, then de-quantize-reduce HBM -> HBM. Interleaved A/Bs:
+                          // staged beats kernels reading pinned memory (218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl);
+                          // the lane's stream beats the process-wide copy queue, where the step's last pieces wait
+                          // behind every other peer's copies before the next min / max exists (188.1 vs 197.9 ms,
+                          // profiles/r4/b23/quant.jsonl; the plain ring keeps the shared queue: 332.9 vs 365.3 ms)
+                    be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
                     dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
+                } else if (ag_staged) { // temporary A/B: forwardable at once; host -> HBM on the lane's stream
+                    rxready[b].add(a, e, nullptr);
+                    be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
+                    be->dequant_reduce(region + a / qs * es, rxdev[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
+                                       st);
                 } else { // forwardable at once; de-quantized straight from pinned memory (interleaved A/B against
                          // copy engine -> HBM first: 193.4 vs 197.8 ms, profiles/r4/b15/ag.jsonl)
                     rxready[b].add(a, e, nullptr);
@@ -1798,8 +1805,6 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     StreamLease stream(device);
     DevStream st = stream.get();
     if (!st) return {false, false};
-    const PcieQueues pq = shared_pcie_queues(be, device);
-    if (!pq.h2d) return {false, false};
 
     Lease backup;
     const bool keep_backup = q.src == q.dst && !q.scratch;
@@ -1833,7 +1838,7 @@ std::pair<bool, bool> Client::ring_reduce_device_quant(OpState &op, const RingVi
     std::atomic<bool> op_failed{false};
     std::vector<LaneGate> gates(nl);
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
-        QLane L{&rv.tx, &rv.rx, ws, rv.rank, lane_tag(q.tag, k, nl), seq, be, pq, lane_streams[k]->get(), ready,
+        QLane L{&rv.tx, &rv.rx, ws, rv.rank, lane_tag(q.tag, k, nl), seq, be, lane_streams[k]->get(), ready,
                 dst + a * es, b - a, es, qs, piece / es, q.dtype, q.qtype, q.qalgo, q.op, device,
                 [&] { return aborted(); }, &op.tx, &op.rx, &op_failed, k > 0 ? &gates[k - 1] : nullptr,
                 k + 1 < nl ? &gates[k] : nullptr};
