@@ -1698,7 +1698,6 @@ int device_quant_lane(QLane &L) {
         gate_opened = true;
     };
     QuantMeta theirs;
-    const bool ag_staged = env_flag("PCCL_QUANT_AG_STAGED", false); // temporary A/B
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb;
         const bool rs = is_rs(g);
@@ -1753,15 +1752,13 @@ int device_quant_lane(QLane &L) {
                           // profiles/r4/b23/quant.jsonl; the plain ring keeps the shared queue: 332.9 vs 365.3 ms)
                     be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
                     dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
-                } else if (ag_staged) { // temporary A/B: forwardable at once; host -> HBM on the lane's stream
+                } else { // forwardable at once (from pinned memory); host -> HBM on the lane's stream, de-quantized
+                         // from HBM. Interleaved A/Bs against kernels reading pinned memory: 186.5 vs 190.4 ms
+                         // (profiles/r4/b25/ag.jsonl); through the process-wide queue it was the slower one (197.8 vs
+                         // 193.4 ms, b15/ag.jsonl)
                     rxready[b].add(a, e, nullptr);
                     be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
                     be->dequant_reduce(region + a / qs * es, rxdev[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
-                                       st);
-                } else { // forwardable at once; de-quantized straight from pinned memory (interleaved A/B against
-                         // copy engine -> HBM first: 193.4 vs 197.8 ms, profiles/r4/b15/ag.jsonl)
-                    rxready[b].add(a, e, nullptr);
-                    be->dequant_reduce(region + a / qs * es, rxbuf[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
                                        st);
                 }
                 step_last = record(st);
