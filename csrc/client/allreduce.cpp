@@ -1698,6 +1698,16 @@ int device_quant_lane(QLane &L) {
         gate_opened = true;
     };
     QuantMeta theirs;
+    // Where received pieces go to HBM. Large steps (>= 4 MiB of quantized bytes per lane and step): on the lane's own
+    // stream, in both phases - in the process-wide queue a step's last pieces wait behind every other peer's copies
+    // before the next min / max exists (8 peers x 1 GiB bf16, interleaved: 188.1 vs 197.9 ms, profiles/r4/b23/;
+    // all-gather 186.5 vs 190.4 ms, b25/). Small steps (many concurrent ops, e.g. config 3 over the WAN emulator with
+    // ~1 MiB steps): the shared queue in the reduce-scatter, kernels reading pinned memory in the all-gather, as
+    // per-lane copies there measured 1.34-1.38 vs 1.09-1.16 s per 2 GiB (b29/). The plain ring keeps the shared queue
+    // at every size (332.9 vs 365.3 ms, b23/).
+    const bool lane_copies = max_chunk * qs >= (size_t{4} << 20);
+    const PcieQueues pq = lane_copies ? PcieQueues{} : shared_pcie_queues(be, L.device);
+    if (!lane_copies && !pq.h2d) return fail(1);
     for (size_t g = 0; g < nsteps; ++g) {
         const size_t b = g % kNb;
         const bool rs = is_rs(g);
@@ -1745,20 +1755,24 @@ int device_quant_lane(QLane &L) {
             g, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
-                if (rs) { // host -> HBM on the lane's own stream, then de-quantize-reduce HBM -> HBM. Interleaved A/Bs:
-                          // staged beats kernels reading pinned memory (218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl);
-                          // the lane's stream beats the process-wide copy queue, where the step's last pieces wait
-                          // behind every other peer's copies before the next min / max exists (188.1 vs 197.9 ms,
-                          // profiles/r4/b23/quant.jsonl; the plain ring keeps the shared queue: 332.9 vs 365.3 ms)
-                    be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
+                if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading pinned
+                          // memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
+                    if (lane_copies) {
+                        be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
+                    } else {
+                        be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, pq.h2d);
+                        be->stream_wait_event(st, record(pq.h2d));
+                    }
                     dequant_consume(region + a / qs * es, rxdev[b] + a, n, params);
-                } else { // forwardable at once (from pinned memory); host -> HBM on the lane's stream, de-quantized
-                         // from HBM. Interleaved A/Bs against kernels reading pinned memory: 186.5 vs 190.4 ms
-                         // (profiles/r4/b25/ag.jsonl); through the process-wide queue it was the slower one (197.8 vs
-                         // 193.4 ms, b15/ag.jsonl)
+                } else if (lane_copies) { // forwardable at once (from pinned memory); host -> HBM on the lane's stream,
+                                          // de-quantized from HBM
                     rxready[b].add(a, e, nullptr);
                     be->memcpy_async(rxdev[b] + a, rxbuf[b] + a, e - a, st);
                     be->dequant_reduce(region + a / qs * es, rxdev[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
+                                       st);
+                } else { // forwardable at once; de-quantized straight from pinned memory
+                    rxready[b].add(a, e, nullptr);
+                    be->dequant_reduce(region + a / qs * es, rxbuf[b] + a, n, L.dtype, L.qtype, ReduceOp::Set, params,
                                        st);
                 }
                 step_last = record(st);
