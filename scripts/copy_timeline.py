@@ -74,6 +74,9 @@ def main(d, bin_ms=20.0, skip_ms=0.0):
     for k in ("H2D", "D2H"):
         if k in nbytes and unions.get(k):
             busy = _cover(unions[k], t0, t1) / 1e9
+            if nbytes[k] == 0:  # this rocprofv3 version's copy trace has no size column
+                print(f"{k}: {len(series[k])} copies, {busy * 1e3:.1f} ms busy (sizes not in the trace)")
+                continue
             print(f"{k}: {nbytes[k] / 2**30:.2f} GiB, {len(series[k])} copies, {nbytes[k] / 1e9 / max(busy, 1e-9):.1f} GB/s "
                   f"while busy")
     step = int(bin_ms * 1e6)
