@@ -254,6 +254,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
             }
             success = r.first && !r.second;
             abort_seen = r.second;
+            if (success) fault_point("op_end", seq); // this peer's part is done, the master has no verdict yet
         } else {
             LOG(WARN) << "all-reduce tag " << tag << ": no usable ring (peers lost)";
         }

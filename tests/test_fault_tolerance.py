@@ -125,6 +125,21 @@ def test_gpu_ipc_sigkill_mid_op(hip, tmp_path, point, inplace, respawn, shareabl
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shareable", [False, True])
+def test_gpu_ipc_sigkill_after_local_success(hip, tmp_path, shareable):
+    """op_end on the xGMI path: op 300 finished on every peer (the gathered barrier passed, every output holds the
+    result) and the victim dies before its completion packet. If the master aborts op 300 the survivors' in-place
+    buffers must hold the input again (the staged original is kept until the verdict, OpState::settle), else the
+    result stands and the next op fails; either way every failed op's buffer is re-read 200 ms later bit-exactly
+    and the survivors continue on the IPC path."""
+    summary = _ipc_kill(tmp_path, "op_end", True, False, shareable, "--verify-restore-ms", "200",
+                        inject="op_end:300")
+    for k in (1, 2):
+        s_k = summary[f"peer{k}"]
+        assert s_k["errors"] >= 1 and s_k["restore_bad"] == 0 and s_k["restore_checked"] >= 1, s_k
+
+
+@pytest.mark.gpu
 def test_gpu_ipc_sigkill_many_threads_restore_is_final(hip, tmp_path):
     """Abort quiescence keyed to GPU state, not process state: the victim runs 48 extra busy threads, so when it is
     SIGKILLed right after launching its push kernel its group leader turns zombie while the other threads still exit
@@ -176,7 +191,9 @@ RING_KILLS = [("ring", 0, "ahead", False), ("ring", 1, "rx", True), ("ring", 2, 
               ("qring", 2, "rx", False), ("qring", 0, "rx", True),
               # the victim dies after its last step: survivors finish their part, the master aborts the op anyway and
               # the in-place input comes back from the backup kept until the verdict (OpState::settle)
-              ("ring", 3, "end", True), ("qring", 3, "end", True)]
+              ("ring", 3, "end", True), ("qring", 3, "end", True),
+              # after the victim's whole part (the op_end point, before its completion packet), plain and quantized
+              ("op_end", None, None, True), ("op_end", None, "q", True)]
 
 
 @pytest.mark.gpu
@@ -185,9 +202,10 @@ def test_gpu_ring_sigkill_mid_op(hip, tmp_path, point, step, phase, inplace):
     """Abort safety of the pipelined device ring (plain and quantized): survivors drain every copy / kernel of the
     aborted op before their in-place buffer is restored (re-read 200 ms later, bit-exact), re-form the ring and keep
     producing exact results for at least 20 more ops in the smaller world (reference reduce.cpp:551-580,657-660)."""
-    quant = point == "qring"
+    quant = point == "qring" or phase == "q"
+    inject = "op_end:12" if point == "op_end" else f"{point}:12:{step}:{phase}"
     summary = _ipc_kill(tmp_path, point, inplace, False, False, "--disable-ipc", "--verify-restore-ms", "200",
-                        "--pool", "2", *(["--quant", "u8"] if quant else []), inject=f"{point}:12:{step}:{phase}",
+                        "--pool", "2", *(["--quant", "u8"] if quant else []), inject=inject,
                         path=2, n=1 << 26, duration=12, min_ops=30)
     for k in (1, 2):
         s_k = summary[f"peer{k}"]
@@ -278,7 +296,13 @@ def test_gpu_ipc_quarantine_reclaimed_on_unchanged_ring(hip):
 # Host ring (CPU tensors): the victim SIGKILLs itself in op 8 at a global ring step (0-1 reduce-scatter, 2-3
 # all-gather) after its first received bytes were reduced (`rx`) or after the step completed (`end`).
 HRING_KILLS = [(0, "rx", True, False), (1, "end", False, False), (2, "rx", True, False), (3, "rx", False, False),
-               (1, "rx", True, True), (2, "end", True, True), (3, "end", True, False), (3, "end", True, True)]
+               (1, "rx", True, True), (2, "end", True, True), (3, "end", True, False), (3, "end", True, True),
+               # op_end: the victim finished its part of op 8 and dies before its completion packet. Depending on
+               # when the master sees the disconnect, op 8 either completes for the survivors (their results stand)
+               # or is aborted after their rings succeeded (the input comes back from the backup kept until the
+               # verdict); either way the next op fails and restores. (2, "end", True, True) above is the case that
+               # needs the late restore every time: one survivor's ring succeeded, the other's failed.
+               (None, "op_end", True, False), (None, "op_end", True, True)]
 
 
 @pytest.mark.parametrize("step,phase,inplace,quant", HRING_KILLS)
@@ -291,7 +315,8 @@ def test_host_ring_sigkill_mid_op(step, phase, inplace, quant):
     with local_master() as addr:
         ps = [spawn_python([WORKER, addr, "3", str(r), "--device", "cpu", "--const", "--n", str(n), "--steps", "30",
                             "--pool", "2", *extra, *(["--verify-restore-ms", "100"] if r else [])],
-                           env={"PCCL_FAULT_INJECT": f"hring:8:{step}:{phase}"} if r == 0 else None,
+                           env={"PCCL_FAULT_INJECT": "op_end:8" if phase == "op_end" else f"hring:8:{step}:{phase}"}
+                           if r == 0 else None,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
         outs = communicate_all(ps, 240, DIAG_SIGNALS)
     assert ps[0].returncode == -9, outs[0][1][-2000:]
