@@ -461,6 +461,9 @@ def latency_python_processes(peers):
     import subprocess
     env = dict(os.environ)
     env.pop("PCCL_DISABLE_IPC", None)
+    # 8 peer processes next to this one on the same GPU: 2 hardware queues each (README: several processes on one
+    # GPU), so their queues plus this process's fit the GPU's queue slots without time-slicing
+    env.setdefault("GPU_MAX_HW_QUEUES", "2")
     try:
         with _full_cpu_mask():
             r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "py_latency.py"), "--peers",
