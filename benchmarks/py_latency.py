@@ -90,13 +90,16 @@ def main():
     import pccl_amd as pccl
     from pccl_amd.utils import DIAG_SIGNALS, communicate_all, free_port
     port = free_port()
+    env = dict(os.environ)
+    if a.device.startswith("cuda"):  # several processes on one GPU: 2 hardware queues each (README), so the peers'
+        env.setdefault("GPU_MAX_HW_QUEUES", "2")  # queues fit the GPU's slots without time-slicing
     master = pccl.MasterNode(f"0.0.0.0:{port}")
     master.run()
     try:
         procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--peer", "--master",
                                    f"127.0.0.1:{port}", "--rank", str(r), "--peers", str(a.peers), "--iters",
                                    str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device],
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
                  for r in range(a.peers)]
         outs = communicate_all(procs, 600, DIAG_SIGNALS)
     finally:
