@@ -462,7 +462,7 @@ def latency_python_processes(peers):
     env = dict(os.environ)
     env.pop("PCCL_DISABLE_IPC", None)
     # 8 peer processes next to this one on the same GPU: 2 hardware queues each (README: several processes on one
-    # GPU), so their queues plus this process's fit the GPU's queue slots without time-slicing
+    # GPU). The blocking latency of this layout is bimodal on the shared boxes either way (docs/ROUND4_RESPONSE.md)
     env.setdefault("GPU_MAX_HW_QUEUES", "2")
     try:
         with _full_cpu_mask():
