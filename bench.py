@@ -22,7 +22,10 @@ reference tests/basic_reduce_test/main.cpp:141-143).
 same-host peers), 2 peers over IPC (N == 1), a busBW-vs-size sweep for both paths, the 1 GiB busBW at 2 / 4 / 8
 peers for both paths (``extra.peer_curve``, N == 1), small-message latencies (2-peer 4-element CPU all-reduce =
 BASELINE config 1; 1 MiB over IPC from the C API, from Python with one process per peer, and from Python threads of
-one process) and the peer-rejoin latency.
+one process) and, N == 1, BASELINE configs 5 and 4 in their own processes (``extra.baseline_configs``): kill + rejoin
+1 of 8 peer processes mid-all-reduce with the ATSP re-solve, on the TCP device ring and on the xGMI path, and the 1B
+fp32 late joiner over TCP and IPC; ``extra.peer_rejoin_latency_ms`` (the metric's second half) is config 5's rejoin on
+the TCP device ring.
 
 vs_baseline is null: the reference publishes only WAN throughputs (25 / 45 Gbit/s), which are not
 comparable with a single-host loopback/HBM measurement.
@@ -62,6 +65,8 @@ def _args():
     ap.add_argument("--no-ipc-extra", action="store_true", help="skip the xGMI/IPC measurements in extra")
     ap.add_argument("--no-peer-curve", action="store_true", help="skip the 2 / 4 peer points of the 1 GiB curve")
     ap.add_argument("--no-quant-extra", action="store_true", help="skip the uint8-quantized device ring in extra")
+    ap.add_argument("--no-config-extra", action="store_true",
+                    help="skip BASELINE configs 4 / 5 (late joiner, kill + rejoin) in extra")
     ap.add_argument("--extras-child", default="", help=argparse.SUPPRESS)  # internal: run only the extras, write JSON
     return ap.parse_args()
 
@@ -479,6 +484,44 @@ def latency_python_processes(peers):
             "blocking_p90_us": row["all_reduce"]["p90_us"], "async_median_us": row["ready"]["median_us"]}
 
 
+def baseline_configs(a, peers):
+    """BASELINE configs 5 and 4 as the reference defines them, each in its own processes (one per peer) and under its
+    own time limit, so a failure is reported here instead of losing the headline:
+      * config 5 (benchmarks/fault_tolerance.py): `peers` peer processes on cuda:0, in-place SUM of `--mib` MiB bf16;
+        the last peer SIGKILLs itself mid-op (PCCL_FAULT_INJECT; TCP device ring: reduce-scatter step 1 with its first
+        received piece in flight; xGMI path: right after launching its push kernel); the survivors abort, re-form the
+        ring and continue; a replacement process joins; every peer re-solves the ring (bandwidth probes + ATSP). On the
+        TCP device ring (PCCL_DISABLE_IPC=1, the reference's data path) and on the xGMI path.
+      * config 4 (benchmarks/shared_state_sync.py): a 1B-parameter fp32 shared state (8 tensors, 4 GB in HBM); a late
+        joiner at revision 0 catches up from a trainer at revision 3, over loopback TCP (pinned staging) and over the
+        same-host IPC hand-off; content and simplehash digests compared with the trainer's."""
+    import subprocess
+    runs = [("config5_kill_rejoin_tcp", ["fault_tolerance.py", "--transport", "tcp", "--peers", str(peers), "--mib",
+                                         str(a.mib)], 240),
+            ("config5_kill_rejoin_ipc", ["fault_tolerance.py", "--transport", "ipc", "--peers", str(peers), "--mib",
+                                         str(a.mib)], 180),
+            ("config4_late_joiner_tcp", ["shared_state_sync.py", "--transport", "tcp", "--params", "1e9"], 180),
+            ("config4_late_joiner_ipc", ["shared_state_sync.py", "--transport", "ipc", "--params", "1e9"], 120)]
+    out = {}
+    env = dict(os.environ)
+    env.pop("PCCL_DISABLE_IPC", None)  # set by this process's TCP-ring phases; the harnesses choose per run
+    for name, args, limit in runs:
+        _log(f"{name}: {' '.join(args)}")
+        t0 = time.time()
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", args[0]), *args[1:],
+                                *(["--timeout", str(limit - 40)] if args[0] == "fault_tolerance.py" else [])],
+                               capture_output=True, text=True, timeout=limit, env=env)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            out[name] = json.loads(line[-1]) if r.returncode == 0 and line else \
+                {"error": f"rc {r.returncode}: {r.stderr[-400:]}"}
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": f"timeout after {limit} s"}
+        out[name]["wall_s"] = round(time.time() - t0, 1)
+        _log(f"  done in {out[name]['wall_s']} s")
+    return out
+
+
 def rejoin_latency(job):
     """A new peer connects mid-run; seconds from its connect() until its first all-reduce completed (admission vote +
     P2P establishment + IPC rendezvous + first op). N == 1 only."""
@@ -576,9 +619,11 @@ def run_extras(job, a, nbytes):
             extra["latency_1MiB_ipc_python_processes"] = latency_python_processes(P)
         with _full_cpu_mask(ccd=True):
             extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
-        with _full_cpu_mask():
-            r = rejoin_latency(job)
-        extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
+        if a.no_config_extra:  # (else: BASELINE config 5 in main(), outside this child's time limit)
+            with _full_cpu_mask():
+                r = rejoin_latency(job)
+            extra["peer_rejoin_latency_ms"] = round(r * 1e3, 1) if r else None
+            extra["peer_rejoin_latency_source"] = "2 threaded peers, xGMI path, connect -> first op (no kill)"
     else:
         extra["multi_gpu_table"] = multi_gpu_table(job, a, nbytes)
     return extra, sweep
@@ -673,6 +718,8 @@ def extras_in_child(job, a):
         args.append("--no-peer-curve")
     if a.no_quant_extra:
         args.append("--no-quant-extra")
+    if a.no_config_extra:
+        args.append("--no-config-extra")
     env = dict(os.environ)
     if job.world > 1:
         env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 11)
@@ -839,6 +886,16 @@ def main():
             x_extra, x_sweep = extras_in_child(job, a)
         extra.update(x_extra)
         sweep.update(x_sweep)
+        if job.world == 1 and not a.no_config_extra:
+            cfg = baseline_configs(a, P)
+            extra["baseline_configs"] = cfg
+            c5 = cfg.get("config5_kill_rejoin_tcp", {})
+            # the metric's "peer-rejoin latency": BASELINE config 5 on the TCP device ring, the replacement process's
+            # connect() -> its first exact all-reduce with the full world (admission vote + P2P establishment + op)
+            extra["peer_rejoin_latency_ms"] = c5.get("joiner_connect_to_first_exact_op_ms")
+            extra["peer_rejoin_latency_source"] = ("BASELINE config 5, TCP device ring: replacement process's connect() "
+                                                   "-> its first exact 1 GiB all-reduce at full world, after a peer was "
+                                                   "SIGKILLed mid-op")
         if "peer_curve" in extra:
             extra["peer_curve"].setdefault("DEVICE_RING", {})[str(P)] = _curve_point(nbytes, ring["t"], P)
     extra["sweep"] = sweep

@@ -1,31 +1,41 @@
 """BASELINE config 5: kill + rejoin 1 of 8 peers mid-all-reduce, then re-solve the ring topology (ATSP).
 
-    python benchmarks/fault_tolerance.py [--peers 8] [--mib 64] [--device cuda:0|cpu]
+    python benchmarks/fault_tolerance.py [--peers 8] [--mib 1024] [--device cuda:0|cpu] [--transport tcp|ipc]
 
-Peer processes and an in-process master on 127.0.0.1 run a loop of AVG all-reduces of --mib MiB (constant inputs,
-so every result is checkable: value 1.0 -> result 1.0 whatever the world size) and log a timestamp per completed or
-failed op. The driver
-  1. lets the 8 peers run, then SIGKILLs one of them mid-run (no clean disconnect),
-  2. starts a replacement peer after --respawn-after seconds,
-  3. once the replacement has completed an all-reduce, every peer calls pcclOptimizeTopology (bandwidth probes
-     between peers + asymmetric TSP solve on the master) and keeps reducing on the new ring.
-Reported: ops that failed because of the kill, recovery time (kill -> first successful op of the 7 survivors),
-rejoin time (replacement process started -> its first successful op; and from its connect() call, i.e. without the
-Python/torch start-up), topology re-solve time, steady-state ms/op before
-the kill, with 7 peers and after the rejoin, and whether every result was exact.
-The reference publishes no number for this configuration.
+One process per peer (the deployment shape) and a master in this process on 127.0.0.1. Every peer runs a loop of
+in-place SUM all-reduces of --mib MiB (bf16 on a GPU, fp32 on the CPU) whose input is 1.0 everywhere, so every result
+is checkable (== the op's world size) and every failed op's buffer must hold the input again (1.0: the in-place
+restore). The sequence (reference python/tests/stress_tests/basic_stress_test/stresstest_orchestrator.py:88-262,
+ccoip/src/cpp/ccoip_master_handler.cpp:1312-1400):
+  1. the last peer SIGKILLs itself in the middle of op --kill-op (PCCL_FAULT_INJECT: on the TCP device ring when its
+     first received piece of reduce-scatter step 1 is in flight, on the xGMI path right after launching its push
+     kernel, on the host ring after its first received frame of step 1); the fault line carries the kill's wall time;
+  2. the master sees the connection drop and aborts the op; the survivors' op fails, they re-form the ring without
+     the dead peer and keep reducing with W-1 peers;
+  3. once every survivor completed an op at W-1, a replacement process starts; the survivors admit it at their next
+     op boundary (pcclArePeersPending / pcclUpdateTopology);
+  4. at the first op with W peers again every peer calls pcclOptimizeTopology (pairwise bandwidth probes, then the
+     master's asymmetric-TSP solve) and keeps reducing on the new ring.
+Reported (ms): kill -> survivors' failed op returned (abort received + ring re-formed), kill -> survivors' first exact
+op at W-1, replacement's connect() -> its first exact op at W (its process start too), the admission vote, the
+optimize call and the master's ATSP solve alone; ms per op in each phase; whether every result and every restore was
+exact. The reference publishes no number for this configuration.
 """
 from __future__ import annotations
 
-import argparse
-import json
-import os
-import signal
-import subprocess
-import sys
-import tempfile
-import threading
 import time
+
+T_PROC = time.time()  # before any import: a replacement's process start
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import re  # noqa: E402
+import signal  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+import tempfile  # noqa: E402
+import threading  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -39,45 +49,59 @@ def peer(a):
     dev = torch.device(a.device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    print(json.dumps({"rank": a.rank, "t": time.time(), "event": "connecting"}), flush=True)
-    comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool)
-    comm.connect(n_attempts=120)
-    if not a.joiner:
-        wait_for_world(comm, a.peers, timeout=300)
-    n = (a.mib << 20) // 4
-    x = torch.ones(n, device=dev)
-    y = torch.empty_like(x)
 
     def log(**kw):
         print(json.dumps({"rank": a.rank, "t": time.time(), **kw}), flush=True)
 
-    log(event="start")
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    log(event="proc_start", t_proc=T_PROC)
+    comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool)
+    t0 = time.time()
+    log(event="connect_call")
+    comm.connect(n_attempts=120)
+    log(event="connected", sec=time.time() - t0)
+    if not a.joiner:
+        wait_for_world(comm, a.peers, timeout=300)
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    x = torch.empty((a.mib << 20) // (2 if dtype == torch.bfloat16 else 4), device=dev, dtype=dtype)
     optimized = False
-    seen_small_world = False
-    left = a.stop_after_optimize
+    saw_small = False
+    post = 0
     it = 0
     while time.time() < a.deadline:
-        if it > 0 and comm.are_peers_pending():
-            comm.update_topology()
+        # the pending query is a vote of every member at the same point of an iteration: a replacement enters right
+        # after the others' admission (their update_topology of this iteration), so nobody asks in iteration 0
         it += 1
+        if it > 1 and comm.are_peers_pending():
+            t0 = time.perf_counter()
+            comm.update_topology()
+            log(event="admit", sec=time.perf_counter() - t0)
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
         if ws < 2:
-            time.sleep(0.01)
+            time.sleep(0.005)
             continue
-        seen_small_world |= ws < a.peers
+        x.fill_(1.0)
+        sync()
+        t0 = time.perf_counter()
         try:
-            t0 = time.perf_counter()
-            info = comm.all_reduce(x, y, op=pccl.ReduceOp.AVG, tag=0)
-            if dev.type == "cuda":
-                torch.cuda.synchronize()
+            info = comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)  # in place
+            sync()
             dt = time.perf_counter() - t0
-            ok = bool(torch.all(y == 1.0))
-            log(event="ok", world=info.local_world_size, sec=dt, exact=ok)
+            w = info.local_world_size
+            exact = bool((x == float(w)).all())
+            log(event="ok", world=w, sec=dt, exact=exact, path=comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH))
         except pccl.PCCLError as e:
-            log(event="fail", error=e.result.name)
+            t_fail = time.time()
+            sync()
+            restore_ok = bool((x == 1.0).all())  # the failed in-place op's buffer holds its input again
+            log(event="fail", t_fail=t_fail, sec=time.perf_counter() - t0, error=e.result.name, restore_ok=restore_ok)
             continue
-        # the first op in which the replacement took part: everyone (incl. the replacement) re-solves the ring
-        if not optimized and info.local_world_size == a.peers and (a.joiner or seen_small_world):
+        saw_small |= w < a.peers
+        # the first op with the full world again (the replacement's first op): everyone re-solves the ring
+        if not optimized and w == a.peers and (a.joiner or saw_small):
             t0 = time.perf_counter()
             try:
                 comm.optimize_topology()
@@ -85,46 +109,41 @@ def peer(a):
             except pccl.PCCLError as e:
                 log(event="optimize_failed", error=e.result.name, sec=time.perf_counter() - t0)
             optimized = True
+            continue
         if optimized:
-            left -= 1
-            if left <= 0:
+            post += 1
+            if post >= a.post_ops:
                 break
     comm.destroy()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--peers", type=int, default=8)
-    ap.add_argument("--mib", type=int, default=64)
-    ap.add_argument("--pool", type=int, default=2)
-    ap.add_argument("--device", default="cuda:0")
-    ap.add_argument("--kill-after", type=float, default=3.0)
-    ap.add_argument("--respawn-after", type=float, default=1.0)
-    ap.add_argument("--rank", type=int, default=None)
-    ap.add_argument("--master", default=None)
-    ap.add_argument("--joiner", action="store_true")
-    ap.add_argument("--deadline", type=float, default=0)
-    ap.add_argument("--stop-after-optimize", type=int, default=20)
-    ap.add_argument("--no-ipc", action="store_true",
-                    help="device ring over TCP instead of the xGMI IPC path (default: IPC, which survives a peer "
-                         "SIGKILLed mid-kernel since round 2; tests/test_fault_tolerance.py::test_gpu_ipc_sigkill_mid_op)")
-    ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
-    a = ap.parse_args()
-    if a.rank is not None:
-        return peer(a)
+def inject_spec(device: str, transport: str, op: int) -> str:
+    """PCCL_FAULT_INJECT of the victim: where in op `op` (the master's sequence number) it SIGKILLs itself."""
+    if not device.startswith("cuda"):
+        return f"hring:{op}:1:rx"
+    return f"ipc_kernel:{op}" if transport == "ipc" else f"ring:{op}:1:rx"
 
-    from pccl_amd.utils import local_master, spawn_python
+
+def run(a) -> dict:
+    import pccl_amd as pccl
+    from pccl_amd.utils import free_port, spawn_python
     me = os.path.abspath(__file__)
-    deadline = time.time() + 240
+    deadline = time.time() + a.timeout
+    port = free_port()
+    addr = f"127.0.0.1:{port}"
+    master = pccl.MasterNode(addr)
+    master.run()
     common = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
-              "--deadline", str(deadline), "--stop-after-optimize", str(a.stop_after_optimize)]
-    env = {"PCCL_BENCHMARK_MILLIS": "300", "PCCL_NUM_BENCHMARK_CONNECTIONS": "2", "PCCL_SAME_HOST_MBPS": "0"}
-    if a.no_ipc:
+              "--deadline", str(deadline), "--post-ops", str(a.post_ops), "--master", addr]
+    # short bandwidth probes (the reference's 10 s per pair is a WAN setting); several processes on one GPU: 2 hardware
+    # queues each (README)
+    env = {"PCCL_BENCHMARK_MILLIS": str(a.probe_ms), "PCCL_NUM_BENCHMARK_CONNECTIONS": "2",
+           "PCCL_SAME_HOST_MBPS": "0", "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "2")}
+    if a.transport == "tcp":
         env["PCCL_DISABLE_IPC"] = "1"
-    lines = []
+    spec = inject_spec(a.device, a.transport, a.kill_op)
+    lines, procs, errs_files = [], [], []
     lock = threading.Lock()
-    if a.log_dir:
-        os.makedirs(a.log_dir, exist_ok=True)
 
     def reader(p):
         for ln in p.stdout:
@@ -132,88 +151,139 @@ def main():
                 with lock:
                     lines.append(json.loads(ln))
 
-    with local_master() as addr:
-        procs, threads = [], []
+    def start(rank, joiner=False, extra_env=None):
+        # a file, not a pipe: a chatty peer never blocks on stderr
+        err = open(os.path.join(a.log_dir, f"peer{rank}.err"), "w+") if a.log_dir else tempfile.TemporaryFile(mode="w+")
+        p = spawn_python([me, "--rank", str(rank), *common] + (["--joiner"] if joiner else []),
+                         env=dict(env, **(extra_env or {})), stdout=subprocess.PIPE, stderr=err, text=True,
+                         start_new_session=True)
+        errs_files.append(err)
+        threading.Thread(target=reader, args=(p,), daemon=True).start()
+        procs.append(p)
+        return p
 
-        def start(rank, joiner=False):
-            # a file, not a pipe: a chatty peer must never block on stderr
-            err = open(os.path.join(a.log_dir, f"peer{rank}.err"), "w+") if a.log_dir else \
-                tempfile.TemporaryFile(mode="w+")
-            p = spawn_python([me, "--rank", str(rank), "--master", addr, *common] + (["--joiner"] if joiner else []),
-                             env=env, stdout=subprocess.PIPE, stderr=err, text=True, start_new_session=True)
-            p.err_file = err
-            t = threading.Thread(target=reader, args=(p,), daemon=True)
-            t.start()
-            procs.append(p)
-            threads.append(t)
-            return p
+    def sel(event, rank=None, world=None, after=0.0):
+        with lock:
+            return [x for x in lines if x["event"] == event and (rank is None or x["rank"] == rank)
+                    and (world is None or x.get("world") == world) and x["t"] > after]
 
+    victim_rank = a.peers - 1
+    t_kill = None
+    t_spawn = None
+    try:
         for r in range(a.peers):
-            start(r)
-
-        def oks(rank=None, world=None, after=0.0):
-            with lock:
-                return [x for x in lines if x["event"] == "ok" and (rank is None or x["rank"] == rank)
-                        and (world is None or x["world"] == world) and x["t"] > after]
-
-        def progress(what):
-            print(json.dumps({"progress": what, "t": time.time(), "ops": len(oks())}), flush=True)
-
-        while len(oks(world=a.peers)) < 3 * a.peers and time.time() < deadline:
-            time.sleep(0.05)
-        progress("running")
-        time.sleep(a.kill_after)
-        victim = procs[a.peers - 1]
-        t_kill = time.time()
-        os.killpg(victim.pid, signal.SIGKILL)  # its own session: only that peer's process group
-        victim.wait()
-        progress("killed")
-        while not oks(world=a.peers - 1, after=t_kill) and time.time() < deadline:
+            start(r, extra_env={"PCCL_FAULT_INJECT": spec} if r == victim_rank else None)
+        victim = procs[victim_rank]
+        while victim.poll() is None and time.time() < deadline:
             time.sleep(0.01)
-        progress("recovered")
-        time.sleep(a.respawn_after)
+        errs_files[victim_rank].seek(0)
+        m = re.search(r"fault injection: SIGKILL at .* t=(\d+\.\d+)", errs_files[victim_rank].read())
+        t_kill = float(m.group(1)) if m else None
+        survivors = [r for r in range(a.peers) if r != victim_rank]
+        while t_kill is not None and time.time() < deadline and \
+                not all(sel("ok", rank=r, world=a.peers - 1, after=t_kill) for r in survivors):
+            time.sleep(0.01)
         t_spawn = time.time()
         start(a.peers, joiner=True)
-        while not oks(rank=a.peers) and time.time() < deadline:
-            time.sleep(0.01)
-        progress("rejoined")
-        for p in procs[:a.peers - 1] + procs[a.peers:]:
+        for p in procs:
             try:
                 p.wait(timeout=max(1.0, deadline - time.time() + 30))
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait()
-        for t in threads:
-            t.join(timeout=5)
-        errs = []
+        time.sleep(0.2)  # readers drain
+        topo = master.topology_stats()
+    finally:
         for p in procs:
-            if p.returncode not in (0, -signal.SIGKILL):
-                p.err_file.seek(0)
-                errs.append(p.err_file.read()[-2000:])
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+        master.interrupt()
+        master.await_termination()
 
-    def ms_per_op(sel):
-        return round(1e3 * sorted(x["sec"] for x in sel)[len(sel) // 2], 3) if sel else None
+    errs = []
+    for k, p in enumerate(procs):
+        if p.returncode not in (0, -signal.SIGKILL) or (k != victim_rank and p.returncode != 0):
+            errs_files[k].seek(0)
+            errs.append({"rank": k, "rc": p.returncode, "stderr": errs_files[k].read()[-1500:]})
 
-    before = [x for x in oks(world=a.peers) if x["t"] < t_kill]
-    seven = [x for x in oks(world=a.peers - 1) if x["t"] > t_kill]
-    rejoin = oks(rank=a.peers)
-    after = [x for x in oks(world=a.peers) if x["t"] > t_spawn]
-    fails = [x for x in lines if x["event"] == "fail" and x["t"] > t_kill]
-    opt = [x for x in lines if x["event"] in ("optimized", "optimize_failed")]
-    connecting = [x["t"] for x in lines if x["event"] == "connecting" and x["rank"] == a.peers]
-    print(json.dumps({
-        "metric": "fault tolerance: kill + rejoin", "config": "Fault tolerance: kill + rejoin 1 of 8 peers "
-        "mid-all-reduce, TSP topology re-solve", "peers": a.peers, "mib": a.mib, "device": a.device,
-        "failed_ops_after_kill": len(fails),
-        "recovery_ms": round(1e3 * (min(x["t"] for x in seven) - t_kill), 1) if seven else None,
-        "rejoin_ms": round(1e3 * (min(x["t"] for x in rejoin) - t_spawn), 1) if rejoin else None,
-        "rejoin_from_connect_ms": round(1e3 * (min(x["t"] for x in rejoin) - connecting[0]), 1)
-        if rejoin and connecting else None,
-        "topology_resolve_ms": round(1e3 * max(x["sec"] for x in opt), 1) if opt else None,
-        "topology_resolve_ok": bool(opt) and all(x["event"] == "optimized" for x in opt),
-        "ms_per_op": {"before_kill": ms_per_op(before), "after_kill": ms_per_op(seven),
-                      "after_rejoin": ms_per_op(after)},
-        "all_results_exact": all(x["exact"] for x in oks()), "peer_errors": errs}), flush=True)
+    def ms(v):
+        return round(v * 1e3, 1) if v is not None else None
+
+    def med_ms(xs):
+        return round(1e3 * sorted(x["sec"] for x in xs)[len(xs) // 2], 2) if xs else None
+
+    survivors = [r for r in range(a.peers) if r != victim_rank]
+    joiner = a.peers
+    fails = [x for x in sel("fail") if t_kill is not None and x["t"] > t_kill]
+    first_fail = [min((x["t_fail"] for x in fails if x["rank"] == r), default=None) for r in survivors]
+    first_small = [min((x["t"] for x in sel("ok", rank=r, world=a.peers - 1, after=t_kill or 0)), default=None)
+                   for r in survivors]
+    j_ok = sel("ok", rank=joiner, world=a.peers)
+    j_first = min((x["t"] for x in j_ok), default=None)
+    j_connect = [x["t"] for x in sel("connect_call", rank=joiner)]
+    j_proc = [x["t_proc"] for x in sel("proc_start", rank=joiner)]
+    opt = sel("optimized") + sel("optimize_failed")
+    admits = [x for x in sel("admit") if t_spawn is not None and x["t"] > t_spawn]
+    t_opt_end = max((x["t"] for x in opt), default=None)
+    oks = sel("ok")
+    full_before = [x for x in oks if x["world"] == a.peers and t_kill is not None and x["t"] < t_kill]
+    small = [x for x in oks if x["world"] == a.peers - 1]
+    rejoined = [x for x in oks if x["world"] == a.peers and t_spawn is not None and x["t"] > t_spawn
+                and (t_opt_end is None or x["t"] < t_opt_end)]
+    after_opt = [x for x in oks if x["world"] == a.peers and t_opt_end is not None and x["t"] > t_opt_end]
+    complete = t_kill is not None and None not in first_fail and None not in first_small and j_first is not None
+    return {
+        "config": f"BASELINE config 5: kill + rejoin 1 of {a.peers} peers mid-all-reduce, TSP topology re-solve",
+        "transport": "xGMI/IPC" if a.transport == "ipc" and a.device.startswith("cuda") else
+        ("TCP device ring" if a.device.startswith("cuda") else "TCP host ring"),
+        "peers": a.peers, "processes": "one per peer", "mib": a.mib, "device": a.device, "inject": spec,
+        "complete": complete,
+        "kill_to_survivors_failed_op_ms": ms(max(first_fail) - t_kill) if complete else None,
+        "kill_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
+        "joiner_connect_to_first_exact_op_ms": ms(j_first - j_connect[0]) if j_first and j_connect else None,
+        "joiner_process_start_to_first_exact_op_ms": ms(j_first - j_proc[0]) if j_first and j_proc else None,
+        "survivors_admission_vote_ms": ms(max(x["sec"] for x in admits)) if admits else None,
+        "optimize_topology_call_ms": ms(max(x["sec"] for x in opt)) if opt else None,
+        "optimize_ok": bool(opt) and all(x["event"] == "optimized" for x in opt) and len(opt) == a.peers,
+        "master_atsp_solve_ms": round(topo["last_solve_us"] / 1e3, 3) if topo["solves"] else None,
+        "master_topology": topo,
+        "failed_ops_per_survivor": max((sum(1 for x in fails if x["rank"] == r) for r in survivors), default=0),
+        "in_place_restore_exact": bool(fails) and all(x["restore_ok"] for x in fails),
+        "all_results_exact": bool(oks) and all(x["exact"] for x in oks),
+        "paths": sorted({x["path"] for x in oks}),
+        "ms_per_op": {"before_kill": med_ms(full_before), f"w{a.peers - 1}": med_ms(small),
+                      "after_rejoin": med_ms(rejoined), "after_optimize": med_ms(after_opt)},
+        "ops": {"before_kill": len(full_before), f"w{a.peers - 1}": len(small), "after_rejoin": len(rejoined),
+                "after_optimize": len(after_opt)},
+        "peer_errors": errs,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--mib", type=int, default=1024)
+    ap.add_argument("--pool", type=int, default=2)
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--transport", default="tcp", choices=["tcp", "ipc"],
+                    help="tcp: the device ring over loopback TCP (PCCL_DISABLE_IPC=1; the reference's data path); "
+                         "ipc: the xGMI path for peers on one host")
+    ap.add_argument("--kill-op", type=int, default=6, help="sequence number of the op the victim dies in")
+    ap.add_argument("--post-ops", type=int, default=5, help="ops after the topology re-solve")
+    ap.add_argument("--probe-ms", type=int, default=300, help="bandwidth probe per peer pair (PCCL_BENCHMARK_MILLIS)")
+    ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
+    ap.add_argument("--rank", type=int, default=None)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--joiner", action="store_true")
+    ap.add_argument("--deadline", type=float, default=0)
+    a = ap.parse_args()
+    if a.rank is not None:
+        return peer(a)
+    if a.log_dir:
+        os.makedirs(a.log_dir, exist_ok=True)
+    print(json.dumps(run(a)), flush=True)
 
 
 if __name__ == "__main__":

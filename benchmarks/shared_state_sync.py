@@ -45,6 +45,13 @@ def _state(torch, pccl, n_params, n_tensors, device, fill, shareable=False):
     return tensors, st
 
 
+def _hashes(tensors):
+    """simplehash of every tensor (the library's content hash: HIP kernel for HBM tensors, host twin otherwise),
+    computed by the benchmark after the sync, independently of the library's own per-entry verification."""
+    from pccl_amd.ops import kernels as K
+    return [int(K.simplehash(t)) for t in tensors]
+
+
 def peer(a):
     import torch
 
@@ -73,7 +80,8 @@ def peer(a):
         st.revision = 3
         info = comm.sync_shared_state(st)
         sums = [float(t.double().sum()) for t in tensors]
-        print(json.dumps({"role": "trainer", "tx_bytes": info.tx_bytes, "sums": sums}), flush=True)
+        print(json.dumps({"role": "trainer", "tx_bytes": info.tx_bytes, "sums": sums, "hashes": _hashes(tensors)}),
+              flush=True)
     else:
         tensors, st = _state(torch, pccl, a.params, a.tensors, dev, "zeros")
         st.revision = 0
@@ -87,7 +95,7 @@ def peer(a):
         sums = [float(t.double().sum()) for t in tensors]  # compared with the trainer's by the driver
         nbytes = sum(t.numel() * 4 for t in tensors)
         print(json.dumps({"role": "joiner", "seconds": dt, "rx_bytes": info.rx_bytes, "bytes": nbytes,
-                          "revision": st.revision, "sums": sums}), flush=True)
+                          "revision": st.revision, "sums": sums, "hashes": _hashes(tensors)}), flush=True)
     comm.destroy()
 
 
@@ -130,7 +138,10 @@ def main():
         "late-joining peer catches up from rev 0", "params": a.params, "tensors": a.tensors, "device": a.device,
         "transport": a.transport, "shareable_state": a.shareable, "seconds": round(j["seconds"], 4), "bytes": j["bytes"],
         "GBps": round(j["bytes"] / j["seconds"] / 1e9, 3), "joiner_rx_bytes": j["rx_bytes"],
-        "trainer_tx_bytes": t["tx_bytes"], "adopted_revision": j["revision"], "content_ok": j["sums"] == t["sums"]}),
+        "trainer_tx_bytes": t["tx_bytes"], "adopted_revision": j["revision"], "content_ok": j["sums"] == t["sums"],
+        # the library re-hashes every received entry against the elected hash (a mismatch fails the sync); this is the
+        # benchmark's own check of the same property
+        "hash_verified": j["hashes"] == t["hashes"]}),
         flush=True)
 
 

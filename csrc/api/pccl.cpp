@@ -407,6 +407,16 @@ extern "C" __attribute__((visibility("default"))) size_t pcclxMasterBandwidthTab
     return t.size();
 }
 
+// topology optimization counters of the master (pccl::master::Master::topology_stats); returns how many it wrote
+extern "C" __attribute__((visibility("default"))) size_t pcclxMasterTopologyStats(pcclMasterInstance_t *m,
+                                                                                  uint64_t *out, size_t n) {
+    if (m == nullptr || m->master == nullptr || out == nullptr) return 0;
+    const auto s = m->master->topology_stats();
+    const size_t k = std::min(n, s.size());
+    for (size_t i = 0; i < k; ++i) out[i] = s[i];
+    return k;
+}
+
 pcclResult_t pcclRunMaster(pcclMasterInstance_t *m) {
     PCCL_REQUIRE(m != nullptr && m->master != nullptr, pcclInvalidArgument);
     if (!m->master->launch()) return pcclInvalidUsage;

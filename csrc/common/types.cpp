@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <thread>
 #include <fcntl.h>
 #include <random>
@@ -162,9 +163,12 @@ void fault_point(const char *point, uint64_t seq, size_t step, const char *phase
     if (!f.armed || f.seq != seq || f.point != point) return;
     if (f.step != SIZE_MAX && f.step != step) return;
     if (!f.phase.empty() && (phase == nullptr || f.phase != phase)) return;
-    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu step %lld phase %s\n", point,
+    // wall-clock time of the kill (harnesses time recovery from it: benchmarks/fault_tolerance.py)
+    timespec now{};
+    ::clock_gettime(CLOCK_REALTIME, &now);
+    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu step %lld phase %s t=%lld.%06ld\n", point,
                  static_cast<unsigned long long>(seq), step == SIZE_MAX ? -1ll : static_cast<long long>(step),
-                 phase ? phase : "-");
+                 phase ? phase : "-", static_cast<long long>(now.tv_sec), now.tv_nsec / 1000);
     std::fflush(stderr);
     if (const char *d = std::getenv("PCCL_FAULT_INJECT_DELAY_MS")) // die a little later (the point's work goes on)
         std::thread([ms = std::atol(d)] {

@@ -599,10 +599,17 @@ void Master::run_topology_optimization(uint32_t group) {
     }
     if (!gs.optimized_once) {
         bool optimal = false, improved = false;
+        const auto t0 = std::chrono::steady_clock::now();
         if (optimize_ring(gs.bw, ring, false, optimal, improved)) {
-            if (improved) gs.ring = ring;
+            if (improved) {
+                gs.ring = ring;
+                topo_changes_.fetch_add(1);
+            }
             gs.ring_optimal = optimal;
         }
+        topo_last_us_.store(static_cast<uint64_t>(
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count()));
+        topo_solves_.fetch_add(1);
         gs.optimized_once = true;
         return;
     }
@@ -615,7 +622,9 @@ void Master::run_topology_optimization(uint32_t group) {
         if (optimize_ring(snapshot, ring, true, optimal, improved, &stopping_) && improved && !stopping_) {
             std::lock_guard lock(pending_mtx_);
             pending_rings_[group] = {ring, optimal};
+            topo_changes_.fetch_add(1);
         }
+        topo_moonshots_.fetch_add(1);
     });
     if (!queued) {
         LOG(DEBUG) << "moonshot topology optimization of group " << group << " already running / queue full";

@@ -16,6 +16,7 @@
 //    falling back to UUID order, so an optimized ring is not thrown away on every join/leave
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -180,6 +181,14 @@ private:
 
 public:
     size_t optimizer_thread_count() { return optimizer_pool_.thread_count(); }
+    // topology optimization counters (pcclxMasterTopologyStats): [0] synchronous ATSP solves, [1] microseconds of the
+    // last one, [2] rings changed by a solve (synchronous or moonshot), [3] moonshot solves finished
+    std::array<uint64_t, 4> topology_stats() const {
+        return {topo_solves_.load(), topo_last_us_.load(), topo_changes_.load(), topo_moonshots_.load()};
+    }
+
+private:
+    std::atomic<uint64_t> topo_solves_{0}, topo_last_us_{0}, topo_changes_{0}, topo_moonshots_{0};
 };
 
 } // namespace pccl::master

@@ -166,6 +166,7 @@ def _load() -> ctypes.CDLL:
         "pcclxIpcStats": ([p(c_uint64)], None),
         "pcclxIpcStatsEx": ([p(c_uint64), c_size_t], c_size_t),
         "pcclxMasterBandwidthTable": ([c_void_p, c_char_p, c_size_t], c_size_t),
+        "pcclxMasterTopologyStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

@@ -599,6 +599,14 @@ class MasterNode:
             out.append((int(g), frm, to, float(mbps)))
         return out
 
+    def topology_stats(self):
+        """The master's topology-optimization counters: synchronous ATSP solves, the last one's duration (us), rings
+        a solve changed (synchronous or moonshot) and finished moonshot solves."""
+        out = (ctypes.c_uint64 * 4)()
+        C.pcclxMasterTopologyStats(self._master, out, 4)
+        return {"solves": int(out[0]), "last_solve_us": int(out[1]), "ring_changes": int(out[2]),
+                "moonshot_solves": int(out[3])}
+
     def await_termination(self):
         if self._running:
             C.pcclMasterAwaitTermination(self._master)
