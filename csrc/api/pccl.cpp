@@ -122,6 +122,7 @@ pcclResult_t pcclGetAttribute(const pcclComm_t *comm, pcclAttribute_t attribute,
         case PCCL_ATTRIBUTE_RING_RANK: *out = c.ring_rank(); break;
         case PCCL_ATTRIBUTE_LAST_REDUCE_PATH: *out = c.last_reduce_path(); break;
         case PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS: *out = static_cast<int>(c.collective_worker_threads()); break;
+        case PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING: *out = c.last_reduce_framing(); break;
         default: return pcclInvalidArgument;
     }
     return pcclSuccess;

@@ -18,7 +18,21 @@ namespace pccl::client {
 using namespace proto;
 using namespace std::chrono_literals;
 
-Client::Client(const ClientConfig &cfg) : cfg_(cfg), master_(cfg.master) { std::signal(SIGPIPE, SIG_IGN); }
+namespace {
+// PCCL_WIRE: "reference" makes this peer speak exactly the reference protocol (interop testing, mixed deployments);
+// unset / "ext" (default) the pccl-amd extensions, negotiated per op with the other participants
+bool wire_reference_env() {
+    const char *e = std::getenv("PCCL_WIRE");
+    if (!e || !*e || std::strcmp(e, "ext") == 0) return false;
+    if (std::strcmp(e, "reference") == 0) return true;
+    LOG(WARN) << "PCCL_WIRE=" << e << " unknown (reference | ext): using ext";
+    return false;
+}
+} // namespace
+
+Client::Client(const ClientConfig &cfg) : cfg_(cfg), wire_reference_(wire_reference_env()), master_(cfg.master) {
+    std::signal(SIGPIPE, SIG_IGN);
+}
 
 Client::~Client() {
     interrupt();
@@ -120,7 +134,7 @@ bool Client::connect() {
 
     C2MRequestSessionRegistration reg;
     reg.peer_group = cfg_.peer_group;
-    reg.host_token = net::host_token();
+    if (!wire_reference_) reg.host_token = net::host_token(); // (no token: the reference's registration bytes)
     // PCCL_XGMI_CAPABLE=0/1 overrides the advertised capability (tests on GPU-less hosts)
     reg.xgmi_capable = std::getenv("PCCL_XGMI_CAPABLE") ? env_flag("PCCL_XGMI_CAPABLE", true)
                                                        : !env_flag("PCCL_DISABLE_IPC", false) && device_backend_available();

@@ -20,6 +20,7 @@
 #include "../net/listener.hpp"
 #include "../net/master_conn.hpp"
 #include "../net/mux.hpp"
+#include "ring_common.hpp"
 
 namespace pccl::client {
 
@@ -128,6 +129,7 @@ public:
     uint64_t connection_revision() const { return conn_revision_.load(); }
     int ring_rank();
     int last_reduce_path() const { return last_path_.load(); }
+    int last_reduce_framing() const { return last_framing_.load(); }
     size_t collective_worker_threads() { return workers_.thread_count(); }
     const Uuid &uuid() const { return uuid_; }
 
@@ -180,6 +182,7 @@ private:
         std::atomic<uint64_t> tx{0}, rx{0};
         uint32_t world = 0;
         bool small_path = false; // every peer agreed on the small-message algorithm (kCollFlagSmallPath)
+        ring::Shape shape;       // the op's agreed data-plane framing (commence: kCollFlagExtWire + WireShape)
         // Set by a data path that finished its part of an in-place op: holds the input's backup until the master's
         // verdict. run_op calls it once with restore = true if the op failed anyway (a peer was lost after this
         // peer's part was done), so a retry reduces the caller's input, not the result.
@@ -208,6 +211,7 @@ private:
     std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);
     std::pair<bool, bool> ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device);
+    std::pair<bool, bool> device_quant_reference_framing(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     bool abort_received(uint64_t tag);
@@ -220,6 +224,10 @@ private:
     bool hash_entries(const std::vector<const SSEntry *> &entries, std::vector<uint64_t> &hashes, HashType &type);
 
     ClientConfig cfg_;
+    // PCCL_WIRE=reference: register and run every op exactly as a reference peer would (no host token, so no IPC /
+    // hierarchical paths; initiate packets without capability flags, so every op of the ring uses the reference
+    // framing; no shared-state IPC hand-off)
+    const bool wire_reference_;
     net::MasterConnection master_;
     std::unique_ptr<net::Listener> p2p_listener_, ss_listener_, bm_listener_;
     Uuid uuid_;
@@ -239,6 +247,7 @@ private:
     std::atomic<uint64_t> conn_revision_{0};
     std::atomic<size_t> global_ws_{0}, local_ws_{0}, n_groups_{0}, largest_group_{0};
     std::atomic<int> last_path_{0};
+    std::atomic<int> last_framing_{0}; // PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING
 
     std::mutex ops_mtx_;
     std::mutex done_mtx_;           // signalled whenever an op finishes (wait_any)

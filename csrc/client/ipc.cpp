@@ -1223,6 +1223,7 @@ std::pair<bool, bool> Client::hier_reduce(OpState &op, const RingView &rv, uint6
         inner.req.dst = part;
         inner.req.count = count;
         inner.req.scratch = true;
+        inner.shape = op.shape;
         if (inner.req.op == ReduceOp::Avg) inner.req.op = ReduceOp::Sum; // divided by the whole world afterwards
         const auto r = ring_reduce_device(inner, sub, seq, device);
         op.tx += inner.tx.load();

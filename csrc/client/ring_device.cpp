@@ -1,0 +1,288 @@
+// Device ring: buffers in HBM. Ring-step payloads are staged to pinned host memory (step 0 by copy-engine copies,
+// later steps by the fused reduce kernel that writes the next payload while it reduces), sent over the striped
+// connections as soon as each piece is ready, and received bytes are copied into HBM staging and reduced HBM -> HBM
+// (reference ccoip/src/cpp/reduce.cpp:528-784 on host memory; SURVEY §2.1 N8 "HIP device pipeline").
+//
+// PCIe is the device ring's second bottleneck after the network (8 peers on one GPU share one x16 link). Measured on
+// MI355X (profiles/r2/pcie_probe.md): one copy-engine queue per direction reaches ~55 GB/s one way and ~94 GB/s full
+// duplex with >= 4 MiB copies, while 4-8 queues per direction fall to ~60 GB/s duplex, kernels reading pinned host
+// memory run at <= 57 GB/s and drop to ~60 GB/s duplex next to copy traffic, and a copy issued behind a kernel on
+// the same stream becomes a blit kernel. Hence:
+//   * every staging copy of the process goes to ONE host->device and ONE device->host stream per GPU (shared by all
+//     ops and all peers of the process); nothing is queued behind a cross-stream wait there, so ROCclr keeps them on
+//     the copy engines;
+//   * reduce-scatter: received bytes are copied into HBM staging by the copy engine and reduced HBM->HBM on the op's
+//     stream (cross-stream event wait, no host round trip) by k_reduce_copy, which also streams the result into
+//     pinned memory as the NEXT step's payload: a ring step's sends start the moment the previous step's last piece
+//     lands, and the only device->host copies left are the step-0 pieces of the input;
+//   * all-gather: received chunks go to HBM as copies on the op's stream (blit kernels reading pinned memory, one per
+//     peer in parallel, next to the shared copy-engine queue that carries the reduce-scatter's bytes): interleaved
+//     A/B, 8 peers x 1 GiB: 347 vs 376 ms and 337 vs 342 ms (profiles/r3/h2d_modes/).
+// PCIe bytes per peer and 1 GiB: D2H 1 GiB (step-0 payload + reduced pieces), H2D 1.75 GiB (received pieces).
+// Round 3 measured the alternatives (several H2D queues, per-op queues, a process-wide reduce stream, CPU-reduced
+// parts, kernels reading received bytes from pinned memory, lanes, a step-synchronous schedule): none was faster, so
+// none is kept (profiles/r3/{ring_ab,h2d_modes,shared_reduce,host_reduce,grid_caps}/).
+#include <cstring>
+
+#include "../common/log.hpp"
+#include "client.hpp"
+#include "ring_common.hpp"
+
+namespace pccl::client {
+
+namespace {
+
+using namespace ring;
+
+// inputs of one device-ring op
+struct DevRing {
+    const Conns &txs, &rxs; // the ring's connections to next / from prev
+    size_t ws, rank;
+    uint64_t tag, seq;
+    const Shape &shape;
+    DeviceBackend *be;
+    PcieQueues pq;
+    DevStream st;       // the op's stream (input copy / backup before any of the ring's work)
+    const uint8_t *src; // step-0 payload source: the caller's input (ready at call time, never written by the op
+                        // before its step-0 copies completed)
+    uint8_t *dst;       // the output, holding the input once `st` reaches the ring's first kernel
+    size_t count, es, piece;
+    DType dtype;
+    ReduceOp rop;
+    int device;
+    std::function<bool()> aborted;
+    std::atomic<uint64_t> &tx, &rx;
+};
+
+// The device ring as one pipeline over all 2(W-1) steps: step g+1's payload is produced (reduced into pinned
+// memory) and sent while step g still receives, and step g+1's sinks are posted as soon as their staging buffer is
+// free. Returns 0 ok, 1 io failure, 2 abort; on return no GPU work or socket write of the op touches any of its
+// buffers any more (the caller may restore the input).
+int device_ring_pipeline(DevRing &R) {
+    DeviceBackend *be = R.be;
+    const PcieQueues pq = R.pq;
+    DevStream st = R.st;
+    const size_t ws = R.ws, rank = R.rank, es = R.es, piece = R.piece;
+    const uint64_t seq = R.seq;
+
+    std::vector<DevEvent> owned; // events of this op (back to the pool once everything they guard has completed)
+    DevEvent last_d2h = nullptr;
+    auto record = [&](DevStream s) {
+        DevEvent e = event_pool().get();
+        owned.push_back(e);
+        be->event_record(e, s);
+        return e;
+    };
+    const auto bounds = chunk_bounds(R.count, ws);
+    size_t max_chunk = 0;
+    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    const size_t stage_bytes = max_chunk * es + 64;
+    // Staging rings of kNb buffers: step g receives into rxbuf[g % kNb] (HBM twin rxdev[g % kNb] for the reduce) and
+    // its reduce writes the next payload into txbuf[(g + 1) % kNb]: a buffer is refilled only after the step two back
+    // finished with it (StepSlots).
+    constexpr size_t kNb = StepSlots::kSlots;
+    Lease txl[kNb], rxl[kNb], dvl[kNb];
+    uint8_t *txbuf[kNb], *rxbuf[kNb], *rxdev[kNb];
+    for (size_t i = 0; i < kNb; ++i) {
+        txl[i] = Lease(pinned_pool(), stage_bytes);
+        rxl[i] = Lease(pinned_pool(), stage_bytes);
+        dvl[i] = Lease(device_pool(), stage_bytes, R.device);
+        if (!txl[i].ok() || !rxl[i].ok() || !dvl[i].ok()) return 1;
+        txbuf[i] = txl[i].data();
+        rxbuf[i] = rxl[i].data();
+        rxdev[i] = dvl[i].data();
+    }
+    // declared after every staging lease: destroyed first, so nothing of this op still reads or writes them when
+    // they go back to the pools (also on the early returns below). The op stream waited for every H2D copy it
+    // issued; the step-0 device->host copies are not behind it.
+    struct Drain {
+        DeviceBackend *be;
+        DevStream st;
+        DevEvent *d2h;
+        std::vector<DevEvent> *ev;
+        ~Drain() {
+            if (*d2h) event_wait_polling(be, *d2h);
+            stream_wait_polling(be, st);
+            for (auto e : *ev) event_pool().put(e);
+        }
+    } drain{be, st, &last_d2h, &owned};
+
+    ReadyRanges txready[kNb];        // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
+    size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
+
+    const size_t nsteps = 2 * (ws - 1);
+    auto is_rs = [&](size_t g) { return g + 1 < ws; };
+    auto region_of = [&](size_t g) { return R.dst + bounds[chunk_rx(g, rank, ws)].first * es; };
+    auto rx_bytes = [&](size_t g) {
+        const auto [c0, c1] = bounds[chunk_rx(g, rank, ws)];
+        return (c1 - c0) * es;
+    };
+
+    size_t max_stripes = 1;
+    for (size_t g = 0; g < nsteps; ++g) {
+        const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
+        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, R.txs.size(), R.shape).off.size());
+    }
+    // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
+    OpSenders senders(R.txs, R.tag, seq, R.shape, piece, nsteps, max_stripes, be, R.tx);
+    RingRx rx(R.rxs, R.tag, seq, R.shape, nsteps); // after the buffers its sinks point into
+    StepSlots slots(be, rx, senders, ws, rxbuf, rx_bytes);
+    auto publish = [&](size_t g) {
+        if (senders.published(g)) return;
+        const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
+        const bool staged = g < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
+        OpSenders::Step stp;
+        stp.payload = staged ? txbuf[g % kNb] + txshift[g % kNb] : slots.buf(g - 1);
+        stp.bytes = (te - ts) * es;
+        stp.ready = staged ? &txready[g % kNb] : &slots.ready(g - 1);
+        senders.publish(g, stp);
+    };
+    auto fail = [&](int code) {
+        senders.cancel();
+        return code;
+    };
+
+    for (size_t g = 0; g < nsteps; ++g) {
+        const size_t b = g % kNb, nb = (g + 1) % kNb;
+        const bool rs = is_rs(g);
+        // 1. step g's sinks (normally posted during step g-1)
+        if (!slots.ensure_posted(g, [&] { return senders.failed(); })) return fail(1);
+        // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
+        uint8_t *region = region_of(g);
+        const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
+        if (rs) {
+            if (g >= 2 && !senders.wait(g - 2)) return fail(1);
+            txready[nb].clear();
+            txshift[nb] = shift;
+        }
+        // 3. own input chunk -> pinned, in pieces (from src: ready at call time)
+        if (g == 0) {
+            const auto [ts, te] = bounds[chunk_tx(0, rank, ws)];
+            txready[0].clear();
+            txshift[0] = 0;
+            for (size_t off = 0; off < (te - ts) * es; off += piece) {
+                const size_t n = std::min(piece, (te - ts) * es - off);
+                be->memcpy_async(txbuf[0] + off, R.src + ts * es + off, n, pq.d2h);
+                last_d2h = record(pq.d2h);
+                txready[0].add(off, off + n, last_d2h);
+            }
+        }
+        publish(g);
+        if (g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
+        fault_point("ring", seq, g, "publish");
+        // 4. receive + consume step g
+        DevEvent step_last = nullptr;
+        std::function<void(size_t, size_t)> consume;
+        if (rs) {
+            // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
+            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift, *sink = slots.buf(g);
+            consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
+                be->memcpy_async(stage + a, sink + a, e - a, pq.h2d);
+                DevEvent ce = record(pq.h2d);
+                be->stream_wait_event(st, ce);
+                be->reduce_copy(region + a, stage + a, out + a, (e - a) / es, R.dtype, R.rop, st);
+                step_last = record(st);
+                txready[nb].add(a, e, step_last);
+            };
+        } else {
+            uint8_t *sink = slots.buf(g);
+            ReadyRanges *fwd = &slots.ready(g);
+            consume = [&, sink, region, fwd](size_t a, size_t e) {
+                be->memcpy_async(region + a, sink + a, e - a, st);
+                step_last = record(st);
+                fwd->add(a, e, nullptr); // in host memory: forwardable at once
+            };
+        }
+        bool first = true;
+        const int rc = rx.receive(
+            g, es, piece,
+            [&](size_t a, size_t e) {
+                consume(a, e);
+                if (first) {
+                    first = false;
+                    fault_point("ring", seq, g, "rx"); // kernels / copies of this step in flight
+                }
+            },
+            [&] { // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
+                if (slots.try_post(g + 1)) fault_point("ring", seq, g, "ahead");
+            },
+            [&] { return senders.failed(); }, R.aborted);
+        slots.free_after(g, step_last);
+        if (rc) return fail(rc);
+        R.rx += rx_bytes(g);
+        rx.unpost(g);
+        step_mark(rs, rs ? g : g - (ws - 1));
+        if (g + 2 == ws) trace_mark("reduce_scatter");
+        fault_point("ring", seq, g, "end");
+    }
+    if (!senders.wait_all()) return fail(1);
+    return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
+}
+
+} // namespace
+
+std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
+    const ReduceRequest &q = op.req;
+    if (q.qalgo != QuantAlgo::None && q.qtype != q.dtype) return ring_reduce_device_quant(op, rv, seq, device);
+    DeviceBackend *be = device_backend();
+    const size_t ws = rv.ring.size(), rank = rv.rank;
+    const size_t es = dtype_size(q.dtype);
+    auto *dst = static_cast<uint8_t *>(q.dst);
+    const size_t bytes = q.count * es;
+    // Copy / reduce / frame granularity. >= 4 MiB keeps the copy engines near their peak (1 MiB copies: ~37 GB/s);
+    // with the send-ahead pipeline the step fill no longer scales with the piece, and 32 MiB measured fastest at
+    // 8 peers x 1 GiB on one MI355X (8 MiB 391-409 ms, 16 MiB 345-421, 32 MiB 331-346 in most runs;
+    // profiles/r3/ring_ab/): fewer copies, kernels, events and socket wake-ups per byte. (A sender choice: frames of
+    // any size up to 1 GiB are accepted, also by the reference.)
+    const size_t piece = std::max<size_t>(1 << 20, env_size("PCCL_DEVICE_PIECE_BYTES", 32u << 20)) / es * es;
+
+    be->set_device(device);
+    StreamLease stream(device);
+    DevStream st = stream.get();
+    if (!st) return {false, false};
+    if (op.small_path) { // latency-bound (agreed by every peer): one D2H, host all-gather + reduce, one H2D
+        Lease hin(pinned_pool(), std::max<size_t>(bytes, 64)), hout(pinned_pool(), std::max<size_t>(bytes, 64));
+        if (!hin.ok() || !hout.ok()) return {false, false};
+        if (!be->memcpy_async(hin.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};
+        const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, op.shape, hin.data(), hout.data(), q.count,
+                                              q.dtype, q.op, ws, rank, [&] { return abort_received(q.tag); }, op.tx,
+                                              op.rx);
+        if (rc) return {false, rc == 2};
+        if (!be->memcpy_async(dst, hout.data(), bytes, st) || !be->stream_sync(st)) return {false, false};
+        trace_mark("allgather_reduce");
+        if (q.src == q.dst && !q.scratch) settle_device_backup(op.settle, be, device, std::move(hin), dst, bytes);
+        return {true, false};
+    }
+    const PcieQueues pq = shared_pcie_queues(be, device);
+    if (!pq.h2d || !pq.d2h) return {false, false};
+
+    // the caller's input -> dst (out of place) or a backup of it (in place, restored on abort), on the op stream
+    Lease backup;
+    const bool keep_backup = q.src == q.dst && !q.scratch;
+    if (keep_backup) {
+        backup = Lease(device_pool(), bytes, device);
+        if (!backup.ok()) return {false, false};
+        be->memcpy_async(backup.data(), q.src, bytes, st);
+    } else if (q.src != q.dst) {
+        be->memcpy_async(dst, q.src, bytes, st);
+    }
+    OpAbort aborted([this, t = q.tag] { return abort_received(t); });
+    DevRing R{rv.tx, rv.rx, ws, rank, q.tag, seq, op.shape, be, pq, st, static_cast<const uint8_t *>(q.src), dst,
+              q.count, es, piece, q.dtype, q.op, device, [&] { return aborted(); }, op.tx, op.rx};
+    const int rc = device_ring_pipeline(R);
+    if (rc != 0) {
+        // the pipeline drained every copy and kernel of the op and no sink of it is posted any more: restore
+        be->stream_sync(st);
+        if (keep_backup) {
+            be->memcpy_async(dst, backup.data(), bytes, st);
+            be->stream_sync(st);
+        }
+        return {rc == 2, rc == 2};
+    }
+    if (q.op == ReduceOp::Avg) be->finalize_avg(dst, q.count, q.dtype, ws, st);
+    if (!stream_wait_polling(be, st)) return {false, false};
+    if (keep_backup) settle_device_backup(op.settle, be, device, std::move(backup), dst, bytes);
+    return {true, false};
+}
+
+} // namespace pccl::client

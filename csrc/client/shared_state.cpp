@@ -452,7 +452,8 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
     // entries are overwritten by the next attempt, and every entry is hash-verified at the end).
     auto fetch_from = [&](const SockAddr &distributor) -> bool {
         // PCCL_SS_IPC_PROTOCOL=1 forces the extension even without a GPU (tests: every entry is then streamed)
-        const bool try_ipc = (be || env_flag("PCCL_SS_IPC_PROTOCOL", false)) && !env_flag("PCCL_SS_NO_IPC", false);
+        const bool try_ipc = (be || env_flag("PCCL_SS_IPC_PROTOCOL", false)) && !env_flag("PCCL_SS_NO_IPC", false) &&
+                             !wire_reference_;
         if (try_ipc && net::is_local_address(distributor)) {
             bool fallback = false;
             if (fetch_ipc(distributor, fallback)) return true;
@@ -537,7 +538,7 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         auto req = decode_payload<C2SRequestSharedState>(pkt->payload.data(), pkt->payload.size());
         if (!req) return;
         keys = std::move(req->keys);
-    } else if (pkt->id == C2SRequestSharedStateIpc::kId) {
+    } else if (pkt->id == C2SRequestSharedStateIpc::kId && !wire_reference_) { // (a reference peer: unknown packet)
         auto req = decode_payload<C2SRequestSharedStateIpc>(pkt->payload.data(), pkt->payload.size());
         if (!req) return;
         keys = std::move(req->keys);

@@ -914,6 +914,7 @@ void Master::handle_coll_initiate(const SockAddr &addr, const C2MCollectiveComms
     c->state = State::CollectiveCommsRunning;
     c->colls[p.tag] = CollState::VoteInitiate;
     c->coll_flags[p.tag] = p.flags;
+    c->coll_shapes[p.tag] = p.shape;
     check_coll_initiate_consensus(c->group, p.tag);
 }
 
@@ -931,10 +932,19 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
     pkt.tag = tag;
     pkt.seq_nr = seq;
     pkt.flags = 0xff; // a capability holds for the op only if every participant announced it
+    // one data-plane shape for every participant: fewest stripes and lanes, largest stripe minimum of the proposals
+    pkt.shape.stripes = 16;
+    pkt.shape.quant_lanes = 4;
+    pkt.shape.stripe_min_mib = 1;
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         auto f = c.coll_flags.find(tag);
         pkt.flags &= f == c.coll_flags.end() ? 0 : f->second;
+        auto sh = c.coll_shapes.find(tag);
+        if (sh == c.coll_shapes.end()) continue;
+        pkt.shape.stripes = std::min(pkt.shape.stripes, sh->second.stripes);
+        pkt.shape.quant_lanes = std::min(pkt.shape.quant_lanes, sh->second.quant_lanes);
+        pkt.shape.stripe_min_mib = std::max(pkt.shape.stripe_min_mib, sh->second.stripe_min_mib);
     }
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
@@ -996,6 +1006,7 @@ void Master::check_coll_complete_consensus(uint32_t group, uint64_t tag) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         c.colls.erase(tag);
         c.coll_flags.erase(tag);
+        c.coll_shapes.erase(tag);
         if (c.colls.empty()) c.state = State::Idle;
         server_.send_packet(c.addr, pkt);
     }

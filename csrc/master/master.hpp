@@ -64,6 +64,7 @@ struct ClientInfo {
     bool voted_pending_query = false;
     std::map<uint64_t, CollState> colls;
     std::map<uint64_t, uint8_t> coll_flags; // initiate capability bits per running tag
+    std::map<uint64_t, proto::WireShape> coll_shapes; // proposed data-plane shape per running tag (kCollFlagExtWire)
     uint32_t group = 0;
     SockAddr p2p{}, ss{}, bm{};
     uint64_t ss_revision = 0; // revision announced in the current shared-state round

@@ -148,6 +148,46 @@ struct C2MDistSharedStateComplete : Empty {
     static constexpr PacketId kId = C2M_DIST_SHARED_STATE_COMPLETE;
 };
 
+// the peer can run this op hierarchically (device buffers, host-local IPC arena, inter-host ring connections)
+constexpr uint8_t kCollFlagHierarchical = 1;
+// this peer's PCCL_SMALL_ALLREDUCE_BYTES selects the all-gather small-message algorithm for this op; ANDed by the
+// master like every capability bit, so a threshold that differs between peers cannot split the ring between the two
+// algorithms (the op then uses the reduce-scatter ring everywhere)
+constexpr uint8_t kCollFlagSmallPath = 2;
+// the peer speaks the pccl-amd data-plane framing for this op: ring steps striped over several pooled connections,
+// quantized ops split into lanes with their dequantization metadata on a separate tag (docs/WIRE_DIVERGENCES.md).
+// Without it on every participant (a reference peer, or PCCL_WIRE=reference) the op runs the reference framing: one
+// connection seq % pool per op, the metadata packet on the data tag before the step's data, one lane.
+constexpr uint8_t kCollFlagExtWire = 4;
+
+// Data-plane shape of one op (extension of the initiate / commence packets, present iff kCollFlagExtWire). Every peer
+// proposes its own settings in its initiate; the master agrees on one shape per op (fewest stripes and lanes, largest
+// stripe minimum) and every peer runs the commence's, so peers whose PCCL_RING_STRIPES / PCCL_STRIPE_MIN_BYTES /
+// PCCL_QUANT_LANES differ still derive identical stripe plans, connections and lane tags.
+struct WireShape {
+    uint8_t stripes = 4;         // PCCL_RING_STRIPES: striped connections per ring step (1..16)
+    uint8_t quant_lanes = 2;     // PCCL_QUANT_LANES: lanes of a quantized op (1..4)
+    uint16_t stripe_min_mib = 8; // PCCL_STRIPE_MIN_BYTES / 1 MiB: smallest stripe (>= 1)
+    void encode(WBuf &w) const {
+        w.u8(stripes);
+        w.u8(quant_lanes);
+        w.u16(stripe_min_mib);
+    }
+    bool decode(RBuf &r) {
+        if (!r.ok() || r.remaining() < 4) return false;
+        stripes = r.u8();
+        quant_lanes = r.u8();
+        stripe_min_mib = r.u16();
+        stripes = stripes < 1 ? 1 : (stripes > 16 ? 16 : stripes);
+        quant_lanes = quant_lanes < 1 ? 1 : (quant_lanes > 4 ? 4 : quant_lanes);
+        if (stripe_min_mib < 1) stripe_min_mib = 1;
+        return r.ok();
+    }
+    bool operator==(const WireShape &o) const {
+        return stripes == o.stripes && quant_lanes == o.quant_lanes && stripe_min_mib == o.stripe_min_mib;
+    }
+};
+
 struct C2MCollectiveCommsInitiate {
     static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_INITIATE;
     uint64_t tag = 0;
@@ -156,12 +196,15 @@ struct C2MCollectiveCommsInitiate {
     ReduceOp op = ReduceOp::Sum;
     // extension (appended, optional): capability bits of this peer for this op (kCollFlagHierarchical)
     uint8_t flags = 0;
+    // extension after flags, present iff flags has kCollFlagExtWire: the data-plane shape this peer proposes
+    WireShape shape{};
     void encode(WBuf &w) const {
         w.u64(tag);
         w.u64(count);
         w.u8(static_cast<uint8_t>(data_type));
         w.u8(static_cast<uint8_t>(op));
         if (flags) w.u8(flags);
+        if (flags & kCollFlagExtWire) shape.encode(w);
     }
     bool decode(RBuf &r) {
         tag = r.u64();
@@ -169,16 +212,11 @@ struct C2MCollectiveCommsInitiate {
         data_type = static_cast<DType>(r.u8());
         op = static_cast<ReduceOp>(r.u8());
         flags = r.ok() && r.remaining() > 0 ? r.u8() : 0;
+        if ((flags & kCollFlagExtWire) && !shape.decode(r)) flags &= static_cast<uint8_t>(~kCollFlagExtWire);
         return r.ok();
     }
 };
 
-// the peer can run this op hierarchically (device buffers, host-local IPC arena, inter-host ring connections)
-constexpr uint8_t kCollFlagHierarchical = 1;
-// this peer's PCCL_SMALL_ALLREDUCE_BYTES selects the all-gather small-message algorithm for this op; ANDed by the
-// master like every capability bit, so a threshold that differs between peers cannot split the ring between the two
-// algorithms (the op then uses the reduce-scatter ring everywhere)
-constexpr uint8_t kCollFlagSmallPath = 2;
 
 struct C2MCollectiveCommsComplete {
     static constexpr PacketId kId = C2M_COLLECTIVE_COMMS_COMPLETE;
@@ -300,15 +338,18 @@ struct M2CCollectiveCommsCommence {
     uint64_t tag = 0;
     uint64_t seq_nr = 0;
     uint8_t flags = 0; // extension (appended, optional): AND of every participant's initiate flags
+    WireShape shape{};  // extension after flags, present iff flags has kCollFlagExtWire: the op's agreed shape
     void encode(WBuf &w) const {
         w.u64(tag);
         w.u64(seq_nr);
         if (flags) w.u8(flags);
+        if (flags & kCollFlagExtWire) shape.encode(w);
     }
     bool decode(RBuf &r) {
         tag = r.u64();
         seq_nr = r.u64();
         flags = r.ok() && r.remaining() > 0 ? r.u8() : 0;
+        if ((flags & kCollFlagExtWire) && !shape.decode(r)) flags &= static_cast<uint8_t>(~kCollFlagExtWire);
         return r.ok();
     }
 };

@@ -96,7 +96,11 @@ typedef enum pcclAttribute_t {
     PCCL_ATTRIBUTE_LAST_REDUCE_PATH = 66,
     /** [pccl-amd extension] worker threads of the async collective pool so far (bounded by
      *  PCCL_MAX_CONCURRENT_COLLECTIVE_OPS, default 16) */
-    PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS = 67
+    PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS = 67,
+    /** [pccl-amd extension] wire framing of the last completed all-reduce: 0 none (no TCP data ring, e.g. xGMI/IPC),
+     *  1 pccl-amd framing (agreed per op by every participant: striped connections, quantized lanes and metadata tag),
+     *  2 reference framing (a participant without the extension, or PCCL_WIRE=reference) */
+    PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING = 68
 } pcclAttribute_t;
 
 typedef enum pcclSharedStateSyncStrategy_t {

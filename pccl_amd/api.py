@@ -98,6 +98,7 @@ class Attribute(Enum):
     RING_RANK = 65
     LAST_REDUCE_PATH = 66
     COLLECTIVE_WORKER_THREADS = 67
+    LAST_REDUCE_FRAMING = 68
 
 
 class ReducePath(Enum):

@@ -1,0 +1,201 @@
+// Reference data-plane framing, byte for byte (reference ccoip/src/cpp/reduce.cpp:149-192,609-774): one quantized
+// all-reduce of a 2-peer ring in which this test plays the reference peer at the socket level. The library peer must
+//   * send each step's P2PDequantizationMeta packet on the op's data tag, on connection seq % pool (here: the only one),
+//   * send no byte of the step's data before it has received the peer's packet,
+//   * then send the step's quantized chunk as data frames on the same tag,
+// and reduce / de-quantize exactly what the peer sent. Frames: u64 BE (payload + 16) | u64 BE tag | u64 BE stream_ctr
+// (reference tinysockets multiplexed_socket.cpp:406-411); packet payload: u16 BE id | u64 BE tag | u8 0 (MIN_MAX) |
+// u8 dtype | min | max (float: 4 bytes little-endian, reference DeQuantizationMetaData).
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "client/ring_common.hpp"
+#include "harness.hpp"
+#include "net/socket.hpp"
+
+using namespace pccl;
+using namespace pccl::client::ring;
+
+namespace {
+
+void put_be64(std::vector<uint8_t> &v, uint64_t x) {
+    for (int i = 7; i >= 0; --i) v.push_back(static_cast<uint8_t>(x >> (8 * i)));
+}
+
+std::vector<uint8_t> frame(uint64_t tag, uint64_t seq, const std::vector<uint8_t> &payload) {
+    std::vector<uint8_t> f;
+    put_be64(f, payload.size() + 16);
+    put_be64(f, tag);
+    put_be64(f, seq);
+    f.insert(f.end(), payload.begin(), payload.end());
+    return f;
+}
+
+// the reference's P2PPacketDequantizationMeta (id 3) for a MIN_MAX float chunk
+std::vector<uint8_t> meta_packet(uint64_t tag, float mn, float mx) {
+    std::vector<uint8_t> p = {0x00, 0x03};
+    put_be64(p, tag);
+    p.push_back(0x00); // MIN_MAX
+    p.push_back(10);   // ccoipFloat
+    uint8_t b[4];
+    std::memcpy(b, &mn, 4);
+    p.insert(p.end(), b, b + 4);
+    std::memcpy(b, &mx, 4);
+    p.insert(p.end(), b, b + 4);
+    return p;
+}
+
+bool readable_within(int fd, int ms) {
+    pollfd p{fd, POLLIN, 0};
+    return ::poll(&p, 1, ms) > 0;
+}
+
+std::vector<uint8_t> read_exact(int fd, size_t n) {
+    std::vector<uint8_t> v(n);
+    size_t got = 0;
+    while (got < n) {
+        if (!readable_within(fd, 5000)) break;
+        const ssize_t r = ::recv(fd, v.data() + got, n - got, 0);
+        if (r <= 0) break;
+        got += static_cast<size_t>(r);
+    }
+    v.resize(got);
+    return v;
+}
+
+} // namespace
+
+TEST(reference_framed_quantized_ring_golden_bytes) {
+    int txsv[2], rxsv[2];
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, txsv) == 0);
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, rxsv) == 0);
+    auto tx = std::make_shared<net::MuxConn>(txsv[0], net::MuxConn::Mode::Tx, SockAddr{});
+    auto rx = std::make_shared<net::MuxConn>(rxsv[1], net::MuxConn::Mode::Rx, SockAddr{});
+    EXPECT(tx->start() && rx->start());
+    const Conns txs{tx}, rxs{rx};
+    const int ref_in = txsv[1], ref_out = rxsv[0]; // the emulated reference peer's ends
+
+    // rank 0 of 2: chunk 0 = [0, 1, 2, 3] is its reduce-scatter payload, chunk 1 = [10] * 4 receives the peer's part
+    std::vector<float> data = {0, 1, 2, 3, 10, 10, 10, 10};
+    const uint64_t tag = 0x1234, seq = 7;
+    const Shape shape = Shape::reference_framing();
+    std::atomic<uint64_t> txc{0}, rxc{0};
+    int rc = -1;
+    std::thread lib([&] {
+        HostRingArgs A{txs, rxs, 2, 0, tag, seq, shape, reinterpret_cast<uint8_t *>(data.data()), data.size(),
+                       DType::F32, DType::U8, QuantAlgo::MinMax, ReduceOp::Sum, true, [] { return false; }, txc, rxc};
+        rc = host_ring(A);
+    });
+
+    // reduce-scatter: the library's metadata packet on the data tag, then nothing until the peer's packet arrived
+    const auto m0 = frame(tag, seq, meta_packet(tag, 0.f, 3.f));
+    EXPECT(read_exact(ref_in, m0.size()) == m0);
+    EXPECT(!readable_within(ref_in, 150));
+    const auto pm0 = frame(tag, seq, meta_packet(tag, 20.f, 23.f));
+    EXPECT(net::send_all(ref_out, pm0.data(), pm0.size()));
+    const auto d0 = frame(tag, seq, {0x00, 0x55, 0xaa, 0xff}); // round((x - 0) / 3 * 255)
+    EXPECT(read_exact(ref_in, d0.size()) == d0);
+    const auto pd0 = frame(tag, seq, {0x00, 0xff, 0x00, 0xff}); // the peer's chunk 1: 20, 23, 20, 23
+    EXPECT(net::send_all(ref_out, pd0.data(), pd0.size()));
+
+    // all-gather: the library owns chunk 1 = [30, 33, 30, 33] (quantized once, its own copy := D(Q(x)))
+    const auto m1 = frame(tag, seq, meta_packet(tag, 30.f, 33.f));
+    EXPECT(read_exact(ref_in, m1.size()) == m1);
+    EXPECT(!readable_within(ref_in, 150));
+    const auto pm1 = frame(tag, seq, meta_packet(tag, 5.f, 8.f));
+    EXPECT(net::send_all(ref_out, pm1.data(), pm1.size()));
+    const auto d1 = frame(tag, seq, {0x00, 0xff, 0x00, 0xff});
+    EXPECT(read_exact(ref_in, d1.size()) == d1);
+    const auto pd1 = frame(tag, seq, {0x00, 0x55, 0xaa, 0xff}); // the peer's chunk 0: 5, 6, 7, 8
+    EXPECT(net::send_all(ref_out, pd1.data(), pd1.size()));
+    lib.join();
+
+    EXPECT(rc == 0);
+    const std::vector<float> want = {5, 6, 7, 8, 30, 33, 30, 33};
+    EXPECT(data == want);
+    // byte counters as the reference keeps them: a metadata packet counts its LTV header (u64 length + u16 id) and
+    // payload, 28 bytes (reduce.cpp:162-165,186-187), data its raw bytes: 2 x 28 + 2 x 4 each way
+    EXPECT(txc.load() == 2 * 28 + 8 && rxc.load() == 2 * 28 + 8);
+    EXPECT(!readable_within(ref_in, 50)); // nothing else on the wire
+    tx->interrupt();
+    rx->interrupt();
+    ::close(ref_in);
+    ::close(ref_out);
+}
+
+// The same op in the pccl-amd framing sends the metadata packet on the metadata tag (data tag | 1 << 63) and the data
+// right behind it, without waiting for the peer's packet.
+TEST(ext_framed_quantized_step_does_not_wait_for_peer_meta) {
+    int txsv[2], rxsv[2];
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, txsv) == 0);
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, rxsv) == 0);
+    auto tx = std::make_shared<net::MuxConn>(txsv[0], net::MuxConn::Mode::Tx, SockAddr{});
+    auto rx = std::make_shared<net::MuxConn>(rxsv[1], net::MuxConn::Mode::Rx, SockAddr{});
+    EXPECT(tx->start() && rx->start());
+    const Conns txs{tx}, rxs{rx};
+    std::vector<float> data = {0, 1, 2, 3, 10, 10, 10, 10};
+    const uint64_t tag = 0x1234, seq = 7;
+    proto::WireShape w;
+    w.stripes = 1;
+    w.quant_lanes = 1;
+    const Shape shape = Shape::from_wire(w);
+    std::atomic<uint64_t> txc{0}, rxc{0};
+    std::atomic<bool> stop{false};
+    std::thread lib([&] {
+        HostRingArgs A{txs, rxs, 2, 0, tag, seq, shape, reinterpret_cast<uint8_t *>(data.data()), data.size(),
+                       DType::F32, DType::U8, QuantAlgo::MinMax, ReduceOp::Sum, true,
+                       [&] { return stop.load(); }, txc, rxc};
+        host_ring(A);
+    });
+    const auto m0 = frame(tag ^ kMetaTagBit, seq, meta_packet(tag, 0.f, 3.f));
+    EXPECT(read_exact(txsv[1], m0.size()) == m0);
+    const auto d0 = frame(tag, seq, {0x00, 0x55, 0xaa, 0xff});
+    EXPECT(read_exact(txsv[1], d0.size()) == d0); // no peer packet was sent
+    stop = true; // abort the op (the test never answers)
+    lib.join();
+    tx->interrupt();
+    rx->interrupt();
+    ::close(txsv[1]);
+    ::close(rxsv[0]);
+}
+
+TEST(stripe_conn_reference_framing_is_seq_mod_pool) {
+    const Shape ref = Shape::reference_framing();
+    for (uint64_t seq : {0ull, 1ull, 5ull, 31ull, 1000ull})
+        for (size_t pool : {1ul, 4ul, 32ul}) EXPECT(stripe_conn(seq, 77, 0, pool, ref) == seq % pool);
+    EXPECT(plan_stripes(size_t{1} << 30, 32, ref).off.size() == 1);
+    EXPECT(quant_lane_bounds(size_t{1} << 30, 2, 1, ref).size() == 2);
+}
+
+TEST(wire_shape_roundtrip_and_clamp) {
+    proto::C2MCollectiveCommsInitiate a;
+    a.tag = 5;
+    a.count = 100;
+    a.flags = proto::kCollFlagExtWire | proto::kCollFlagSmallPath;
+    a.shape.stripes = 8;
+    a.shape.quant_lanes = 3;
+    a.shape.stripe_min_mib = 16;
+    auto bytes = proto::encode_with_id(a);
+    auto b = proto::decode_payload<proto::C2MCollectiveCommsInitiate>(bytes.data() + 2, bytes.size() - 2);
+    EXPECT(b && b->flags == a.flags && b->shape == a.shape);
+    // a reference initiate (no extension bytes) decodes with no flags
+    proto::C2MCollectiveCommsInitiate r;
+    r.tag = 5;
+    auto rb = proto::encode_with_id(r);
+    EXPECT(rb.size() == 2 + 18);
+    auto rd = proto::decode_payload<proto::C2MCollectiveCommsInitiate>(rb.data() + 2, rb.size() - 2);
+    EXPECT(rd && rd->flags == 0);
+    // the ext flag without its shape bytes (truncated) is dropped instead of misreading the packet
+    std::vector<uint8_t> trunc(rb.begin(), rb.end());
+    trunc.push_back(proto::kCollFlagExtWire);
+    auto td = proto::decode_payload<proto::C2MCollectiveCommsInitiate>(trunc.data() + 2, trunc.size() - 2);
+    EXPECT(td && td->flags == 0);
+    const Shape s = Shape::from_wire(a.shape);
+    EXPECT(!s.reference && s.stripes == 8 && s.quant_lanes == 3 && s.stripe_min == (size_t{16} << 20));
+}
