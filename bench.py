@@ -509,9 +509,12 @@ def baseline_configs(a, peers):
         _log(f"{name}: {' '.join(args)}")
         t0 = time.time()
         try:
-            r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", args[0]), *args[1:],
-                                *(["--timeout", str(limit - 40)] if args[0] == "fault_tolerance.py" else [])],
-                               capture_output=True, text=True, timeout=limit, env=env)
+            # the process's CPU mask from before the bench's per-CCD spread (as for the latency measurements): one
+            # process per peer, whose spinning op threads and shared-memory barriers suffer when spread over CCDs
+            with _full_cpu_mask():
+                r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", args[0]), *args[1:],
+                                    *(["--timeout", str(limit - 40)] if args[0] == "fault_tolerance.py" else [])],
+                                   capture_output=True, text=True, timeout=limit, env=env)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             out[name] = json.loads(line[-1]) if r.returncode == 0 and line else \
                 {"error": f"rc {r.returncode}: {r.stderr[-400:]}"}

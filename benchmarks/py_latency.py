@@ -9,10 +9,16 @@ With every peer on one GPU the buffers are fd-shareable and the ops run the xGMI
 the host ring.
 
 Per size: the median / p90 of the per-op wall time maximum over the peers (ops are matched by index: every peer runs
-the same sequence), and two call variants on the same buffers:
-  * ``all_reduce``: the public blocking call (synchronises the tensor's current stream first);
-  * ``ready``: ``_all_reduce_async_ready(...).wait()``, which skips that synchronisation (producers already waited
-    for), so the difference is the stream-sync cost.
+the same sequence). Call variants on the same buffers, interleaved op by op (a machine-wide slow phase hits every
+variant alike):
+  * ``all_reduce``: the public blocking call - stream-ordered (pcclxAllReduceOnStream: the op waits for an event
+    recorded on the current stream; no stream synchronisation) and run on the calling thread;
+  * ``async``: the public ``all_reduce_async(...).wait()`` - stream-ordered, run on a collective worker thread;
+  * ``ready``: ``_all_reduce_async_ready(...).wait()`` - no readiness handling at all (producers already waited for),
+    worker thread: the floor of the two above;
+  * ``sync_inline`` / ``sync_worker``: the round-4 behaviour - ``current_stream().synchronize()`` on the caller, then
+    the op inline (pcclAllReduce) / on a worker; with ``ready`` and ``ready_inline`` (no sync, inline) this is the
+    {host stream sync, none} x {inline, worker} matrix that isolates what the round-4 blocking call paid.
 Prints one JSON object.
 """
 from __future__ import annotations
@@ -34,7 +40,11 @@ def peer(a):
 
     import torch
 
+    import ctypes
+
     import pccl_amd as pccl
+    from pccl_amd import _native
+    from pccl_amd._native import C
     from pccl_amd.utils import wait_for_world
     dev = torch.device(a.device)
     if dev.type == "cuda":
@@ -49,20 +59,39 @@ def peer(a):
         with pccl.memory.maybe_shareable(dev) if dev.type == "cuda" else contextlib.nullcontext():
             x = torch.full((n,), float(a.rank + 1), device=dev, dtype=torch.bfloat16)
             y = torch.empty_like(x)
-        res = {}
-        for variant in ("all_reduce", "ready"):
-            ts = []
-            for i in range(a.iters + a.warmup):
+        variants = a.variants.split(",")
+        res = {v: [] for v in variants}
+        cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+
+        def run(variant):
+            nonlocal tag
+            if variant == "all_reduce":
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+            elif variant == "async":
+                ok, _, _ = comm.all_reduce_async(x, y, op=pccl.ReduceOp.SUM, tag=tag).wait()
+                assert ok
+            elif variant in ("ready", "sync_worker"):
+                if variant == "sync_worker" and cur is not None:
+                    cur.synchronize()
+                ok, _, _ = comm._all_reduce_async_ready(x, y, op=pccl.ReduceOp.SUM, tag=tag).wait()
+                assert ok
+            elif variant in ("ready_inline", "sync_inline"):
+                if variant == "sync_inline" and cur is not None:
+                    cur.synchronize()
+                sptr, rptr, desc = comm._descriptor(x, y, pccl.ReduceOp.SUM, tag, None, None, sync=False)
+                info = _native.ReduceInfoC()
+                pccl.PCCLError.check(C.pcclAllReduce(sptr, rptr, ctypes.byref(desc), comm._comm, ctypes.byref(info)),
+                                     "pcclAllReduce")
+            else:
+                raise ValueError(variant)
+            tag += 1
+
+        for i in range(a.iters + a.warmup):
+            for variant in variants:
                 t0 = time.perf_counter()
-                if variant == "all_reduce":
-                    comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
-                else:
-                    ok, _, _ = comm._all_reduce_async_ready(x, y, op=pccl.ReduceOp.SUM, tag=tag).wait()
-                    assert ok
+                run(variant)
                 if i >= a.warmup:
-                    ts.append(time.perf_counter() - t0)
-                tag += 1
-            res[variant] = ts
+                    res[variant].append(time.perf_counter() - t0)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         want = a.peers * (a.peers + 1) / 2
@@ -80,6 +109,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--sizes", default="65536,1048576,16777216")
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--variants", default="all_reduce,async,ready",
+                    help="comma list of all_reduce, async, ready, ready_inline, sync_inline, sync_worker")
     ap.add_argument("--peer", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--master", default="")
     ap.add_argument("--rank", type=int, default=0)
@@ -98,7 +129,8 @@ def main():
     try:
         procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--peer", "--master",
                                    f"127.0.0.1:{port}", "--rank", str(r), "--peers", str(a.peers), "--iters",
-                                   str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device],
+                                   str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device,
+                                   "--variants", a.variants],
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
                  for r in range(a.peers)]
         outs = communicate_all(procs, 600, DIAG_SIGNALS)
@@ -114,7 +146,7 @@ def main():
     summary = {"peers": a.peers, "device": a.device, "iters": a.iters, "processes": "one per peer", "sizes": {}}
     for b in res[0]:
         row = {"path": names.get(res[0][b]["path"], "?")}
-        for v in ("all_reduce", "ready"):
+        for v in a.variants.split(","):
             per_op = [max(r[b][v][i] for r in res) for i in range(a.iters)]
             q = statistics.quantiles(per_op, n=10)
             row[v] = {"median_us": round(statistics.median(per_op) * 1e6, 1), "p90_us": round(q[-1] * 1e6, 1),

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../client/client.hpp"
+#include "../client/pools.hpp"
 #include "../common/device_backend.hpp"
 #include "../common/log.hpp"
 #include "../master/master.hpp"
@@ -199,8 +200,10 @@ pcclResult_t pcclOptimizeTopology(const pcclComm_t *comm) {
 
 // Validates and starts one all-reduce. `inline_run` executes the op on the calling thread (blocking pcclAllReduce:
 // no hand-off to a worker thread on the latency-critical path); otherwise a collective worker thread runs it.
+// `stream` (optional, device buffers): the op's input is ready once the work queued on it so far has completed.
 static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
-                                     const pcclComm_t *comm, pcclAsyncReduceOp_t *handle_out, bool inline_run) {
+                                     const pcclComm_t *comm, pcclAsyncReduceOp_t *handle_out, bool inline_run,
+                                     void *const *stream = nullptr) {
     PCCL_CHECK_INIT();
     PCCL_REQUIRE(comm != nullptr && descriptor != nullptr && handle_out != nullptr, pcclInvalidArgument);
     PCCL_REQUIRE(comm->client != nullptr, pcclInvalidUsage);
@@ -226,7 +229,22 @@ static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const
     req.qalgo = *qt == *dt ? pccl::QuantAlgo::None : *qa;
     req.op = *op;
     req.tag = descriptor->tag;
-    if (!comm->client->all_reduce_async(req, inline_run)) return pcclInvalidArgument;
+    pccl::DeviceBackend *be = pccl::device_backend();
+    if (stream != nullptr && be != nullptr && descriptor->count > 0) {
+        pccl::DevPtrInfo pi{};
+        if (be->pointer_info(sendbuff, pi) && pi.is_device) {
+            // an event on the caller's stream marks the input's producers; the op waits for it, the caller does not
+            req.ready = pccl::client::event_pool().get();
+            if (req.ready == nullptr || !be->event_record(req.ready, static_cast<pccl::DevStream>(*stream))) {
+                pccl::client::event_pool().put(req.ready);
+                return pcclInvalidArgument;
+            }
+        }
+    }
+    if (!comm->client->all_reduce_async(req, inline_run)) {
+        pccl::client::event_pool().put(req.ready);
+        return pcclInvalidArgument;
+    }
     handle_out->comm = const_cast<pcclComm_t *>(comm);
     handle_out->tag = descriptor->tag;
     return pcclSuccess;
@@ -259,6 +277,19 @@ pcclResult_t pcclAllReduce(const void *sendbuff, void *recvbuff, const pcclReduc
                            const pcclComm_t *comm, pcclReduceInfo_t *info_out) {
     pcclAsyncReduceOp_t h{};
     const pcclResult_t r = start_all_reduce(sendbuff, recvbuff, descriptor, comm, &h, true);
+    if (r != pcclSuccess) return r;
+    return pcclAwaitAsyncReduce(&h, info_out);
+}
+
+pcclResult_t pcclxAllReduceAsyncOnStream(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
+                                        const pcclComm_t *comm, void *hip_stream, pcclAsyncReduceOp_t *handle_out) {
+    return start_all_reduce(sendbuff, recvbuff, descriptor, comm, handle_out, false, &hip_stream);
+}
+
+pcclResult_t pcclxAllReduceOnStream(const void *sendbuff, void *recvbuff, const pcclReduceDescriptor_t *descriptor,
+                                   const pcclComm_t *comm, void *hip_stream, pcclReduceInfo_t *info_out) {
+    pcclAsyncReduceOp_t h{};
+    const pcclResult_t r = start_all_reduce(sendbuff, recvbuff, descriptor, comm, &h, true, &hip_stream);
     if (r != pcclSuccess) return r;
     return pcclAwaitAsyncReduce(&h, info_out);
 }

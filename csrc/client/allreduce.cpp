@@ -196,6 +196,14 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
             trace_mark("commence");
         }
     }
+    if (op->req.ready) { // stream-ordered op: its input's producers (overlapped with the master round trip)
+        if (commenced) {
+            event_wait_polling(device_backend(), op->req.ready);
+            trace_mark("input_ready");
+        }
+        event_pool().put(op->req.ready);
+        op->req.ready = nullptr;
+    }
     if (commenced) {
         if (rv && rv->ring.size() >= 2) {
             op->world = static_cast<uint32_t>(rv->ring.size());
@@ -351,3 +359,18 @@ bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {
 
 } // namespace pccl::client
 
+// Staging pools of this process: [0..2] pinned host (in use, peak in use, cached free), [3..5] HBM, [6..8] plain host
+// bytes; returns how many counters exist (writes at most n). `reset` restarts the peaks at the current use.
+extern "C" __attribute__((visibility("default"))) size_t pcclxPoolStats(uint64_t *out, size_t n, int reset) {
+    using namespace pccl::client;
+    BufferPool *pools[3] = {&pinned_pool(), &device_pool(), &host_pool()};
+    uint64_t v[9];
+    for (int k = 0; k < 3; ++k) {
+        v[3 * k] = pools[k]->in_use();
+        v[3 * k + 1] = pools[k]->peak();
+        v[3 * k + 2] = pools[k]->cached();
+        if (reset) pools[k]->reset_peak();
+    }
+    for (size_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
+    return 9;
+}

@@ -70,6 +70,9 @@ struct ReduceRequest {
     ReduceOp op = ReduceOp::Sum;
     uint64_t tag = 0;
     bool scratch = false; // internal: dst is library scratch, no abort backup needed (hierarchical inner ring)
+    // stream-ordered ops (pcclxAllReduce*OnStream): recorded on the caller's stream at submission; the op waits for it
+    // before its data path reads `src`, then returns it to the event pool
+    DevEvent ready = nullptr;
 };
 
 class IpcArena; // intra-node shared-memory + IPC rendezvous (ipc.cpp)

@@ -440,6 +440,26 @@ bool IpcArena::op_quiet(uint64_t seq) const {
     return true;
 }
 
+// Every peer that may still be inside op `seq` (see op_quiet) is another process: such a peer reaches my segments
+// only through its own VMM import, which keeps the pages alive after I free my mapping. A peer thread of this process
+// writes through raw pointers into my mapping (no import), so a buffer it may still touch is never freed.
+bool IpcArena::unquiet_peers_remote(uint64_t seq) const {
+    const uint32_t slot = static_cast<uint32_t>(seq % kSlots);
+    const int self = static_cast<int>(::getpid());
+    for (size_t k = 0; k < ring_.size(); ++k) {
+        if (k == rank_) continue;
+        if (!pid_alive(pids_[k])) {
+            if (!pid_quiesced(pids_[k]) && pids_[k] == self) return false;
+            continue;
+        }
+        const uint64_t v = shm_->op(slot, static_cast<uint32_t>(k))->phase.load(std::memory_order_acquire);
+        const uint32_t vp = static_cast<uint32_t>(v & 0xff);
+        const bool quiet = (v >> 8) != seq + 1 || vp == PH_GATHERED || vp == PH_RELEASED || vp == PH_ABORTED;
+        if (!quiet && pids_[k] == self) return false;
+    }
+    return true;
+}
+
 void IpcArena::reclaim_quarantined_locked() {
     constexpr size_t kQuarantineCapBytes = size_t{8} << 30;
     size_t held = 0;
@@ -459,7 +479,7 @@ void IpcArena::reclaim_quarantined_locked() {
     for (auto it = bufs_.begin(); it != bufs_.end() && held > kQuarantineCapBytes;) {
         CommBuf *b = it->get();
         const bool vmm = std::all_of(b->share_ids.begin(), b->share_ids.end(), [](uint64_t id) { return id != 0; });
-        if (!b->quarantined || !vmm) {
+        if (!b->quarantined || !vmm || !unquiet_peers_remote(b->qseq)) {
             ++it;
             continue;
         }

@@ -146,6 +146,7 @@ private:
     // every other ring member is provably past op `seq`: its phase word shows a later op in that slot, or the op at
     // PH_GATHERED / PH_RELEASED / PH_ABORTED, or no vote for it yet (it then sees my PH_ABORTED and never launches);
     // a dead member's threads have all left its address space (pid_quiesced)
+    bool unquiet_peers_remote(uint64_t seq) const;
     bool op_quiet(uint64_t seq) const;
     struct Mapping {
         void *ptr = nullptr;

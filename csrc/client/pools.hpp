@@ -1,6 +1,7 @@
 // Reusable buffer pools (pinned host / device / plain host) so collectives never allocate on the hot path.
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
@@ -29,6 +30,29 @@ public:
     };
 
     Buf get(size_t n, int device = -1) {
+        Buf b = get_raw(n, device);
+        if (b.p) note_lease(b.cap);
+        return b;
+    }
+
+    // Bytes leased out right now, the most ever leased out at once (since the last reset_peak) and cached free bytes
+    // (pcclxPoolStats: what a peer's staging actually holds, e.g. pinned memory per device-ring op).
+    size_t in_use() const { return in_use_.load(std::memory_order_relaxed); }
+    size_t peak() const { return peak_.load(std::memory_order_relaxed); }
+    size_t cached() {
+        std::lock_guard l(mtx_);
+        return free_bytes_;
+    }
+    void reset_peak() { peak_.store(in_use_.load()); }
+
+private:
+    void note_lease(size_t cap) {
+        const size_t now = in_use_.fetch_add(cap) + cap;
+        size_t pk = peak_.load(std::memory_order_relaxed);
+        while (now > pk && !peak_.compare_exchange_weak(pk, now)) {
+        }
+    }
+    Buf get_raw(size_t n, int device) {
         {
             std::lock_guard l(mtx_);
             size_t best = SIZE_MAX;
@@ -57,12 +81,14 @@ public:
         return b;
     }
 
+public:
     // Returned buffers stay cached up to kMaxFree buffers and PCCL_POOL_MAX_FREE_MIB (default 32 GiB) per pool,
     // oldest released first. The cap must cover a whole op's working set: the device ring holds 9 staging buffers
     // per peer (8 threaded peers x 1 GiB: 6 GiB of pinned memory), and a pool that trims below that frees and
     // re-allocates pinned memory on every op (hipHostFree / hipHostMalloc of 128 MiB cost milliseconds each).
     void put(const Buf &b) {
         if (b.p == nullptr) return;
+        in_use_.fetch_sub(b.cap);
         static const size_t max_bytes = env_size("PCCL_POOL_MAX_FREE_MIB", 32u << 10) << 20;
         std::lock_guard l(mtx_);
         free_.push_back(b);
@@ -93,6 +119,7 @@ private:
         }
     }
     static constexpr size_t kMaxFree = 256;
+    std::atomic<size_t> in_use_{0}, peak_{0};
     Kind kind_;
     std::mutex mtx_;
     std::vector<Buf> free_;

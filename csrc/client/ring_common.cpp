@@ -32,6 +32,7 @@ Shape Shape::from_wire(const proto::WireShape &w) {
     s.stripes = std::max<size_t>(1, std::min<size_t>(16, w.stripes));
     s.quant_lanes = std::max<size_t>(1, std::min<size_t>(4, w.quant_lanes));
     s.stripe_min = std::max<size_t>(1, w.stripe_min_mib) << 20;
+    s.segment_chunk = static_cast<size_t>(w.segment_chunk_mib) << 20;
     return s;
 }
 
@@ -40,6 +41,7 @@ Shape Shape::reference_framing() {
     s.reference = true;
     s.stripes = 1;
     s.quant_lanes = 1;
+    s.segment_chunk = 0;
     return s;
 }
 
@@ -49,7 +51,21 @@ proto::WireShape local_wire_shape() {
     w.quant_lanes = static_cast<uint8_t>(std::max<size_t>(1, std::min<size_t>(4, env_size("PCCL_QUANT_LANES", 2))));
     const size_t min_bytes = std::max<size_t>(1 << 20, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20));
     w.stripe_min_mib = static_cast<uint16_t>(std::min<size_t>(65535, min_bytes >> 20));
+    w.segment_chunk_mib = static_cast<uint16_t>(std::min<size_t>(65535, env_size("PCCL_SEGMENT_CHUNK_MIB", 128)));
     return w;
+}
+
+std::vector<size_t> segment_bounds(size_t count, size_t es, size_t ws, const Shape &shape) {
+    constexpr size_t kAlign = 4096; // elements
+    size_t nseg = 1;
+    if (!shape.reference && shape.segment_chunk > 0 && count > 0) {
+        const size_t per_seg = std::max(kAlign * ws, shape.segment_chunk / std::max<size_t>(1, es) * ws);
+        nseg = (count + per_seg - 1) / per_seg;
+    }
+    std::vector<size_t> lo(nseg + 1, 0);
+    for (size_t k = 1; k < nseg; ++k) lo[k] = count / nseg * k / kAlign * kAlign;
+    lo[nseg] = count;
+    return lo;
 }
 
 // A quantized reduce-scatter step must receive and reduce its whole chunk before the next step's min / max, and so its
@@ -552,7 +568,7 @@ bool StepSlots::can_post(size_t g) const {
     const size_t b = g % kSlots, prev = g - kSlots;
     if (free_[b] && be_->event_query(free_[b]) == 0) return false;
     // an all-gather step's bytes are forwarded by the next step's sends (straight from the pinned slot)
-    if (!is_rs(prev) && prev + 1 < nsteps_ && !senders_.sent(prev + 1)) return false;
+    if (forwarded(prev) && !senders_.sent(prev + 1)) return false;
     return true;
 }
 

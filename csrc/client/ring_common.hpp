@@ -52,6 +52,7 @@ struct Shape {
     size_t stripes = 4;             // striped connections per step
     size_t stripe_min = 8u << 20;   // smallest stripe (bytes)
     size_t quant_lanes = 2;         // lanes of a quantized op
+    size_t segment_chunk = 128u << 20; // largest ring chunk of one segment, value bytes (0: the op is one segment)
     static Shape from_wire(const proto::WireShape &w);
     static Shape reference_framing();
 };
@@ -72,6 +73,14 @@ inline uint64_t lane_tag(uint64_t tag, size_t lane, size_t lanes) {
 // Lane split of a quantized all-reduce of `count` elements (wire element size `qs`) over `ws` peers: element offsets
 // lo[0] = 0 < lo[1] < ... < lo[nl] = count, from values every peer shares (count, ring size, wire type, agreed shape).
 std::vector<size_t> quant_lane_bounds(size_t count, size_t ws, size_t qs, const Shape &shape);
+
+// Segments: an op (or a quantized lane) of `count` elements of `es` value bytes is run as consecutive ring
+// all-reduces over contiguous element ranges, each small enough that one ring chunk holds at most
+// shape.segment_chunk bytes, so every per-step staging buffer (pinned TX / RX, HBM) is bounded by the segment instead
+// of growing with the tensor. The pipelined device rings run the segments as one pipeline (the next segment's first
+// payload is staged while the current one's last step still receives). Offsets lo[0] = 0 < ... < lo[S] = count,
+// multiples of 4096 elements, from values every peer shares; one segment in the reference framing.
+std::vector<size_t> segment_bounds(size_t count, size_t es, size_t ws, const Shape &shape);
 
 // Striping: a large ring-step payload is split into up to `stripes` contiguous stripes, each sent on its own pooled
 // TCP connection (one loopback / WAN TCP stream tops out well below the NIC / memory bandwidth). Stripe boundaries
@@ -315,12 +324,14 @@ private:
 // (g - kSlots) is finished with it: its GPU work completed (`free_after`) and, in the all-gather, the step after it
 // has forwarded its bytes. Three slots, because step g+1's sinks are posted while step g still receives and step
 // g+1's sends run while step g's do.
+// Steps are numbered across the op's segments (global step G = segment * 2(ws-1) + ring step).
 class StepSlots {
 public:
     static constexpr size_t kSlots = 3;
-    StepSlots(DeviceBackend *be, RingRx &rx, OpSenders &senders, size_t ws, uint8_t *const bufs[kSlots],
-              std::function<size_t(size_t)> rx_bytes)
-        : be_(be), rx_(rx), senders_(senders), ws_(ws), nsteps_(2 * (ws - 1)), rx_bytes_(std::move(rx_bytes)) {
+    StepSlots(DeviceBackend *be, RingRx &rx, OpSenders &senders, size_t ws, size_t nsteps,
+              uint8_t *const bufs[kSlots], std::function<size_t(size_t)> rx_bytes)
+        : be_(be), rx_(rx), senders_(senders), ws_(ws), nps_(2 * (ws - 1)), nsteps_(nsteps),
+          rx_bytes_(std::move(rx_bytes)) {
         for (size_t i = 0; i < kSlots; ++i) buf_[i] = bufs[i];
     }
     uint8_t *buf(size_t g) const { return buf_[g % kSlots]; }
@@ -335,11 +346,13 @@ public:
     void free_after(size_t g, DevEvent e) { free_[g % kSlots] = e; }
 
 private:
-    bool is_rs(size_t g) const { return g + 1 < ws_; }
+    bool is_rs(size_t g) const { return g % nps_ + 1 < ws_; }
+    // step g's received bytes are forwarded by step g+1 (an all-gather step that is not its segment's last)
+    bool forwarded(size_t g) const { return !is_rs(g) && g % nps_ + 1 < nps_; }
     DeviceBackend *be_;
     RingRx &rx_;
     OpSenders &senders_;
-    size_t ws_, nsteps_;
+    size_t ws_, nps_, nsteps_;
     std::function<size_t(size_t)> rx_bytes_;
     uint8_t *buf_[kSlots];
     ReadyRanges ready_[kSlots];

@@ -54,10 +54,11 @@ struct DevRing {
     std::atomic<uint64_t> &tx, &rx;
 };
 
-// The device ring as one pipeline over all 2(W-1) steps: step g+1's payload is produced (reduced into pinned
-// memory) and sent while step g still receives, and step g+1's sinks are posted as soon as their staging buffer is
-// free. Returns 0 ok, 1 io failure, 2 abort; on return no GPU work or socket write of the op touches any of its
-// buffers any more (the caller may restore the input).
+// The device ring as one pipeline over all 2(W-1) steps of every segment (ring_common.hpp segment_bounds): step G+1's
+// payload is produced (reduced into pinned memory, or - a segment's first step - staged from the input) and sent
+// while step G still receives, and step G+1's sinks are posted as soon as their staging buffer is free. Staging is
+// sized by the largest segment chunk, not by the tensor. Returns 0 ok, 1 io failure, 2 abort; on return no GPU work
+// or socket write of the op touches any of its buffers any more (the caller may restore the input).
 int device_ring_pipeline(DevRing &R) {
     DeviceBackend *be = R.be;
     const PcieQueues pq = R.pq;
@@ -73,12 +74,32 @@ int device_ring_pipeline(DevRing &R) {
         be->event_record(e, s);
         return e;
     };
-    const auto bounds = chunk_bounds(R.count, ws);
+    // segments (global step G = segment * nps + ring step) and their chunks, as absolute element ranges
+    const std::vector<size_t> seg = segment_bounds(R.count, es, ws, R.shape);
+    const size_t nseg = seg.size() - 1, nps = 2 * (ws - 1), nsteps = nseg * nps;
+    std::vector<std::vector<std::pair<size_t, size_t>>> sbounds(nseg);
     size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    for (size_t k = 0; k < nseg; ++k) {
+        sbounds[k] = chunk_bounds(seg[k + 1] - seg[k], ws);
+        for (auto &b : sbounds[k]) max_chunk = std::max(max_chunk, b.second - b.first);
+    }
+    auto lstep = [&](size_t G) { return G % nps; };
+    auto is_rs = [&](size_t G) { return lstep(G) + 1 < ws; };
+    auto tx_range = [&](size_t G) {
+        const auto c = sbounds[G / nps][chunk_tx(lstep(G), rank, ws)];
+        return std::pair<size_t, size_t>{seg[G / nps] + c.first, seg[G / nps] + c.second};
+    };
+    auto rx_range = [&](size_t G) {
+        const auto c = sbounds[G / nps][chunk_rx(lstep(G), rank, ws)];
+        return std::pair<size_t, size_t>{seg[G / nps] + c.first, seg[G / nps] + c.second};
+    };
+    auto rx_bytes = [&](size_t G) {
+        const auto [a, b] = rx_range(G);
+        return (b - a) * es;
+    };
     const size_t stage_bytes = max_chunk * es + 64;
-    // Staging rings of kNb buffers: step g receives into rxbuf[g % kNb] (HBM twin rxdev[g % kNb] for the reduce) and
-    // its reduce writes the next payload into txbuf[(g + 1) % kNb]: a buffer is refilled only after the step two back
+    // Staging rings of kNb buffers: step G receives into rxbuf[G % kNb] (HBM twin rxdev[G % kNb] for the reduce) and
+    // its reduce writes the next payload into txbuf[(G + 1) % kNb]: a buffer is refilled only after the step two back
     // finished with it (StepSlots).
     constexpr size_t kNb = StepSlots::kSlots;
     Lease txl[kNb], rxl[kNb], dvl[kNb];
@@ -109,73 +130,77 @@ int device_ring_pipeline(DevRing &R) {
 
     ReadyRanges txready[kNb];        // payload ranges of txbuf[i] (relative to txbuf[i] + txshift[i])
     size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
-
-    const size_t nsteps = 2 * (ws - 1);
-    auto is_rs = [&](size_t g) { return g + 1 < ws; };
-    auto region_of = [&](size_t g) { return R.dst + bounds[chunk_rx(g, rank, ws)].first * es; };
-    auto rx_bytes = [&](size_t g) {
-        const auto [c0, c1] = bounds[chunk_rx(g, rank, ws)];
-        return (c1 - c0) * es;
-    };
+    auto region_of = [&](size_t G) { return R.dst + rx_range(G).first * es; };
 
     size_t max_stripes = 1;
-    for (size_t g = 0; g < nsteps; ++g) {
-        const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
+    for (size_t G = 0; G < nsteps; ++G) {
+        const auto [ts, te] = tx_range(G);
         max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, R.txs.size(), R.shape).off.size());
     }
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
     OpSenders senders(R.txs, R.tag, seq, R.shape, piece, nsteps, max_stripes, be, R.tx);
     RingRx rx(R.rxs, R.tag, seq, R.shape, nsteps); // after the buffers its sinks point into
-    StepSlots slots(be, rx, senders, ws, rxbuf, rx_bytes);
-    auto publish = [&](size_t g) {
-        if (senders.published(g)) return;
-        const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
-        const bool staged = g < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
-        OpSenders::Step stp;
-        stp.payload = staged ? txbuf[g % kNb] + txshift[g % kNb] : slots.buf(g - 1);
-        stp.bytes = (te - ts) * es;
-        stp.ready = staged ? &txready[g % kNb] : &slots.ready(g - 1);
-        senders.publish(g, stp);
-    };
+    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, rx_bytes);
     auto fail = [&](int code) {
         senders.cancel();
         return code;
     };
+    // a segment's first payload: its own input chunk -> pinned, in pieces (from src: ready at call time, never
+    // written by the op). Its slot was last read by the sends of step G - kNb.
+    std::vector<bool> staged0(nsteps, false);
+    auto stage_first = [&](size_t G) -> bool {
+        if (staged0[G]) return true;
+        if (G >= kNb && !senders.wait(G - kNb)) return false;
+        const size_t b = G % kNb;
+        const auto [ts, te] = tx_range(G);
+        txready[b].clear();
+        txshift[b] = 0;
+        for (size_t off = 0; off < (te - ts) * es; off += piece) {
+            const size_t n = std::min(piece, (te - ts) * es - off);
+            be->memcpy_async(txbuf[b] + off, R.src + ts * es + off, n, pq.d2h);
+            last_d2h = record(pq.d2h);
+            txready[b].add(off, off + n, last_d2h);
+        }
+        staged0[G] = true;
+        return true;
+    };
+    auto publish = [&](size_t G) {
+        if (senders.published(G)) return true;
+        if (lstep(G) == 0 && !stage_first(G)) return false;
+        const auto [ts, te] = tx_range(G);
+        const bool staged = lstep(G) < ws; // reduce-scatter steps and all-gather step 0 send txbuf payloads
+        OpSenders::Step stp;
+        stp.payload = staged ? txbuf[G % kNb] + txshift[G % kNb] : slots.buf(G - 1);
+        stp.bytes = (te - ts) * es;
+        stp.ready = staged ? &txready[G % kNb] : &slots.ready(G - 1);
+        senders.publish(G, stp);
+        return true;
+    };
 
-    for (size_t g = 0; g < nsteps; ++g) {
-        const size_t b = g % kNb, nb = (g + 1) % kNb;
-        const bool rs = is_rs(g);
-        // 1. step g's sinks (normally posted during step g-1)
-        if (!slots.ensure_posted(g, [&] { return senders.failed(); })) return fail(1);
-        // 2. this step's reduce writes txbuf[nb], last read by step g-2's sends
-        uint8_t *region = region_of(g);
+    for (size_t G = 0; G < nsteps; ++G) {
+        const size_t g = lstep(G), b = G % kNb, nb = (G + 1) % kNb;
+        const bool rs = is_rs(G);
+        // 1. step G's sinks (normally posted during step G-1)
+        if (!slots.ensure_posted(G, [&] { return senders.failed(); })) return fail(1);
+        // 2. this step's reduce writes txbuf[nb], last read by step G-2's sends
+        uint8_t *region = region_of(G);
         const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;
         if (rs) {
-            if (g >= 2 && !senders.wait(g - 2)) return fail(1);
+            if (G >= 2 && !senders.wait(G - 2)) return fail(1);
             txready[nb].clear();
             txshift[nb] = shift;
         }
-        // 3. own input chunk -> pinned, in pieces (from src: ready at call time)
-        if (g == 0) {
-            const auto [ts, te] = bounds[chunk_tx(0, rank, ws)];
-            txready[0].clear();
-            txshift[0] = 0;
-            for (size_t off = 0; off < (te - ts) * es; off += piece) {
-                const size_t n = std::min(piece, (te - ts) * es - off);
-                be->memcpy_async(txbuf[0] + off, R.src + ts * es + off, n, pq.d2h);
-                last_d2h = record(pq.d2h);
-                txready[0].add(off, off + n, last_d2h);
-            }
-        }
-        publish(g);
-        if (g + 1 < nsteps) publish(g + 1); // its payload fills while this step runs
+        // 3. this step's and (send-ahead) the next step's payloads may leave as they become ready; a segment's first
+        //    payload is staged from the input here
+        if (!publish(G)) return fail(1);
+        if (G + 1 < nsteps && !publish(G + 1)) return fail(1); // its payload fills while this step runs
         fault_point("ring", seq, g, "publish");
-        // 4. receive + consume step g
+        // 4. receive + consume step G
         DevEvent step_last = nullptr;
         std::function<void(size_t, size_t)> consume;
         if (rs) {
             // HBM staging and the next payload share the 16-byte phase of `region`: the fused kernel stays vectorised
-            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift, *sink = slots.buf(g);
+            uint8_t *stage = rxdev[b] + shift, *out = txbuf[nb] + shift, *sink = slots.buf(G);
             consume = [&, stage, out, sink, region, nb](size_t a, size_t e) {
                 be->memcpy_async(stage + a, sink + a, e - a, pq.h2d);
                 DevEvent ce = record(pq.h2d);
@@ -185,8 +210,8 @@ int device_ring_pipeline(DevRing &R) {
                 txready[nb].add(a, e, step_last);
             };
         } else {
-            uint8_t *sink = slots.buf(g);
-            ReadyRanges *fwd = &slots.ready(g);
+            uint8_t *sink = slots.buf(G);
+            ReadyRanges *fwd = &slots.ready(G);
             consume = [&, sink, region, fwd](size_t a, size_t e) {
                 be->memcpy_async(region + a, sink + a, e - a, st);
                 step_last = record(st);
@@ -195,7 +220,7 @@ int device_ring_pipeline(DevRing &R) {
         }
         bool first = true;
         const int rc = rx.receive(
-            g, es, piece,
+            G, es, piece,
             [&](size_t a, size_t e) {
                 consume(a, e);
                 if (first) {
@@ -204,13 +229,13 @@ int device_ring_pipeline(DevRing &R) {
                 }
             },
             [&] { // post the next step's sinks as soon as its buffer is free (its sender may already be streaming)
-                if (slots.try_post(g + 1)) fault_point("ring", seq, g, "ahead");
+                if (slots.try_post(G + 1)) fault_point("ring", seq, g, "ahead");
             },
             [&] { return senders.failed(); }, R.aborted);
-        slots.free_after(g, step_last);
+        slots.free_after(G, step_last);
         if (rc) return fail(rc);
-        R.rx += rx_bytes(g);
-        rx.unpost(g);
+        R.rx += rx_bytes(G);
+        rx.unpost(G);
         step_mark(rs, rs ? g : g - (ws - 1));
         if (g + 2 == ws) trace_mark("reduce_scatter");
         fault_point("ring", seq, g, "end");

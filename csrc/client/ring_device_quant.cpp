@@ -98,9 +98,26 @@ int device_quant_lane(QLane &L) {
         be->event_record(e, s);
         return e;
     };
-    const auto bounds = chunk_bounds(L.count, ws);
+    // the lane's segments (global step G = segment * nps + ring step); staging is sized by the largest segment chunk
+    const std::vector<size_t> seg = segment_bounds(L.count, es, ws, shape);
+    const size_t nseg = seg.size() - 1, nps = 2 * (ws - 1);
+    std::vector<std::vector<std::pair<size_t, size_t>>> sbounds(nseg);
     size_t max_chunk = 0;
-    for (auto &b : bounds) max_chunk = std::max(max_chunk, b.second - b.first);
+    for (size_t k = 0; k < nseg; ++k) {
+        sbounds[k] = chunk_bounds(seg[k + 1] - seg[k], ws);
+        for (auto &b : sbounds[k]) max_chunk = std::max(max_chunk, b.second - b.first);
+    }
+    // element range (lane-relative) a global step sends / receives
+    auto tx_range = [&](size_t G) {
+        const auto c = sbounds[G / nps][chunk_tx(G % nps, rank, ws)];
+        return std::pair<size_t, size_t>{seg[G / nps] + c.first, seg[G / nps] + c.second};
+    };
+    auto rx_range = [&](size_t G) {
+        const auto c = sbounds[G / nps][chunk_rx(G % nps, rank, ws)];
+        return std::pair<size_t, size_t>{seg[G / nps] + c.first, seg[G / nps] + c.second};
+    };
+    auto ntx = [&](size_t G) { return tx_range(G).second - tx_range(G).first; };
+    auto nrx = [&](size_t G) { return rx_range(G).second - rx_range(G).first; };
     const size_t qbytes = max_chunk * qs + 64;
     constexpr size_t kNb = StepSlots::kSlots;
     // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
@@ -139,16 +156,15 @@ int device_quant_lane(QLane &L) {
     } drain{be, st, &owned};
 
     ReadyRanges txready[2];
-    const size_t nsteps = 2 * (ws - 1);
-    auto is_rs = [&](size_t g) { return g + 1 < ws; };
-    auto nel = [&](size_t c) { return bounds[c].second - bounds[c].first; };
+    const size_t nsteps = nseg * nps;
+    auto is_rs = [&](size_t G) { return G % nps + 1 < ws; };
 
     size_t max_stripes = 1;
-    for (size_t g = 0; g < nsteps; ++g)
-        max_stripes = std::max(max_stripes, plan_stripes(nel(chunk_tx(g, rank, ws)) * qs, L.txs->size(), shape).off.size());
+    for (size_t G = 0; G < nsteps; ++G)
+        max_stripes = std::max(max_stripes, plan_stripes(ntx(G) * qs, L.txs->size(), shape).off.size());
     OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, max_stripes, be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, shape, nsteps);
-    StepSlots slots(be, rx, senders, ws, rxbuf, [&](size_t g) { return nel(chunk_rx(g, rank, ws)) * qs; });
+    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);
 
     auto fail = [&](int code) {
@@ -192,7 +208,7 @@ int device_quant_lane(QLane &L) {
     auto publish = [&](size_t g, const uint8_t *payload, ReadyRanges *ready) {
         OpSenders::Step stp;
         stp.payload = payload;
-        stp.bytes = nel(chunk_tx(g, rank, ws)) * qs;
+        stp.bytes = ntx(g) * qs;
         stp.ready = ready;
         senders.publish(g, stp);
     };
@@ -215,15 +231,17 @@ int device_quant_lane(QLane &L) {
     const bool lane_copies = max_chunk * qs >= (size_t{4} << 20);
     const PcieQueues pq = lane_copies ? PcieQueues{} : shared_pcie_queues(be, L.device);
     if (!lane_copies && !pq.h2d) return fail(1);
-    for (size_t g = 0; g < nsteps; ++g) {
-        const size_t b = g % kNb;
-        const bool rs = is_rs(g);
-        if (!slots.ensure_posted(g, failed)) return fail(1);
+    for (size_t G = 0; G < nsteps; ++G) {
+        const size_t g = G % nps, b = G % kNb;
+        const bool rs = is_rs(G);
+        if (!slots.ensure_posted(G, failed)) return fail(1);
         if (g < ws) { // own payload: reduce-scatter steps and the all-gather's first step
-            const size_t slot = g % 2, c = chunk_tx(g, rank, ws);
-            uint8_t *src = L.dst + bounds[c].first * es;
-            const size_t n = nel(c);
-            if (g >= 2 && !senders.wait(g - 2)) return fail(1); // txq[slot] was step g-2's payload
+            const size_t slot = G % 2;
+            const auto [c0, c1] = tx_range(G);
+            uint8_t *src = L.dst + c0 * es;
+            const size_t n = c1 - c0;
+            if (G >= 2 && !senders.wait(G - 2)) return fail(1); // txq[slot] was step G-2's payload
+            // min / max folded from the previous step's partials, except for a segment's first payload
             const QuantMeta mine = make_step_meta(src, n, g > 0);
             const auto params = kernels::make_params(mine, L.qtype);
             txready[slot].clear();
@@ -235,26 +253,26 @@ int device_quant_lane(QLane &L) {
                     be->quantize(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
                 DevEvent e = record(st);
                 txready[slot].add(off * qs, (off + k) * qs, e);
-                if (g == 0) first_payload = e;
+                if (G == 0) first_payload = e;
             }
             if (int m = send_meta(io, mine, *L.tx)) return fail(m);
-            publish(g, txq[slot], &txready[slot]);
-            step_sub_mark('q', g);
-        } // else: forwarded chunk, published with its metadata when step g-1's metadata arrived
+            publish(G, txq[slot], &txready[slot]);
+            step_sub_mark('q', G);
+        } // else: forwarded chunk, published with its metadata when step G-1's metadata arrived
         fault_point("qring", seq, g, "meta");
         if (int m = recv_meta(io, theirs, *L.rx, L.aborted, failed)) return fail(m);
         const auto params = kernels::make_params(theirs, L.qtype);
-        if (!rs && g + 1 < nsteps) { // cut-through all-gather: the next step forwards this chunk as it lands
+        if (!rs && g + 1 < nps) { // cut-through all-gather: the next step forwards this chunk as it lands
             if (int m = send_meta(io, theirs, *L.tx)) return fail(m);
-            publish(g + 1, slots.buf(g), &slots.ready(g));
+            publish(G + 1, slots.buf(G), &slots.ready(G));
         }
-        uint8_t *region = L.dst + bounds[chunk_rx(g, rank, ws)].first * es;
-        uint8_t *sink = slots.buf(g);
-        ReadyRanges *fwd = &slots.ready(g);
+        uint8_t *region = L.dst + rx_range(G).first * es;
+        uint8_t *sink = slots.buf(G);
+        ReadyRanges *fwd = &slots.ready(G);
         DevEvent step_last = nullptr;
         bool first = true;
         const int rc = rx.receive(
-            g, qs, piece_el * qs,
+            G, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
                 if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading pinned
@@ -279,19 +297,19 @@ int device_quant_lane(QLane &L) {
                 step_last = record(st);
                 if (first) {
                     first = false;
-                    step_sub_mark('f', g);
+                    step_sub_mark('f', G);
                     fault_point("qring", seq, g, "rx");
                 }
             },
             [&] {
                 maybe_open_gate();
-                slots.try_post(g + 1);
+                slots.try_post(G + 1);
             },
             failed, L.aborted);
-        slots.free_after(g, step_last);
+        slots.free_after(G, step_last);
         if (rc) return fail(rc);
-        *L.rx += nel(chunk_rx(g, rank, ws)) * qs;
-        rx.unpost(g);
+        *L.rx += nrx(G) * qs;
+        rx.unpost(G);
         step_mark(rs, rs ? g : g - (ws - 1));
         fault_point("qring", seq, g, "end");
     }

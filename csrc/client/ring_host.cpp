@@ -143,9 +143,15 @@ int host_allreduce(const Conns &txs, const Conns &rxs, size_t ws, size_t rank, u
     const std::vector<size_t> lo = quant ? quant_lane_bounds(count, ws, dtype_size(qtype), shape)
                                          : std::vector<size_t>{0, count};
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
-        HostRingArgs A{txs, rxs, ws, rank, lane_tag(tag, k, lo.size() - 1), seq, shape, dst + a * es, b - a,
-                       dtype, qtype, qalgo, op, quant, aborted, tx, rx};
-        return host_ring(A);
+        // the lane's segments one after the other (the device rings pipeline them; the wire is the same)
+        const std::vector<size_t> seg = segment_bounds(b - a, es, ws, shape);
+        for (size_t s = 0; s + 1 < seg.size(); ++s) {
+            HostRingArgs A{txs, rxs, ws, rank, lane_tag(tag, k, lo.size() - 1), seq, shape,
+                           dst + (a + seg[s]) * es, seg[s + 1] - seg[s], dtype, qtype, qalgo, op, quant, aborted, tx,
+                           rx};
+            if (const int r = host_ring(A)) return r;
+        }
+        return 0;
     });
     if (rc == 0 && op == ReduceOp::Avg) kernels::host_finalize_avg(dst, count, dtype, ws);
     return rc;

@@ -936,6 +936,8 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
     pkt.shape.stripes = 16;
     pkt.shape.quant_lanes = 4;
     pkt.shape.stripe_min_mib = 1;
+    pkt.shape.segment_chunk_mib = 0;
+    bool seg_any = false;
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         auto f = c.coll_flags.find(tag);
@@ -945,6 +947,12 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
         pkt.shape.stripes = std::min(pkt.shape.stripes, sh->second.stripes);
         pkt.shape.quant_lanes = std::min(pkt.shape.quant_lanes, sh->second.quant_lanes);
         pkt.shape.stripe_min_mib = std::max(pkt.shape.stripe_min_mib, sh->second.stripe_min_mib);
+        // smallest non-zero segment (0 = unsegmented only if every proposal says so)
+        const uint16_t sg = sh->second.segment_chunk_mib;
+        if (sg != 0 && (!seg_any || sg < pkt.shape.segment_chunk_mib)) {
+            pkt.shape.segment_chunk_mib = sg;
+            seg_any = true;
+        }
     }
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;

@@ -309,6 +309,23 @@ PCCL_EXPORT pcclResult_t pcclGetBuildInfoEx(pcclBuildInfoEx_t *info);
  *  fp16/bf16/int16. */
 PCCL_EXPORT size_t pcclDataTypeSize(pcclDataType_t datatype);
 
+/** [pccl-amd extension] Stream-ordered all-reduce of HIP device buffers. The op reads its input after the work
+ *  queued on `hip_stream` (a hipStream_t, NULL = the null stream) before this call - an event recorded on it, waited
+ *  for by the op itself, so the caller's thread never synchronises the stream - and runs on a collective worker;
+ *  await it with pcclAwaitAsyncReduce, which returns once the op's last device write has completed (the result is
+ *  then visible to every stream). Host buffers: `hip_stream` is ignored (same as pcclAllReduceAsync). */
+PCCL_EXPORT pcclResult_t pcclxAllReduceAsyncOnStream(const void *sendbuff, void *recvbuff,
+                                                     const pcclReduceDescriptor_t *descriptor,
+                                                     const pcclComm_t *communicator, void *hip_stream,
+                                                     pcclAsyncReduceOp_t *reduce_handle_out);
+
+/** [pccl-amd extension] Blocking form of pcclxAllReduceAsyncOnStream: the op runs on the calling thread, which
+ *  waits only for the input's producers on `hip_stream` (not for the whole stream) after the master's commence. */
+PCCL_EXPORT pcclResult_t pcclxAllReduceOnStream(const void *sendbuff, void *recvbuff,
+                                                const pcclReduceDescriptor_t *descriptor,
+                                                const pcclComm_t *communicator, void *hip_stream,
+                                                pcclReduceInfo_t *reduce_info_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -129,6 +129,10 @@ def _load() -> ctypes.CDLL:
         "pcclOptimizeTopology": ([c_void_p], c_int),
         "pcclAllReduce": ([c_void_p, c_void_p, p(ReduceDescriptorC), c_void_p, p(ReduceInfoC)], c_int),
         "pcclAllReduceAsync": ([c_void_p, c_void_p, p(ReduceDescriptorC), c_void_p, p(AsyncReduceOpC)], c_int),
+        "pcclxAllReduceOnStream": ([c_void_p, c_void_p, p(ReduceDescriptorC), c_void_p, c_void_p, p(ReduceInfoC)],
+                                   c_int),
+        "pcclxAllReduceAsyncOnStream": ([c_void_p, c_void_p, p(ReduceDescriptorC), c_void_p, c_void_p,
+                                        p(AsyncReduceOpC)], c_int),
         "pcclAllReduceMultipleWithRetry": ([p(ReduceOpDescriptorC), c_size_t, c_void_p, p(ReduceInfoC), c_int], c_int),
         "pcclAwaitAsyncReduce": ([p(AsyncReduceOpC), p(ReduceInfoC)], c_int),
         "pcclSynchronizeSharedState": ([c_void_p, p(SharedStateC), c_int, p(SharedStateSyncInfoC)], c_int),
@@ -165,6 +169,7 @@ def _load() -> ctypes.CDLL:
         "pcclxShareableLiveBytes": ([], c_size_t),
         "pcclxIpcStats": ([p(c_uint64)], None),
         "pcclxIpcStatsEx": ([p(c_uint64), c_size_t], c_size_t),
+        "pcclxPoolStats": ([p(c_uint64), c_size_t, c_int], c_size_t),
         "pcclxMasterBandwidthTable": ([c_void_p, c_char_p, c_size_t], c_size_t),
         "pcclxMasterTopologyStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),
     }

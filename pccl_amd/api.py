@@ -251,6 +251,14 @@ def _sync_device(t) -> None:
         torch.cuda.current_stream(t.device).synchronize()
 
 
+def _hip_stream(t, stream):
+    """The hipStream_t (int) a stream-ordered op of GPU tensor ``t`` waits on: ``stream`` (a torch.cuda.Stream) or the
+    device's current stream; None for host tensors / non-torch buffers (they take the plain entry points)."""
+    if isinstance(torch, _ModuleDummy) or not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        return None
+    return (stream if stream is not None else torch.cuda.current_stream(t.device)).cuda_stream
+
+
 def _check_pair_torch(send, recv):
     assert send.is_contiguous(), "Input tensor must be contiguous"
     assert recv.is_contiguous(), "Output tensor must be contiguous"
@@ -534,20 +542,37 @@ class Communicator:
 
     def all_reduce(self, send, recv, *, op: ReduceOp, tag: int = 0,
                    operand_descriptor: Optional[ReduceOperandDescriptor] = None,
-                   quantization_options: Optional[QuantizationOptions] = None) -> ReduceInfo:
-        sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options)
+                   quantization_options: Optional[QuantizationOptions] = None, stream=None) -> ReduceInfo:
+        """Blocking all-reduce. GPU tensors are stream-ordered: the op reads ``send`` after the work queued on
+        ``stream`` (default: the current stream) before this call, without the caller synchronising that stream; the
+        result is complete on return."""
+        hs = _hip_stream(send, stream)
+        sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options,
+                                            sync=hs is None)
         info = _native.ReduceInfoC()
-        PCCLError.check(C.pcclAllReduce(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(info)),
-                        "pcclAllReduce")
+        if hs is None:
+            PCCLError.check(C.pcclAllReduce(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(info)),
+                            "pcclAllReduce")
+        else:
+            PCCLError.check(C.pcclxAllReduceOnStream(sptr, rptr, ctypes.byref(desc), self._comm, hs,
+                                                     ctypes.byref(info)), "pcclxAllReduceOnStream")
         return ReduceInfo(info.local_world_size, info.tx_bytes, info.rx_bytes)
 
     def all_reduce_async(self, send, recv, *, op: ReduceOp, tag: int = 0,
                          operand_descriptor: Optional[ReduceOperandDescriptor] = None,
-                         quantization_options: Optional[QuantizationOptions] = None) -> AsyncReduceHandle:
-        sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options)
+                         quantization_options: Optional[QuantizationOptions] = None, stream=None) -> AsyncReduceHandle:
+        """Asynchronous all-reduce; ``handle.wait()`` awaits it. GPU tensors are stream-ordered (see all_reduce): this
+        call returns at once, even while ``send``'s producers are still queued on ``stream``."""
+        hs = _hip_stream(send, stream)
+        sptr, rptr, desc = self._descriptor(send, recv, op, tag, operand_descriptor, quantization_options,
+                                            sync=hs is None)
         handle = _native.AsyncReduceOpC()
-        PCCLError.check(C.pcclAllReduceAsync(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(handle)),
-                        "pcclAllReduceAsync")
+        if hs is None:
+            PCCLError.check(C.pcclAllReduceAsync(sptr, rptr, ctypes.byref(desc), self._comm, ctypes.byref(handle)),
+                            "pcclAllReduceAsync")
+        else:
+            PCCLError.check(C.pcclxAllReduceAsyncOnStream(sptr, rptr, ctypes.byref(desc), self._comm, hs,
+                                                          ctypes.byref(handle)), "pcclxAllReduceAsyncOnStream")
         return AsyncReduceHandle(handle, keepalive=(send, recv))
 
     def _all_reduce_async_ready(self, send, recv, *, op: ReduceOp, tag: int,

@@ -155,6 +155,17 @@ def ipc_buffer_stats() -> dict:
     return {k: int(out[i]) for i, k in enumerate(keys[:n])}
 
 
+def staging_pool_stats(reset_peak: bool = False) -> dict:
+    """Bytes of the library's staging pools in this process: per pool (``pinned`` host, ``device`` HBM, plain
+    ``host``) the bytes leased out now (``in_use``), the most leased out at once (``peak``, since the last
+    ``reset_peak=True`` call) and the free bytes kept cached for reuse (``cached``). The device rings size their staging
+    by the op's segment chunk (PCCL_SEGMENT_CHUNK_MIB), not by the tensor."""
+    out = (ctypes.c_uint64 * 9)()
+    _native.C.pcclxPoolStats(out, 9, 1 if reset_peak else 0)
+    return {pool: {"in_use": int(out[3 * k]), "peak": int(out[3 * k + 1]), "cached": int(out[3 * k + 2])}
+            for k, pool in enumerate(("pinned", "device", "host"))}
+
+
 def maybe_shareable(device) -> contextlib.AbstractContextManager:
     """``shareable_memory(device)`` for HIP devices when available, a no-op context otherwise (CPU tensors, no GPU,
     or PCCL_SHAREABLE_BUFFERS=0)."""

@@ -8,8 +8,9 @@ otherwise) with no gather/scatter copies. Large buckets (default 1 GiB) suit 288
 overhead negligible; they are reduced concurrently (one tag each) with retry on peer churn.
 
 ``overlap=True`` starts each bucket's all-reduce during the backward pass, as soon as every gradient in it has been
-accumulated (post-accumulate-grad hooks; a comm thread waits on a HIP event recorded on the producing stream, so the
-autograd thread never blocks). Gradients arrive roughly in reverse parameter order, so buckets are cut from the end
+accumulated (post-accumulate-grad hooks). The launch is stream-ordered (pcclxAllReduceAsyncOnStream): the op waits
+for an event recorded on the stream that queued the gradient kernels, so no thread synchronises that stream and the
+autograd thread returns at once. Gradients arrive roughly in reverse parameter order, so buckets are cut from the end
 of the flat buffer; with buckets smaller than the model, the reduction of late layers runs while the early layers are
 still back-propagating. ``sync_gradients`` launches buckets whose hooks did not all fire (unused parameters), waits
 for every op and re-reduces failed buckets through the retry path (the library restores an aborted in-place buffer,
@@ -18,7 +19,6 @@ and the master's per-tag abort decision is the same on every peer, so all peers 
 from __future__ import annotations
 
 import contextlib
-import queue
 import threading
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
@@ -76,9 +76,6 @@ class GradBuckets:
             per = max(1, bucket_bytes // buf.element_size())
             out.extend(buf[i:i + per] for i in range(0, buf.numel(), per))
         return out
-
-
-_FLUSH = -1  # comm-thread queue marker: everything queued before it has been launched
 
 
 class DataParallel:
@@ -158,10 +155,7 @@ class DataParallel:
         self._launched = [False] * len(self._bucket_views)
         self._handles: List[Optional[object]] = [None] * len(self._bucket_views)
         self._errors: List[BaseException] = []
-        self._q: "queue.Queue" = queue.Queue()
         self._lock = threading.Lock()
-        self._thread = threading.Thread(target=self._comm_loop, name="pccl-ddp-comm", daemon=True)
-        self._thread.start()
         for p in self._bucket_of:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
@@ -182,36 +176,23 @@ class DataParallel:
                     self._launched[i] = True
                     ready.append(i)
         for i in ready:
-            ev = None
-            if self._bucket_views[i].is_cuda:  # the gradient kernels are queued, not done: hand over an event
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(self._bucket_views[i].device))
-            self._q.put((i, ev, None))
+            self._start(i)
 
-    def _launch(self, i: int):
+    def _start(self, i: int) -> None:
+        """Launches bucket i's all-reduce from the hook: stream-ordered on the stream the gradient kernels were queued
+        on (pcclxAllReduceAsyncOnStream), so neither the autograd thread nor any other thread synchronises it - the op
+        waits for those kernels itself."""
         t = self._bucket_views[i]
         dt = DataType.from_torch_dtype(t.dtype)
         q = self.quantization or QuantizationOptions(dt, QuantizationAlgorithm.NONE)
-        return self.comm._all_reduce_async_ready(t, t, op=self.op, tag=self.tag_base + i,
-                                                 operand_descriptor=ReduceOperandDescriptor(dt, DistributionHint.NONE),
-                                                 quantization_options=q)
-
-    def _comm_loop(self) -> None:
-        while True:
-            item = self._q.get()
-            if item is None:
-                return
-            i, ev, done = item
-            if i == _FLUSH:
-                done.set()
-                continue
-            try:
-                if ev is not None:
-                    ev.synchronize()
-                self._handles[i] = self._launch(i)
-            except BaseException as e:  # surfaced by sync_gradients
-                self._errors.append(e)
-                self._handles[i] = None
+        try:
+            self._handles[i] = self.comm.all_reduce_async(
+                t, t, op=self.op, tag=self.tag_base + i,
+                operand_descriptor=ReduceOperandDescriptor(dt, DistributionHint.NONE), quantization_options=q,
+                stream=torch.cuda.current_stream(t.device) if t.is_cuda else None)
+        except BaseException as e:  # surfaced by sync_gradients
+            self._errors.append(e)
+            self._handles[i] = None
 
     def _finish_overlapped(self) -> RetryResult:
         # buckets whose hooks did not all fire (unused parameters, or no_sync ended mid-step) start now; unused
@@ -221,14 +202,8 @@ class DataParallel:
             rest = [i for i, l in enumerate(self._launched) if not l]
             for i in rest:
                 self._launched[i] = True
-        if rest and self._bucket_views[0].is_cuda:
-            torch.cuda.current_stream(self._bucket_views[0].device).synchronize()
         for i in rest:
-            self._q.put((i, None, None))
-        # wait until the comm thread has launched everything queued so far
-        flushed = threading.Event()
-        self._q.put((_FLUSH, None, flushed))
-        flushed.wait()
+            self._start(i)
         tx = rx = 0
         failed = []
         for i, h in enumerate(self._handles):
@@ -262,6 +237,3 @@ class DataParallel:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        if self.overlap and self._thread.is_alive():
-            self._q.put(None)
-            self._thread.join(timeout=10)

@@ -6,6 +6,7 @@ process and between two processes (real hipIpc export/open).
 import json
 import os
 import subprocess
+import time
 
 import pytest
 import torch
@@ -503,3 +504,99 @@ def test_device_ring_fewer_elements_than_peers(hip, n, quant, monkeypatch):
             assert torch.equal(y[:n], expect)
         else:
             assert (y[:n].float() - expect.float()).abs().max() <= 0.5
+
+
+@pytest.mark.parametrize("disable_ipc", [False, True])
+@pytest.mark.parametrize("blocking", [False, True])
+def test_stream_ordered_all_reduce_with_queued_producer(hip, disable_ipc, blocking, monkeypatch):
+    """pcclxAllReduce[Async]OnStream: the input's producer is still queued (a ~150 ms spin kernel, then the fill)
+    when all_reduce(_async) is called on its stream; the async call returns at once (no host synchronisation of the
+    stream), the op waits for the producer itself, and the result is exact."""
+    if disable_ipc:
+        monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    n = (1 << 20) + 3
+    cycles = int(3e8)  # ~150 ms at MI355X clocks
+
+    def fn(rank, comm):
+        s = torch.cuda.Stream(hip)
+        x = torch.zeros(n, device=hip, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        outs = []
+        for it in range(3):
+            with torch.cuda.stream(s):
+                torch.cuda._sleep(cycles)
+                x.fill_(float(rank + 1 + it))
+            t0 = time.perf_counter()
+            if blocking:
+                comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=it, stream=s)
+                call = time.perf_counter() - t0
+            else:
+                h = comm.all_reduce_async(x, y, op=pccl.ReduceOp.SUM, tag=it, stream=s)
+                call = time.perf_counter() - t0
+                ok, _, _ = h.wait()
+                assert ok
+            outs.append((call, time.perf_counter() - t0, float(y.float().min()), float(y.float().max())))
+        return outs, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    res = _run(2, fn)
+    for outs, path in res:
+        assert path == (pccl.ReducePath.DEVICE_RING if disable_ipc else pccl.ReducePath.DEVICE_IPC).value
+        for it, (call, total, lo, hi) in enumerate(outs):
+            assert lo == hi == 3 + 2 * it, outs  # (1 + it) + (2 + it)
+            assert total > 0.05, outs  # the op did wait for the queued producer
+            if not blocking:
+                assert call < 0.05, outs  # ... without the caller waiting for it
+
+
+def test_ddp_overlap_launches_without_stream_sync(hip):
+    """DataParallel(overlap=True) starts bucket all-reduces from the backward hooks as stream-ordered ops (no thread
+    synchronises the backward stream) and the averaged gradients are exact."""
+    import copy
+
+    from pccl_amd.parallel import DataParallel
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(*[torch.nn.Linear(256, 256) for _ in range(6)])
+
+    def fn(rank, comm):
+        model = copy.deepcopy(base).to(hip)
+        dp = DataParallel(model, comm, bucket_bytes=256 * 1024, overlap=True)
+        x = torch.full((32, 256), float(rank + 1), device=hip)
+        model(x).sum().backward()
+        res = dp.sync_gradients()
+        torch.cuda.synchronize()
+        grads = [p.grad.detach().clone() for p in model.parameters()]
+        dp.close()
+        return res.ok, grads
+
+    outs = _run(2, fn)
+    # reference: the mean of both peers' gradients, computed locally
+    ref = []
+    for r in range(2):
+        model = copy.deepcopy(base).to(hip)
+        model(torch.full((32, 256), float(r + 1), device=hip)).sum().backward()
+        ref.append([p.grad.detach().clone() for p in model.parameters()])
+    for ok, grads in outs:
+        assert ok
+        for g, a, b in zip(grads, ref[0], ref[1]):
+            torch.testing.assert_close(g, (a + b) / 2, rtol=1e-5, atol=1e-5)
+
+
+def test_device_ring_staging_bounded_by_segment(hip):
+    """2 peer processes x 8 GiB bf16, in place, TCP device ring: the op runs as 64 pipelined segments of 128 MiB ring
+    chunks (PCCL_SEGMENT_CHUNK_MIB), so each peer's pinned staging peaks at 6 x 128 MiB, not 6 x 4 GiB; exact sums."""
+    worker = os.path.join(HERE, "workers", "allreduce_peer.py")
+    n = 4 << 30  # bf16 elements: 8 GiB per peer
+    with local_master() as addr:
+        ps = [spawn_python([worker, addr, "2", str(r), "--device", "cuda:0", "--dtype", "bf16", "--n", str(n),
+                            "--const", "--inplace", "--steps", "2", "--pool", "4"],
+                           env={"PCCL_DISABLE_IPC": "1"}, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for r in range(2)]
+        outs = communicate_all(ps, 280, DIAG_SIGNALS)
+    for p, (o, e) in zip(ps, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = [json.loads(ln) for ln in o.splitlines() if ln.startswith("{")]
+        assert len(lines) == 2 and not any(ln.get("bad") for ln in lines), lines
+        assert all(ln["path"] == pccl.ReducePath.DEVICE_RING.value for ln in lines), lines
+        pinned_peak = max(ln["staging"]["pinned"]["peak"] for ln in lines)
+        assert pinned_peak <= (1 << 30), lines[-1]["staging"]

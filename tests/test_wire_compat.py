@@ -61,12 +61,14 @@ def test_uniform_rings_pick_their_framing(envs, framing):
 
 @pytest.mark.parametrize("quant", ["none", "u8"])
 def test_peers_with_different_shape_settings_agree(quant):
-    """Peers whose PCCL_RING_STRIPES / PCCL_STRIPE_MIN_BYTES / PCCL_QUANT_LANES differ used to post their sinks on
-    different connections and lane tags and hang; the master's agreed shape makes them derive one plan. 48 Mi f32
-    elements: 64 MiB chunks, so stripes and (quantized) two lanes are in play."""
-    envs = [{"PCCL_RING_STRIPES": "8", "PCCL_STRIPE_MIN_BYTES": str(1 << 20), "PCCL_QUANT_LANES": "4"},
-            {"PCCL_RING_STRIPES": "2", "PCCL_STRIPE_MIN_BYTES": str(4 << 20), "PCCL_QUANT_LANES": "1"},
-            {"PCCL_RING_STRIPES": "4", "PCCL_QUANT_LANES": "2"}]
+    """Peers whose PCCL_RING_STRIPES / PCCL_STRIPE_MIN_BYTES / PCCL_QUANT_LANES / PCCL_SEGMENT_CHUNK_MIB differ used
+    to post their sinks on different connections and lane tags and hang; the master's agreed shape makes them derive
+    one plan. 48 Mi f32 elements: 64 MiB chunks, so stripes, (quantized) two lanes and 16 MiB segments are in play."""
+    envs = [{"PCCL_RING_STRIPES": "8", "PCCL_STRIPE_MIN_BYTES": str(1 << 20), "PCCL_QUANT_LANES": "4",
+             "PCCL_SEGMENT_CHUNK_MIB": "16"},
+            {"PCCL_RING_STRIPES": "2", "PCCL_STRIPE_MIN_BYTES": str(4 << 20), "PCCL_QUANT_LANES": "1",
+             "PCCL_SEGMENT_CHUNK_MIB": "0"},
+            {"PCCL_RING_STRIPES": "4", "PCCL_QUANT_LANES": "2", "PCCL_SEGMENT_CHUNK_MIB": "24"}]
     lines = _ring(envs, "--pool", "8", "--quant", quant, "--n", str(48 << 20), "--steps", "1", timeout=400)
     _check(lines, framing=1, err=1e-4 if quant == "none" else 0.3, path=1)
 
@@ -101,8 +103,9 @@ def test_mixed_host_and_hbm_reference_peer(hip):
 
 @pytest.mark.gpu
 def test_peers_with_different_shape_settings_agree_hbm(hip):
-    envs = [{"PCCL_RING_STRIPES": "8", "PCCL_QUANT_LANES": "4"}, {"PCCL_RING_STRIPES": "1", "PCCL_QUANT_LANES": "1"},
-            {"PCCL_RING_STRIPES": "4", "PCCL_QUANT_LANES": "2"}]
+    envs = [{"PCCL_RING_STRIPES": "8", "PCCL_QUANT_LANES": "4", "PCCL_SEGMENT_CHUNK_MIB": "8"},
+            {"PCCL_RING_STRIPES": "1", "PCCL_QUANT_LANES": "1"},
+            {"PCCL_RING_STRIPES": "4", "PCCL_QUANT_LANES": "2", "PCCL_SEGMENT_CHUNK_MIB": "32"}]
     for quant in ("none", "u8"):
         lines = _ring(envs, "--pool", "8", "--quant", quant, "--dtype", "bf16", "--n", str(64 << 20), "--steps", "2",
                       device="cuda:0")

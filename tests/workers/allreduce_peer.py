@@ -128,6 +128,7 @@ def main():
         rec = {"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
                "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
                "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
+        rec["staging"] = pccl.memory.staging_pool_stats()
         if dev.type == "cuda":
             rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
             if a.report_mem:
