@@ -128,6 +128,14 @@ class Job:
             v = float(t.item())
         return v
 
+    def gather(self, obj):
+        """[obj of every rank] on every rank (rank order)."""
+        if self.dist is None:
+            return [obj]
+        box = [None] * self.world
+        self.dist.all_gather_object(box, obj)
+        return box
+
     def broadcast(self, obj):
         if self.dist is None:
             return obj
@@ -220,6 +228,7 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None, qopt=None):
     torch.cuda.synchronize()
     job.sync(i)
     tc0 = _task_cpu() if i == 0 and tag0 == 0 else None  # the phase's main window only
+    pc0 = pccl.memory.pcie_stats() if i == 0 and tag0 == 0 else None
     t0 = time.perf_counter()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     tx = rx = 0
@@ -239,6 +248,8 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None, qopt=None):
     cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     if tc0 is not None:
         job.cpu_by_thread = _cpu_by_thread(tc0, _task_cpu(), cpu, dt)
+        pc1 = pccl.memory.pcie_stats()
+        job.pcie = {k: (pc1[k] - pc0[k]) / steps for k in pc1}  # this process's (= GPU's) staging bytes per op
     return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), cpu
 
 
@@ -359,6 +370,12 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, 
            "path": res[0]["main"][3], "sweep": {}, "cpu_cores": res[0]["main"][4] / max(dt, 1e-9),
            "op_ms": [round(v * 1e3, 2) for v in res[0]["ops"]], "pool": job.phase_pool}
     out["windows"] = [out["t"]] + [job.max_over_job([r["win"][w] for r in res]) / steps for w in range(windows - 1)]
+    # per rank (= per GPU): socket bytes of its peers, PCIe staging bytes and CPU by thread over the main window
+    local_tx = sum(r["main"][1] for r in res) / steps
+    local_rx = sum(r["main"][2] for r in res) / steps
+    out["per_rank"] = job.gather({"rank": job.rank, "gpu": job.gpu, "peers": len(res), "tx": local_tx, "rx": local_rx,
+                                  "pcie": getattr(job, "pcie", None), "cpu_cores": res[0]["main"][4] / max(dt, 1e-9),
+                                  "cpu_by_thread": getattr(job, "cpu_by_thread", None)})
     for b in sweep:
         out["sweep"][b] = job.max_over_job([r[b] for r in res])
     if check:
@@ -369,6 +386,34 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, 
             ok = t.item() == 0.0
         out["ok"] = ok
     return out
+
+
+def _per_rank_diag(ring, nbytes, P):
+    """Per rank (one GPU each at N > 1) over the headline window, per op: the PCIe staging bytes the library queued
+    (``pcie_*_GB``, pcclxPcieStats) next to the ring's model (per peer D2H = S, H2D = 1.75 S at 8 peers: the step-0
+    payload and every reduced piece leave the GPU once, every received piece enters it once, 2(W-1)/W S each way on
+    the wire), the peers' loopback-TCP bytes and an estimate of the host DRAM traffic they cause: every socket byte is
+    read and written once by the sender's copy into the kernel and once by the receiver's copy out of it (4 x tx), and
+    every PCIe byte is one DMA access of pinned memory. What the N >= 4 host-memory-bound prediction
+    (docs/PERFORMANCE.md) hinges on, measured rather than assumed."""
+    rows = []
+    t = ring["t"]
+    for r in ring.get("per_rank") or []:
+        peers = r["peers"]
+        wire = 2 * (P - 1) / P * nbytes
+        row = {"rank": r["rank"], "gpu": r["gpu"], "peers": peers,
+               "socket_tx_GB": round(r["tx"] / 1e9, 3), "socket_rx_GB": round(r["rx"] / 1e9, 3),
+               "model_pcie_d2h_GB": round(peers * nbytes / 1e9, 3) if P > 1 else 0.0,
+               "model_pcie_h2d_GB": round(peers * wire / 1e9, 3),
+               "cpu_cores_busy": round(r["cpu_cores"], 2), "cpu_by_thread": r["cpu_by_thread"]}
+        if r.get("pcie"):
+            h2d, d2h = r["pcie"]["h2d"], r["pcie"]["d2h"]
+            dram = 4 * r["tx"] + h2d + d2h
+            row.update({"pcie_h2d_GB": round(h2d / 1e9, 3), "pcie_d2h_GB": round(d2h / 1e9, 3),
+                        "pcie_GBps": round((h2d + d2h) / t / 1e9, 2),
+                        "host_dram_est_GB": round(dram / 1e9, 2), "host_dram_est_GBps": round(dram / t / 1e9, 1)})
+        rows.append(row)
+    return rows
 
 
 def latency_cpu(job, n_ops=300):
@@ -480,8 +525,12 @@ def latency_python_processes(peers):
     if r.returncode != 0 or not line:
         return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
     row = json.loads(line[-1])["sizes"]["1024KiB"]
+    # every call variant of the run (interleaved op by op on the same buffers), median / p90 us
+    variants = {k: {"median_us": v["median_us"], "p90_us": v["p90_us"]} for k, v in row.items()
+                if isinstance(v, dict) and "median_us" in v}
     return {"peers": peers, "path": row["path"], "blocking_median_us": row["all_reduce"]["median_us"],
-            "blocking_p90_us": row["all_reduce"]["p90_us"], "async_median_us": row["ready"]["median_us"]}
+            "blocking_p90_us": row["all_reduce"]["p90_us"], "async_median_us": row["ready"]["median_us"],
+            "variants": variants}
 
 
 def baseline_configs(a, peers):
@@ -876,6 +925,7 @@ def main():
                   "cpu_cores_busy_rank0": round(ring["cpu_cores"], 2), "cpus_available": _cpu_quota(),
                   "cpu_by_thread_rank0": getattr(job, "cpu_by_thread", None),
                   "result_exact": ring.get("ok")})
+    extra["per_rank"] = _per_rank_diag(ring, nbytes, P)
     sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
                                                     "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
                              for b, t in ring["sweep"].items()}}

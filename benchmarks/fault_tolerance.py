@@ -85,6 +85,7 @@ def peer(a):
             continue
         x.fill_(1.0)
         sync()
+        pools0 = pccl.memory.staging_pool_stats()
         t0 = time.perf_counter()
         try:
             info = comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=0)  # in place
@@ -92,7 +93,11 @@ def peer(a):
             dt = time.perf_counter() - t0
             w = info.local_world_size
             exact = bool((x == float(w)).all())
-            log(event="ok", world=w, sec=dt, exact=exact, path=comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH))
+            pools = pccl.memory.staging_pool_stats()
+            # staging memory the op had to allocate (pool misses: a fresh process's first ops)
+            alloc_ms = sum(pools[k].get("alloc_us", 0) - pools0[k].get("alloc_us", 0) for k in pools) / 1e3
+            log(event="ok", world=w, sec=dt, exact=exact, path=comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH),
+                alloc_ms=alloc_ms)
         except pccl.PCCLError as e:
             t_fail = time.time()
             sync()
@@ -243,6 +248,8 @@ def run(a) -> dict:
         "kill_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
         "joiner_connect_to_first_exact_op_ms": ms(j_first - j_connect[0]) if j_first and j_connect else None,
         "joiner_process_start_to_first_exact_op_ms": ms(j_first - j_proc[0]) if j_first and j_proc else None,
+        "joiner_first_op_ms": round(1e3 * min(j_ok, key=lambda x: x["t"])["sec"], 1) if j_ok else None,
+        "joiner_first_op_staging_alloc_ms": round(min(j_ok, key=lambda x: x["t"]).get("alloc_ms", 0), 1) if j_ok else None,
         "survivors_admission_vote_ms": ms(max(x["sec"] for x in admits)) if admits else None,
         "optimize_topology_call_ms": ms(max(x["sec"] for x in opt)) if opt else None,
         "optimize_ok": bool(opt) and all(x["event"] == "optimized" for x in opt) and len(opt) == a.peers,

@@ -81,15 +81,28 @@ def peer(a):
             rd = pccl.ReduceDescriptor(hi - lo, pccl.ReduceOp.AVG, tag, pccl.ReduceOperandDescriptor(D.FLOAT), q)
             descs.append(pccl.ReduceOpDescriptor.from_torch(x[lo:hi], y[lo:hi], rd))
             tag += 1
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        reps = []
+        for rep in range(a.repeat):
+            if rep:  # the same ops again under fresh tags (every peer derives the same tag sequence)
+                for d in descs:
+                    d.reduce_descriptor.tag = tag
+                    tag += 1
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            pstats0 = pccl.memory.staging_pool_stats(reset_peak=True)
+            t0 = time.perf_counter()
+            info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            pstats = pccl.memory.staging_pool_stats()
+            reps.append({"seconds": dt, "tx": info.tx_bytes, "rx": info.rx_bytes,
+                         "pinned_peak": pstats["pinned"]["peak"], "pinned_allocs": pstats["pinned"].get("allocs", 0)
+                         - pstats0["pinned"].get("allocs", 0),
+                         "alloc_ms": sum(pstats[k].get("alloc_us", 0) - pstats0[k].get("alloc_us", 0)
+                                         for k in ("pinned", "device")) / 1e3})
         err = float((y[:check].cpu() - exact).abs().max())
-        out[f] = {"seconds": dt, "tx": info.tx_bytes, "rx": info.rx_bytes, "max_abs_err": err}
+        out[f] = dict(reps[-1], max_abs_err=err, reps=reps)
     print(json.dumps({"rank": a.rank, "res": out}), flush=True)
     comm.destroy()
 
@@ -114,6 +127,8 @@ def main():
     ap.add_argument("--concurrent-quant", type=int, default=32, help="the same for the quantized formats (0: --concurrent)")
     ap.add_argument("--stripes", type=int, default=0, help="PCCL_RING_STRIPES (connections per ring step; 0 = default)")
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="run each format's multi-op this many times (the summary is the last one; 2 = cold + warm)")
     ap.add_argument("--formats", default=",".join(FORMATS))
     ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
     ap.add_argument("--ports", default="", help=argparse.SUPPRESS)  # internal: Communicator port kwargs (JSON)
@@ -129,7 +144,7 @@ def main():
         env["PCCL_RING_STRIPES"] = str(a.stripes)
     args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
             "--concurrent", str(a.concurrent), "--concurrent-quant", str(a.concurrent_quant),
-            "--formats", a.formats]
+            "--formats", a.formats, "--repeat", str(a.repeat)]
     relay = None
     peer_ports = [{} for _ in range(a.peers)]
     if a.emulator == "builtin":
@@ -184,7 +199,14 @@ def main():
                       "bus_GBps": round(alg * 2 * (a.peers - 1) / a.peers / 1e9, 3),
                       "ref_metric_rx_plus_tx_Gbit_per_peer": round(wire * 8 / 1e9, 2),
                       "effective_fp32_Gbit_per_peer": round(2 * nbytes * (a.peers - 1) / a.peers * 2 / t * 8 / 1e9, 2),
-                      "max_abs_err": max(r[f]["max_abs_err"] for r in res)}
+                      "max_abs_err": max(r[f]["max_abs_err"] for r in res),
+                      "seconds_per_repeat": [round(max(r[f]["reps"][k]["seconds"] for r in res), 4)
+                                             for k in range(a.repeat)],
+                      "pinned_peak_MiB_max_peer": round(max(r[f]["pinned_peak"] for r in res) / 2**20, 1),
+                      "pinned_allocs_per_repeat_max_peer": [max(r[f]["reps"][k]["pinned_allocs"] for r in res)
+                                                            for k in range(a.repeat)],
+                      "alloc_ms_per_repeat_max_peer": [round(max(r[f]["reps"][k]["alloc_ms"] for r in res), 1)
+                                                       for k in range(a.repeat)]}
     print(json.dumps({"metric": "quantized all-reduce over emulated WAN",
                       "config": "int8-quantized all-reduce over tc-netem 50 ms simulated WAN, 8 peers",
                       "peers": a.peers, "mib_per_peer": a.mib, "device": a.device,

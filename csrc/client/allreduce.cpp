@@ -35,18 +35,6 @@ EventPool &event_pool() {
     return *p;
 }
 
-BufferPool &host_pool() {
-    static BufferPool p(BufferPool::Kind::Host);
-    return p;
-}
-BufferPool &pinned_pool() {
-    static BufferPool p(BufferPool::Kind::Pinned);
-    return p;
-}
-BufferPool &device_pool() {
-    static BufferPool p(BufferPool::Kind::Device);
-    return p;
-}
 
 bool Client::abort_received(uint64_t tag) {
     auto p = master_.receive<M2CCollectiveCommsAbort>([tag](const M2CCollectiveCommsAbort &a) { return a.tag == tag; },
@@ -360,17 +348,21 @@ bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {
 } // namespace pccl::client
 
 // Staging pools of this process: [0..2] pinned host (in use, peak in use, cached free), [3..5] HBM, [6..8] plain host
-// bytes; returns how many counters exist (writes at most n). `reset` restarts the peaks at the current use.
+// bytes; [9..11] fresh runtime allocations of the pinned / HBM / host pool and [12..14] the microseconds they took.
+// Returns how many counters exist (writes at most n). `reset` restarts the peaks at the current use.
 extern "C" __attribute__((visibility("default"))) size_t pcclxPoolStats(uint64_t *out, size_t n, int reset) {
     using namespace pccl::client;
     BufferPool *pools[3] = {&pinned_pool(), &device_pool(), &host_pool()};
-    uint64_t v[9];
+    constexpr size_t kN = 15;
+    uint64_t v[kN];
     for (int k = 0; k < 3; ++k) {
         v[3 * k] = pools[k]->in_use();
         v[3 * k + 1] = pools[k]->peak();
         v[3 * k + 2] = pools[k]->cached();
+        v[9 + k] = pools[k]->allocs();
+        v[12 + k] = pools[k]->alloc_us();
         if (reset) pools[k]->reset_peak();
     }
-    for (size_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
-    return 9;
+    for (size_t i = 0; i < n && i < kN; ++i) out[i] = v[i];
+    return kN;
 }

@@ -84,7 +84,7 @@ bool ipc_needs_preflight(const std::vector<uint64_t> &gpu_uids, bool done, size_
 int ipc_push_grid(const std::vector<uint64_t> &gpu_uids, size_t rank, int remote_grid);
 bool ipc_pid_quiesced_for_test(int pid);
 
-struct OpCtx; // per-op mapping context (ipc.cpp)
+struct OpCtx; // per-op mapping context (ipc_shm.hpp)
 
 class IpcArena {
 public:
@@ -169,8 +169,13 @@ private:
     bool wait_slot_free(Client &c, uint64_t seq);
     // waits until no live peer can still write into my receive buffer for `seq` (push algorithm, abort path)
     void drain_peers(Client &c, uint64_t seq);
-    // PCCL_IPC_ALGO: "push" (default, one-shot reduce + broadcast) or "two_shot" (reduce-scatter, then gather)
-    static bool push_algorithm();
+    // PCCL_IPC_ALGO: "push" (default, one-shot reduce + broadcast) or "two_shot" (reduce-scatter, then gather) and
+    // PCCL_IPC_REMOTE_GRID, read once when the arena is created (a ring establishment), never on op threads: a
+    // process that switches them (the bench's per-phase variants) does so between establishments, and the vote still
+    // checks that every peer runs the same algorithm
+    bool push_algo_ = true;
+    int remote_grid_ = 0;
+    static bool push_algorithm_env();
     // PCCL_IPC_MODE: "safe" (default: VMM-shared staging buffers only) or "fast" (hipIpc, zero-copy user buffers)
     static bool safe_mode();
     void release_mapping(const MapKey &key, Mapping &m);

@@ -15,115 +15,71 @@
 
 namespace pccl::client {
 
+// Staging memory of the collectives. Requests up to kSlabMaxRequest are carved out of kSlabBytes slabs (one runtime
+// allocation per slab, first-fit with coalescing, 4 KiB granules); larger ones are whole runtime allocations kept in a
+// best-fit cache. Pinned allocations are expensive (hipHostMalloc pins every page; milliseconds per call, serialised
+// across processes by the driver), so a burst of concurrent small ops - e.g. 64 quantized ops in flight, each leasing
+// ~8 staging buffers per peer - would otherwise pay hundreds of allocations on its first pass and churn the cache
+// afterwards. A failed runtime allocation releases the pool's idle memory (cached buffers, empty slabs) and retries
+// once before the lease reports failure.
 class BufferPool {
 public:
     enum class Kind { Host, Pinned, Device };
     explicit BufferPool(Kind k) : kind_(k) {}
-    ~BufferPool() {
-        for (auto &b : free_) release(b);
-    }
+    ~BufferPool();
 
+    struct Slab;
     struct Buf {
         void *p = nullptr;
         size_t cap = 0;
         int device = -1;
+        Slab *slab = nullptr; // carved out of this slab (nullptr: a whole runtime allocation)
     };
 
-    Buf get(size_t n, int device = -1) {
-        Buf b = get_raw(n, device);
-        if (b.p) note_lease(b.cap);
-        return b;
-    }
+    Buf get(size_t n, int device = -1);
+    void put(const Buf &b);
 
     // Bytes leased out right now, the most ever leased out at once (since the last reset_peak) and cached free bytes
     // (pcclxPoolStats: what a peer's staging actually holds, e.g. pinned memory per device-ring op).
     size_t in_use() const { return in_use_.load(std::memory_order_relaxed); }
     size_t peak() const { return peak_.load(std::memory_order_relaxed); }
-    size_t cached() {
-        std::lock_guard l(mtx_);
-        return free_bytes_;
-    }
+    size_t cached();
     void reset_peak() { peak_.store(in_use_.load()); }
+    // fresh allocations from the runtime (cache misses, slabs included) and the time they took (microseconds)
+    uint64_t allocs() const { return allocs_.load(std::memory_order_relaxed); }
+    uint64_t alloc_us() const { return alloc_us_.load(std::memory_order_relaxed); }
+
+    static constexpr size_t kSlabBytes = 128u << 20;
+    static constexpr size_t kSlabMaxRequest = 32u << 20;
+    static constexpr size_t kGranule = 4096;
+
+    struct Slab {
+        uint8_t *base = nullptr;
+        size_t size = 0;
+        int device = -1;
+        size_t used = 0;
+        std::map<size_t, size_t> free; // offset -> length of free extents (coalesced)
+    };
 
 private:
-    void note_lease(size_t cap) {
-        const size_t now = in_use_.fetch_add(cap) + cap;
-        size_t pk = peak_.load(std::memory_order_relaxed);
-        while (now > pk && !peak_.compare_exchange_weak(pk, now)) {
-        }
-    }
-    Buf get_raw(size_t n, int device) {
-        {
-            std::lock_guard l(mtx_);
-            size_t best = SIZE_MAX;
-            size_t bi = 0;
-            for (size_t i = 0; i < free_.size(); ++i)
-                if (free_[i].cap >= n && free_[i].device == device && free_[i].cap < best) {
-                    best = free_[i].cap;
-                    bi = i;
-                }
-            if (best != SIZE_MAX) {
-                Buf b = free_[bi];
-                free_.erase(free_.begin() + static_cast<long>(bi));
-                free_bytes_ -= b.cap;
-                return b;
-            }
-        }
-        Buf b;
-        b.cap = n < 4096 ? 4096 : n;
-        b.device = device;
-        switch (kind_) {
-            case Kind::Host: b.p = std::aligned_alloc(4096, (b.cap + 4095) / 4096 * 4096); break;
-            case Kind::Pinned: b.p = device_backend() ? device_backend()->alloc_pinned(b.cap) : nullptr; break;
-            case Kind::Device: b.p = device_backend() ? device_backend()->alloc_device(b.cap) : nullptr; break;
-        }
-        if (b.p == nullptr) b.cap = 0;
-        return b;
-    }
+    void note_lease(size_t cap);
+    void *runtime_alloc(size_t n, int device);
+    void runtime_free(void *p, int device);
+    Buf carve_locked(size_t n, int device);
+    void trim_idle_locked(bool everything);
 
-public:
-    // Returned buffers stay cached up to kMaxFree buffers and PCCL_POOL_MAX_FREE_MIB (default 32 GiB) per pool,
-    // oldest released first. The cap must cover a whole op's working set: the device ring holds 9 staging buffers
-    // per peer (8 threaded peers x 1 GiB: 6 GiB of pinned memory), and a pool that trims below that frees and
-    // re-allocates pinned memory on every op (hipHostFree / hipHostMalloc of 128 MiB cost milliseconds each).
-    void put(const Buf &b) {
-        if (b.p == nullptr) return;
-        in_use_.fetch_sub(b.cap);
-        static const size_t max_bytes = env_size("PCCL_POOL_MAX_FREE_MIB", 32u << 10) << 20;
-        std::lock_guard l(mtx_);
-        free_.push_back(b);
-        free_bytes_ += b.cap;
-        while (free_.size() > 1 && (free_.size() > kMaxFree || free_bytes_ > max_bytes)) {
-            free_bytes_ -= free_.front().cap;
-            release(free_.front());
-            free_.erase(free_.begin());
-        }
-    }
-
-private:
-    void release(const Buf &b) {
-        if (!b.p) return;
-        switch (kind_) {
-            case Kind::Host: std::free(b.p); break;
-            case Kind::Pinned:
-                if (device_backend()) device_backend()->free_pinned(b.p);
-                break;
-            case Kind::Device:
-                if (device_backend()) {
-                    const int cur = device_backend()->current_device();
-                    if (b.device >= 0) device_backend()->set_device(b.device);
-                    device_backend()->free_device(b.p);
-                    if (cur >= 0) device_backend()->set_device(cur);
-                }
-                break;
-        }
-    }
+    // Whole buffers stay cached up to kMaxFree buffers and PCCL_POOL_MAX_FREE_MIB (default 32 GiB) per pool (idle
+    // slabs count against the same budget), oldest released first. The cap must cover a whole op's working set: the
+    // device ring holds 9 staging buffers per peer (8 threaded peers: ~9 GiB of pinned memory with 128 MiB segment
+    // chunks), and a pool that trims below that frees and re-allocates pinned memory on every op.
     static constexpr size_t kMaxFree = 256;
     std::atomic<size_t> in_use_{0}, peak_{0};
+    std::atomic<uint64_t> allocs_{0}, alloc_us_{0};
     Kind kind_;
     std::mutex mtx_;
     std::vector<Buf> free_;
     size_t free_bytes_ = 0;
+    std::vector<std::unique_ptr<Slab>> slabs_;
 };
 
 // RAII lease of a pooled buffer.

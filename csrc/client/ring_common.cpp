@@ -12,6 +12,18 @@ namespace pccl::client::ring {
 
 using namespace std::chrono_literals;
 
+namespace {
+std::atomic<uint64_t> g_pcie_h2d{0}, g_pcie_d2h{0};
+}
+void pcie_note(size_t h2d, size_t d2h) {
+    if (h2d) g_pcie_h2d.fetch_add(h2d, std::memory_order_relaxed);
+    if (d2h) g_pcie_d2h.fetch_add(d2h, std::memory_order_relaxed);
+}
+void pcie_read(uint64_t &h2d, uint64_t &d2h) {
+    h2d = g_pcie_h2d.load(std::memory_order_relaxed);
+    d2h = g_pcie_d2h.load(std::memory_order_relaxed);
+}
+
 std::vector<std::pair<size_t, size_t>> chunk_bounds(size_t total, size_t ws) {
     std::vector<std::pair<size_t, size_t>> b(ws);
     const size_t base = total / ws, rem = total % ws;
@@ -97,11 +109,18 @@ StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape) {
     return s;
 }
 
+// Op o (= seq * lanes + lane) starts at connection o*s + floor(o*s / pool) (s = stripes it may use, at most the
+// pool): consecutive ops start s connections apart and every lap around the pool shifts the starts by one, so ops
+// whose steps use fewer than s stripes (small steps: 64 concurrent 32 MiB ops have 1 MiB steps, one stripe each)
+// still spread over the whole pool. Without the shift they would all start on multiples of s and leave the other
+// connections idle: 64 uint8 ops over a 16-connection pool of 1 Gbit/s WAN flows used 4 of them (1.99 s per 2 GiB
+// vs 1.09 s with 32 ops of two stripes each, profiles/r5/b3/).
 size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool, const Shape &shape) {
     if (shape.reference) return static_cast<size_t>((seq + k) % pool);
     const uint64_t lanes = ((tag >> 58) & 3) + 1, lane = (tag >> 60) & 3;
-    const uint64_t base = (seq * lanes + lane) * shape.stripes;
-    return static_cast<size_t>((base + k) % pool);
+    const uint64_t s = std::max<uint64_t>(1, std::min<uint64_t>(shape.stripes, pool));
+    const uint64_t base = (seq * lanes + lane) * s;
+    return static_cast<size_t>((base + base / pool + k) % pool);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -610,3 +629,12 @@ void settle_device_backup(std::function<void(bool)> &settle, DeviceBackend *be, 
 }
 
 } // namespace pccl::client::ring
+
+// Host <-> device staging bytes of the device rings in this process: [0] host->device, [1] device->host (pcie_note).
+// Returns how many counters exist (writes at most n).
+extern "C" __attribute__((visibility("default"))) size_t pcclxPcieStats(uint64_t *out, size_t n) {
+    uint64_t v[2];
+    pccl::client::ring::pcie_read(v[0], v[1]);
+    for (size_t i = 0; i < n && i < 2; ++i) out[i] = v[i];
+    return 2;
+}

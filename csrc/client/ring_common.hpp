@@ -197,6 +197,12 @@ struct PcieQueues {
 // process-wide copy queues of `device` (never destroyed: they may outlive static destruction order)
 PcieQueues shared_pcie_queues(DeviceBackend *be, int device);
 
+// Host <-> device bytes the device rings move across the GPU's PCIe link (copies between pinned staging and HBM, and
+// kernels that read / write pinned memory), per process: what a multi-GPU run's per-GPU link carries per op
+// (pcclxPcieStats). Counted where the work is queued.
+void pcie_note(size_t h2d, size_t d2h);
+void pcie_read(uint64_t &h2d, uint64_t &d2h);
+
 // per-step phase marks for PCCL_TRACE_OPS (first 16 steps of each phase)
 void step_mark(bool reduce_scatter, size_t step);
 // finer per-step marks (global step g < 32): `kind` q = payload metadata known and its quantize kernels queued,

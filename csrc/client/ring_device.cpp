@@ -158,6 +158,7 @@ int device_ring_pipeline(DevRing &R) {
         for (size_t off = 0; off < (te - ts) * es; off += piece) {
             const size_t n = std::min(piece, (te - ts) * es - off);
             be->memcpy_async(txbuf[b] + off, R.src + ts * es + off, n, pq.d2h);
+            pcie_note(0, n);
             last_d2h = record(pq.d2h);
             txready[b].add(off, off + n, last_d2h);
         }
@@ -206,6 +207,7 @@ int device_ring_pipeline(DevRing &R) {
                 DevEvent ce = record(pq.h2d);
                 be->stream_wait_event(st, ce);
                 be->reduce_copy(region + a, stage + a, out + a, (e - a) / es, R.dtype, R.rop, st);
+                pcie_note(e - a, e - a); // received bytes in, the next payload out
                 step_last = record(st);
                 txready[nb].add(a, e, step_last);
             };
@@ -214,6 +216,7 @@ int device_ring_pipeline(DevRing &R) {
             ReadyRanges *fwd = &slots.ready(G);
             consume = [&, sink, region, fwd](size_t a, size_t e) {
                 be->memcpy_async(region + a, sink + a, e - a, st);
+                pcie_note(e - a, 0);
                 step_last = record(st);
                 fwd->add(a, e, nullptr); // in host memory: forwardable at once
             };
@@ -269,11 +272,13 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
         Lease hin(pinned_pool(), std::max<size_t>(bytes, 64)), hout(pinned_pool(), std::max<size_t>(bytes, 64));
         if (!hin.ok() || !hout.ok()) return {false, false};
         if (!be->memcpy_async(hin.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};
+        pcie_note(0, bytes);
         const int rc = small_allgather_reduce(rv.tx, rv.rx, q.tag, seq, op.shape, hin.data(), hout.data(), q.count,
                                               q.dtype, q.op, ws, rank, [&] { return abort_received(q.tag); }, op.tx,
                                               op.rx);
         if (rc) return {false, rc == 2};
         if (!be->memcpy_async(dst, hout.data(), bytes, st) || !be->stream_sync(st)) return {false, false};
+        pcie_note(bytes, 0);
         trace_mark("allgather_reduce");
         if (q.src == q.dst && !q.scratch) settle_device_backup(op.settle, be, device, std::move(hin), dst, bytes);
         return {true, false};

@@ -229,6 +229,13 @@ int device_quant_lane(QLane &L) {
     // per-lane copies there measured 1.34-1.38 vs 1.09-1.16 s per 2 GiB (b29/). The plain ring keeps the shared queue
     // at every size (332.9 vs 365.3 ms, b23/).
     const bool lane_copies = max_chunk * qs >= (size_t{4} << 20);
+    // Small reduce-scatter steps without per-lane copies: PCCL_QUANT_SMALL_RS=pinned has the de-quantize-reduce
+    // kernels read the received bytes from pinned memory (no copy, no cross-queue wait in the lane's stream), =copy
+    // stages them through the process-wide host->device queue first (a local choice, not part of the wire).
+    static const bool small_rs_pinned = [] {
+        const char *v = std::getenv("PCCL_QUANT_SMALL_RS");
+        return v && std::strcmp(v, "pinned") == 0;
+    }();
     const PcieQueues pq = lane_copies ? PcieQueues{} : shared_pcie_queues(be, L.device);
     if (!lane_copies && !pq.h2d) return fail(1);
     for (size_t G = 0; G < nsteps; ++G) {
@@ -252,6 +259,7 @@ int device_quant_lane(QLane &L) {
                 else
                     be->quantize(txq[slot] + off * qs, src + off * es, k, L.dtype, L.qtype, params, st);
                 DevEvent e = record(st);
+                pcie_note(0, k * qs);
                 txready[slot].add(off * qs, (off + k) * qs, e);
                 if (G == 0) first_payload = e;
             }
@@ -275,8 +283,11 @@ int device_quant_lane(QLane &L) {
             G, qs, piece_el * qs,
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
-                if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading pinned
-                          // memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
+                pcie_note(e - a, 0); // every received byte crosses once (a copy to HBM or a kernel reading it)
+                if (rs && !lane_copies && small_rs_pinned) { // de-quantize-reduce straight from pinned memory
+                    dequant_consume(region + a / qs * es, sink + a, n, params);
+                } else if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading
+                                 // pinned memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
                     if (lane_copies) {
                         be->memcpy_async(rxdev[b] + a, sink + a, e - a, st);
                     } else {
@@ -334,6 +345,7 @@ std::pair<bool, bool> Client::device_quant_reference_framing(OpState &op, const 
     Lease hbuf(pinned_pool(), std::max<size_t>(bytes, 64));
     if (!st || !hbuf.ok()) return {false, false};
     if (!be->memcpy_async(hbuf.data(), q.src, bytes, st) || !be->stream_sync(st)) return {false, false};
+    pcie_note(0, bytes);
     Lease backup; // in place: the input, restored if the master aborts the op after this peer's part (settle)
     const bool keep_backup = q.src == q.dst && !q.scratch;
     if (keep_backup) {
@@ -346,6 +358,7 @@ std::pair<bool, bool> Client::device_quant_reference_framing(OpState &op, const 
                                   q.dtype, q.qtype, q.qalgo, q.op, [&] { return aborted(); }, op.tx, op.rx);
     if (rc) return {rc == 2, rc == 2};
     if (!be->memcpy_async(q.dst, hbuf.data(), bytes, st) || !be->stream_sync(st)) return {false, false};
+    pcie_note(bytes, 0);
     if (keep_backup) settle_device_backup(op.settle, be, device, std::move(backup), q.dst, bytes);
     return {true, false};
 }

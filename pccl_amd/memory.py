@@ -158,12 +158,27 @@ def ipc_buffer_stats() -> dict:
 def staging_pool_stats(reset_peak: bool = False) -> dict:
     """Bytes of the library's staging pools in this process: per pool (``pinned`` host, ``device`` HBM, plain
     ``host``) the bytes leased out now (``in_use``), the most leased out at once (``peak``, since the last
-    ``reset_peak=True`` call) and the free bytes kept cached for reuse (``cached``). The device rings size their staging
+    ``reset_peak=True`` call), the free bytes kept cached for reuse (``cached``) and the fresh runtime allocations so far
+    (``allocs``, pool misses) with the microseconds they took (``alloc_us``). The device rings size their staging
     by the op's segment chunk (PCCL_SEGMENT_CHUNK_MIB), not by the tensor."""
-    out = (ctypes.c_uint64 * 9)()
-    _native.C.pcclxPoolStats(out, 9, 1 if reset_peak else 0)
-    return {pool: {"in_use": int(out[3 * k]), "peak": int(out[3 * k + 1]), "cached": int(out[3 * k + 2])}
-            for k, pool in enumerate(("pinned", "device", "host"))}
+    out = (ctypes.c_uint64 * 15)()
+    n = int(_native.C.pcclxPoolStats(out, 15, 1 if reset_peak else 0))
+    res = {pool: {"in_use": int(out[3 * k]), "peak": int(out[3 * k + 1]), "cached": int(out[3 * k + 2])}
+           for k, pool in enumerate(("pinned", "device", "host"))}
+    if n >= 15:  # fresh runtime allocations (pool misses) and the microseconds they took
+        for k, pool in enumerate(("pinned", "device", "host")):
+            res[pool]["allocs"] = int(out[9 + k])
+            res[pool]["alloc_us"] = int(out[12 + k])
+    return res
+
+
+def pcie_stats() -> dict:
+    """Bytes this process's device rings moved between pinned host staging and HBM so far (counted where the copies and
+    the kernels that read / write pinned memory are queued): ``h2d`` and ``d2h``. With one process per GPU this is
+    what that GPU's PCIe link carried for the library."""
+    out = (ctypes.c_uint64 * 2)()
+    _native.C.pcclxPcieStats(out, 2)
+    return {"h2d": int(out[0]), "d2h": int(out[1])}
 
 
 def maybe_shareable(device) -> contextlib.AbstractContextManager:

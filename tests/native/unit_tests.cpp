@@ -3,6 +3,7 @@
 // (cmake -DPCCL_SANITIZE=ON: ASan + UBSan on host code).
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <functional>
 #include <random>
 #include <string>
@@ -17,6 +18,7 @@
 #include "proto/packets.hpp"
 #include "client/ipc.hpp"
 #include "client/vmm_share.hpp"
+#include "client/pools.hpp"
 
 #include <signal.h>
 #include <sys/socket.h>
@@ -680,6 +682,43 @@ TEST(ipc_peer_access_precheck) {
     EXPECT(ipc_unreachable_peer(uids, 0, 0, invisible, [](int, int) { return false; }) == -1);
     const std::vector<uint64_t> same = {5, 5, 5};
     EXPECT(ipc_unreachable_peer(same, 1, 0, visible, [](int, int) { return false; }) == -1);
+}
+
+TEST(pool_slabs_carve_coalesce_and_reuse) {
+    using client::BufferPool;
+    BufferPool pool(BufferPool::Kind::Host);
+    // 64 small leases share slabs: 2 runtime allocations (128 MiB slabs) instead of 64
+    std::vector<BufferPool::Buf> bufs;
+    for (int i = 0; i < 64; ++i) bufs.push_back(pool.get(3u << 20));
+    EXPECT(pool.allocs() == 2);
+    EXPECT(pool.in_use() == 64u * (3u << 20));
+    for (auto &b : bufs) {
+        EXPECT(b.p != nullptr && b.slab != nullptr && reinterpret_cast<uintptr_t>(b.p) % BufferPool::kGranule == 0);
+        std::memset(b.p, 0x5a, b.cap); // every lease is writable and disjoint from the others
+    }
+    for (size_t i = 0; i < bufs.size(); ++i)
+        for (size_t j = i + 1; j < bufs.size(); ++j) {
+            auto *a = static_cast<uint8_t *>(bufs[i].p), *b = static_cast<uint8_t *>(bufs[j].p);
+            EXPECT(a + bufs[i].cap <= b || b + bufs[j].cap <= a);
+        }
+    // return every other lease, then the rest: extents coalesce back into whole slabs
+    for (size_t i = 0; i < bufs.size(); i += 2) pool.put(bufs[i]);
+    for (size_t i = 1; i < bufs.size(); i += 2) pool.put(bufs[i]);
+    EXPECT(pool.in_use() == 0);
+    // a lease as large as a whole slab fits again (the extents merged), without a new allocation
+    auto big = pool.get(BufferPool::kSlabMaxRequest);
+    auto again = pool.get(BufferPool::kSlabMaxRequest);
+    EXPECT(big.p && again.p && pool.allocs() == 2);
+    pool.put(big);
+    pool.put(again);
+    // large leases are whole allocations, cached best-fit
+    auto huge = pool.get(BufferPool::kSlabMaxRequest + 1);
+    EXPECT(huge.p != nullptr && huge.slab == nullptr && pool.allocs() == 3);
+    pool.put(huge);
+    auto huge2 = pool.get(BufferPool::kSlabMaxRequest + 4096);
+    EXPECT(huge2.p == huge.p && pool.allocs() == 3);
+    pool.put(huge2);
+    EXPECT(pool.in_use() == 0 && pool.peak() >= 64u * (3u << 20));
 }
 
 int main() {
