@@ -25,7 +25,9 @@ BASELINE config 1; 1 MiB over IPC from the C API, from Python with one process p
 one process) and, N == 1, BASELINE configs 5 and 4 in their own processes (``extra.baseline_configs``): kill + rejoin
 1 of 8 peer processes mid-all-reduce with the ATSP re-solve, on the TCP device ring and on the xGMI path, and the 1B
 fp32 late joiner over TCP and IPC; ``extra.peer_rejoin_latency_ms`` (the metric's second half) is config 5's rejoin on
-the TCP device ring.
+the TCP device ring. The measurements with one process per peer (configs 5 / 4, the per-process Python latency) run
+before this process creates its GPU context (pre_gpu_measurements); ``extra.per_rank`` holds each rank's PCIe
+staging bytes, socket bytes, a host DRAM traffic estimate and CPU by thread for the headline window.
 
 vs_baseline is null: the reference publishes only WAN throughputs (25 / 45 Gbit/s), which are not
 comparable with a single-host loopback/HBM measurement.
@@ -574,6 +576,18 @@ def baseline_configs(a, peers):
     return out
 
 
+def pre_gpu_measurements(a):
+    """N == 1, before this process touches the GPU: the per-process Python latency (8 peer processes over the xGMI
+    path) and BASELINE configs 5 and 4 (one process per peer), each failure-isolated in its own children."""
+    out = {}
+    if not a.no_ipc_extra:
+        _log("latency_1MiB_ipc_python_processes: py_latency.py")
+        out["latency_1MiB_ipc_python_processes"] = latency_python_processes(a.peers)
+    if not a.no_config_extra:
+        out["baseline_configs"] = baseline_configs(a, a.peers)
+    return out
+
+
 def rejoin_latency(job):
     """A new peer connects mid-run; seconds from its connect() until its first all-reduce completed (admission vote +
     P2P establishment + IPC rendezvous + first op). N == 1 only."""
@@ -667,8 +681,6 @@ def run_extras(job, a, nbytes):
         nat = extra["latency_native"].get(f"{P}_peers_1MiB", {})
         if "median_us" in nat:  # the library's latency: C API, threaded peers, no interpreter in the loop
             extra["latency_1MiB_ipc_us"] = nat["median_us"]
-        if not a.no_ipc_extra:
-            extra["latency_1MiB_ipc_python_processes"] = latency_python_processes(P)
         with _full_cpu_mask(ccd=True):
             extra["latency_cpu_4elem_2peers"] = latency_cpu(job)
         if a.no_config_extra:  # (else: BASELINE config 5 in main(), outside this child's time limit)
@@ -893,6 +905,14 @@ def main():
     if os.environ.get("PCCL_BENCH_WATCHDOG"):  # periodic Python stacks of every thread (hang diagnosis)
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["PCCL_BENCH_WATCHDOG"]), repeat=True)
+    # N == 1: the measurements with one process per peer (BASELINE configs 5 / 4, the per-process Python latency) run
+    # first, before this process creates its own GPU context: 8-9 peer processes on one GPU next to a process holding
+    # its queues (the headline's 8 peers, copy queues, stream pools) oversubscribe the GPU's hardware queues, and the
+    # time-sliced queues made config 5 on the xGMI path run into its deadline (55.9 vs 8.9 ms per op standalone,
+    # profiles/r5/b2 vs b4) and the small-op latency bimodal
+    pre = {}
+    if not a.extras_child and not a.quick and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        pre = pre_gpu_measurements(a)
     job = Job(a)
     nbytes = a.mib << 20
     P = job.total
@@ -939,8 +959,10 @@ def main():
             x_extra, x_sweep = extras_in_child(job, a)
         extra.update(x_extra)
         sweep.update(x_sweep)
-        if job.world == 1 and not a.no_config_extra:
-            cfg = baseline_configs(a, P)
+        if "latency_1MiB_ipc_python_processes" in pre:
+            extra["latency_1MiB_ipc_python_processes"] = pre["latency_1MiB_ipc_python_processes"]
+        if "baseline_configs" in pre:
+            cfg = pre["baseline_configs"]
             extra["baseline_configs"] = cfg
             c5 = cfg.get("config5_kill_rejoin_tcp", {})
             # the metric's "peer-rejoin latency": BASELINE config 5 on the TCP device ring, the replacement process's

@@ -18,8 +18,11 @@ ccoip/src/cpp/ccoip_master_handler.cpp:1312-1400):
      master's asymmetric-TSP solve) and keeps reducing on the new ring.
 Reported (ms): kill -> survivors' failed op returned (abort received + ring re-formed), kill -> survivors' first exact
 op at W-1, replacement's connect() -> its first exact op at W (its process start too), the admission vote, the
-optimize call and the master's ATSP solve alone; ms per op in each phase; whether every result and every restore was
-exact. The reference publishes no number for this configuration.
+optimize call and the master's ATSP solve alone; ms per op in each phase (``after_rejoin`` holds each peer's first op
+at W again, which waits for the replacement's first initiate: ~87 ms of a 111 ms xGMI op, profiles/r5/b6/
+ft_ipc_traces/, the later ops are as fast as before the kill); the replacement's first op and the staging memory it had
+to allocate; whether every result and every restore was exact. The reference publishes no number for this
+configuration (BASELINE.md).
 """
 from __future__ import annotations
 

@@ -109,18 +109,24 @@ StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape) {
     return s;
 }
 
-// Op o (= seq * lanes + lane) starts at connection o*s + floor(o*s / pool) (s = stripes it may use, at most the
-// pool): consecutive ops start s connections apart and every lap around the pool shifts the starts by one, so ops
-// whose steps use fewer than s stripes (small steps: 64 concurrent 32 MiB ops have 1 MiB steps, one stripe each)
-// still spread over the whole pool. Without the shift they would all start on multiples of s and leave the other
-// connections idle: 64 uint8 ops over a 16-connection pool of 1 Gbit/s WAN flows used 4 of them (1.99 s per 2 GiB
-// vs 1.09 s with 32 ops of two stripes each, profiles/r5/b3/).
+// Op o (= seq * lanes + lane) uses connections o*s .. o*s + s-1 (mod pool), s = the op's stripe count (op_stripes, the
+// most stripes any of its steps uses; shape.stripes if unset): concurrent ops tile the pool in groups that every one
+// of their steps uses in the same order. Ops whose steps need fewer stripes than shape.stripes (64 concurrent 32 MiB
+// ops have 1 MiB steps, one stripe each) then still spread over the whole pool: starting them shape.stripes apart
+// left 12 of 16 WAN flows idle (64 uint8 ops: 2.0 s per 2 GiB vs 1.07 s with 32 ops). Starts that overlap other
+// ops' groups partially measured slower than aligned groups at 16 / 32 ops (1.55-1.64 vs 1.22-1.25 s, 1.40-1.64 vs
+// 1.07 s; profiles/r5/b5/): an op's step waits for its slowest stripe, and partly shared connections desynchronise them.
 size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool, const Shape &shape) {
     if (shape.reference) return static_cast<size_t>((seq + k) % pool);
     const uint64_t lanes = ((tag >> 58) & 3) + 1, lane = (tag >> 60) & 3;
-    const uint64_t s = std::max<uint64_t>(1, std::min<uint64_t>(shape.stripes, pool));
-    const uint64_t base = (seq * lanes + lane) * s;
-    return static_cast<size_t>((base + base / pool + k) % pool);
+    const uint64_t s = shape.op_stripes ? shape.op_stripes : shape.stripes;
+    return static_cast<size_t>(((seq * lanes + lane) * s + k) % pool);
+}
+
+Shape op_shape(const Shape &shape, size_t max_step_bytes, size_t conns) {
+    Shape s = shape;
+    s.op_stripes = plan_stripes(max_step_bytes, conns, shape).off.size();
+    return s;
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -299,11 +305,12 @@ bool use_small_path(size_t bytes, size_t ws) {
     return bytes <= lim && bytes * (ws - 1) <= 8 * lim;
 }
 
-int small_allgather_reduce(const Conns &txs, const Conns &rxs, uint64_t tag, uint64_t seq, const Shape &shape,
+int small_allgather_reduce(const Conns &txs, const Conns &rxs, uint64_t tag, uint64_t seq, const Shape &agreed,
                            const void *src, void *dst, size_t count, DType dt, ReduceOp op, size_t ws, size_t rank,
                            const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
                            std::atomic<uint64_t> &rx_ctr) {
     const size_t es = dtype_size(dt), bytes = count * es;
+    const Shape shape = op_shape(agreed, bytes, txs.size());
     Lease all(host_pool(), std::max<size_t>(ws * bytes, 64));
     if (!all.ok()) return 1;
     uint8_t *v = all.data();

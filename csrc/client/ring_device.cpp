@@ -132,14 +132,11 @@ int device_ring_pipeline(DevRing &R) {
     size_t txshift[kNb] = {0, 0, 0}; // payload of txbuf[i] starts at this offset (16-byte phase of its HBM source)
     auto region_of = [&](size_t G) { return R.dst + rx_range(G).first * es; };
 
-    size_t max_stripes = 1;
-    for (size_t G = 0; G < nsteps; ++G) {
-        const auto [ts, te] = tx_range(G);
-        max_stripes = std::max(max_stripes, plan_stripes((te - ts) * es, R.txs.size(), R.shape).off.size());
-    }
+    // every chunk of the op is sent by this peer at some step: the largest one sets the op's stripe count
+    const Shape shape = op_shape(R.shape, max_chunk * es, R.txs.size());
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
-    OpSenders senders(R.txs, R.tag, seq, R.shape, piece, nsteps, max_stripes, be, R.tx);
-    RingRx rx(R.rxs, R.tag, seq, R.shape, nsteps); // after the buffers its sinks point into
+    OpSenders senders(R.txs, R.tag, seq, shape, piece, nsteps, shape.op_stripes, be, R.tx);
+    RingRx rx(R.rxs, R.tag, seq, shape, nsteps); // after the buffers its sinks point into
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, rx_bytes);
     auto fail = [&](int code) {
         senders.cancel();

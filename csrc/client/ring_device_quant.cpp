@@ -81,7 +81,7 @@ int device_quant_lane(QLane &L) {
     DevStream st = L.st;
     const size_t ws = L.ws, rank = L.rank, es = L.es, qs = L.qs, piece_el = L.piece_el;
     const uint64_t seq = L.seq;
-    const Shape &shape = *L.shape;
+    const Shape &agreed = *L.shape;
     struct GateOpener { // the next lane never waits for a lane that ended (any exit)
         LaneGate *g;
         ~GateOpener() {
@@ -99,7 +99,7 @@ int device_quant_lane(QLane &L) {
         return e;
     };
     // the lane's segments (global step G = segment * nps + ring step); staging is sized by the largest segment chunk
-    const std::vector<size_t> seg = segment_bounds(L.count, es, ws, shape);
+    const std::vector<size_t> seg = segment_bounds(L.count, es, ws, agreed);
     const size_t nseg = seg.size() - 1, nps = 2 * (ws - 1);
     std::vector<std::vector<std::pair<size_t, size_t>>> sbounds(nseg);
     size_t max_chunk = 0;
@@ -119,6 +119,7 @@ int device_quant_lane(QLane &L) {
     auto ntx = [&](size_t G) { return tx_range(G).second - tx_range(G).first; };
     auto nrx = [&](size_t G) { return rx_range(G).second - rx_range(G).first; };
     const size_t qbytes = max_chunk * qs + 64;
+    const Shape shape = op_shape(agreed, max_chunk * qs, L.txs->size()); // the lane's stripe count
     constexpr size_t kNb = StepSlots::kSlots;
     // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
     // into `mm_partials`: the chunk a step receives is the chunk the next step quantizes (and the last step's is the
@@ -159,10 +160,7 @@ int device_quant_lane(QLane &L) {
     const size_t nsteps = nseg * nps;
     auto is_rs = [&](size_t G) { return G % nps + 1 < ws; };
 
-    size_t max_stripes = 1;
-    for (size_t G = 0; G < nsteps; ++G)
-        max_stripes = std::max(max_stripes, plan_stripes(ntx(G) * qs, L.txs->size(), shape).off.size());
-    OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, max_stripes, be, *L.tx);
+    OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, shape.op_stripes, be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, shape, nsteps);
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);

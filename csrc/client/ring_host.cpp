@@ -145,8 +145,11 @@ int host_allreduce(const Conns &txs, const Conns &rxs, size_t ws, size_t rank, u
     const int rc = run_lanes(lo, [&](size_t k, size_t a, size_t b) {
         // the lane's segments one after the other (the device rings pipeline them; the wire is the same)
         const std::vector<size_t> seg = segment_bounds(b - a, es, ws, shape);
+        size_t max_chunk = 0; // elements of the lane's largest ring chunk: its stripe count (as the device rings)
+        for (size_t s = 0; s + 1 < seg.size(); ++s) max_chunk = std::max(max_chunk, (seg[s + 1] - seg[s] + ws - 1) / ws);
+        const Shape lane_shape = op_shape(shape, max_chunk * (quant ? dtype_size(qtype) : es), txs.size());
         for (size_t s = 0; s + 1 < seg.size(); ++s) {
-            HostRingArgs A{txs, rxs, ws, rank, lane_tag(tag, k, lo.size() - 1), seq, shape,
+            HostRingArgs A{txs, rxs, ws, rank, lane_tag(tag, k, lo.size() - 1), seq, lane_shape,
                            dst + (a + seg[s]) * es, seg[s + 1] - seg[s], dtype, qtype, qalgo, op, quant, aborted, tx,
                            rx};
             if (const int r = host_ring(A)) return r;

@@ -177,25 +177,30 @@ TEST(stripe_conn_spreads_concurrent_ops_over_the_pool) {
     Shape sh;
     sh.stripes = 4;
     for (size_t pool : {2ul, 4ul, 8ul, 16ul, 32ul}) {
-        // ops with one stripe per step (small steps): `pool` consecutive ops from a multiple of the pool start on
-        // every connection once; from anywhere else on none more than twice, and twice that many ops cover the pool
-        for (uint64_t first : {0ull, 7ull, 1000ull, 4096ull}) {
-            std::vector<int> hits(pool, 0), hits2(pool, 0);
-            for (uint64_t seq = first; seq < first + pool; ++seq) ++hits[stripe_conn(seq, 77, 0, pool, sh)];
-            for (uint64_t seq = first; seq < first + 2 * pool; ++seq) ++hits2[stripe_conn(seq, 77, 0, pool, sh)];
-            for (size_t c = 0; c < pool; ++c) {
-                EXPECT(first % pool != 0 || hits[c] == 1);
-                EXPECT(hits[c] <= 2 && hits2[c] >= 1);
-            }
+        // ops with one stripe per step (small steps): any `pool` consecutive ops use every connection once
+        const Shape one = op_shape(sh, 1u << 20, pool);
+        EXPECT(one.op_stripes == 1);
+        for (uint64_t first : {0ull, 7ull, 1000ull}) {
+            std::vector<int> hits(pool, 0);
+            for (uint64_t seq = first; seq < first + pool; ++seq) ++hits[stripe_conn(seq, 77, 0, pool, one)];
+            for (size_t c = 0; c < pool; ++c) EXPECT(hits[c] == 1);
         }
-        // an op's stripes are consecutive connections
-        for (uint64_t seq : {0ull, 3ull, 9ull})
-            for (size_t k = 1; k < std::min<size_t>(4, pool); ++k)
-                EXPECT(stripe_conn(seq, 77, k, pool, sh) == (stripe_conn(seq, 77, 0, pool, sh) + k) % pool);
+        // wider ops take aligned groups of consecutive connections: pool / s consecutive ops tile the pool
+        const Shape wide = op_shape(sh, 64u << 20, pool);
+        const size_t s = wide.op_stripes;
+        EXPECT(s == std::min<size_t>(4, pool));
+        std::vector<int> hits(pool, 0);
+        for (uint64_t seq = 5; seq < 5 + pool / s; ++seq)
+            for (size_t k = 0; k < s; ++k) {
+                const size_t c = stripe_conn(seq, 77, k, pool, wide);
+                EXPECT(c == (stripe_conn(seq, 77, 0, pool, wide) + k) % pool && c % s == k);
+                ++hits[c];
+            }
+        for (size_t c = 0; c < pool; ++c) EXPECT(hits[c] == 1);
     }
-    // lanes of one quantized op start on different connections
-    const uint64_t t2 = lane_tag(77, 1, 2), t1 = lane_tag(77, 0, 2);
-    EXPECT(stripe_conn(5, t1, 0, 16, sh) != stripe_conn(5, t2, 0, 16, sh));
+    // lanes of one quantized op take different groups
+    const Shape wide = op_shape(sh, 64u << 20, 16);
+    EXPECT(stripe_conn(5, lane_tag(77, 0, 2), 0, 16, wide) != stripe_conn(5, lane_tag(77, 1, 2), 0, 16, wide));
 }
 
 TEST(wire_shape_roundtrip_and_clamp) {
