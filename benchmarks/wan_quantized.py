@@ -125,12 +125,15 @@ def main():
     ap.add_argument("--pool", type=int, default=16)
     ap.add_argument("--concurrent", type=int, default=8, help="all-reduces in flight (slices of the tensor)")
     ap.add_argument("--concurrent-quant", type=int, default=32, help="the same for the quantized formats (0: --concurrent)")
+    ap.add_argument("--stripe-min-kib", type=int, default=1024,
+                    help="PCCL_STRIPE_MIN_BYTES / 1024: smallest stripe of a ring step (>= 256)")
     ap.add_argument("--stripes", type=int, default=0, help="PCCL_RING_STRIPES (connections per ring step; 0 = default)")
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--repeat", type=int, default=1,
                     help="run each format's multi-op this many times (the summary is the last one; 2 = cold + warm)")
     ap.add_argument("--formats", default=",".join(FORMATS))
     ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
+    ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
     ap.add_argument("--ports", default="", help=argparse.SUPPRESS)  # internal: Communicator port kwargs (JSON)
     ap.add_argument("--rank", type=int, default=None)
     ap.add_argument("--master", default=None)
@@ -138,7 +141,7 @@ def main():
     if a.rank is not None:
         return peer(a)
     from pccl_amd.utils import free_ports, local_master, spawn_python
-    env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(1 << 20),
+    env = {"PCCL_DISABLE_IPC": "1", "OMP_NUM_THREADS": "2", "PCCL_STRIPE_MIN_BYTES": str(a.stripe_min_kib << 10),
            "PCCL_MAX_CONCURRENT_COLLECTIVE_OPS": str(max(16, a.concurrent, a.concurrent_quant))}
     if a.stripes:
         env["PCCL_RING_STRIPES"] = str(a.stripes)
@@ -171,6 +174,11 @@ def main():
                                 json.dumps(peer_ports[r]), *args], env=env,
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(a.peers)]
             outs = [p.communicate(timeout=1500) for p in ps]
+            if a.log_dir:  # every peer's stderr (e.g. PCCL_TRACE_OPS=1 phase lines)
+                os.makedirs(a.log_dir, exist_ok=True)
+                for r, (_, e) in enumerate(outs):
+                    with open(os.path.join(a.log_dir, f"peer{r}.err"), "w") as f:
+                        f.write(e)
     finally:
         relayed = None
         if relay is not None and relay.poll() is None:

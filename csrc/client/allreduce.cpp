@@ -269,10 +269,12 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     if (current_trace()) {
         trace.mark("complete");
         static const char *names[] = {"none", "host_ring", "device_ring", "ipc", "hier", "?", "?", "?"};
-        std::fprintf(stderr, "[pccl-trace] tag %llu seq %llu bytes %zu world %u path %s %s%s\n",
+        // t0: the op thread's start on the host-wide monotonic clock (us), so traces of several processes line up
+        const auto t0_us = std::chrono::duration_cast<std::chrono::microseconds>(trace.t0.time_since_epoch()).count();
+        std::fprintf(stderr, "[pccl-trace] tag %llu seq %llu bytes %zu world %u t0 %lld path %s %s%s\n",
                      static_cast<unsigned long long>(tag), static_cast<unsigned long long>(seq),
-                     op->req.count * dtype_size(op->req.dtype), op->world, names[last_path_.load() & 7],
-                     ok ? "ok" : "FAILED", trace.str().c_str());
+                     op->req.count * dtype_size(op->req.dtype), op->world, static_cast<long long>(t0_us),
+                     names[last_path_.load() & 7], ok ? "ok" : "FAILED", trace.str().c_str());
         current_trace() = nullptr;
     }
     op->success = ok;

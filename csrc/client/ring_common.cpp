@@ -43,7 +43,7 @@ Shape Shape::from_wire(const proto::WireShape &w) {
     Shape s;
     s.stripes = std::max<size_t>(1, std::min<size_t>(16, w.stripes));
     s.quant_lanes = std::max<size_t>(1, std::min<size_t>(4, w.quant_lanes));
-    s.stripe_min = std::max<size_t>(1, w.stripe_min_mib) << 20;
+    s.stripe_min = std::max<size_t>(256, w.stripe_min_kib) << 10;
     s.segment_chunk = static_cast<size_t>(w.segment_chunk_mib) << 20;
     return s;
 }
@@ -61,8 +61,8 @@ proto::WireShape local_wire_shape() {
     proto::WireShape w;
     w.stripes = static_cast<uint8_t>(std::max<size_t>(1, std::min<size_t>(16, env_size("PCCL_RING_STRIPES", 4))));
     w.quant_lanes = static_cast<uint8_t>(std::max<size_t>(1, std::min<size_t>(4, env_size("PCCL_QUANT_LANES", 2))));
-    const size_t min_bytes = std::max<size_t>(1 << 20, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20));
-    w.stripe_min_mib = static_cast<uint16_t>(std::min<size_t>(65535, min_bytes >> 20));
+    const size_t min_bytes = std::max<size_t>(256 << 10, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20));
+    w.stripe_min_kib = static_cast<uint16_t>(std::min<size_t>(65535, min_bytes >> 10));
     w.segment_chunk_mib = static_cast<uint16_t>(std::min<size_t>(65535, env_size("PCCL_SEGMENT_CHUNK_MIB", 128)));
     return w;
 }
@@ -590,8 +590,8 @@ int RingRx::receive(size_t g, size_t unit, size_t gran, const std::function<void
 }
 
 bool StepSlots::can_post(size_t g) const {
-    if (g < kSlots) return true;
-    const size_t b = g % kSlots, prev = g - kSlots;
+    if (g < n_) return true;
+    const size_t b = g % n_, prev = g - n_;
     if (free_[b] && be_->event_query(free_[b]) == 0) return false;
     // an all-gather step's bytes are forwarded by the next step's sends (straight from the pinned slot)
     if (forwarded(prev) && !senders_.sent(prev + 1)) return false;
@@ -599,7 +599,7 @@ bool StepSlots::can_post(size_t g) const {
 }
 
 void StepSlots::post(size_t g) {
-    const size_t b = g % kSlots;
+    const size_t b = g % n_;
     free_[b] = nullptr;
     if (!is_rs(g)) ready_[b].clear();
     rx_.post(g, buf_[b], rx_bytes_(g));

@@ -92,7 +92,7 @@ std::vector<size_t> segment_bounds(size_t count, size_t es, size_t ws, const Sha
 struct StripePlan {
     std::vector<size_t> off, len;
 };
-constexpr size_t kStripeAlign = 1 << 20; // multiple of every element size and of the device staging piece
+constexpr size_t kStripeAlign = 256 << 10; // multiple of every element size (and 16-byte vector phase)
 StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape);
 // Connection of stripe k of op `seq` (data tag `tag`) in a pool of `pool`. Pccl-amd framing: consecutive ops, and the
 // lanes of one quantized op (lane_tag: lane in bits 60-61, lane count - 1 in bits 58-59), take consecutive groups of
@@ -330,23 +330,25 @@ private:
     std::vector<Step> steps_;
 };
 
-// The receive staging of a pipelined device op: step g receives into slot g % kSlots (a pinned buffer, with an HBM
+// The receive staging of a pipelined device op: step g receives into slot g % slots (a pinned buffer, with an HBM
 // twin where the path stages through HBM). A slot takes a new step's bytes once the step that used it before
-// (g - kSlots) is finished with it: its GPU work completed (`free_after`) and, in the all-gather, the step after it
-// has forwarded its bytes. Three slots, because step g+1's sinks are posted while step g still receives and step
-// g+1's sends run while step g's do.
+// (g - slots) is finished with it: its GPU work completed (`free_after`) and, in the all-gather, the step after it
+// has forwarded its bytes. At least three slots, because step g+1's sinks are posted while step g still receives and
+// step g+1's sends run while step g's do; more let a step's sinks be posted while older forwarded bytes still wait
+// for a congested downstream link (the quantized ring's small WAN steps).
 // Steps are numbered across the op's segments (global step G = segment * 2(ws-1) + ring step).
 class StepSlots {
 public:
-    static constexpr size_t kSlots = 3;
-    StepSlots(DeviceBackend *be, RingRx &rx, OpSenders &senders, size_t ws, size_t nsteps,
-              uint8_t *const bufs[kSlots], std::function<size_t(size_t)> rx_bytes)
+    static constexpr size_t kDefaultSlots = 3, kMaxSlots = 8;
+    StepSlots(DeviceBackend *be, RingRx &rx, OpSenders &senders, size_t ws, size_t nsteps, uint8_t *const *bufs,
+              size_t slots, std::function<size_t(size_t)> rx_bytes)
         : be_(be), rx_(rx), senders_(senders), ws_(ws), nps_(2 * (ws - 1)), nsteps_(nsteps),
-          rx_bytes_(std::move(rx_bytes)) {
-        for (size_t i = 0; i < kSlots; ++i) buf_[i] = bufs[i];
+          n_(std::max<size_t>(kDefaultSlots, std::min(slots, kMaxSlots))), rx_bytes_(std::move(rx_bytes)) {
+        for (size_t i = 0; i < n_; ++i) buf_[i] = bufs[i];
     }
-    uint8_t *buf(size_t g) const { return buf_[g % kSlots]; }
-    ReadyRanges &ready(size_t g) { return ready_[g % kSlots]; } // received ranges (the all-gather forwards them)
+    size_t slots() const { return n_; }
+    uint8_t *buf(size_t g) const { return buf_[g % n_]; }
+    ReadyRanges &ready(size_t g) { return ready_[g % n_]; } // received ranges (the all-gather forwards them)
     bool can_post(size_t g) const;
     void post(size_t g);
     // posts step g's sinks (normally already posted during step g-1), waiting for its slot; false if `failed`
@@ -354,7 +356,7 @@ public:
     // posts step g's sinks if not yet posted and its slot is free (non-blocking; from the receive loop)
     bool try_post(size_t g);
     // the last GPU work reading step g's slot
-    void free_after(size_t g, DevEvent e) { free_[g % kSlots] = e; }
+    void free_after(size_t g, DevEvent e) { free_[g % n_] = e; }
 
 private:
     bool is_rs(size_t g) const { return g % nps_ + 1 < ws_; }
@@ -363,11 +365,11 @@ private:
     DeviceBackend *be_;
     RingRx &rx_;
     OpSenders &senders_;
-    size_t ws_, nps_, nsteps_;
+    size_t ws_, nps_, nsteps_, n_;
     std::function<size_t(size_t)> rx_bytes_;
-    uint8_t *buf_[kSlots];
-    ReadyRanges ready_[kSlots];
-    DevEvent free_[kSlots] = {nullptr, nullptr, nullptr};
+    uint8_t *buf_[kMaxSlots] = {};
+    ReadyRanges ready_[kMaxSlots];
+    DevEvent free_[kMaxSlots] = {};
 };
 
 // An in-place device op finished its part: keep the input's backup (HBM or pinned) until the master's verdict and

@@ -101,7 +101,7 @@ int device_ring_pipeline(DevRing &R) {
     // Staging rings of kNb buffers: step G receives into rxbuf[G % kNb] (HBM twin rxdev[G % kNb] for the reduce) and
     // its reduce writes the next payload into txbuf[(G + 1) % kNb]: a buffer is refilled only after the step two back
     // finished with it (StepSlots).
-    constexpr size_t kNb = StepSlots::kSlots;
+    constexpr size_t kNb = StepSlots::kDefaultSlots;
     Lease txl[kNb], rxl[kNb], dvl[kNb];
     uint8_t *txbuf[kNb], *rxbuf[kNb], *rxdev[kNb];
     for (size_t i = 0; i < kNb; ++i) {
@@ -137,7 +137,7 @@ int device_ring_pipeline(DevRing &R) {
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
     OpSenders senders(R.txs, R.tag, seq, shape, piece, nsteps, shape.op_stripes, be, R.tx);
     RingRx rx(R.rxs, R.tag, seq, shape, nsteps); // after the buffers its sinks point into
-    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, rx_bytes);
+    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, rx_bytes);
     auto fail = [&](int code) {
         senders.cancel();
         return code;

@@ -120,14 +120,16 @@ int device_quant_lane(QLane &L) {
     auto nrx = [&](size_t G) { return rx_range(G).second - rx_range(G).first; };
     const size_t qbytes = max_chunk * qs + 64;
     const Shape shape = op_shape(agreed, max_chunk * qs, L.txs->size()); // the lane's stripe count
-    constexpr size_t kNb = StepSlots::kSlots;
+    // receive slots (3, 6 and 8 slots for the small steps of 32 / 64 concurrent WAN ops measured the same:
+    // profiles/r5/b10/)
+    constexpr size_t kNb = StepSlots::kDefaultSlots;
     // The reduce-scatter's de-quantize-reduce kernels emit per-workgroup (min, max) partials of the values they store
     // into `mm_partials`: the chunk a step receives is the chunk the next step quantizes (and the last step's is the
     // all-gather's first payload), so its min / max is one fold of those partials instead of a second pass. A step
     // whose launches do not fit the partials buffer falls back to a separate min / max pass.
     constexpr int kMmSlots = 65536, kMmMinRoom = 64; // 1 MiB of partials: ~1 GiB bf16 chunks
-    Lease txl[2], rxl[kNb], dvl[kNb], mml, mmp;
-    uint8_t *txq[2], *rxbuf[kNb], *rxdev[kNb];
+    Lease txl[2], rxl[StepSlots::kMaxSlots], dvl[StepSlots::kMaxSlots], mml, mmp;
+    uint8_t *txq[2], *rxbuf[StepSlots::kMaxSlots], *rxdev[StepSlots::kMaxSlots];
     for (size_t i = 0; i < kNb; ++i) {
         if (i < 2) {
             txl[i] = Lease(pinned_pool(), qbytes);
@@ -162,7 +164,7 @@ int device_quant_lane(QLane &L) {
 
     OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, shape.op_stripes, be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, shape, nsteps);
-    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, [&](size_t G) { return nrx(G) * qs; });
+    StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);
 
     auto fail = [&](int code) {
@@ -227,13 +229,6 @@ int device_quant_lane(QLane &L) {
     // per-lane copies there measured 1.34-1.38 vs 1.09-1.16 s per 2 GiB (b29/). The plain ring keeps the shared queue
     // at every size (332.9 vs 365.3 ms, b23/).
     const bool lane_copies = max_chunk * qs >= (size_t{4} << 20);
-    // Small reduce-scatter steps without per-lane copies: PCCL_QUANT_SMALL_RS=pinned has the de-quantize-reduce
-    // kernels read the received bytes from pinned memory (no copy, no cross-queue wait in the lane's stream), =copy
-    // stages them through the process-wide host->device queue first (a local choice, not part of the wire).
-    static const bool small_rs_pinned = [] {
-        const char *v = std::getenv("PCCL_QUANT_SMALL_RS");
-        return v && std::strcmp(v, "pinned") == 0;
-    }();
     const PcieQueues pq = lane_copies ? PcieQueues{} : shared_pcie_queues(be, L.device);
     if (!lane_copies && !pq.h2d) return fail(1);
     for (size_t G = 0; G < nsteps; ++G) {
@@ -282,10 +277,9 @@ int device_quant_lane(QLane &L) {
             [&](size_t a, size_t e) {
                 const size_t n = (e - a) / qs;
                 pcie_note(e - a, 0); // every received byte crosses once (a copy to HBM or a kernel reading it)
-                if (rs && !lane_copies && small_rs_pinned) { // de-quantize-reduce straight from pinned memory
-                    dequant_consume(region + a / qs * es, sink + a, n, params);
-                } else if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading
-                                 // pinned memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl)
+                if (rs) { // host -> HBM, then de-quantize-reduce HBM -> HBM (staged beats kernels reading pinned
+                          // memory: 218.5 vs 223.7 ms, profiles/r4/b9/q_rs.jsonl; small steps of 64 concurrent WAN
+                          // ops: the same either way, 1.98-1.99 vs 1.98-2.07 s, profiles/r5/b3/)
                     if (lane_copies) {
                         be->memcpy_async(rxdev[b] + a, sink + a, e - a, st);
                     } else {

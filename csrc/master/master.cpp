@@ -935,7 +935,7 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
     // one data-plane shape for every participant: fewest stripes and lanes, largest stripe minimum of the proposals
     pkt.shape.stripes = 16;
     pkt.shape.quant_lanes = 4;
-    pkt.shape.stripe_min_mib = 1;
+    pkt.shape.stripe_min_kib = 256;
     pkt.shape.segment_chunk_mib = 0;
     bool seg_any = false;
     for (auto &[_, c] : clients_) {
@@ -946,7 +946,7 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
         if (sh == c.coll_shapes.end()) continue;
         pkt.shape.stripes = std::min(pkt.shape.stripes, sh->second.stripes);
         pkt.shape.quant_lanes = std::min(pkt.shape.quant_lanes, sh->second.quant_lanes);
-        pkt.shape.stripe_min_mib = std::max(pkt.shape.stripe_min_mib, sh->second.stripe_min_mib);
+        pkt.shape.stripe_min_kib = std::max(pkt.shape.stripe_min_kib, sh->second.stripe_min_kib);
         // smallest non-zero segment (0 = unsegmented only if every proposal says so)
         const uint16_t sg = sh->second.segment_chunk_mib;
         if (sg != 0 && (!seg_any || sg < pkt.shape.segment_chunk_mib)) {

@@ -168,27 +168,27 @@ constexpr uint8_t kCollFlagExtWire = 4;
 struct WireShape {
     uint8_t stripes = 4;            // PCCL_RING_STRIPES: striped connections per ring step (1..16)
     uint8_t quant_lanes = 2;        // PCCL_QUANT_LANES: lanes of a quantized op (1..4)
-    uint16_t stripe_min_mib = 8;    // PCCL_STRIPE_MIN_BYTES / 1 MiB: smallest stripe (>= 1)
+    uint16_t stripe_min_kib = 8192; // PCCL_STRIPE_MIN_BYTES / 1 KiB: smallest stripe (>= 256 KiB)
     uint16_t segment_chunk_mib = 128; // PCCL_SEGMENT_CHUNK_MIB: largest ring chunk of one segment (0: one segment)
     void encode(WBuf &w) const {
         w.u8(stripes);
         w.u8(quant_lanes);
-        w.u16(stripe_min_mib);
+        w.u16(stripe_min_kib);
         w.u16(segment_chunk_mib);
     }
     bool decode(RBuf &r) {
         if (!r.ok() || r.remaining() < 6) return false;
         stripes = r.u8();
         quant_lanes = r.u8();
-        stripe_min_mib = r.u16();
+        stripe_min_kib = r.u16();
         segment_chunk_mib = r.u16();
         stripes = stripes < 1 ? 1 : (stripes > 16 ? 16 : stripes);
         quant_lanes = quant_lanes < 1 ? 1 : (quant_lanes > 4 ? 4 : quant_lanes);
-        if (stripe_min_mib < 1) stripe_min_mib = 1;
+        if (stripe_min_kib < 256) stripe_min_kib = 256;
         return r.ok();
     }
     bool operator==(const WireShape &o) const {
-        return stripes == o.stripes && quant_lanes == o.quant_lanes && stripe_min_mib == o.stripe_min_mib &&
+        return stripes == o.stripes && quant_lanes == o.quant_lanes && stripe_min_kib == o.stripe_min_kib &&
                segment_chunk_mib == o.segment_chunk_mib;
     }
 };

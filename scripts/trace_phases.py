@@ -15,7 +15,7 @@ def main(path, skip=50):
     for ln in open(path, errors="replace"):
         if "[pccl-trace]" not in ln:
             continue
-        m = re.search(r"world (\d+) path (\S+) (ok|FAILED)(.*)", ln)
+        m = re.search(r"world (\d+)(?: t0 -?\d+)? path (\S+) (ok|FAILED)(.*)", ln)
         if not m:
             continue
         marks = {k: int(v) for k, v in re.findall(r"(\w+) (\d+)us", m.group(4))}

@@ -210,7 +210,7 @@ TEST(wire_shape_roundtrip_and_clamp) {
     a.flags = proto::kCollFlagExtWire | proto::kCollFlagSmallPath;
     a.shape.stripes = 8;
     a.shape.quant_lanes = 3;
-    a.shape.stripe_min_mib = 16;
+    a.shape.stripe_min_kib = 16384;
     auto bytes = proto::encode_with_id(a);
     auto b = proto::decode_payload<proto::C2MCollectiveCommsInitiate>(bytes.data() + 2, bytes.size() - 2);
     EXPECT(b && b->flags == a.flags && b->shape == a.shape);
