@@ -549,7 +549,8 @@ def baseline_configs(a, peers):
       * config 3 (benchmarks/wan_quantized.py, EMULATED WAN: pccl_wan_relay, a separate process delaying and pacing
         every byte; tc-netem needs root): `peers` peer processes on cuda:0, 2 GiB fp32 AVG per peer, 50 ms one way,
         1 Gbit/s flows, 25 Gbit/s links, 16 connections per neighbour; fp32 (8 ops in flight) and uint8 / int8
-        zero-point-scale / fp8 (32 ops in flight); seconds and the reference's metric (rx + tx Gbit/s per peer, its
+        zero-point-scale / fp8 (32 ops in flight, 512 KiB stripes: groups of 4 connections shared by 8 ops measured
+        fastest, profiles/r5/b12/); seconds and the reference's metric (rx + tx Gbit/s per peer, its
         published 25 / 45 Gbit/s). Plus the collocated-sites emulation: 5 ms one way, 10 Gbit/s flows, 50 Gbit/s
         links, fp32, 4 peers (8 peers plus the relay exceed the box's CPU share)."""
     import subprocess
@@ -561,7 +562,8 @@ def baseline_configs(a, peers):
             ("config4_late_joiner_ipc", ["shared_state_sync.py", "--transport", "ipc", "--params", "1e9"], 120),
             ("config3_wan_50ms", ["wan_quantized.py", "--peers", str(peers), "--mib", "2048", "--latency-ms", "50",
                                   "--flow-mbit", "1000", "--link-mbit", "25000", "--pool", "16", "--concurrent", "8",
-                                  "--concurrent-quant", "32", "--formats", "fp32,uint8,int8_zps,fp8"], 180),
+                                  "--concurrent-quant", "32", "--stripe-min-kib", "512",
+                                  "--formats", "fp32,uint8,int8_zps,fp8"], 180),
             ("collocated_5ms_4peers", ["wan_quantized.py", "--peers", "4", "--mib", "2048", "--latency-ms", "5",
                                        "--flow-mbit", "10000", "--link-mbit", "50000", "--pool", "16",
                                        "--concurrent", "8", "--formats", "fp32"], 120)]
