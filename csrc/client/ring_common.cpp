@@ -109,8 +109,8 @@ StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape) {
     return s;
 }
 
-// Op o (= seq * lanes + lane) uses connections o*s .. o*s + s-1 (mod pool), s = the op's stripe count (op_stripes, the
-// most stripes any of its steps uses; shape.stripes if unset): concurrent ops tile the pool in groups that every one
+// Op o (= seq * lanes + lane) uses connections o*s .. o*s + s-1 (mod pool), s = the op's stripe count on this pool
+// (op_stripes: the most stripes any of its steps uses; shape.stripes if unset): concurrent ops tile the pool in groups that every one
 // of their steps uses in the same order. Ops whose steps need fewer stripes than shape.stripes (64 concurrent 32 MiB
 // ops have 1 MiB steps, one stripe each) then still spread over the whole pool: starting them shape.stripes apart
 // left 12 of 16 WAN flows idle (64 uint8 ops: 2.0 s per 2 GiB vs 1.07 s with 32 ops). Starts that overlap other
@@ -119,14 +119,26 @@ StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape) {
 size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool, const Shape &shape) {
     if (shape.reference) return static_cast<size_t>((seq + k) % pool);
     const uint64_t lanes = ((tag >> 58) & 3) + 1, lane = (tag >> 60) & 3;
-    const uint64_t s = shape.op_stripes ? shape.op_stripes : shape.stripes;
+    const uint64_t s = op_stripes(shape, pool);
     return static_cast<size_t>(((seq * lanes + lane) * s + k) % pool);
 }
 
-Shape op_shape(const Shape &shape, size_t max_step_bytes, size_t conns) {
+Shape op_shape(const Shape &shape, size_t max_step_bytes) {
     Shape s = shape;
-    s.op_stripes = plan_stripes(max_step_bytes, conns, shape).off.size();
+    s.op_max_step = std::max<size_t>(1, max_step_bytes);
     return s;
+}
+
+size_t stripe_count(size_t bytes, size_t conns, const Shape &shape) {
+    if (shape.reference) return 1;
+    const size_t p = std::min({shape.stripes, std::max<size_t>(1, conns), std::max<size_t>(1, bytes / shape.stripe_min)});
+    const size_t per = (bytes / p + kStripeAlign - 1) / kStripeAlign * kStripeAlign;
+    // stripes of `per` bytes until the bytes run out (the last one takes the rest); at least one
+    return per == 0 ? 1 : std::max<size_t>(1, std::min(p, (bytes + per - 1) / per));
+}
+
+size_t op_stripes(const Shape &shape, size_t conns) {
+    return shape.op_max_step ? stripe_count(shape.op_max_step, conns, shape) : shape.stripes;
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -310,7 +322,7 @@ int small_allgather_reduce(const Conns &txs, const Conns &rxs, uint64_t tag, uin
                            const std::function<bool()> &aborted, std::atomic<uint64_t> &tx_ctr,
                            std::atomic<uint64_t> &rx_ctr) {
     const size_t es = dtype_size(dt), bytes = count * es;
-    const Shape shape = op_shape(agreed, bytes, txs.size());
+    const Shape shape = op_shape(agreed, bytes);
     Lease all(host_pool(), std::max<size_t>(ws * bytes, 64));
     if (!all.ok()) return 1;
     uint8_t *v = all.data();

@@ -53,9 +53,10 @@ struct Shape {
     size_t stripe_min = 8u << 20;   // smallest stripe (bytes)
     size_t quant_lanes = 2;         // lanes of a quantized op
     size_t segment_chunk = 128u << 20; // largest ring chunk of one segment, value bytes (0: the op is one segment)
-    // stripes of the op's largest step (op_shape; 0: not derived, stripe_conn assumes `stripes`): every peer derives
-    // it from the op's agreed values, so it places the op's stripes on the same connections everywhere
-    size_t op_stripes = 0;
+    // bytes of the op's largest ring step (op_shape; 0: not derived, stripe_conn assumes `stripes`): every peer
+    // derives it from the op's agreed values; with the size of a connection pool it gives the op's stripe count on
+    // that pool (stripe_count), the same at both of its ends even when neighbours' pools differ in size
+    size_t op_max_step = 0;
     static Shape from_wire(const proto::WireShape &w);
     static Shape reference_framing();
 };
@@ -96,11 +97,15 @@ constexpr size_t kStripeAlign = 256 << 10; // multiple of every element size (an
 StripePlan plan_stripes(size_t bytes, size_t conns, const Shape &shape);
 // Connection of stripe k of op `seq` (data tag `tag`) in a pool of `pool`. Pccl-amd framing: consecutive ops, and the
 // lanes of one quantized op (lane_tag: lane in bits 60-61, lane count - 1 in bits 58-59), take consecutive groups of
-// op_stripes connections, so concurrent ops spread over the whole pool (a long-fat pipe is filled by many concurrent
+// op_stripes(shape, pool) connections, so concurrent ops spread over the whole pool (a long-fat pipe is filled by many concurrent
 // ops, reference src/pccl.cpp:345-523). Reference framing: seq % pool (reference reduce.cpp:149-151).
 size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool, const Shape &shape);
 // `shape` for one op (or quantized lane) whose largest ring step carries `max_step_bytes` over `conns` connections
-Shape op_shape(const Shape &shape, size_t max_step_bytes, size_t conns);
+Shape op_shape(const Shape &shape, size_t max_step_bytes);
+// stripes plan_stripes(bytes, conns, shape) makes (without building the plan)
+size_t stripe_count(size_t bytes, size_t conns, const Shape &shape);
+// stripes of the op's largest step on a pool of `conns` connections (shape.stripes if op_max_step is unset)
+size_t op_stripes(const Shape &shape, size_t conns);
 
 // Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first
 // poll that sees it (Client::abort_received), so that poll records it here for every other thread of the op.

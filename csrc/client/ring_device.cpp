@@ -133,9 +133,9 @@ int device_ring_pipeline(DevRing &R) {
     auto region_of = [&](size_t G) { return R.dst + rx_range(G).first * es; };
 
     // every chunk of the op is sent by this peer at some step: the largest one sets the op's stripe count
-    const Shape shape = op_shape(R.shape, max_chunk * es, R.txs.size());
+    const Shape shape = op_shape(R.shape, max_chunk * es);
     // declared after the buffers and ready lists it reads: destroyed (cancelled + joined) before them
-    OpSenders senders(R.txs, R.tag, seq, shape, piece, nsteps, shape.op_stripes, be, R.tx);
+    OpSenders senders(R.txs, R.tag, seq, shape, piece, nsteps, op_stripes(shape, R.txs.size()), be, R.tx);
     RingRx rx(R.rxs, R.tag, seq, shape, nsteps); // after the buffers its sinks point into
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, rx_bytes);
     auto fail = [&](int code) {

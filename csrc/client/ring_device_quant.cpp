@@ -119,7 +119,7 @@ int device_quant_lane(QLane &L) {
     auto ntx = [&](size_t G) { return tx_range(G).second - tx_range(G).first; };
     auto nrx = [&](size_t G) { return rx_range(G).second - rx_range(G).first; };
     const size_t qbytes = max_chunk * qs + 64;
-    const Shape shape = op_shape(agreed, max_chunk * qs, L.txs->size()); // the lane's stripe count
+    const Shape shape = op_shape(agreed, max_chunk * qs); // the lane's connection groups
     // receive slots (3, 6 and 8 slots for the small steps of 32 / 64 concurrent WAN ops measured the same:
     // profiles/r5/b10/)
     constexpr size_t kNb = StepSlots::kDefaultSlots;
@@ -162,7 +162,7 @@ int device_quant_lane(QLane &L) {
     const size_t nsteps = nseg * nps;
     auto is_rs = [&](size_t G) { return G % nps + 1 < ws; };
 
-    OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, shape.op_stripes, be, *L.tx);
+    OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, op_stripes(shape, L.txs->size()), be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, shape, nsteps);
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);

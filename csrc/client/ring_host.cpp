@@ -147,7 +147,7 @@ int host_allreduce(const Conns &txs, const Conns &rxs, size_t ws, size_t rank, u
         const std::vector<size_t> seg = segment_bounds(b - a, es, ws, shape);
         size_t max_chunk = 0; // elements of the lane's largest ring chunk: its stripe count (as the device rings)
         for (size_t s = 0; s + 1 < seg.size(); ++s) max_chunk = std::max(max_chunk, (seg[s + 1] - seg[s] + ws - 1) / ws);
-        const Shape lane_shape = op_shape(shape, max_chunk * (quant ? dtype_size(qtype) : es), txs.size());
+        const Shape lane_shape = op_shape(shape, max_chunk * (quant ? dtype_size(qtype) : es));
         for (size_t s = 0; s + 1 < seg.size(); ++s) {
             HostRingArgs A{txs, rxs, ws, rank, lane_tag(tag, k, lo.size() - 1), seq, lane_shape,
                            dst + (a + seg[s]) * es, seg[s + 1] - seg[s], dtype, qtype, qalgo, op, quant, aborted, tx,

@@ -178,16 +178,16 @@ TEST(stripe_conn_spreads_concurrent_ops_over_the_pool) {
     sh.stripes = 4;
     for (size_t pool : {2ul, 4ul, 8ul, 16ul, 32ul}) {
         // ops with one stripe per step (small steps): any `pool` consecutive ops use every connection once
-        const Shape one = op_shape(sh, 1u << 20, pool);
-        EXPECT(one.op_stripes == 1);
+        const Shape one = op_shape(sh, 1u << 20);
+        EXPECT(op_stripes(one, pool) == 1);
         for (uint64_t first : {0ull, 7ull, 1000ull}) {
             std::vector<int> hits(pool, 0);
             for (uint64_t seq = first; seq < first + pool; ++seq) ++hits[stripe_conn(seq, 77, 0, pool, one)];
             for (size_t c = 0; c < pool; ++c) EXPECT(hits[c] == 1);
         }
         // wider ops take aligned groups of consecutive connections: pool / s consecutive ops tile the pool
-        const Shape wide = op_shape(sh, 64u << 20, pool);
-        const size_t s = wide.op_stripes;
+        const Shape wide = op_shape(sh, 64u << 20);
+        const size_t s = op_stripes(wide, pool);
         EXPECT(s == std::min<size_t>(4, pool));
         std::vector<int> hits(pool, 0);
         for (uint64_t seq = 5; seq < 5 + pool / s; ++seq)
@@ -199,8 +199,22 @@ TEST(stripe_conn_spreads_concurrent_ops_over_the_pool) {
         for (size_t c = 0; c < pool; ++c) EXPECT(hits[c] == 1);
     }
     // lanes of one quantized op take different groups
-    const Shape wide = op_shape(sh, 64u << 20, 16);
+    const Shape wide = op_shape(sh, 64u << 20);
     EXPECT(stripe_conn(5, lane_tag(77, 0, 2), 0, 16, wide) != stripe_conn(5, lane_tag(77, 1, 2), 0, 16, wide));
+}
+
+TEST(stripe_count_matches_plan_and_pools_of_any_size) {
+    Shape sh;
+    sh.stripes = 4;
+    sh.stripe_min = 1u << 20;
+    for (size_t conns : {1ul, 2ul, 3ul, 4ul, 16ul})
+        for (size_t bytes : {0ul, 1ul, 4096ul, (1ul << 20) - 1, 1ul << 20, (3ul << 20) + 7, 9000011ul * 2, 64ul << 20})
+            EXPECT(stripe_count(bytes, conns, sh) == plan_stripes(bytes, conns, sh).off.size());
+    // neighbours with pools of different sizes: both ends of a pool derive the same groups from the op's largest step
+    const Shape op = op_shape(sh, 9000011ul * 2 / 3 + 2);
+    for (size_t pool : {1ul, 2ul, 3ul})
+        for (uint64_t seq : {0ull, 1ull, 2ull, 7ull})
+            for (size_t k = 0; k < op_stripes(op, pool); ++k) EXPECT(stripe_conn(seq, 77, k, pool, op) < pool);
 }
 
 TEST(wire_shape_roundtrip_and_clamp) {

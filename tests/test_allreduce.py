@@ -287,6 +287,34 @@ def test_striped_large_all_reduce(world, pool, quant, monkeypatch):
     assert (res[0] - expect).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize("quant", [False, True])
+def test_mixed_pool_sizes_host(quant, monkeypatch):
+    """Neighbours with different P2P connection pool sizes (1 / 3 / 2): the two ends of every pool derive the same
+    stripe count and connection group for each op from the pool they share, also with several ops in flight."""
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(256 << 10))
+    world, n, ops = 3, 1_500_007, 4
+    pools = [1, 3, 2]
+    inputs = [_peer_tensor(r, n, torch.float32) for r in range(world)]
+    qopt = pccl.QuantizationOptions(pccl.DataType.UINT8, pccl.QuantizationAlgorithm.MIN_MAX) if quant else None
+
+    def fn(rank, comm):
+        outs = [torch.empty(n) for _ in range(ops)]
+        handles = [comm.all_reduce_async(inputs[rank], outs[k], op=pccl.ReduceOp.SUM, tag=k,
+                                         quantization_options=qopt) for k in range(ops)]
+        assert all(h.wait()[0] for h in handles)
+        return outs
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr, timeout=120,
+                                 comm_kwargs=lambda r: {"p2p_connection_pool_size": pools[r]})
+    expect = _expected(inputs, pccl.ReduceOp.SUM).float()
+    tol = 3 * world * max(float(t.max() - t.min()) for t in inputs) / 255 if quant else 1e-4
+    for k in range(ops):
+        for outs in res[1:]:
+            assert torch.equal(outs[k], res[0][k])
+        assert (res[0][k] - expect).abs().max().item() <= tol
+
+
 @pytest.mark.parametrize("lanes,inplace", [("1", False), ("2", True), ("3", False)])
 def test_quantized_lanes(lanes, inplace, monkeypatch):
     """Quantized all-reduce split into lanes (PCCL_QUANT_LANES, each >= 8 MiB of wire bytes per ring chunk): every

@@ -600,3 +600,39 @@ def test_device_ring_staging_bounded_by_segment(hip):
         assert all(ln["path"] == pccl.ReducePath.DEVICE_RING.value for ln in lines), lines
         pinned_peak = max(ln["staging"]["pinned"]["peak"] for ln in lines)
         assert pinned_peak <= (1 << 30), lines[-1]["staging"]
+
+
+def test_device_ring_pcie_bytes_match_model(hip, monkeypatch):
+    """pcclxPcieStats (bench.py extra.per_rank): a device-ring op queues exactly the ring's staging traffic - per peer
+    S device->host (the step-0 payload and every reduced next payload) and 2(W-1)/W S host->device (every received
+    piece) - for W = 3 threaded peers of this process, 8 MiB + 3 elements each (chunks of unequal size)."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    n = (4 << 20) + 3
+    es = 2
+    state = {}
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(rank + 1), device=hip, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)  # warm-up (pools, connections)
+        torch.cuda.synchronize()
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=1)  # barrier: every peer finished the warm-up op
+        torch.cuda.synchronize()
+        if rank == 0:
+            state["before"] = pccl.memory.pcie_stats()
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=2)
+        torch.cuda.synchronize()
+        comm.all_reduce(x[:1], y[:1], op=pccl.ReduceOp.SUM, tag=3)  # (small path: host all-gather, 2 + 2 bytes)
+        torch.cuda.synchronize()
+        return float(y[:1].float().item()), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    res = _run(3, fn)
+    after = pccl.memory.pcie_stats()
+    assert all(v == 6.0 for v, _ in res)
+    S = n * es
+    d2h = after["d2h"] - state["before"]["d2h"]
+    h2d = after["h2d"] - state["before"]["h2d"]
+    # three peers' op 2 (+ the 1-element small-path op 3: one element each way per peer), plus whatever of op 1 was
+    # still being counted when peer 0 sampled (at most its last steps: bounded by the op itself)
+    assert 3 * S + 3 * es <= d2h <= 2 * (3 * S) + 3 * es, (d2h, S)
+    assert 3 * (4 * S // 3) <= h2d <= 2 * 3 * (4 * S // 3) + 3 * es + 16, (h2d, S)
