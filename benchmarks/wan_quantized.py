@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import subprocess
 import sys
 import time
@@ -90,13 +91,16 @@ def peer(a):
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             pstats0 = pccl.memory.staging_pool_stats(reset_peak=True)
+            ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             pstats = pccl.memory.staging_pool_stats()
-            reps.append({"seconds": dt, "tx": info.tx_bytes, "rx": info.rx_bytes,
+            ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+            reps.append({"seconds": dt, "tx": info.tx_bytes, "rx": info.rx_bytes, "cpu_cores": cpu / max(dt, 1e-9),
                          "pinned_peak": pstats["pinned"]["peak"], "pinned_allocs": pstats["pinned"].get("allocs", 0)
                          - pstats0["pinned"].get("allocs", 0),
                          "alloc_ms": sum(pstats[k].get("alloc_us", 0) - pstats0[k].get("alloc_us", 0)
@@ -214,7 +218,10 @@ def main():
                       "pinned_allocs_per_repeat_max_peer": [max(r[f]["reps"][k]["pinned_allocs"] for r in res)
                                                             for k in range(a.repeat)],
                       "alloc_ms_per_repeat_max_peer": [round(max(r[f]["reps"][k]["alloc_ms"] for r in res), 1)
-                                                       for k in range(a.repeat)]}
+                                                       for k in range(a.repeat)],
+                      # CPU cores the peer processes kept busy (sum over peers) while the multi-op ran
+                      "peer_cpu_cores_per_repeat": [round(sum(r[f]["reps"][k]["cpu_cores"] for r in res), 2)
+                                                    for k in range(a.repeat)]}
     print(json.dumps({"metric": "quantized all-reduce over emulated WAN",
                       "config": "int8-quantized all-reduce over tc-netem 50 ms simulated WAN, 8 peers",
                       "peers": a.peers, "mib_per_peer": a.mib, "device": a.device,
