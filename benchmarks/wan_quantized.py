@@ -93,7 +93,7 @@ def peer(a):
             pstats0 = pccl.memory.staging_pool_stats(reset_peak=True)
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
-            info = comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
+            info = run_multi(comm, descs, conc, a.cohorts, a.cohort_delay_ms)
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             dt = time.perf_counter() - t0
@@ -109,6 +109,36 @@ def peer(a):
         out[f] = dict(reps[-1], max_abs_err=err, reps=reps)
     print(json.dumps({"rank": a.rank, "res": out}), flush=True)
     comm.destroy()
+
+
+def run_multi(comm, descs, conc, cohorts=1, delay_ms=0.0):
+    """all_reduce_multiple_with_retry over `descs` with `conc` in flight; with --cohorts K > 1 (experiment) the ops are
+    split into K interleaved cohorts, each its own multi-op call on its own thread, cohort k starting k x delay_ms
+    later, so the cohorts' ring steps are out of phase (one cohort transfers while another waits out the latency)."""
+    if cohorts <= 1:
+        return comm.all_reduce_multiple_with_retry(descs, max_in_flight=conc)
+    import threading
+    groups = [descs[k::cohorts] for k in range(cohorts)]
+    infos = [None] * cohorts
+    errs = []
+
+    def body(k):
+        try:
+            time.sleep(k * delay_ms / 1e3)
+            infos[k] = comm.all_reduce_multiple_with_retry(groups[k], max_in_flight=max(1, conc // cohorts))
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    ths = [threading.Thread(target=body, args=(k,)) for k in range(cohorts)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    tx = sum(i.tx_bytes for i in infos)
+    rx = sum(i.rx_bytes for i in infos)
+    return type(infos[0])(infos[0].local_world_size, tx, rx)
 
 
 def _proc_cpu_s(pid):
@@ -138,6 +168,8 @@ def main():
     ap.add_argument("--formats", default=",".join(FORMATS))
     ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
     ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
+    ap.add_argument("--cohorts", type=int, default=1, help=argparse.SUPPRESS)  # experiment: out-of-phase op cohorts
+    ap.add_argument("--cohort-delay-ms", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--ports", default="", help=argparse.SUPPRESS)  # internal: Communicator port kwargs (JSON)
     ap.add_argument("--rank", type=int, default=None)
     ap.add_argument("--master", default=None)
@@ -151,7 +183,8 @@ def main():
         env["PCCL_RING_STRIPES"] = str(a.stripes)
     args = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
             "--concurrent", str(a.concurrent), "--concurrent-quant", str(a.concurrent_quant),
-            "--formats", a.formats, "--repeat", str(a.repeat)]
+            "--formats", a.formats, "--repeat", str(a.repeat), "--cohorts", str(a.cohorts),
+            "--cohort-delay-ms", str(a.cohort_delay_ms)]
     relay = None
     peer_ports = [{} for _ in range(a.peers)]
     if a.emulator == "builtin":

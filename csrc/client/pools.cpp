@@ -16,7 +16,8 @@ size_t max_free_bytes() {
 
 BufferPool::~BufferPool() {
     for (auto &b : free_) runtime_free(b.p, b.device);
-    for (auto &s : slabs_) runtime_free(s->base, s->device);
+    for (auto &s : slabs_)
+        if (s->used == 0) runtime_free(s->base, s->device); // (a lease still out at exit keeps its slab)
 }
 
 void BufferPool::note_lease(size_t cap) {
@@ -111,48 +112,59 @@ void BufferPool::trim_idle_locked(bool everything) {
     }
 }
 
+// Runtime allocations happen outside the pool's lock (a 128 MiB hipHostMalloc takes tens of ms; other threads keep
+// leasing and returning meanwhile); only a failed one trims the idle memory under the lock and retries.
 BufferPool::Buf BufferPool::get(size_t n, int device) {
     n = round_up(std::max<size_t>(n, 1), kGranule);
-    Buf b;
-    std::unique_lock l(mtx_);
-    if (n <= kSlabMaxRequest) {
-        b = carve_locked(n, device);
-        if (!b.p) {
-            auto s = std::make_unique<Slab>();
-            s->base = static_cast<uint8_t *>(runtime_alloc(kSlabBytes, device));
-            if (!s->base) {
+    auto alloc_or_trim = [&](size_t bytes) {
+        void *p = runtime_alloc(bytes, device);
+        if (!p) {
+            {
+                std::lock_guard l(mtx_);
                 trim_idle_locked(true);
-                s->base = static_cast<uint8_t *>(runtime_alloc(kSlabBytes, device));
             }
-            if (s->base) {
-                s->size = kSlabBytes;
-                s->device = device;
-                s->free.emplace(0, kSlabBytes);
-                slabs_.push_back(std::move(s));
-                b = carve_locked(n, device);
+            p = runtime_alloc(bytes, device);
+        }
+        return p;
+    };
+    Buf b;
+    if (n <= kSlabMaxRequest) {
+        {
+            std::lock_guard l(mtx_);
+            b = carve_locked(n, device);
+        }
+        if (!b.p) {
+            auto slab = std::make_unique<Slab>();
+            slab->base = static_cast<uint8_t *>(alloc_or_trim(kSlabBytes));
+            if (slab->base) {
+                slab->size = kSlabBytes;
+                slab->device = device;
+                slab->free.emplace(0, kSlabBytes);
+                std::lock_guard l(mtx_);
+                slabs_.push_back(std::move(slab));
+                b = carve_locked(n, device); // (another thread may have added a slab meanwhile: either fits)
             }
         }
     } else {
-        size_t best = SIZE_MAX, bi = 0;
-        for (size_t i = 0; i < free_.size(); ++i)
-            if (free_[i].cap >= n && free_[i].device == device && free_[i].cap < best) {
-                best = free_[i].cap;
-                bi = i;
+        {
+            std::lock_guard l(mtx_);
+            size_t best = SIZE_MAX, bi = 0;
+            for (size_t i = 0; i < free_.size(); ++i)
+                if (free_[i].cap >= n && free_[i].device == device && free_[i].cap < best) {
+                    best = free_[i].cap;
+                    bi = i;
+                }
+            if (best != SIZE_MAX) {
+                b = free_[bi];
+                free_.erase(free_.begin() + static_cast<long>(bi));
+                free_bytes_ -= b.cap;
             }
-        if (best != SIZE_MAX) {
-            b = free_[bi];
-            free_.erase(free_.begin() + static_cast<long>(bi));
-            free_bytes_ -= b.cap;
-        } else {
-            b = Buf{runtime_alloc(n, device), n, device, nullptr};
-            if (!b.p) {
-                trim_idle_locked(true);
-                b.p = runtime_alloc(n, device);
-            }
+        }
+        if (!b.p) {
+            b = Buf{alloc_or_trim(n), n, device, nullptr};
             if (!b.p) b = Buf{};
         }
     }
-    l.unlock();
     if (b.p) note_lease(b.cap);
     return b;
 }

@@ -721,6 +721,41 @@ TEST(pool_slabs_carve_coalesce_and_reuse) {
     EXPECT(pool.in_use() == 0 && pool.peak() >= 64u * (3u << 20));
 }
 
+TEST(pool_concurrent_leases_stay_disjoint) {
+    using client::BufferPool;
+    BufferPool pool(BufferPool::Kind::Host);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> ths;
+    for (int t = 0; t < 8; ++t)
+        ths.emplace_back([&, t] {
+            std::mt19937 rng(static_cast<unsigned>(t));
+            std::vector<BufferPool::Buf> held;
+            for (int i = 0; i < 400; ++i) {
+                if (!held.empty() && (rng() % 3 == 0 || held.size() > 6)) {
+                    const size_t k = rng() % held.size();
+                    auto *p = static_cast<uint8_t *>(held[k].p);
+                    for (size_t j = 0; j < held[k].cap; j += 4096)
+                        if (p[j] != static_cast<uint8_t>(t)) ++bad; // nobody else wrote into my lease
+                    pool.put(held[k]);
+                    held.erase(held.begin() + static_cast<long>(k));
+                } else {
+                    const size_t n = (rng() % 2) ? (rng() % (8u << 20)) + 1 : (rng() % (48u << 20)) + 1;
+                    auto b = pool.get(n);
+                    if (!b.p || b.cap < n) {
+                        ++bad;
+                        continue;
+                    }
+                    std::memset(b.p, t, b.cap);
+                    held.push_back(b);
+                }
+            }
+            for (auto &b : held) pool.put(b);
+        });
+    for (auto &t : ths) t.join();
+    EXPECT(bad.load() == 0);
+    EXPECT(pool.in_use() == 0);
+}
+
 int main() {
     for (auto &[name, fn] : registry()) {
         const int before = g_failures;
