@@ -395,8 +395,8 @@ def _per_rank_diag(ring, nbytes, P):
     (``pcie_*_GB``, pcclxPcieStats) next to the ring's model (per peer D2H = S, H2D = 1.75 S at 8 peers: the step-0
     payload and every reduced piece leave the GPU once, every received piece enters it once, 2(W-1)/W S each way on
     the wire), the peers' loopback-TCP bytes and an estimate of the host DRAM traffic they cause: every socket byte is
-    read and written once by the sender's copy into the kernel and once by the receiver's copy out of it (4 x tx), and
-    every PCIe byte is one DMA access of pinned memory. What the N >= 4 host-memory-bound prediction
+    read and written once by the receiver's copy (same-host data sockets send MSG_ZEROCOPY: the kernel reads the
+    sender's pinned pages in place; 2 x tx), and every PCIe byte is one DMA access of pinned memory. What the N >= 4 host-memory-bound prediction
     (docs/PERFORMANCE.md) hinges on, measured rather than assumed."""
     rows = []
     t = ring["t"]
@@ -410,7 +410,7 @@ def _per_rank_diag(ring, nbytes, P):
                "cpu_cores_busy": round(r["cpu_cores"], 2), "cpu_by_thread": r["cpu_by_thread"]}
         if r.get("pcie"):
             h2d, d2h = r["pcie"]["h2d"], r["pcie"]["d2h"]
-            dram = 4 * r["tx"] + h2d + d2h
+            dram = 2 * r["tx"] + h2d + d2h
             row.update({"pcie_h2d_GB": round(h2d / 1e9, 3), "pcie_d2h_GB": round(d2h / 1e9, 3),
                         "pcie_GBps": round((h2d + d2h) / t / 1e9, 2),
                         "host_dram_est_GB": round(dram / 1e9, 2), "host_dram_est_GBps": round(dram / t / 1e9, 1)})

@@ -69,7 +69,7 @@ def test_full_cpu_mask_ccd_narrows_to_one_l3_domain(monkeypatch):
 
 def test_per_rank_diag_models_pcie_and_dram():
     """extra.per_rank: measured staging bytes next to the ring model (per peer D2H = S, H2D = 2(W-1)/W S) and the host
-    DRAM estimate (4 x socket tx + PCIe bytes) per op."""
+    DRAM estimate (2 x socket tx + PCIe bytes) per op."""
     S, P = 1 << 30, 8
     wire = 2 * (P - 1) / P * S
     ring = {"t": 0.25, "per_rank": [
@@ -80,7 +80,7 @@ def test_per_rank_diag_models_pcie_and_dram():
     r0 = rows[0]
     assert r0["model_pcie_d2h_GB"] == round(2 * S / 1e9, 3) and r0["pcie_d2h_GB"] == r0["model_pcie_d2h_GB"]
     assert r0["model_pcie_h2d_GB"] == round(2 * wire / 1e9, 3) == r0["pcie_h2d_GB"]
-    dram = 4 * 2 * wire + 2 * wire + 2 * S
+    dram = 2 * 2 * wire + 2 * wire + 2 * S
     assert r0["host_dram_est_GB"] == round(dram / 1e9, 2)
     assert r0["host_dram_est_GBps"] == round(dram / 0.25 / 1e9, 1)
     # a rank without staging counters (e.g. an older library) still reports its socket bytes
