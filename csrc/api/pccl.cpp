@@ -232,11 +232,11 @@ static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const
     pccl::DeviceBackend *be = pccl::device_backend();
     if (stream != nullptr && be != nullptr && descriptor->count > 0) {
         pccl::DevPtrInfo pi{};
-        // an event on the caller's stream marks the input's producers; the op waits for it, the caller does not. A
-        // stream with nothing pending needs no event: its marker would cost a GPU round trip per op (the small ops of
-        // a blocking call measured ~50 us slower with it, profiles/r5/full/)
+        // an event on the caller's stream marks the input's producers; the op waits for it, the caller does not.
+        // (Skipping it for an idle stream, checked with hipStreamQuery, saved ~20 us per small op but was followed
+        // by a SIGSEGV inside that call on a peer thread once in three GPU suites, profiles/r5/full2/: not kept.)
         const auto s = static_cast<pccl::DevStream>(*stream);
-        if (be->pointer_info(sendbuff, pi) && pi.is_device && be->stream_query(s) != 1) {
+        if (be->pointer_info(sendbuff, pi) && pi.is_device) {
             req.ready = pccl::client::event_pool().get();
             if (req.ready == nullptr || !be->event_record(req.ready, s)) {
                 pccl::client::event_pool().put(req.ready);

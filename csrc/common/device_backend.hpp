@@ -131,8 +131,6 @@ public:
                              DevStream s) = 0;
     virtual bool outer_sgd(float *outer, float *mom, const float *pg, void *local, size_t count, DType local_t,
                            const kernels::OuterSgdParams &p, DevStream s) = 0;
-    // 1: every piece of work queued on `s` so far has completed, 0: some is pending, -1: error (host-side check)
-    virtual int stream_query(DevStream s) = 0;
 };
 
 // Waits for `e` by polling with short sleeps (2 us doubling to 100 us) instead of the runtime's synchronize, which

@@ -243,6 +243,27 @@ void bt_handler(int) {
         }
     }
 }
+// fatal signals (PCCL_DEBUG_BACKTRACE_SIGNAL): the faulting thread's native frames, then the handler that was
+// installed before (e.g. Python's faulthandler, which adds the Python stacks) or the default action
+struct sigaction g_prev_fatal[32];
+void fatal_handler(int sig, siginfo_t *info, void *uctx) {
+    void *frames[64];
+    const int n = ::backtrace(frames, 64);
+    char hdr[96];
+    const int k = std::snprintf(hdr, sizeof(hdr), "[pccl] fatal signal %d (addr %p) tid %ld:\n", sig,
+                                info ? info->si_addr : nullptr, static_cast<long>(::syscall(SYS_gettid)));
+    if (k > 0) (void)!::write(2, hdr, static_cast<size_t>(k));
+    ::backtrace_symbols_fd(frames, n, 2);
+    const struct sigaction &prev = g_prev_fatal[sig & 31];
+    if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
+        prev.sa_sigaction(sig, info, uctx);
+    } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler != nullptr) {
+        prev.sa_handler(sig);
+    } else {
+        ::signal(sig, SIG_DFL);
+        ::raise(sig);
+    }
+}
 } // namespace
 
 void install_debug_backtrace_signal() {
@@ -255,6 +276,12 @@ void install_debug_backtrace_signal() {
         sa.sa_handler = bt_handler;
         sa.sa_flags = SA_RESTART;
         ::sigaction(SIGUSR2, &sa, nullptr);
+        for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) {
+            struct sigaction fa{};
+            fa.sa_sigaction = fatal_handler;
+            fa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+            ::sigaction(sig, &fa, &g_prev_fatal[sig & 31]);
+        }
     });
 }
 

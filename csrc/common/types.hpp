@@ -108,8 +108,10 @@ void fault_stall(const char *point, uint64_t seq);
 void fault_delay(uint64_t tag);
 bool fault_delay_armed(); // PCCL_FAULT_DELAY is set (ops then initiate on their worker, after the delay)
 
-// PCCL_DEBUG_BACKTRACE_SIGNAL=1 (debugging hangs on the GPU box, where debuggers may not attach): SIGUSR2 prints the
-// native backtrace of every thread of the process to stderr (each thread is signalled in turn).
+// PCCL_DEBUG_BACKTRACE_SIGNAL=1 (debugging hangs and crashes on the GPU box, where debuggers may not attach): SIGUSR2
+// prints the native backtrace of every thread of the process to stderr (each thread is signalled in turn), and a
+// fatal signal (SIGSEGV / SIGBUS / SIGFPE / SIGILL) prints the faulting thread's before the previously installed
+// handler (e.g. Python's faulthandler) runs.
 void install_debug_backtrace_signal();
 
 } // namespace pccl

@@ -376,12 +376,6 @@ public:
         n_partials = grid;
         return true;
     }
-    int stream_query(DevStream s) override {
-        const hipError_t r = hipStreamQuery(static_cast<hipStream_t>(s));
-        if (r == hipSuccess) return 1;
-        if (r == hipErrorNotReady) return 0;
-        return -1;
-    }
     bool fill_test_pattern(void *dev_ptr, size_t n_u64, DevStream s) override {
         return hipk::launch_test_pattern(dev_ptr, n_u64, static_cast<hipStream_t>(s));
     }

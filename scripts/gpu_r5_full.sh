@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${OUTDIR:-r5_full}
 mkdir -p $OUT
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PCCL_DEBUG_BACKTRACE_SIGNAL=${PCCL_DEBUG_BACKTRACE_SIGNAL:-1}
 log() { echo "[$(date +%T)] $*" >> $OUT/steps.log; }
 log pytest
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider -rfE \

@@ -13,6 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# a crash inside the library prints the faulting thread's native frames before Python's faulthandler runs (and
+# SIGUSR2 dumps every thread of a hung test); the library reads this when it initialises
+os.environ.setdefault("PCCL_DEBUG_BACKTRACE_SIGNAL", "1")
 os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
 
 
