@@ -186,7 +186,10 @@ void Client::run_op(const std::shared_ptr<OpState> &op) {
     }
     if (op->req.ready) { // stream-ordered op: its input's producers (overlapped with the master round trip)
         if (commenced) {
-            event_wait_polling(device_backend(), op->req.ready);
+            // usually complete by now or within microseconds (an idle stream's marker): spin briefly before the
+            // sleeping poll, whose 2-100 us back-off would round a short wait up
+            DeviceBackend *be = device_backend();
+            if (!spin_until([&] { return be->event_query(op->req.ready) != 0; })) event_wait_polling(be, op->req.ready);
             trace_mark("input_ready");
         }
         event_pool().put(op->req.ready);
