@@ -5,8 +5,8 @@
 
 Layout: the job always has ``--peers`` peers (default 8, the config's peer count), spread evenly over the N GPUs:
   N == 1 : all 8 peers are threads of this process on cuda:0 (as literally as one GPU allows).
-  N  > 1 : launched by torch.distributed.run, one process per GPU (LOCAL_RANK), 8/N peer threads per process;
-           rank 0 also hosts the CCoIP master. torch.distributed (gloo) only carries the bench's own barriers,
+  N  > 1 : launched by torch.distributed.run, one process per GPU (LOCAL_RANK), 8/N peer threads per process, each
+           process bound to its GPU's NUMA node (extra.numa_bind); rank 0 also hosts the CCoIP master. torch.distributed (gloo) only carries the bench's own barriers,
            the master port and the max-over-ranks of the timings.
 The total work (8 x 1 GiB) is fixed as N grows, so ``scaling`` is "strong".
 
@@ -821,35 +821,49 @@ def extras_in_child(job, a):
     return res.get("extra", {}), res.get("sweep", {})
 
 
+def _gpu_numa_node(local_rank: int) -> int:
+    """NUMA node of the GPU this rank drives (cuda:LOCAL_RANK), from its PCI address (torch device properties) and
+    sysfs; -1 if unknown. Initialises the GPU runtime of this process."""
+    import torch
+    props = torch.cuda.get_device_properties(local_rank % max(1, torch.cuda.device_count()))
+    addr = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
+    with open(f"/sys/bus/pci/devices/{addr}/numa_node") as f:
+        return int(f.read().strip())
+
+
 def _numa_bind():
-    """PCCL_BENCH_NUMA_BIND=1: restrict the process to the CPUs of cuda:LOCAL_RANK's NUMA node (sysfs; before any GPU
-    call). Returns a description for extra, or None."""
-    if os.environ.get("PCCL_BENCH_NUMA_BIND") != "1":
+    """With several ranks (default on when WORLD_SIZE > 1; PCCL_BENCH_NUMA_BIND=0 / 1 overrides): restricts the
+    process to the CPUs of its GPU's NUMA node before it starts any thread of its own, so the pinned staging memory the
+    library allocates (first touch by these threads) and the socket copies stay on the socket the GPU's PCIe link is
+    attached to. The GPU is identified by its PCI address, not by the order of /sys/class/drm. Returns a description
+    for extra, or None."""
+    default = "1" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "0"
+    if os.environ.get("PCCL_BENCH_NUMA_BIND", default) != "1":
         return None
-    import glob
     try:
-        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        nodes = []
-        for card in sorted(glob.glob("/sys/class/drm/card*/device/numa_node")):
-            with open(os.path.join(os.path.dirname(card), "vendor")) as f:
-                if f.read().strip() != "0x1002":
-                    continue
-            with open(card) as f:
-                nodes.append(int(f.read().strip()))
-        node = nodes[local_rank % len(nodes)] if nodes else -1
+        node = _gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0")))
         if node < 0:
             return {"numa_bind": "no node"}
         with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
-            spec = f.read().strip()
-        cpus = set()
-        for part in spec.split(","):
-            lo, _, hi = part.partition("-")
-            cpus.update(range(int(lo), int(hi or lo) + 1))
+            cpus = _parse_cpulist(f.read())
         cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return {"numa_bind": "node outside the CPU mask", "numa_node": node}
         os.sched_setaffinity(0, cpus)
         return {"numa_node": node, "cpus": len(cpus)}
-    except (OSError, ValueError) as e:
+    except (OSError, ValueError, RuntimeError, AttributeError) as e:
         return {"numa_bind_error": repr(e)[:200]}
+
+
+def _parse_cpulist(spec: str) -> set:
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11}"""
+    cpus = set()
+    for part in spec.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
 
 
 def _peer_cpu_groups(local: int):

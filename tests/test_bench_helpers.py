@@ -86,3 +86,31 @@ def test_per_rank_diag_models_pcie_and_dram():
     # a rank without staging counters (e.g. an older library) still reports its socket bytes
     ring["per_rank"][1]["pcie"] = None
     assert "pcie_h2d_GB" not in bench._per_rank_diag(ring, S, P)[1]
+
+
+def test_parse_cpulist():
+    assert bench._parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench._parse_cpulist("5") == {5}
+
+
+def test_numa_bind_default_on_with_several_ranks(monkeypatch):
+    """N > 1: each rank binds to its GPU's NUMA node (by PCI address); N == 1 leaves the mask alone."""
+    if not os.path.exists("/sys/devices/system/node/node0/cpulist"):
+        return
+    own = os.sched_getaffinity(0)
+    monkeypatch.setattr(bench, "_gpu_numa_node", lambda local_rank: 0)
+    monkeypatch.delenv("PCCL_BENCH_NUMA_BIND", raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench._numa_bind() is None and os.sched_getaffinity(0) == own
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    try:
+        with open("/sys/devices/system/node/node0/cpulist") as f:
+            node0 = bench._parse_cpulist(f.read())
+        res = bench._numa_bind()
+        if node0 & own:
+            assert res == {"numa_node": 0, "cpus": len(node0 & own)}
+            assert os.sched_getaffinity(0) == node0 & own
+        monkeypatch.setenv("PCCL_BENCH_NUMA_BIND", "0")
+        assert bench._numa_bind() is None
+    finally:
+        os.sched_setaffinity(0, own)
