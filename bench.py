@@ -5,8 +5,9 @@
 
 Layout: the job always has ``--peers`` peers (default 8, the config's peer count), spread evenly over the N GPUs:
   N == 1 : all 8 peers are threads of this process on cuda:0 (as literally as one GPU allows).
-  N  > 1 : launched by torch.distributed.run, one process per GPU (LOCAL_RANK), 8/N peer threads per process, each
-           process bound to its GPU's NUMA node (extra.numa_bind); rank 0 also hosts the CCoIP master. torch.distributed (gloo) only carries the bench's own barriers,
+  N  > 1 : launched by torch.distributed.run, one process per GPU (LOCAL_RANK), 8/N peer threads per process;
+           rank 0 also hosts the CCoIP master.
+Every process binds to its GPU's NUMA node before it starts peer threads (extra.numa_bind). torch.distributed (gloo) only carries the bench's own barriers,
            the master port and the max-over-ranks of the timings.
 The total work (8 x 1 GiB) is fixed as N grows, so ``scaling`` is "strong".
 
@@ -832,13 +833,12 @@ def _gpu_numa_node(local_rank: int) -> int:
 
 
 def _numa_bind():
-    """With several ranks (default on when WORLD_SIZE > 1; PCCL_BENCH_NUMA_BIND=0 / 1 overrides): restricts the
-    process to the CPUs of its GPU's NUMA node before it starts any thread of its own, so the pinned staging memory the
-    library allocates (first touch by these threads) and the socket copies stay on the socket the GPU's PCIe link is
-    attached to. The GPU is identified by its PCI address, not by the order of /sys/class/drm. Returns a description
-    for extra, or None."""
-    default = "1" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "0"
-    if os.environ.get("PCCL_BENCH_NUMA_BIND", default) != "1":
+    """PCCL_BENCH_NUMA_BIND (default 1; 0 = off): restricts the process to the CPUs of its GPU's NUMA node before it
+    starts any thread of its own, so the pinned staging memory the library allocates (first touch by these threads)
+    and the socket copies stay on the socket the GPU's PCIe link is attached to. The GPU is identified by its PCI
+    address, not by the order of /sys/class/drm. N == 1, on top of the per-CCD spread: 330.3 / 328.3 vs 332.9 /
+    331.1 ms per op, interleaved (profiles/r5/b18/). Returns a description for extra, or None."""
+    if os.environ.get("PCCL_BENCH_NUMA_BIND", "1") != "1":
         return None
     try:
         node = _gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0")))
@@ -923,7 +923,8 @@ def _cpu_spread():
 
 def main():
     spread = _cpu_spread()
-    numa = _numa_bind()
+    several = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    numa = _numa_bind() if several else None  # (N == 1: after the multi-process measurements, see below)
     a = _args()
     # stdout carries exactly one line, the result JSON: everything else any library, child process or the gloo
     # rendezvous writes to fd 1 goes to stderr
@@ -939,8 +940,10 @@ def main():
     # time-sliced queues made config 5 on the xGMI path run into its deadline (55.9 vs 8.9 ms per op standalone,
     # profiles/r5/b2 vs b4) and the small-op latency bimodal
     pre = {}
-    if not a.extras_child and not a.quick and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+    if not a.extras_child and not a.quick and not several:
         pre = pre_gpu_measurements(a)
+    if not several:  # reading the GPU's PCI address initialises this process's GPU runtime
+        numa = _numa_bind()
     job = Job(a)
     nbytes = a.mib << 20
     P = job.total

@@ -93,16 +93,13 @@ def test_parse_cpulist():
     assert bench._parse_cpulist("5") == {5}
 
 
-def test_numa_bind_default_on_with_several_ranks(monkeypatch):
-    """N > 1: each rank binds to its GPU's NUMA node (by PCI address); N == 1 leaves the mask alone."""
+def test_numa_bind_to_the_gpus_node(monkeypatch):
+    """Each process binds to its GPU's NUMA node (by PCI address), unless PCCL_BENCH_NUMA_BIND=0."""
     if not os.path.exists("/sys/devices/system/node/node0/cpulist"):
         return
     own = os.sched_getaffinity(0)
     monkeypatch.setattr(bench, "_gpu_numa_node", lambda local_rank: 0)
     monkeypatch.delenv("PCCL_BENCH_NUMA_BIND", raising=False)
-    monkeypatch.setenv("WORLD_SIZE", "1")
-    assert bench._numa_bind() is None and os.sched_getaffinity(0) == own
-    monkeypatch.setenv("WORLD_SIZE", "2")
     try:
         with open("/sys/devices/system/node/node0/cpulist") as f:
             node0 = bench._parse_cpulist(f.read())
