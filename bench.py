@@ -887,14 +887,16 @@ def _peer_cpu_groups(local: int):
 
 
 def _cpu_spread():
-    """PCCL_BENCH_CPU_SPREAD=k (default 3 on one GPU, 0 = off; off by default with several ranks): restrict the
+    """PCCL_BENCH_CPU_SPREAD=k (default 4 on one GPU, 0 = off; off by default with several ranks): restrict the
     process to the first k CPUs of every L3 domain (CCD) in its affinity mask, before any thread exists. The
     loopback-TCP ring moves ~15 GB through socket copies per op on a 16-CPU quota; with all 256 CPUs of the host in the
     mask its ~40 threads migrate over every CCD and both sockets and burst past the quota (the cgroup then throttles
     the whole process, GPU feeding included), while k cores per CCD keep the memory bandwidth of every CCD at hand.
     Measured, 8 peers x 1 GiB, 3 runs each (profiles/r3/cpu_spread/): all 256 CPUs 374 / 355 / 389 ms, 2 per CCD
-    337 / 349 / 342, 3 per CCD 330 / 344 / 328, 4 per CCD 329 / 331 / 359. Returns a description for extra."""
-    default = "3" if int(os.environ.get("WORLD_SIZE", "1")) == 1 else "0"
+    337 / 349 / 342, 3 per CCD 330 / 344 / 328, 4 per CCD 329 / 331 / 359. Round 5, with the NUMA binding on top
+    (the GPU's node keeps k x 8 CPUs), interleaved over two passes (profiles/r5/b19/): 2 per CCD 362 / 425, 3 per CCD
+    324.6 / 327.0, 4 per CCD 322.7 / 324.4, 8 per CCD 322.2 / 326.0 ms. Returns a description for extra."""
+    default = "4" if int(os.environ.get("WORLD_SIZE", "1")) == 1 else "0"
     k = int(os.environ.get("PCCL_BENCH_CPU_SPREAD", default))
     if k <= 0:
         return None

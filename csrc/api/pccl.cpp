@@ -232,22 +232,16 @@ static pcclResult_t start_all_reduce(const void *sendbuff, void *recvbuff, const
     pccl::DeviceBackend *be = pccl::device_backend();
     if (stream != nullptr && be != nullptr && descriptor->count > 0) {
         pccl::DevPtrInfo pi{};
-        // an event on the caller's stream marks the input's producers; the op waits for it, the caller does not.
+        // an event on the caller's stream marks the input's producers; the op waits for it, the caller does not. The
+        // client records it on this thread right after the op's initiate packet went out (Client::arm_ready).
         // (Skipping it for an idle stream, checked with hipStreamQuery, saved ~20 us per small op but was followed
         // by a SIGSEGV inside that call on a peer thread once in three GPU suites, profiles/r5/full2/: not kept.)
-        const auto s = static_cast<pccl::DevStream>(*stream);
         if (be->pointer_info(sendbuff, pi) && pi.is_device) {
-            req.ready = pccl::client::event_pool().get();
-            if (req.ready == nullptr || !be->event_record(req.ready, s)) {
-                pccl::client::event_pool().put(req.ready);
-                return pcclInvalidArgument;
-            }
+            req.stream_ordered = true;
+            req.ready_stream = static_cast<pccl::DevStream>(*stream);
         }
     }
-    if (!comm->client->all_reduce_async(req, inline_run)) {
-        pccl::client::event_pool().put(req.ready);
-        return pcclInvalidArgument;
-    }
+    if (!comm->client->all_reduce_async(req, inline_run)) return pcclInvalidArgument;
     handle_out->comm = const_cast<pcclComm_t *>(comm);
     handle_out->tag = descriptor->tag;
     return pcclSuccess;

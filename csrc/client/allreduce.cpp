@@ -113,12 +113,28 @@ bool Client::all_reduce_async(const ReduceRequest &req, bool inline_run) {
         ops_[req.tag] = op;
     }
     if (inline_run) {
-        run_op(op);
+        run_op(op, true);
     } else {
         if (!fault_delay_armed()) initiate_op(*op);
-        workers_.submit([this, op] { run_op(op); });
+        arm_ready(*op);
+        workers_.submit([this, op] { run_op(op, false); });
     }
     return true;
+}
+
+// A stream-ordered op's readiness event, on the submitting thread (before the call returns: it marks the work queued
+// on the caller's stream up to this call). If it cannot be recorded the stream is synchronised instead.
+void Client::arm_ready(OpState &op) {
+    if (!op.req.stream_ordered || op.req.ready) return;
+    op.req.stream_ordered = false;
+    DeviceBackend *be = device_backend();
+    DevEvent e = be ? event_pool().get() : nullptr;
+    if (e && be->event_record(e, op.req.ready_stream)) {
+        op.req.ready = e;
+        return;
+    }
+    event_pool().put(e);
+    if (be) be->stream_sync(op.req.ready_stream);
 }
 
 // Snapshot of the ring, the buffers' location and the initiate packet. The ring cannot change while the op is
@@ -151,13 +167,14 @@ void Client::initiate_op(OpState &op) {
     op.init_sent = master_.send(init);
 }
 
-void Client::run_op(const std::shared_ptr<OpState> &op) {
+void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
     const uint64_t tag = op->req.tag;
     low_timer_slack();
     if (!op->initiated) {
         fault_delay(tag);
         initiate_op(*op);
     }
+    if (on_caller) arm_ready(*op); // (async ops armed it on the submitting thread before the hand-off)
     OpTrace trace;
     current_trace() = trace_ops_enabled() ? &trace : nullptr;
     char range_name[96];

@@ -70,8 +70,11 @@ struct ReduceRequest {
     ReduceOp op = ReduceOp::Sum;
     uint64_t tag = 0;
     bool scratch = false; // internal: dst is library scratch, no abort backup needed (hierarchical inner ring)
-    // stream-ordered ops (pcclxAllReduce*OnStream): recorded on the caller's stream at submission; the op waits for it
+    // stream-ordered ops (pcclxAllReduce*OnStream): an event recorded on `ready_stream` on the submitting thread,
+    // right after the initiate packet went out (its host cost overlaps the master round trip); the op waits for it
     // before its data path reads `src`, then returns it to the event pool
+    bool stream_ordered = false;
+    DevStream ready_stream = nullptr;
     DevEvent ready = nullptr;
 };
 
@@ -209,7 +212,9 @@ private:
 
     // collectives
     void initiate_op(OpState &op);
-    void run_op(const std::shared_ptr<OpState> &op);
+    // on_caller: running on the submitting thread (blocking call), which then also records the readiness event
+    void run_op(const std::shared_ptr<OpState> &op, bool on_caller);
+    void arm_ready(OpState &op);
     // returns {success, abort_received}
     std::pair<bool, bool> ring_reduce_host(OpState &op, const RingView &rv, uint64_t seq);
     std::pair<bool, bool> ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device);
