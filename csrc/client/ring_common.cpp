@@ -137,8 +137,14 @@ size_t stripe_count(size_t bytes, size_t conns, const Shape &shape) {
     return per == 0 ? 1 : std::max<size_t>(1, std::min(p, (bytes + per - 1) / per));
 }
 
+// The stripe-count bound min(stripes, conns, bytes / stripe_min) of the op's largest step: it grows with the step
+// size, so it bounds the stripes of every step of the op (the stripe count itself does not: rounding stripes up to
+// kStripeAlign can give a slightly larger step fewer stripes: with 256 KiB stripes over 4 connections, 2 MiB + 2 KiB
+// go in 3 stripes of <= 768 KiB, 2 MiB in 4)
 size_t op_stripes(const Shape &shape, size_t conns) {
-    return shape.op_max_step ? stripe_count(shape.op_max_step, conns, shape) : shape.stripes;
+    if (!shape.op_max_step) return shape.stripes;
+    if (shape.reference) return 1;
+    return std::min({shape.stripes, std::max<size_t>(1, conns), std::max<size_t>(1, shape.op_max_step / shape.stripe_min)});
 }
 
 // ------------------------------------------------------------------------------------------------------------------

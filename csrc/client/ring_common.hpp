@@ -104,7 +104,8 @@ size_t stripe_conn(uint64_t seq, uint64_t tag, size_t k, size_t pool, const Shap
 Shape op_shape(const Shape &shape, size_t max_step_bytes);
 // stripes plan_stripes(bytes, conns, shape) makes (without building the plan)
 size_t stripe_count(size_t bytes, size_t conns, const Shape &shape);
-// stripes of the op's largest step on a pool of `conns` connections (shape.stripes if op_max_step is unset)
+// upper bound of the stripes of every step of the op on a pool of `conns` connections (the size of its connection
+// group and the number of its sender threads; shape.stripes if op_max_step is unset)
 size_t op_stripes(const Shape &shape, size_t conns);
 
 // Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first

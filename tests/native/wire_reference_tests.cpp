@@ -210,6 +210,16 @@ TEST(stripe_count_matches_plan_and_pools_of_any_size) {
     for (size_t conns : {1ul, 2ul, 3ul, 4ul, 16ul})
         for (size_t bytes : {0ul, 1ul, 4096ul, (1ul << 20) - 1, 1ul << 20, (3ul << 20) + 7, 9000011ul * 2, 64ul << 20})
             EXPECT(stripe_count(bytes, conns, sh) == plan_stripes(bytes, conns, sh).off.size());
+    // an op's group bounds the stripes of every step, also where rounding gives a larger step fewer stripes
+    Shape s256 = sh;
+    s256.stripe_min = 256u << 10;
+    EXPECT(stripe_count((2u << 20) + 2048, 4, s256) == 3 && stripe_count(2u << 20, 4, s256) == 4);
+    for (size_t conns : {1ul, 3ul, 4ul, 16ul})
+        for (size_t maxb : {(2ul << 20) + 2048, (3ul << 20) + 4097, 9000011ul, 64ul << 20}) {
+            const Shape op256 = op_shape(s256, maxb);
+            for (size_t b = maxb > 600000 ? maxb - 600000 : 0; b <= maxb; b += 997)
+                EXPECT(stripe_count(b, conns, s256) <= op_stripes(op256, conns));
+        }
     // neighbours with pools of different sizes: both ends of a pool derive the same groups from the op's largest step
     const Shape op = op_shape(sh, 9000011ul * 2 / 3 + 2);
     for (size_t pool : {1ul, 2ul, 3ul})

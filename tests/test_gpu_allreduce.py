@@ -636,3 +636,26 @@ def test_device_ring_pcie_bytes_match_model(hip, monkeypatch):
     # still being counted when peer 0 sampled (at most its last steps: bounded by the op itself)
     assert 3 * S + 3 * es <= d2h <= 2 * (3 * S) + 3 * es, (d2h, S)
     assert 3 * (4 * S // 3) <= h2d <= 2 * 3 * (4 * S // 3) + 3 * es + 16, (h2d, S)
+
+
+def test_device_ring_stripe_bound_with_uneven_chunks(hip, monkeypatch):
+    """Chunks of 2 MiB + 4 bytes and 2 MiB with 256 KiB stripes over 4 connections: the larger chunk rounds to 3
+    stripes, the smaller one to 4. The op's connection group and sender threads are sized by the stripe bound of its
+    largest step, which covers every step (sizing them by the largest step's own stripe count left a stripe unsent)."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    monkeypatch.setenv("PCCL_STRIPE_MIN_BYTES", str(256 << 10))
+    n = 2 * 524288 + 1  # fp32: chunks of 524289 and 524288 elements
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(rank + 1), device=hip)
+        y = torch.empty_like(x)
+        for tag in range(2):
+            comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=tag)
+        torch.cuda.synchronize()
+        return float(y.min()), float(y.max()), comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    with local_master() as addr:
+        res = run_threaded_peers(2, fn, address=addr, timeout=120, comm_kwargs={"p2p_connection_pool_size": 4})
+    for lo, hi, path in res:
+        assert path == pccl.ReducePath.DEVICE_RING.value
+        assert lo == hi == 3.0
