@@ -476,6 +476,62 @@ class _full_cpu_mask:
         return False
 
 
+class _cpu_mask:
+    """Runs a block with the given CPU mask; threads and processes started inside inherit it."""
+
+    def __init__(self, mask):
+        self.mask = set(mask)
+
+    def __enter__(self):
+        self.own = os.sched_getaffinity(0)
+        if self.mask != self.own:
+            os.sched_setaffinity(0, self.mask)
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.own)
+        return False
+
+
+def _gpu_numa_node_child() -> int:
+    """_gpu_numa_node(0) read by a child process, so this process's GPU runtime stays uninitialised; -1 if unknown."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, "-c", "import bench; print(bench._gpu_numa_node(0))"], cwd=ROOT,
+                           capture_output=True, text=True, timeout=180)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else -1
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return -1
+
+
+# baseline_configs runs that take _config_tcp_mask's mask. Interleaved over two passes (profiles/r5/b23/): config 5 over
+# TCP 372 / 367 ms per op on the node vs 383 / 414 with the full mask (kill -> survivors' failed op 193 / 187 vs
+# 220 / 219 ms), config 3 uint8 1.09 / 1.11 vs 1.21 / 1.17 s; the collocated run (its relay moves 10 Gbit/s flows)
+# is faster with the full mask: 62.3 / 66.1 vs 60.3 / 57.3 Gbit/s.
+_NODE_MASKED = ("config5_kill_rejoin_tcp", "config3_wan_50ms")
+
+
+def _config_tcp_mask():
+    """CPU mask for the one-process-per-peer runs over loopback TCP named in _NODE_MASKED. PCCL_BENCH_CONFIG_MASK:
+    full (the mask from before the per-CCD spread), spread (the bench's per-CCD spread), numa (default: the spread
+    restricted to the GPU's NUMA node, as the headline runs). None = the full mask."""
+    mode = os.environ.get("PCCL_BENCH_CONFIG_MASK", "numa")
+    if mode == "full" or not os.environ.get("PCCL_BENCH_FULL_CPUS"):
+        return None  # (no spread applied: the harnesses keep this process's mask)
+    own = os.sched_getaffinity(0)
+    if mode == "spread":
+        return own
+    node = _gpu_numa_node_child()
+    if node < 0:
+        return own
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = _parse_cpulist(f.read()) & own
+    except (OSError, ValueError):
+        return own
+    return cpus if len(cpus) >= 8 else own
+
+
 def latency_native(peers):
     """Small-op latency of the xGMI/IPC path without Python in the loop: pccl_amd/lib/pccl_latency (the C API with
     hipMalloc'd buffers, threaded peers on cuda:0, csrc/tools/latency_native.hip), 1 MiB bf16 at `peers` and 2 peers;
@@ -568,16 +624,21 @@ def baseline_configs(a, peers):
             ("collocated_5ms_4peers", ["wan_quantized.py", "--peers", "4", "--mib", "2048", "--latency-ms", "5",
                                        "--flow-mbit", "10000", "--link-mbit", "50000", "--pool", "16",
                                        "--concurrent", "8", "--formats", "fp32"], 120)]
+    only = os.environ.get("PCCL_BENCH_CONFIGS")
+    if only:
+        runs = [r for r in runs if r[0] in only.split(",")]
     out = {}
     env = dict(os.environ)
     env.pop("PCCL_DISABLE_IPC", None)  # set by this process's TCP-ring phases; the harnesses choose per run
+    tcp_mask = _config_tcp_mask()
     for name, args, limit in runs:
         _log(f"{name}: {' '.join(args)}")
         t0 = time.time()
         try:
             # the process's CPU mask from before the bench's per-CCD spread (as for the latency measurements): one
-            # process per peer, whose spinning op threads and shared-memory barriers suffer when spread over CCDs
-            with _full_cpu_mask():
+            # process per peer, whose spinning op threads and shared-memory barriers suffer when spread over CCDs;
+            # config 5 over TCP and config 3 run on the GPU's NUMA node instead (_config_tcp_mask)
+            with (_cpu_mask(tcp_mask) if tcp_mask and name in _NODE_MASKED else _full_cpu_mask()):
                 r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", args[0]), *args[1:],
                                     *(["--timeout", str(limit - 40)] if args[0] == "fault_tolerance.py" else [])],
                                    capture_output=True, text=True, timeout=limit, env=env)

@@ -111,3 +111,23 @@ def test_numa_bind_to_the_gpus_node(monkeypatch):
         assert bench._numa_bind() is None
     finally:
         os.sched_setaffinity(0, own)
+
+
+def test_config_tcp_mask_modes(monkeypatch):
+    own = os.sched_getaffinity(0)
+    monkeypatch.setenv("PCCL_BENCH_FULL_CPUS", ",".join(map(str, sorted(own))))
+    monkeypatch.setenv("PCCL_BENCH_CONFIG_MASK", "full")
+    assert bench._config_tcp_mask() is None
+    monkeypatch.setenv("PCCL_BENCH_CONFIG_MASK", "spread")
+    assert bench._config_tcp_mask() == own
+    monkeypatch.setenv("PCCL_BENCH_CONFIG_MASK", "numa")
+    monkeypatch.setattr(bench, "_gpu_numa_node_child", lambda: -1)
+    assert bench._config_tcp_mask() == own  # node unknown: the spread
+    monkeypatch.setattr(bench, "_gpu_numa_node_child", lambda: 0)
+    m = bench._config_tcp_mask()
+    assert m and m <= own
+    monkeypatch.delenv("PCCL_BENCH_FULL_CPUS")
+    assert bench._config_tcp_mask() is None  # no spread applied
+    with bench._cpu_mask({min(own)}):
+        assert os.sched_getaffinity(0) == {min(own)}
+    assert os.sched_getaffinity(0) == own
