@@ -588,7 +588,9 @@ def latency_python_processes(peers):
     variants = {k: {"median_us": v["median_us"], "p90_us": v["p90_us"]} for k, v in row.items()
                 if isinstance(v, dict) and "median_us" in v}
     return {"peers": peers, "path": row["path"], "blocking_median_us": row["all_reduce"]["median_us"],
-            "blocking_p90_us": row["all_reduce"]["p90_us"], "async_median_us": row["ready"]["median_us"],
+            "blocking_p90_us": row["all_reduce"]["p90_us"],
+            "async_median_us": row["async"]["median_us"] if "async" in row else None,
+            "ready_median_us": row["ready"]["median_us"] if "ready" in row else None,
             "variants": variants}
 
 

@@ -42,7 +42,7 @@ def main():
         print(json.dumps({"rep": rep, "wall_s": round(t1 - t0, 2), "cores_busy": round(d["usage_usec"] / 1e6 / (t1 - t0), 2),
                           "nr_throttled": d["nr_throttled"], "throttled_ms": round(d["throttled_usec"] / 1e3, 1),
                           "blocking_median_us": row.get("all_reduce", {}).get("median_us"),
-                          "async_median_us": row.get("ready", {}).get("median_us"),
+                          "ready_median_us": row.get("ready", {}).get("median_us"),
                           "cpus_allowed": len(os.sched_getaffinity(0))}), flush=True)
 
 
