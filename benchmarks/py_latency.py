@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--variants", default="all_reduce,async,ready",
                     help="comma list of all_reduce, async, ready, ready_inline, sync_inline, sync_worker")
+    ap.add_argument("--trace-dir", default="", help="PCCL_TRACE_OPS=1 in every peer, its stderr to <dir>/peer<r>.err")
     ap.add_argument("--peer", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--master", default="")
     ap.add_argument("--rank", type=int, default=0)
@@ -124,6 +125,11 @@ def main():
     env = dict(os.environ)
     if a.device.startswith("cuda"):  # several processes on one GPU: 2 hardware queues each (README), so the peers'
         env.setdefault("GPU_MAX_HW_QUEUES", "2")  # queues fit the GPU's slots without time-slicing
+    errs = []
+    if a.trace_dir:
+        os.makedirs(a.trace_dir, exist_ok=True)
+        env["PCCL_TRACE_OPS"] = "1"
+        errs = [open(os.path.join(a.trace_dir, f"peer{r}.err"), "w") for r in range(a.peers)]
     master = pccl.MasterNode(f"0.0.0.0:{port}")
     master.run()
     try:
@@ -131,7 +137,8 @@ def main():
                                    f"127.0.0.1:{port}", "--rank", str(r), "--peers", str(a.peers), "--iters",
                                    str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device,
                                    "--variants", a.variants],
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                                  stdout=subprocess.PIPE, stderr=errs[r] if errs else subprocess.PIPE, text=True,
+                                  env=env)
                  for r in range(a.peers)]
         outs = communicate_all(procs, 600, DIAG_SIGNALS)
     finally:
@@ -140,7 +147,7 @@ def main():
     res = []
     for p, (o, e) in zip(procs, outs):
         if p.returncode != 0:
-            raise SystemExit(f"peer failed rc={p.returncode}: {e[-3000:]}")
+            raise SystemExit(f"peer failed rc={p.returncode}: {(e or '')[-3000:]}")
         res.append(json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]))
     names = {0: "none", 1: "host_ring", 2: "device_ring", 3: "ipc", 4: "hier"}
     summary = {"peers": a.peers, "device": a.device, "iters": a.iters, "processes": "one per peer", "sizes": {}}
