@@ -61,15 +61,29 @@ def peer(a):
             torch.cuda.synchronize()
 
     log(event="proc_start", t_proc=T_PROC)
+    # the peer's tensor exists before it connects, as in the reference's stress-test peer (its weights are created
+    # before connect(), stresstest_peer.py:134-144): allocating and first touching 1 GiB of HBM is the application's
+    # start-up, not part of the rejoin
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    x = torch.empty((a.mib << 20) // (2 if dtype == torch.bfloat16 else 4), device=dev, dtype=dtype)
+    x.fill_(1.0)
+    sync()
     comm = pccl.Communicator(a.master, 0, p2p_connection_pool_size=a.pool)
     t0 = time.time()
     log(event="connect_call")
+    # the device ring's staging for this op size fills the library's pools while connect() waits for admission
+    # (inside the measured connect -> first op window; a fresh process otherwise allocates it in its first op)
+    reserve = None
+    if dev.type == "cuda" and a.transport == "tcp" and not a.no_reserve:
+        reserve = threading.Thread(target=pccl.memory.reserve_device_ring_staging,
+                                   args=(a.mib << 20, a.peers), kwargs={"device": dev, "in_place": True}, daemon=True)
+        reserve.start()
     comm.connect(n_attempts=120)
     log(event="connected", sec=time.time() - t0)
+    if reserve is not None:
+        reserve.join()
     if not a.joiner:
         wait_for_world(comm, a.peers, timeout=300)
-    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    x = torch.empty((a.mib << 20) // (2 if dtype == torch.bfloat16 else 4), device=dev, dtype=dtype)
     optimized = False
     saw_small = False
     post = 0
@@ -142,7 +156,8 @@ def run(a) -> dict:
     master = pccl.MasterNode(addr)
     master.run()
     common = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
-              "--deadline", str(deadline), "--post-ops", str(a.post_ops), "--master", addr]
+              "--deadline", str(deadline), "--post-ops", str(a.post_ops), "--master", addr, "--transport", a.transport,
+              *(["--no-reserve"] if a.no_reserve else [])]
     # short bandwidth probes (the reference's 10 s per pair is a WAN setting); several processes on one GPU: 2 hardware
     # queues each (README)
     env = {"PCCL_BENCHMARK_MILLIS": str(a.probe_ms), "PCCL_NUM_BENCHMARK_CONNECTIONS": "2",
@@ -251,6 +266,9 @@ def run(a) -> dict:
         "kill_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
         "joiner_connect_to_first_exact_op_ms": ms(j_first - j_connect[0]) if j_first and j_connect else None,
         "joiner_process_start_to_first_exact_op_ms": ms(j_first - j_proc[0]) if j_first and j_proc else None,
+        # connect() returns once the survivors admitted the replacement at their next op boundary and the ring with it
+        # is established
+        "joiner_connect_call_ms": ms(sel("connected", rank=joiner)[0]["sec"]) if sel("connected", rank=joiner) else None,
         "joiner_first_op_ms": round(1e3 * min(j_ok, key=lambda x: x["t"])["sec"], 1) if j_ok else None,
         "joiner_first_op_staging_alloc_ms": round(min(j_ok, key=lambda x: x["t"]).get("alloc_ms", 0), 1) if j_ok else None,
         "survivors_admission_vote_ms": ms(max(x["sec"] for x in admits)) if admits else None,
@@ -284,6 +302,8 @@ def main():
     ap.add_argument("--probe-ms", type=int, default=300, help="bandwidth probe per peer pair (PCCL_BENCHMARK_MILLIS)")
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
+    ap.add_argument("--no-reserve", action="store_true",
+                    help="no staging reserve next to connect() (the first op allocates it)")
     ap.add_argument("--rank", type=int, default=None)
     ap.add_argument("--master", default=None)
     ap.add_argument("--joiner", action="store_true")

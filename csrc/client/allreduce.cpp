@@ -388,3 +388,25 @@ extern "C" __attribute__((visibility("default"))) size_t pcclxPoolStats(uint64_t
     for (size_t i = 0; i < n && i < kN; ++i) out[i] = v[i];
     return kN;
 }
+
+// Fills the staging pools ahead of the first ops: leases `pinned_count` pinned buffers of `pinned_bytes` and
+// `device_count` HBM buffers of `device_bytes` on `device` at once and hands them back to the pools, which keep them
+// cached (PCCL_POOL_MAX_FREE_MIB). An application can run it next to connect(), whose admission wait it overlaps
+// (RCCL allocates its buffers at communicator init; these pools otherwise fill on the first op). 0 on success.
+extern "C" __attribute__((visibility("default"))) int pcclxPoolReserve(uint64_t pinned_bytes, uint32_t pinned_count,
+                                                                      uint64_t device_bytes, uint32_t device_count,
+                                                                      int device) {
+    using namespace pccl::client;
+    std::vector<Lease> held;
+    held.reserve(pinned_count + device_count);
+    for (uint32_t i = 0; i < pinned_count && pinned_bytes > 0; ++i) {
+        held.emplace_back(pinned_pool(), pinned_bytes);
+        if (!held.back().ok()) return 1;
+    }
+    for (uint32_t i = 0; i < device_count && device_bytes > 0; ++i) {
+        if (device < 0 || pccl::device_backend() == nullptr) return 2;
+        held.emplace_back(device_pool(), device_bytes, device);
+        if (!held.back().ok()) return 1;
+    }
+    return 0;
+}

@@ -170,6 +170,7 @@ def _load() -> ctypes.CDLL:
         "pcclxIpcStats": ([p(c_uint64)], None),
         "pcclxIpcStatsEx": ([p(c_uint64), c_size_t], c_size_t),
         "pcclxPoolStats": ([p(c_uint64), c_size_t, c_int], c_size_t),
+        "pcclxPoolReserve": ([c_uint64, c_uint32, c_uint64, c_uint32, c_int], c_int),
         "pcclxPcieStats": ([p(c_uint64), c_size_t], c_size_t),
         "pcclxMasterBandwidthTable": ([c_void_p, c_char_p, c_size_t], c_size_t),
         "pcclxMasterTopologyStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),

@@ -172,6 +172,34 @@ def staging_pool_stats(reset_peak: bool = False) -> dict:
     return res
 
 
+def reserve_staging(*, pinned_bytes: int = 0, pinned_count: int = 0, device_bytes: int = 0, device_count: int = 0,
+                    device=None) -> None:
+    """Fills the library's staging pools ahead of the first ops: ``pinned_count`` pinned host buffers of
+    ``pinned_bytes`` and ``device_count`` HBM buffers of ``device_bytes`` on ``device`` (default: the current GPU) are
+    allocated and kept cached for the ops' leases (``pcclxPoolReserve``). The call releases the GIL, so a thread can
+    run it next to ``Communicator.connect()``, whose wait for admission it then overlaps (otherwise a fresh process
+    allocates this staging inside its first op)."""
+    dev = -1
+    if device_count and device_bytes:
+        torch = _torch()
+        d = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dev = d.index if d.index is not None else torch.cuda.current_device()
+    rc = int(_native.C.pcclxPoolReserve(int(pinned_bytes), int(pinned_count), int(device_bytes), int(device_count), dev))
+    if rc != 0:
+        raise MemoryError(f"pcclxPoolReserve failed ({rc})")
+
+
+def reserve_device_ring_staging(nbytes: int, world: int, *, device=None, in_place: bool = False,
+                                segment_chunk: int = 128 << 20) -> None:
+    """reserve_staging with what one device-ring all-reduce of ``nbytes`` per peer at ``world`` peers leases: 3 pinned
+    send + 3 pinned receive + 3 HBM buffers of one ring chunk (at most the segment chunk, PCCL_SEGMENT_CHUNK_MIB), and
+    for an in-place op an HBM backup of the input (csrc/client/ring_device.cpp)."""
+    stage = min(-(-int(nbytes) // max(1, int(world))), int(segment_chunk)) + 4096
+    reserve_staging(pinned_bytes=stage, pinned_count=6, device_bytes=stage, device_count=3, device=device)
+    if in_place:
+        reserve_staging(device_bytes=int(nbytes), device_count=1, device=device)
+
+
 def pcie_stats() -> dict:
     """Bytes this process's device rings moved between pinned host staging and HBM so far (counted where the copies and
     the kernels that read / write pinned memory are queued): ``h2d`` and ``d2h``. With one process per GPU this is

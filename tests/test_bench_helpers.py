@@ -131,3 +131,8 @@ def test_config_tcp_mask_modes(monkeypatch):
     with bench._cpu_mask({min(own)}):
         assert os.sched_getaffinity(0) == {min(own)}
     assert os.sched_getaffinity(0) == own
+
+
+def test_pool_reserve_nothing_is_a_no_op():
+    import pccl_amd as pccl
+    pccl.memory.reserve_staging()  # zero counts: nothing leased, success

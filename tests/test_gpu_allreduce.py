@@ -638,6 +638,41 @@ def test_device_ring_pcie_bytes_match_model(hip, monkeypatch):
     assert 3 * (4 * S // 3) <= h2d <= 2 * 3 * (4 * S // 3) + 3 * es + 16, (h2d, S)
 
 
+def test_reserved_staging_serves_the_first_device_ring_op(hip, monkeypatch):
+    """pccl.memory.reserve_device_ring_staging (pcclxPoolReserve) fills the pools with what a device-ring op of that
+    size leases, so the op itself allocates nothing (benchmarks/fault_tolerance.py runs it next to a replacement's
+    connect()). Two threaded peers share the process's pools: reserved twice."""
+    monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
+    C = (48 << 20) + 4096  # one ring chunk (bytes), a size no other test leases
+    n = C  # bf16 elements per peer: 2 C bytes, W = 2 -> chunks of C bytes
+    for _ in range(2):
+        pccl.memory.reserve_device_ring_staging(2 * C, 2, device=hip)
+    st = pccl.memory.staging_pool_stats()
+    assert st["pinned"]["cached"] >= 12 * C and st["device"]["cached"] >= 6 * C, st
+    state = {}
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(rank + 1), device=hip, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        comm.all_reduce(x[:1024], y[:1024], op=pccl.ReduceOp.SUM, tag=0)  # connections up, both peers here
+        torch.cuda.synchronize()
+        if rank == 0:
+            state["before"] = pccl.memory.staging_pool_stats()
+        comm.all_reduce(x[:1024], y[:1024], op=pccl.ReduceOp.SUM, tag=1)  # (rank 0 sampled before the big op)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=2)
+        torch.cuda.synchronize()
+        return float(y.float().min().item()), float(y.float().max().item()), \
+            comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+
+    res = _run(2, fn)
+    after = pccl.memory.staging_pool_stats()
+    assert all(r[0] == r[1] == 3.0 for r in res), res
+    assert all(r[2] == pccl.ReducePath.DEVICE_RING.value for r in res), res
+    for pool in ("pinned", "device"):
+        assert after[pool]["allocs"] == state["before"][pool]["allocs"], (pool, state["before"], after)
+
+
 def test_device_ring_stripe_bound_with_uneven_chunks(hip, monkeypatch):
     """Chunks of 2 MiB + 4 bytes and 2 MiB with 256 KiB stripes over 4 connections: the larger chunk rounds to 3
     stripes, the smaller one to 4. The op's connection group and sender threads are sized by the stripe bound of its
