@@ -190,14 +190,16 @@ def reserve_staging(*, pinned_bytes: int = 0, pinned_count: int = 0, device_byte
 
 
 def reserve_device_ring_staging(nbytes: int, world: int, *, device=None, in_place: bool = False,
-                                segment_chunk: int = 128 << 20) -> None:
+                                segment_chunk: int = 128 << 20, peers: int = 1) -> None:
     """reserve_staging with what one device-ring all-reduce of ``nbytes`` per peer at ``world`` peers leases: 3 pinned
     send + 3 pinned receive + 3 HBM buffers of one ring chunk (at most the segment chunk, PCCL_SEGMENT_CHUNK_MIB), and
-    for an in-place op an HBM backup of the input (csrc/client/ring_device.cpp)."""
+    for an in-place op an HBM backup of the input (csrc/client/ring_device.cpp); ``peers``: how many peers of this
+    process (threads) run such an op at the same time."""
     stage = min(-(-int(nbytes) // max(1, int(world))), int(segment_chunk)) + 4096
-    reserve_staging(pinned_bytes=stage, pinned_count=6, device_bytes=stage, device_count=3, device=device)
+    k = max(1, int(peers))
+    reserve_staging(pinned_bytes=stage, pinned_count=6 * k, device_bytes=stage, device_count=3 * k, device=device)
     if in_place:
-        reserve_staging(device_bytes=int(nbytes), device_count=1, device=device)
+        reserve_staging(device_bytes=int(nbytes), device_count=k, device=device)
 
 
 def pcie_stats() -> dict:

@@ -641,12 +641,11 @@ def test_device_ring_pcie_bytes_match_model(hip, monkeypatch):
 def test_reserved_staging_serves_the_first_device_ring_op(hip, monkeypatch):
     """pccl.memory.reserve_device_ring_staging (pcclxPoolReserve) fills the pools with what a device-ring op of that
     size leases, so the op itself allocates nothing (benchmarks/fault_tolerance.py runs it next to a replacement's
-    connect()). Two threaded peers share the process's pools: reserved twice."""
+    connect()). Two threaded peers share the process's pools: reserved for both."""
     monkeypatch.setenv("PCCL_DISABLE_IPC", "1")
     C = (48 << 20) + 4096  # one ring chunk (bytes), a size no other test leases
     n = C  # bf16 elements per peer: 2 C bytes, W = 2 -> chunks of C bytes
-    for _ in range(2):
-        pccl.memory.reserve_device_ring_staging(2 * C, 2, device=hip)
+    pccl.memory.reserve_device_ring_staging(2 * C, 2, device=hip, peers=2)
     st = pccl.memory.staging_pool_stats()
     assert st["pinned"]["cached"] >= 12 * C and st["device"]["cached"] >= 6 * C, st
     state = {}
