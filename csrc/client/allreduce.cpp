@@ -392,7 +392,8 @@ extern "C" __attribute__((visibility("default"))) size_t pcclxPoolStats(uint64_t
 // Fills the staging pools ahead of the first ops: leases `pinned_count` pinned buffers of `pinned_bytes` and
 // `device_count` HBM buffers of `device_bytes` on `device` at once and hands them back to the pools, which keep them
 // cached (PCCL_POOL_MAX_FREE_MIB). An application can run it next to connect(), whose admission wait it overlaps
-// (RCCL allocates its buffers at communicator init; these pools otherwise fill on the first op). 0 on success.
+// (RCCL allocates its buffers at communicator init; these pools otherwise fill on the first op). With HBM buffers it
+// also warms the device side a first op would set up (copy queues, a stream, the kernels' code object). 0 on success.
 extern "C" __attribute__((visibility("default"))) int pcclxPoolReserve(uint64_t pinned_bytes, uint32_t pinned_count,
                                                                       uint64_t device_bytes, uint32_t device_count,
                                                                       int device) {
@@ -407,6 +408,21 @@ extern "C" __attribute__((visibility("default"))) int pcclxPoolReserve(uint64_t 
         if (device < 0 || pccl::device_backend() == nullptr) return 2;
         held.emplace_back(device_pool(), device_bytes, device);
         if (!held.back().ok()) return 1;
+    }
+    if (device_count > 0 && device_bytes > 0) {
+        // the rest of a fresh process's first device op: the process-wide copy queues (created on first use), a
+        // pooled stream and the kernels' code object (loaded at the first launch)
+        pccl::DeviceBackend *be = pccl::device_backend();
+        be->set_device(device);
+        const ring::PcieQueues pq = ring::shared_pcie_queues(be, device);
+        StreamLease st(device);
+        Lease h(pinned_pool(), 4096), d(device_pool(), 4096, device);
+        if (!h.ok() || !d.ok() || !pq.h2d || !pq.d2h || !st.get()) return 1;
+        const bool ok = be->memcpy_async(d.data(), h.data(), 4096, pq.h2d) && be->stream_sync(pq.h2d) &&
+                        be->reduce_copy(d.data(), d.data(), h.data(), 16, pccl::DType::F32, pccl::ReduceOp::Sum, st.get()) &&
+                        be->stream_sync(st.get()) && be->memcpy_async(h.data(), d.data(), 4096, pq.d2h) &&
+                        be->stream_sync(pq.d2h);
+        if (!ok) return 1;
     }
     return 0;
 }

@@ -11,7 +11,7 @@ log pytest
 timeout -k 10 300 python -u -m pytest tests/test_gpu_allreduce.py -x -v --timeout 120 --timeout-method thread \
   -p no:cacheprovider -k "reserved_staging or pcie_bytes" > $OUT/pytest.log 2>&1
 rc=$?; log "rc=$rc"; [ $rc -eq 0 ] || exit $rc
-for k in 1 2; do
+for k in ${PAIRS:-1 2}; do
   for v in reserve noreserve; do
     log "ft $k $v"
     extra=""; [ $v = noreserve ] && extra="--no-reserve"
