@@ -413,15 +413,21 @@ extern "C" __attribute__((visibility("default"))) int pcclxPoolReserve(uint64_t 
         // the rest of a fresh process's first device op: the process-wide copy queues (created on first use), a
         // pooled stream and the kernels' code object (loaded at the first launch)
         pccl::DeviceBackend *be = pccl::device_backend();
+        const int cur = be->current_device(); // (the caller's thread keeps its current device)
         be->set_device(device);
-        const ring::PcieQueues pq = ring::shared_pcie_queues(be, device);
-        StreamLease st(device);
-        Lease h(pinned_pool(), 4096), d(device_pool(), 4096, device);
-        if (!h.ok() || !d.ok() || !pq.h2d || !pq.d2h || !st.get()) return 1;
-        const bool ok = be->memcpy_async(d.data(), h.data(), 4096, pq.h2d) && be->stream_sync(pq.h2d) &&
-                        be->reduce_copy(d.data(), d.data(), h.data(), 16, pccl::DType::F32, pccl::ReduceOp::Sum, st.get()) &&
-                        be->stream_sync(st.get()) && be->memcpy_async(h.data(), d.data(), 4096, pq.d2h) &&
-                        be->stream_sync(pq.d2h);
+        bool ok = false;
+        {
+            const ring::PcieQueues pq = ring::shared_pcie_queues(be, device);
+            StreamLease st(device);
+            Lease h(pinned_pool(), 4096), d(device_pool(), 4096, device);
+            ok = h.ok() && d.ok() && pq.h2d && pq.d2h && st.get() &&
+                 be->memcpy_async(d.data(), h.data(), 4096, pq.h2d) && be->stream_sync(pq.h2d) &&
+                 be->reduce_copy(d.data(), d.data(), h.data(), 16, pccl::DType::F32, pccl::ReduceOp::Sum,
+                                 st.get()) &&
+                 be->stream_sync(st.get()) && be->memcpy_async(h.data(), d.data(), 4096, pq.d2h) &&
+                 be->stream_sync(pq.d2h);
+        }
+        if (cur >= 0) be->set_device(cur);
         if (!ok) return 1;
     }
     return 0;
