@@ -61,6 +61,8 @@ def peer(a):
             y = torch.empty_like(x)
         variants = a.variants.split(",")
         res = {v: [] for v in variants}
+        if dev.type == "cuda" and a.caller_stream == "side":
+            torch.cuda.set_stream(torch.cuda.Stream(dev))
         cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
 
         def run(variant):
@@ -112,6 +114,8 @@ def main():
     ap.add_argument("--variants", default="all_reduce,async,ready",
                     help="comma list of all_reduce, async, ready, ready_inline, sync_inline, sync_worker")
     ap.add_argument("--trace-dir", default="", help="PCCL_TRACE_OPS=1 in every peer, its stderr to <dir>/peer<r>.err")
+    ap.add_argument("--caller-stream", default="default", choices=["default", "side"],
+                    help="the stream the peers' calls are ordered on: torch's default (null) stream or a created one")
     ap.add_argument("--peer", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--master", default="")
     ap.add_argument("--rank", type=int, default=0)
@@ -136,7 +140,7 @@ def main():
         procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--peer", "--master",
                                    f"127.0.0.1:{port}", "--rank", str(r), "--peers", str(a.peers), "--iters",
                                    str(a.iters), "--warmup", str(a.warmup), "--sizes", a.sizes, "--device", a.device,
-                                   "--variants", a.variants],
+                                   "--variants", a.variants, "--caller-stream", a.caller_stream],
                                   stdout=subprocess.PIPE, stderr=errs[r] if errs else subprocess.PIPE, text=True,
                                   env=env)
                  for r in range(a.peers)]
