@@ -134,15 +134,7 @@ bool Client::connect() {
 
     C2MRequestSessionRegistration reg;
     reg.peer_group = cfg_.peer_group;
-    if (!wire_reference_) { // (no token: the reference's registration bytes)
-        reg.host_token = net::host_token();
-        char state = 0;
-        uint64_t flags = 0, start = 0;
-        if (net::proc_stat(0, state, flags, start)) { // a same-host master watches this process (exit detection)
-            reg.pid = static_cast<uint32_t>(::getpid());
-            reg.pid_start = start;
-        }
-    }
+    if (!wire_reference_) reg.host_token = net::host_token(); // (no token: the reference's registration bytes)
     // PCCL_XGMI_CAPABLE=0/1 overrides the advertised capability (tests on GPU-less hosts)
     reg.xgmi_capable = std::getenv("PCCL_XGMI_CAPABLE") ? env_flag("PCCL_XGMI_CAPABLE", true)
                                                        : !env_flag("PCCL_DISABLE_IPC", false) && device_backend_available();

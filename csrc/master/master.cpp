@@ -4,10 +4,8 @@
 #include <functional>
 #include <future>
 #include <sstream>
-#include <unistd.h>
 
 #include "../common/log.hpp"
-#include "../net/socket.hpp"
 
 namespace pccl::master {
 
@@ -22,8 +20,6 @@ Master::Master(const SockAddr &listen_addr) : server_(listen_addr, false) {
 Master::~Master() {
     interrupt();
     join();
-    watch_stop_ = true;
-    if (watcher_.joinable()) watcher_.join();
     stopping_ = true;
     optimizer_pool_.stop();
 }
@@ -33,7 +29,6 @@ bool Master::launch() {
     if (!server_.listen()) return false;
     if (!server_.run_async()) return false;
     running_ = true;
-    if (env_flag("PCCL_PEER_EXIT_WATCH", true) && !watcher_.joinable()) watcher_ = std::thread([this] { watch_loop(); });
     LOG(INFO) << "Master listening on port " << server_.port();
     return true;
 }
@@ -66,48 +61,6 @@ ClientInfo *Master::client_by_uuid(const Uuid &u) {
 void Master::kick(const SockAddr &addr) {
     LOG(WARN) << "Master: kicking client " << sockaddr_str(addr);
     server_.close_client(addr);
-}
-
-void Master::watch_peer(const SockAddr &addr, const C2MRequestSessionRegistration &p) {
-    // only a process of this host (same host token) that is the one registering (pid and start time match /proc);
-    // peers that are threads of this very process are never watched
-    if (!watcher_.joinable() || p.pid == 0 || p.host_token.empty() || p.host_token != net::host_token() ||
-        p.pid == static_cast<uint32_t>(::getpid()))
-        return;
-    char state = 0;
-    uint64_t flags = 0, start = 0;
-    if (!net::proc_stat(p.pid, state, flags, start) || start != p.pid_start) return;
-    std::lock_guard l(watch_mtx_);
-    watched_.push_back({addr, p.pid, p.pid_start});
-}
-
-void Master::unwatch_peer(const SockAddr &addr) {
-    std::lock_guard l(watch_mtx_);
-    watched_.erase(std::remove_if(watched_.begin(), watched_.end(),
-                                  [&](const WatchedPeer &w) { return sockaddr_equal(w.addr, addr); }),
-                   watched_.end());
-}
-
-void Master::watch_loop() {
-    static const size_t period_ms = std::max<size_t>(1, env_size("PCCL_PEER_EXIT_WATCH_MS", 5));
-    while (!watch_stop_.load()) {
-        std::this_thread::sleep_for(std::chrono::milliseconds(period_ms));
-        std::vector<WatchedPeer> snapshot;
-        {
-            std::lock_guard l(watch_mtx_);
-            snapshot = watched_;
-        }
-        for (const auto &w : snapshot) {
-            if (!net::proc_exiting(w.pid, w.start)) continue;
-            unwatch_peer(w.addr); // once
-            LOG(WARN) << "Master: the process of peer " << sockaddr_str(w.addr) << " (pid " << w.pid
-                      << ") is exiting; dropping it";
-            const SockAddr a = w.addr;
-            server_.post([this, a] {
-                if (client_by_addr(a)) kick(a);
-            });
-        }
-    }
 }
 
 void Master::on_peer_accepted(ClientInfo &c) {
@@ -393,7 +346,6 @@ void Master::handle_join(const SockAddr &addr, const C2MRequestSessionRegistrati
         c.group = p.peer_group;
         c.host_token = p.host_token;
         c.xgmi = p.xgmi_capable;
-        watch_peer(addr, p);
         if (p.use_explicit_addresses) {
             c.p2p = p.advertised_p2p;
             c.ss = p.advertised_ss;
@@ -1072,7 +1024,6 @@ void Master::check_coll_complete_consensus(uint32_t group, uint64_t tag) {
 // disconnect
 // ------------------------------------------------------------------------------------------------------------------
 void Master::on_disconnect(const SockAddr &addr) {
-    unwatch_peer(addr);
     auto ait = by_addr_.find(SockAddrKey::of(addr));
     if (ait == by_addr_.end()) return;
     const Uuid u = ait->second;

@@ -174,23 +174,6 @@ private:
     bool peer_dropped_ = false;
     bool running_ = false;
 
-    // Same-host peers' processes (registration extension: pid + start time, checked against /proc when the peer
-    // registers): a watcher thread drops a peer as soon as its process starts exiting. A SIGKILLed process tears down
-    // its address space first -- ~100-200 ms with GPU memory mapped -- and only then closes its sockets, which is when
-    // the master would otherwise notice (profiles/r5/b33/). PCCL_PEER_EXIT_WATCH=0 disables it.
-    struct WatchedPeer {
-        SockAddr addr{};
-        uint32_t pid = 0;
-        uint64_t start = 0;
-    };
-    std::mutex watch_mtx_;
-    std::vector<WatchedPeer> watched_;
-    std::thread watcher_;
-    std::atomic<bool> watch_stop_{false};
-    void watch_loop();
-    void watch_peer(const SockAddr &addr, const proto::C2MRequestSessionRegistration &p);
-    void unwatch_peer(const SockAddr &addr);
-
     // async moonshot optimization
     std::mutex pending_mtx_;
     std::map<uint32_t, std::pair<std::vector<Uuid>, bool>> pending_rings_;

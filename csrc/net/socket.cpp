@@ -14,8 +14,6 @@
 #include <poll.h>
 #include <sys/uio.h>
 #include <unistd.h>
-#include <string>
-#include <vector>
 
 #include "../common/log.hpp"
 
@@ -398,38 +396,6 @@ const std::string &host_token() {
         token += host;
     });
     return token;
-}
-
-bool proc_stat(uint32_t pid, char &state, uint64_t &flags, uint64_t &start_time) {
-    const std::string path = pid == 0 ? std::string("/proc/self/stat") : "/proc/" + std::to_string(pid) + "/stat";
-    std::ifstream f(path);
-    std::string line;
-    if (!f || !std::getline(f, line)) return false;
-    const size_t close = line.rfind(')'); // the command name may contain spaces and parentheses
-    if (close == std::string::npos || close + 2 >= line.size()) return false;
-    // fields from 3 (state) on, space separated
-    std::vector<std::string> fld;
-    size_t a = close + 2;
-    while (a < line.size() && fld.size() < 20) {
-        size_t b = line.find(' ', a);
-        if (b == std::string::npos) b = line.size();
-        fld.push_back(line.substr(a, b - a));
-        a = b + 1;
-    }
-    if (fld.size() < 20 || fld[0].empty()) return false; // fld[k] is field k + 3
-    state = fld[0][0];
-    char *end = nullptr;
-    flags = std::strtoull(fld[6].c_str(), &end, 10);
-    start_time = std::strtoull(fld[19].c_str(), &end, 10);
-    return true;
-}
-
-bool proc_exiting(uint32_t pid, uint64_t start_time) {
-    constexpr uint64_t kPfExiting = 0x4; // include/linux/sched.h
-    char state = 0;
-    uint64_t flags = 0, start = 0;
-    if (!proc_stat(pid, state, flags, start)) return true;
-    return start != start_time || state == 'Z' || state == 'X' || (flags & kPfExiting) != 0;
 }
 
 } // namespace pccl::net

@@ -68,14 +68,6 @@ bool is_local_address(const SockAddr &a);
 // Identifies this host (kernel boot id + hostname): equal tokens mean two processes can share HIP IPC handles.
 // PCCL_HOST_TOKEN overrides it (tests simulate several hosts on one machine).
 const std::string &host_token();
-
-// /proc/<pid>/stat of a process on this host: state (field 3), kernel flags (field 9) and start time (field 22, clock
-// ticks since boot). False if the process does not exist (or the file cannot be parsed). pid 0: this process.
-bool proc_stat(uint32_t pid, char &state, uint64_t &flags, uint64_t &start_time);
-// true once the process `pid` started at `start_time` is exiting or gone: PF_EXITING (set at the start of do_exit,
-// before the address space is torn down and long before its sockets close), zombie / dead, or a different process
-// under that pid
-bool proc_exiting(uint32_t pid, uint64_t start_time);
 bool is_connected(int fd); // MSG_PEEK probe (non-blocking)
 
 } // namespace pccl::net

@@ -19,8 +19,6 @@ void C2MRequestSessionRegistration::encode(WBuf &w) const {
     if (!host_token.empty()) {
         w.str(host_token);
         w.boolean(xgmi_capable);
-        w.u32(pid);
-        w.u64(pid_start);
     }
 }
 
@@ -42,12 +40,6 @@ bool C2MRequestSessionRegistration::decode(RBuf &r) {
     if (r.ok() && r.remaining() > 0) host_token = r.str(); // absent when the peer is a reference implementation
     xgmi_capable = true;
     if (r.ok() && r.remaining() > 0) xgmi_capable = r.boolean();
-    pid = 0;
-    pid_start = 0;
-    if (r.ok() && r.remaining() >= 12) {
-        pid = r.u32();
-        pid_start = r.u64();
-    }
     return r.ok();
 }
 

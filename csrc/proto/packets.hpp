@@ -75,11 +75,6 @@ struct C2MRequestSessionRegistration {
     // no PCCL_DISABLE_IPC). Same-host pairs of which one cannot are benchmarked like remote pairs: their traffic
     // crosses loopback TCP, so a fixed xGMI-class cost would mislead the ring optimiser.
     bool xgmi_capable = true;
-    // extension after xgmi_capable (optional, 0 = unknown): the peer's process id and its start time (clock ticks
-    // since boot, /proc/<pid>/stat field 22). A master on the same host watches that process and drops the peer as
-    // soon as it starts exiting, instead of when its sockets close at the end of its teardown.
-    uint32_t pid = 0;
-    uint64_t pid_start = 0;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };

@@ -2,7 +2,6 @@
 // Built as build/pccl_unit_tests, run by tests/test_native.py; also the target of the sanitizer build
 // (cmake -DPCCL_SANITIZE=ON: ASan + UBSan on host code).
 #include <cmath>
-#include <csignal>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -100,15 +99,6 @@ TEST(packet_extensions_backward_compatible) {
     const size_t legacy = 2 + 4 + 1 + 6; // id + group + bool + 3 ports: the reference layout
     auto old = proto::decode_payload<proto::C2MRequestSessionRegistration>(bytes.data() + 2, legacy - 2);
     EXPECT(old && old->host_token.empty() && old->peer_group == 3 && old->bm_port == 4);
-
-    // the process extension after the host token (pid + start time), absent in older extended registrations
-    r.pid = 4242;
-    r.pid_start = 1234567;
-    bytes = proto::encode_with_id(r);
-    auto withpid = proto::decode_payload<proto::C2MRequestSessionRegistration>(bytes.data() + 2, bytes.size() - 2);
-    EXPECT(withpid && withpid->pid == 4242 && withpid->pid_start == 1234567 && withpid->host_token == "boot-id|host");
-    auto nopid = proto::decode_payload<proto::C2MRequestSessionRegistration>(bytes.data() + 2, bytes.size() - 2 - 12);
-    EXPECT(nopid && nopid->pid == 0 && nopid->pid_start == 0 && nopid->host_token == "boot-id|host");
 
     proto::M2CP2PConnectionsEstablished e;
     e.success = true;
@@ -764,38 +754,6 @@ TEST(pool_concurrent_leases_stay_disjoint) {
     for (auto &t : ths) t.join();
     EXPECT(bad.load() == 0);
     EXPECT(pool.in_use() == 0);
-}
-
-// The master's exit watcher (net::proc_exiting): this process is alive, a pid that does not exist and a start time
-// that does not match (a reused pid) count as gone, and a child that was SIGKILLed is seen exiting before it is reaped.
-TEST(proc_exiting_detects_dead_and_reused) {
-    char state = 0;
-    uint64_t flags = 0, start = 0;
-    EXPECT(net::proc_stat(0, state, flags, start) && start > 0);
-    const auto me = static_cast<uint32_t>(::getpid());
-    EXPECT(!net::proc_exiting(me, start));
-    EXPECT(net::proc_exiting(me, start + 1));
-    EXPECT(net::proc_exiting(0x7ffffff0u, 0));
-    const pid_t child = ::fork();
-    if (child == 0) {
-        ::pause();
-        ::_exit(0);
-    }
-    uint64_t cstart = 0;
-    char cs = 0;
-    uint64_t cf = 0;
-    EXPECT(child > 0 && net::proc_stat(static_cast<uint32_t>(child), cs, cf, cstart));
-    EXPECT(!net::proc_exiting(static_cast<uint32_t>(child), cstart));
-    ::kill(child, SIGKILL);
-    bool seen = false;
-    for (int i = 0; i < 2000 && !seen; ++i) { // not reaped yet: exiting, then a zombie
-        seen = net::proc_exiting(static_cast<uint32_t>(child), cstart);
-        if (!seen) ::usleep(1000);
-    }
-    EXPECT(seen);
-    int st = 0;
-    ::waitpid(child, &st, 0);
-    EXPECT(net::proc_exiting(static_cast<uint32_t>(child), cstart));
 }
 
 int main() {
