@@ -193,12 +193,14 @@ def run(a) -> dict:
     victim_rank = a.peers - 1
     t_kill = None
     t_spawn = None
+    t_victim_gone = None
     try:
         for r in range(a.peers):
             start(r, extra_env={"PCCL_FAULT_INJECT": spec} if r == victim_rank else None)
         victim = procs[victim_rank]
         while victim.poll() is None and time.time() < deadline:
-            time.sleep(0.01)
+            time.sleep(0.002)
+        t_victim_gone = time.time()  # reaped: its exit (address space teardown, then its sockets) completed
         errs_files[victim_rank].seek(0)
         m = re.search(r"fault injection: SIGKILL at .* t=(\d+\.\d+)", errs_files[victim_rank].read())
         t_kill = float(m.group(1)) if m else None
@@ -262,6 +264,7 @@ def run(a) -> dict:
         ("TCP device ring" if a.device.startswith("cuda") else "TCP host ring"),
         "peers": a.peers, "processes": "one per peer", "mib": a.mib, "device": a.device, "inject": spec,
         "complete": complete,
+        "kill_to_victim_reaped_ms": ms(t_victim_gone - t_kill) if t_kill is not None else None,
         "kill_to_survivors_failed_op_ms": ms(max(first_fail) - t_kill) if complete else None,
         "kill_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
         "joiner_connect_to_first_exact_op_ms": ms(j_first - j_connect[0]) if j_first and j_connect else None,
