@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -460,34 +461,72 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             if (!fallback) return false;
             info.rx_bytes = 0;
         }
-        const int fd = net::connect_tcp(distributor, 10000);
-        if (fd < 0) {
-            LOG(WARN) << "Shared state sync: cannot reach distributor " << sockaddr_str(distributor);
-            return false;
+        // The outdated keys are requested over up to PCCL_SS_STREAMS (default 4) connections at once, each an ordinary
+        // request for a subset of the keys (balanced by size), so a reference distributor serves them as well; one
+        // TCP stream carries ~9 GB/s over loopback and far less over a long path, where parallel streams add up.
+        const size_t nkeys = resp->outdated_keys.size();
+        const size_t streams = wire_reference_ ? 1 : std::max<size_t>(1, std::min(env_size("PCCL_SS_STREAMS", 4), nkeys));
+        std::vector<std::vector<size_t>> bins(streams);
+        {
+            std::vector<size_t> order(nkeys);
+            for (size_t i = 0; i < nkeys; ++i) order[i] = i;
+            auto bytes_of = [&](size_t i) -> uint64_t {
+                auto it = by_key.find(resp->outdated_keys[i]);
+                return it == by_key.end() ? 0 : it->second->bytes;
+            };
+            std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return bytes_of(a) > bytes_of(b); });
+            std::vector<uint64_t> load(streams, 0);
+            for (size_t i : order) {
+                const size_t k = static_cast<size_t>(std::min_element(load.begin(), load.end()) - load.begin());
+                bins[k].push_back(i);
+                load[k] += bytes_of(i);
+            }
+            for (auto &b : bins) std::sort(b.begin(), b.end());
         }
-        FdGuard fdg{fd};
-        C2SRequestSharedState req;
-        req.keys = resp->outdated_keys;
-        if (!net::send_packet(fd, req)) return false;
-        auto sresp = net::recv_packet<S2CSharedStateResponse>(fd);
-        if (!sresp || sresp->status != SharedStateStatus::Success) {
-            LOG(WARN) << "Shared state sync: distributor refused (status "
-                     << (sresp ? static_cast<int>(sresp->status) : -1) << ")";
-            return false;
-        }
-        ss.revision = sresp->revision;
-        if (sresp->entries.size() != resp->outdated_keys.size()) return false;
-        for (size_t i = 0; i < sresp->entries.size(); ++i) {
-            const auto &se = sresp->entries[i];
-            SSEntry *dst = lookup(i, se.key, se.size_bytes);
-            if (!dst) return false;
-            if (!recv_stream_entry(fd, *dst)) {
-                LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
+        std::atomic<uint64_t> rx{0}, revision{0};
+        // one connection: the keys of `idx` (indices into the master's outdated-key list), received in that order
+        // (no key at all: the request still runs, its response carries the revision)
+        auto fetch_keys = [&](const std::vector<size_t> &idx) -> bool {
+            const int fd = net::connect_tcp(distributor, 10000);
+            if (fd < 0) {
+                LOG(WARN) << "Shared state sync: cannot reach distributor " << sockaddr_str(distributor);
                 return false;
             }
-            info.rx_bytes += dst->bytes;
-            if (!verify(i, *dst)) return false;
-        }
+            FdGuard fdg{fd};
+            C2SRequestSharedState req;
+            for (size_t i : idx) req.keys.push_back(resp->outdated_keys[i]);
+            if (!net::send_packet(fd, req)) return false;
+            auto sresp = net::recv_packet<S2CSharedStateResponse>(fd);
+            if (!sresp || sresp->status != SharedStateStatus::Success) {
+                LOG(WARN) << "Shared state sync: distributor refused (status "
+                          << (sresp ? static_cast<int>(sresp->status) : -1) << ")";
+                return false;
+            }
+            revision.store(sresp->revision);
+            if (sresp->entries.size() != idx.size()) return false;
+            for (size_t j = 0; j < idx.size(); ++j) {
+                const auto &se = sresp->entries[j];
+                SSEntry *dst = lookup(idx[j], se.key, se.size_bytes);
+                if (!dst) return false;
+                if (!recv_stream_entry(fd, *dst)) {
+                    LOG(ERR) << "Shared state sync: transfer of " << se.key << " failed";
+                    return false;
+                }
+                rx += dst->bytes;
+            }
+            return true;
+        };
+        std::vector<char> ok(streams, 0);
+        std::vector<std::thread> ts;
+        for (size_t k = 1; k < streams; ++k) ts.emplace_back([&, k] { ok[k] = fetch_keys(bins[k]); });
+        ok[0] = fetch_keys(bins[0]);
+        for (auto &t : ts) t.join();
+        info.rx_bytes += rx.load();
+        if (std::find(ok.begin(), ok.end(), 0) != ok.end()) return false;
+        ss.revision = revision.load();
+        // hashes verified once every stream is done (one thread: the hash kernels share their scratch)
+        for (size_t i = 0; i < nkeys; ++i)
+            if (!verify(i, *by_key[resp->outdated_keys[i]])) return false;
         return true;
     };
     bool fetched = !resp->is_outdated;

@@ -219,3 +219,29 @@ def test_concurrent_control_plane_call_is_refused():
     with local_master() as addr:
         res = run_threaded_peers(2, fn, address=addr)
     assert res[0] == (pccl.Result.INVALID_USAGE, True)
+
+
+@pytest.mark.parametrize("streams", ["1", "3"])
+def test_outdated_keys_over_parallel_streams(streams, monkeypatch):
+    """PCCL_SS_STREAMS: the outdated keys are fetched over that many connections at once (each an ordinary request
+    for a size-balanced subset of the keys); contents, byte accounting and revision are the same as over one."""
+    monkeypatch.setenv("PCCL_SS_STREAMS", streams)
+    world = 3
+    sizes = [100_000, 3, 50_000, 7, 20_000, 1]
+
+    def fn(rank, comm):
+        ts = {f"t{k}": torch.full((n,), float(k + 1)) for k, n in enumerate(sizes)}
+        if rank == 2:  # the outdated peer: every key differs
+            for t in ts.values():
+                t.fill_(-5.0)
+        st = _state(ts)
+        st.revision = 0 if rank == 2 else 4
+        info = comm.sync_shared_state(st)
+        return {k: v.clone() for k, v in ts.items()}, info.rx_bytes, st.revision
+
+    with local_master() as addr:
+        res = run_threaded_peers(world, fn, address=addr)
+    state, rx, rev = res[2]
+    assert rx == 4 * sum(sizes) and rev == 4
+    for k, n in enumerate(sizes):
+        assert torch.all(state[f"t{k}"] == float(k + 1))
