@@ -467,36 +467,29 @@ bool Client::optimize_topology() {
         if (!master_.send(C2MOptimizeTopology{})) return false;
         auto resp = master_.receive<M2COptimizeTopologyResponse>();
         if (!resp) return false;
+        // The master orders the probes as a round-robin schedule (every peer sends to one peer and receives from one
+        // per round): probe them in that order; a target still serving the previous round's sender is retried
+        // shortly, and only moved behind the others after repeated refusals.
         std::list<BenchmarkRequest> todo(resp->requests.begin(), resp->requests.end());
-        std::map<Uuid, std::chrono::steady_clock::time_point> last_attempt;
+        std::map<Uuid, int> refusals;
         while (!todo.empty()) {
-            bool progressed = false;
-            for (auto it = todo.begin(); it != todo.end();) {
-                auto la = last_attempt.find(it->to_peer);
-                if (la != last_attempt.end() && std::chrono::steady_clock::now() - la->second < 1s) {
-                    ++it;
-                    continue;
-                }
-                double mbps = 0;
-                const BenchResult r = benchmark_send(uuid_, it->to_peer_endpoint, mbps);
-                if (r == BenchResult::Success) {
-                    C2MReportPeerBandwidth rep;
-                    rep.to_peer = it->to_peer;
-                    rep.bandwidth_mbps = mbps;
-                    if (!master_.send(rep)) return false;
-                    LOG(INFO) << "Bandwidth to " << it->to_peer.str() << ": " << mbps << " Mbit/s";
-                    it = todo.erase(it);
-                    progressed = true;
-                } else if (r == BenchResult::Busy || r == BenchResult::SendFailure) {
-                    last_attempt[it->to_peer] = std::chrono::steady_clock::now();
-                    ++it;
-                } else {
-                    LOG(WARN) << "Benchmark to " << sockaddr_str(it->to_peer_endpoint) << " failed; skipping";
-                    it = todo.erase(it);
-                    progressed = true;
-                }
+            auto it = todo.begin();
+            double mbps = 0;
+            const BenchResult r = benchmark_send(uuid_, it->to_peer_endpoint, mbps);
+            if (r == BenchResult::Success) {
+                C2MReportPeerBandwidth rep;
+                rep.to_peer = it->to_peer;
+                rep.bandwidth_mbps = mbps;
+                if (!master_.send(rep)) return false;
+                LOG(INFO) << "Bandwidth to " << it->to_peer.str() << ": " << mbps << " Mbit/s";
+                todo.erase(it);
+            } else if (r == BenchResult::Busy || r == BenchResult::SendFailure) {
+                if (++refusals[it->to_peer] % 10 == 0 && todo.size() > 1) todo.splice(todo.end(), todo, it);
+                std::this_thread::sleep_for(20ms);
+            } else {
+                LOG(WARN) << "Benchmark to " << sockaddr_str(it->to_peer_endpoint) << " failed; skipping";
+                todo.erase(it);
             }
-            if (!progressed && !todo.empty()) std::this_thread::sleep_for(250ms);
         }
         if (!master_.send(C2MOptimizeTopologyWorkComplete{})) return false;
         auto done = master_.receive<M2COptimizeTopologyComplete>();

@@ -546,6 +546,16 @@ void Master::check_optimize_consensus() {
             any = true;
         }
     if (!any) return;
+    // Each sender's probes in round-robin tournament order: the i-th peer (uuid order, per group) measures peer
+    // i + 1, i + 2, ... in turn, so in every round each peer sends to one peer and receives from one, instead of all of
+    // them queueing at the same first target (whose benchmark server takes one probe at a time).
+    std::map<uint32_t, std::vector<Uuid>> members;
+    for (const auto &[u, c] : clients_)
+        if (c.phase == Phase::Accepted) members[c.group].push_back(u);
+    auto index_in = [&](uint32_t group, const Uuid &u) -> size_t {
+        const auto &m = members[group];
+        return static_cast<size_t>(std::find(m.begin(), m.end(), u) - m.begin());
+    };
     for (auto &[u, c] : clients_) {
         if (c.phase != Phase::Accepted) continue;
         M2COptimizeTopologyResponse resp;
@@ -565,6 +575,10 @@ void Master::check_optimize_consensus() {
             }
             resp.requests.push_back(BenchmarkRequest{u, e.to, to->bm});
         }
+        const size_t n = std::max<size_t>(1, members[c.group].size()), me = index_in(c.group, u);
+        std::stable_sort(resp.requests.begin(), resp.requests.end(), [&](const BenchmarkRequest &a, const BenchmarkRequest &b) {
+            return (index_in(c.group, a.to_peer) + n - me) % n < (index_in(c.group, b.to_peer) + n - me) % n;
+        });
         server_.send_packet(c.addr, resp);
     }
 }
