@@ -525,8 +525,10 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         if (std::find(ok.begin(), ok.end(), 0) != ok.end()) return false;
         ss.revision = revision.load();
         // hashes verified once every stream is done (one thread: the hash kernels share their scratch)
-        for (size_t i = 0; i < nkeys; ++i)
-            if (!verify(i, *by_key[resp->outdated_keys[i]])) return false;
+        for (size_t i = 0; i < nkeys; ++i) {
+            auto it = by_key.find(resp->outdated_keys[i]);
+            if (it == by_key.end() || !verify(i, *it->second)) return false;
+        }
         return true;
     };
     bool fetched = !resp->is_outdated;
