@@ -16,6 +16,11 @@ ccoip/src/cpp/ccoip_master_handler.cpp:1312-1400):
      op boundary (pcclArePeersPending / pcclUpdateTopology);
   4. at the first op with W peers again every peer calls pcclOptimizeTopology (pairwise bandwidth probes, then the
      master's asymmetric-TSP solve) and keeps reducing on the new ring.
+With --signal stop the victim SIGSTOPs itself instead (PCCL_FAULT_SIGNAL=STOP: its sockets stay open and its kernel
+keeps ACKing, so no connection ever closes): the master drops it once its heartbeats stop (PCCL_PEER_TIMEOUT_MS,
+--peer-timeout-ms) and the survivors' op fails through the liveness path (docs/ARCHITECTURE.md); the stopped victim is
+SIGKILLed after the survivors' first op at W-1 (cleanup) and the replacement joins as above. The fields are then named
+stop_to_* instead of kill_to_*.
 Reported (ms): kill -> survivors' failed op returned (abort received + ring re-formed), kill -> survivors' first exact
 op at W-1, replacement's connect() -> its first exact op at W (its process start too), the admission vote, the
 optimize call and the master's ATSP solve alone; ms per op in each phase (``after_rejoin`` holds each peer's first op
@@ -139,6 +144,14 @@ def peer(a):
     comm.destroy()
 
 
+def _proc_state(pid: int):
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0]
+    except (OSError, IndexError):
+        return None
+
+
 def inject_spec(device: str, transport: str, op: int) -> str:
     """PCCL_FAULT_INJECT of the victim: where in op `op` (the master's sequence number) it SIGKILLs itself."""
     if not device.startswith("cuda"):
@@ -153,6 +166,8 @@ def run(a) -> dict:
     deadline = time.time() + a.timeout
     port = free_port()
     addr = f"127.0.0.1:{port}"
+    if a.peer_timeout_ms is not None:  # read by the master (this process) when it is created
+        os.environ["PCCL_PEER_TIMEOUT_MS"] = str(a.peer_timeout_ms)
     master = pccl.MasterNode(addr)
     master.run()
     common = ["--peers", str(a.peers), "--mib", str(a.mib), "--pool", str(a.pool), "--device", a.device,
@@ -165,6 +180,8 @@ def run(a) -> dict:
     if a.transport == "tcp":
         env["PCCL_DISABLE_IPC"] = "1"
     spec = inject_spec(a.device, a.transport, a.kill_op)
+    stop = a.signal == "stop"
+    victim_env = {"PCCL_FAULT_INJECT": spec, **({"PCCL_FAULT_SIGNAL": "STOP"} if stop else {})}
     lines, procs, errs_files = [], [], []
     lock = threading.Lock()
 
@@ -196,18 +213,21 @@ def run(a) -> dict:
     t_victim_gone = None
     try:
         for r in range(a.peers):
-            start(r, extra_env={"PCCL_FAULT_INJECT": spec} if r == victim_rank else None)
+            start(r, extra_env=victim_env if r == victim_rank else None)
         victim = procs[victim_rank]
-        while victim.poll() is None and time.time() < deadline:
+        while victim.poll() is None and time.time() < deadline and not (stop and _proc_state(victim.pid) == "T"):
             time.sleep(0.002)
-        t_victim_gone = time.time()  # reaped: its exit (address space teardown, then its sockets) completed
+        t_victim_gone = time.time()  # reaped (its address space torn down, then its sockets closed) / stopped
         errs_files[victim_rank].seek(0)
-        m = re.search(r"fault injection: SIGKILL at .* t=(\d+\.\d+)", errs_files[victim_rank].read())
+        m = re.search(r"fault injection: SIG(?:KILL|STOP) at .* t=(\d+\.\d+)", errs_files[victim_rank].read())
         t_kill = float(m.group(1)) if m else None
         survivors = [r for r in range(a.peers) if r != victim_rank]
         while t_kill is not None and time.time() < deadline and \
                 not all(sel("ok", rank=r, world=a.peers - 1, after=t_kill) for r in survivors):
             time.sleep(0.01)
+        if stop and victim.poll() is None:  # stopped, dropped by the master: clean it up before the replacement
+            os.killpg(victim.pid, signal.SIGKILL)
+            victim.wait()
         t_spawn = time.time()
         start(a.peers, joiner=True)
         for p in procs:
@@ -258,15 +278,20 @@ def run(a) -> dict:
                 and (t_opt_end is None or x["t"] < t_opt_end)]
     after_opt = [x for x in oks if x["world"] == a.peers and t_opt_end is not None and x["t"] > t_opt_end]
     complete = t_kill is not None and None not in first_fail and None not in first_small and j_first is not None
+    ev = "stop" if stop else "kill"
     return {
-        "config": f"BASELINE config 5: kill + rejoin 1 of {a.peers} peers mid-all-reduce, TSP topology re-solve",
+        "config": f"BASELINE config 5: {'SIGSTOP (no socket closes)' if stop else 'kill'} + rejoin 1 of {a.peers} "
+                  f"peers mid-all-reduce, TSP topology re-solve",
+        "fault_signal": "SIGSTOP" if stop else "SIGKILL",
+        "peer_timeout_ms": (a.peer_timeout_ms if a.peer_timeout_ms is not None else
+                            int(os.environ.get("PCCL_PEER_TIMEOUT_MS", "10000"))) if stop else None,
         "transport": "xGMI/IPC" if a.transport == "ipc" and a.device.startswith("cuda") else
         ("TCP device ring" if a.device.startswith("cuda") else "TCP host ring"),
         "peers": a.peers, "processes": "one per peer", "mib": a.mib, "device": a.device, "inject": spec,
         "complete": complete,
-        "kill_to_victim_reaped_ms": ms(t_victim_gone - t_kill) if t_kill is not None else None,
-        "kill_to_survivors_failed_op_ms": ms(max(first_fail) - t_kill) if complete else None,
-        "kill_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
+        f"{ev}_to_victim_{'stopped' if stop else 'reaped'}_ms": ms(t_victim_gone - t_kill) if t_kill is not None else None,
+        f"{ev}_to_survivors_failed_op_ms": ms(max(first_fail) - t_kill) if complete else None,
+        f"{ev}_to_survivors_first_exact_op_ms": ms(max(first_small) - t_kill) if complete else None,
         "joiner_connect_to_first_exact_op_ms": ms(j_first - j_connect[0]) if j_first and j_connect else None,
         "joiner_process_start_to_first_exact_op_ms": ms(j_first - j_proc[0]) if j_first and j_proc else None,
         # connect() returns once the survivors admitted the replacement at their next op boundary and the ring with it
@@ -301,6 +326,10 @@ def main():
                     help="tcp: the device ring over loopback TCP (PCCL_DISABLE_IPC=1; the reference's data path); "
                          "ipc: the xGMI path for peers on one host")
     ap.add_argument("--kill-op", type=int, default=6, help="sequence number of the op the victim dies in")
+    ap.add_argument("--signal", default="kill", choices=["kill", "stop"],
+                    help="kill: the victim SIGKILLs itself; stop: it SIGSTOPs itself (sockets stay open)")
+    ap.add_argument("--peer-timeout-ms", type=int, default=None,
+                    help="PCCL_PEER_TIMEOUT_MS of the master (default: the environment's, else 10 s)")
     ap.add_argument("--post-ops", type=int, default=5, help="ops after the topology re-solve")
     ap.add_argument("--probe-ms", type=int, default=300, help="bandwidth probe per peer pair (PCCL_BENCHMARK_MILLIS)")
     ap.add_argument("--timeout", type=float, default=240.0)

@@ -124,6 +124,7 @@ pcclResult_t pcclGetAttribute(const pcclComm_t *comm, pcclAttribute_t attribute,
         case PCCL_ATTRIBUTE_LAST_REDUCE_PATH: *out = c.last_reduce_path(); break;
         case PCCL_ATTRIBUTE_COLLECTIVE_WORKER_THREADS: *out = static_cast<int>(c.collective_worker_threads()); break;
         case PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING: *out = c.last_reduce_framing(); break;
+        case PCCL_ATTRIBUTE_MASTER_CONNECTED: *out = c.master_connected() ? 1 : 0; break;
         default: return pcclInvalidArgument;
     }
     return pcclSuccess;
@@ -441,6 +442,26 @@ extern "C" __attribute__((visibility("default"))) size_t pcclxMasterTopologyStat
                                                                                   uint64_t *out, size_t n) {
     if (m == nullptr || m->master == nullptr || out == nullptr) return 0;
     const auto s = m->master->topology_stats();
+    const size_t k = std::min(n, s.size());
+    for (size_t i = 0; i < k; ++i) out[i] = s[i];
+    return k;
+}
+
+// liveness counters of the master (pccl::master::Master::liveness_stats); returns how many it wrote
+extern "C" __attribute__((visibility("default"))) size_t pcclxMasterLivenessStats(pcclMasterInstance_t *m,
+                                                                                  uint64_t *out, size_t n) {
+    if (m == nullptr || m->master == nullptr || out == nullptr) return 0;
+    const auto s = m->master->liveness_stats();
+    const size_t k = std::min(n, s.size());
+    for (size_t i = 0; i < k; ++i) out[i] = s[i];
+    return k;
+}
+
+// liveness counters of a peer (pccl::client::Client::liveness_stats); returns how many it wrote
+extern "C" __attribute__((visibility("default"))) size_t pcclxLivenessStats(const pcclComm_t *comm, uint64_t *out,
+                                                                            size_t n) {
+    if (comm == nullptr || comm->client == nullptr || out == nullptr) return 0;
+    const auto s = comm->client->liveness_stats();
     const size_t k = std::min(n, s.size());
     for (size_t i = 0; i < k; ++i) out[i] = s[i];
     return k;

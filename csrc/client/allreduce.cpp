@@ -236,6 +236,9 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
                 }
             }
             if (!done) {
+                // the TCP rings run under the stall watchdog (liveness_loop); xGMI barriers watch peers themselves
+                ring::current_watch() = &op->watch;
+                watch_op(op, *rv);
                 if (device) {
                     r = ring_reduce_device(*op, *rv, seq, di.device);
                     if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceRing);
@@ -248,6 +251,8 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
                     LOG(ERR) << "all-reduce: send and receive buffers must both be host or both be on one GPU";
                     r = {false, false};
                 }
+                unwatch_op(op.get());
+                ring::current_watch() = nullptr;
             }
             success = r.first && !r.second;
             abort_seen = r.second;

@@ -138,6 +138,7 @@ bool Client::connect() {
     // PCCL_XGMI_CAPABLE=0/1 overrides the advertised capability (tests on GPU-less hosts)
     reg.xgmi_capable = std::getenv("PCCL_XGMI_CAPABLE") ? env_flag("PCCL_XGMI_CAPABLE", true)
                                                        : !env_flag("PCCL_DISABLE_IPC", false) && device_backend_available();
+    reg.liveness = !wire_reference_; // (encoded only with the host token: a reference peer's bytes stay unchanged)
     reg.use_explicit_addresses = cfg_.explicit_addresses;
     if (cfg_.explicit_addresses) {
         reg.advertised_p2p = cfg_.adv_p2p;
@@ -149,7 +150,10 @@ bool Client::connect() {
         reg.bm_port = bm_listener_->port();
     }
     if (!master_.send(reg)) return false;
-    auto resp = master_.receive<M2CSessionRegistrationResponse>();
+    // a live master answers at once; one that accepted the connection but does not run (stopped, wedged) must not
+    // hang connect() (the liveness thread watches the master only from the response on)
+    auto resp = master_.receive<M2CSessionRegistrationResponse>(
+        nullptr, std::chrono::milliseconds(env_size("PCCL_REGISTRATION_TIMEOUT_MS", 30000)));
     if (!resp) {
         LOG(ERR) << "No registration response from master";
         return false;
@@ -160,6 +164,14 @@ bool Client::connect() {
     }
     uuid_ = resp->assigned_uuid;
     LOG(INFO) << "Registered with master as " << uuid_.str();
+    // liveness parameters: the master's (it runs the protocol), else only the local op watchdog (a reference
+    // master: a stalled op fails here instead of being reported). PCCL_OP_STALL_MS overrides the stall timeout.
+    master_liveness_ = !wire_reference_ && (resp->heartbeat_ms || resp->peer_timeout_ms || resp->op_stall_ms);
+    hb_ms_ = master_liveness_ ? resp->heartbeat_ms : 0;
+    peer_timeout_ms_ = master_liveness_ ? resp->peer_timeout_ms : 0;
+    stall_ms_ = master_liveness_ ? resp->op_stall_ms : 15000;
+    if (std::getenv("PCCL_OP_STALL_MS")) stall_ms_ = static_cast<uint32_t>(env_size("PCCL_OP_STALL_MS", stall_ms_));
+    if (hb_ms_ || peer_timeout_ms_ || stall_ms_) liveness_thread_ = std::thread([this] { liveness_loop(); });
     const EstablishResult r = establish();
     if (r == EstablishResult::Failed) return false;
     accepted_ = true;
@@ -501,6 +513,107 @@ bool Client::optimize_topology() {
 }
 
 // ------------------------------------------------------------------------------------------------------------------
+// liveness: heartbeats, master silence, op stall watchdog
+// ------------------------------------------------------------------------------------------------------------------
+void Client::watch_op(const std::shared_ptr<OpState> &op, const RingView &rv) {
+    if (stall_ms_ == 0 || rv.ring.size() < 2) return;
+    Watched w;
+    w.op = op;
+    w.rx = rv.rx;
+    w.tx = rv.tx;
+    w.prev = rv.ring[(rv.rank + rv.ring.size() - 1) % rv.ring.size()];
+    w.next = rv.ring[(rv.rank + 1) % rv.ring.size()];
+    w.progress = std::chrono::steady_clock::now();
+    for (const auto &c : w.rx) w.bytes += c ? c->rx_bytes_total() : 0;
+    for (const auto &c : w.tx) w.bytes += c ? c->tx_bytes_total() : 0;
+    std::lock_guard l(live_mtx_);
+    watched_[op.get()] = std::move(w);
+}
+
+void Client::unwatch_op(const OpState *op) {
+    std::lock_guard l(live_mtx_);
+    watched_.erase(op);
+}
+
+void Client::liveness_loop() {
+    name_thread("pccl-liveness");
+    using clock = std::chrono::steady_clock;
+    const auto hb = std::chrono::milliseconds(hb_ms_), stall = std::chrono::milliseconds(stall_ms_);
+    auto next_hb = clock::now();
+    std::unique_lock l(live_mtx_);
+    while (!live_stop_) {
+        live_cv_.wait_for(l, std::chrono::milliseconds(50));
+        if (live_stop_) break;
+        const auto now = clock::now();
+        if (hb_ms_ > 0 && now >= next_hb && master_.is_open()) {
+            l.unlock();
+            if (master_.send(C2MHeartbeat{})) heartbeats_++;
+            l.lock();
+            next_hb = now + hb;
+        }
+        // a master that has been silent for twice the peer timeout (it sends M2CHeartbeat every heartbeat interval)
+        // is lost: closing the connection fails every wait on it instead of hanging the application
+        if (peer_timeout_ms_ > 0 && master_.is_open()) {
+            const auto silent = std::chrono::nanoseconds(
+                std::chrono::duration_cast<std::chrono::nanoseconds>(now.time_since_epoch()).count() -
+                master_.last_rx_ns());
+            if (silent > 2 * std::chrono::milliseconds(peer_timeout_ms_)) {
+                LOG(ERR) << "Master silent for " << std::chrono::duration_cast<std::chrono::milliseconds>(silent).count()
+                         << " ms: treating it as lost";
+                master_lost_++;
+                l.unlock();
+                master_.interrupt();
+                l.lock();
+            }
+        }
+        if (stall_ms_ == 0) continue;
+        for (auto &[_, w] : watched_) {
+            uint64_t bytes = 0;
+            for (const auto &c : w.rx) bytes += c ? c->rx_bytes_total() : 0;
+            for (const auto &c : w.tx) bytes += c ? c->tx_bytes_total() : 0;
+            if (bytes != w.bytes) {
+                w.bytes = bytes;
+                w.progress = now;
+                continue;
+            }
+            const auto idle = now - w.progress;
+            if (!w.reported && idle >= stall) {
+                // the evidence: a send to the next peer blocked for half the timeout means it does not drain its
+                // socket; otherwise nothing arrives from the previous peer
+                std::chrono::nanoseconds blocked{0};
+                for (const auto &c : w.tx)
+                    if (c) blocked = std::max(blocked, c->send_blocked_for());
+                C2MOpStalled rep;
+                rep.tag = w.op->req.tag;
+                rep.kind = blocked >= stall / 2 ? kStallTxBlocked : kStallRxIdle;
+                rep.suspect = rep.kind == kStallTxBlocked ? w.next : w.prev;
+                rep.step = w.op->watch.step.load(std::memory_order_relaxed);
+                rep.idle_ms = static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::milliseconds>(idle).count());
+                LOG(WARN) << "all-reduce tag " << rep.tag << ": no progress for " << rep.idle_ms << " ms in ring step "
+                          << rep.step << " (" << (rep.kind == kStallTxBlocked ? "send to " : "nothing from ")
+                          << rep.suspect.str() << ")";
+                w.reported = true;
+                w.reported_at = now;
+                if (master_liveness_ && master_.is_open()) {
+                    l.unlock();
+                    const bool sent = master_.send(rep);
+                    l.lock();
+                    if (sent) stall_reports_++;
+                    break; // watched_ may have changed while unlocked: rescan at the next tick
+                }
+                w.op->watch.failed.store(true, std::memory_order_release);
+                stall_fails_++;
+            } else if (w.reported && now - w.reported_at >= stall && !w.op->watch.failed.load()) {
+                // the master did not resolve the stall (no abort): fail the op here
+                LOG(WARN) << "all-reduce tag " << w.op->req.tag << ": stall unresolved by the master; failing the op";
+                w.op->watch.failed.store(true, std::memory_order_release);
+                stall_fails_++;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
 // lifecycle
 // ------------------------------------------------------------------------------------------------------------------
 bool Client::any_collective_running() {
@@ -512,6 +625,11 @@ bool Client::any_collective_running() {
 
 bool Client::interrupt() {
     if (interrupted_.exchange(true)) return true;
+    {
+        std::lock_guard l(live_mtx_);
+        live_stop_ = true;
+    }
+    live_cv_.notify_all();
     master_.interrupt();
     {
         std::lock_guard lock(p2p_mtx_);
@@ -535,6 +653,7 @@ bool Client::join() {
         for (auto &[_, op] : ops_) ops.push_back(op);
     }
     for (auto &op : ops) op->wait();
+    if (liveness_thread_.joinable()) liveness_thread_.join();
     if (p2p_listener_) p2p_listener_->join();
     if (ss_listener_) ss_listener_->join();
     if (bm_listener_) bm_listener_->join();

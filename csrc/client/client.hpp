@@ -2,7 +2,9 @@
 // (reference behaviour: ccoip/src/cpp/ccoip_client_handler.cpp, ccoip_client_state.cpp, reduce.cpp).
 #pragma once
 
+#include <array>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -138,6 +140,12 @@ public:
     int last_reduce_framing() const { return last_framing_.load(); }
     size_t collective_worker_threads() { return workers_.thread_count(); }
     const Uuid &uuid() const { return uuid_; }
+    bool master_connected() const { return master_.is_open(); }
+    // liveness counters (pcclxLivenessStats): [0] stall reports sent, [1] ops failed by the local watchdog,
+    // [2] master declared lost (silent for 2 x the peer timeout), [3] heartbeats sent
+    std::array<uint64_t, 4> liveness_stats() const {
+        return {stall_reports_.load(), stall_fails_.load(), master_lost_.load(), heartbeats_.load()};
+    }
 
 private:
     friend class IpcArena;
@@ -198,7 +206,25 @@ private:
         bool initiated = false, init_sent = false, device = false;
         std::optional<RingView> rv;
         DevPtrInfo si{}, di{};
+        ring::OpWatch watch; // progress of the op's TCP data path (the liveness thread's stall watchdog)
     };
+
+    // Liveness (negotiated at registration, proto::C2MRequestSessionRegistration::liveness; docs/ARCHITECTURE.md):
+    // a thread that sends the master heartbeats, declares a silent master lost, and watches the TCP data paths of
+    // running ops - an op whose connections moved no byte for the stall timeout is reported to the master
+    // (C2MOpStalled), which kicks the peer the evidence names and aborts the op; if the master cannot (a reference
+    // master) or does not resolve it within another timeout, the op fails locally (OpWatch::failed).
+    struct Watched {
+        std::shared_ptr<OpState> op;
+        ring::Conns rx, tx;
+        Uuid prev, next;
+        uint64_t bytes = 0;
+        std::chrono::steady_clock::time_point progress, reported_at;
+        bool reported = false;
+    };
+    void liveness_loop();
+    void watch_op(const std::shared_ptr<OpState> &op, const RingView &rv);
+    void unwatch_op(const OpState *op);
 
     // connection management
     bool start_listeners();
@@ -270,6 +296,16 @@ private:
     std::condition_variable ss_cv_;  // signalled when a serve ends
     std::atomic<uint64_t> ss_tx_bytes_{0};
     std::vector<std::thread> ss_threads_;
+
+    // liveness (see Watched)
+    uint32_t hb_ms_ = 0, peer_timeout_ms_ = 0, stall_ms_ = 0;
+    bool master_liveness_ = false; // the master runs the protocol (its registration response carried the parameters)
+    std::mutex live_mtx_;
+    std::condition_variable live_cv_;
+    bool live_stop_ = false;
+    std::map<const OpState *, Watched> watched_;
+    std::thread liveness_thread_;
+    std::atomic<uint64_t> stall_reports_{0}, stall_fails_{0}, master_lost_{0}, heartbeats_{0};
 
     // benchmark server
     std::mutex bm_mtx_;

@@ -527,7 +527,28 @@ bool ipc_detail::pid_quiesced(int pid) {
     return quiet;
 }
 
+bool ipc_detail::pid_stopped(int pid) {
+    char path[64];
+    std::snprintf(path, sizeof(path), "/proc/%d/task", pid);
+    DIR *d = ::opendir(path);
+    if (!d) return false;
+    bool stopped = true, any = false;
+    while (dirent *e = ::readdir(d)) {
+        if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+        const char st = proc_state(pid, std::atoi(e->d_name));
+        if (st == 0 || st == 'Z' || st == 'X' || st == 'x') continue;
+        any = true;
+        if (st != 'T' && st != 't') {
+            stopped = false;
+            break;
+        }
+    }
+    ::closedir(d);
+    return stopped && any;
+}
+
 bool ipc_pid_quiesced_for_test(int pid) { return pid_quiesced(pid); }
+bool ipc_pid_stopped_for_test(int pid) { return pid_stopped(pid); }
 bool ipc_pid_alive_for_test(int pid) { return pid_alive(pid); }
 
 int IpcArena::barrier(Client &c, uint64_t tag, uint64_t seq, uint32_t phase) {
@@ -626,6 +647,11 @@ void IpcArena::drain_peers(Client &c, uint64_t seq) {
                 if (pid_quiesced(pids_[k])) break;
                 if (!waited_zombie) ++g_buf_stats[5];
                 waited_zombie = true;
+            } else if (p->launch.load(std::memory_order_acquire) != seq + 1 && pid_stopped(pids_[k])) {
+                // stopped before its pre-launch check: on resume it sees the abort and never launches (run)
+                LOG(WARN) << "IPC: peer " << k << " (pid " << pids_[k] << ") is stopped outside its launch window of "
+                          << "op seq " << seq << "; not waiting for it";
+                break;
             }
             if (steady_clock::now() - t0 > timeout) {
                 LOG(WARN) << "IPC: peer " << k << " did not finish op seq " << seq << " before the restore";

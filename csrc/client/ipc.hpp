@@ -83,6 +83,7 @@ bool ipc_needs_preflight(const std::vector<uint64_t> &gpu_uids, bool done, size_
 // destination lives on another GPU (remote xGMI writes and reads have more latency to cover).
 int ipc_push_grid(const std::vector<uint64_t> &gpu_uids, size_t rank, int remote_grid);
 bool ipc_pid_quiesced_for_test(int pid);
+bool ipc_pid_stopped_for_test(int pid);
 
 struct OpCtx; // per-op mapping context (ipc_shm.hpp)
 

@@ -310,11 +310,13 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
     const size_t W = ring_.size();
     const size_t es = dtype_size(dtype);
     const size_t bytes = ctx.bytes;
-    const bool push = inter != nullptr || shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_))->algo == 0;
+    OpPeerShm *mine = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(rank_));
+    const bool push = inter != nullptr || mine->algo == 0;
 
     auto finish = [&](int rc) -> std::pair<bool, bool> {
         if (rc != 0) {
             if (st) be->stream_sync(st); // my kernels are done: no further accesses from this peer
+            mine->launch.store(0, std::memory_order_release);
             set_phase(seq, PH_ABORTED);
             // peers may still be running kernels that read my input / write my output for this op: nothing is
             // restored, recycled or handed back to the caller before every live peer is past them
@@ -324,6 +326,7 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
                 be->stream_sync(st);
             }
         } else {
+            mine->launch.store(0, std::memory_order_release);
             set_phase(seq, PH_RELEASED);
         }
         unpin_mappings(ctx.pins);
@@ -354,6 +357,17 @@ std::pair<bool, bool> IpcArena::run(Client &c, uint64_t tag, uint64_t seq, const
         LOG(ERR) << "IPC: no stream on device " << device;
         return finish(1);
     }
+    // Last check before the first kernel that touches other peers' buffers: a peer that was stopped (SIGSTOP, a
+    // wedged call) after the vote barrier and resumed after the others gave up on the op - the master dropped it,
+    // or a peer aborted - must not write into buffers they restored or reused. The launch window is published so
+    // that survivors waiting for a stopped peer know whether it could still launch (drain_peers).
+    mine->launch.store(seq + 1, std::memory_order_seq_cst);
+    if (!c.master_.is_open()) return finish(1);
+    for (size_t k = 0; k < W; ++k) {
+        const uint64_t v = shm_->op(static_cast<uint32_t>(seq % kSlots), static_cast<uint32_t>(k))->phase.load();
+        if ((v >> 8) > seq + 1 || ((v >> 8) == seq + 1 && (v & 0xff) == PH_ABORTED)) return finish(1);
+    }
+    if (c.abort_received(tag)) return finish(2);
 
     // shard bounds: 256-byte aligned so every peer's shard is 16-byte-vector aligned
     const size_t align_el = std::max<size_t>(1, 256 / es);

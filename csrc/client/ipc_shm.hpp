@@ -16,7 +16,7 @@
 #include "ipc.hpp"
 
 namespace pccl::client::ipc_detail {
-constexpr uint64_t kMagic = 0x5043434c49504331ull; // "PCCLIPC1"
+constexpr uint64_t kMagic = 0x5043434c49504332ull; // "PCCLIPC2" (layout version)
 constexpr uint32_t kClosed = 0x80000000u;
 constexpr uint32_t kSlots = 128; // ops in flight per ring (slot = seq % kSlots)
 constexpr uint32_t kMaxWorld = 16;
@@ -65,6 +65,10 @@ struct alignas(64) PeerSlotShm {
 // Peers may mix the two modes. *_raw are usable directly by peers in the same process (threaded peers).
 struct alignas(64) OpPeerShm {
     std::atomic<uint64_t> phase; // (seq + 1) << 8 | phase
+    // seq + 1 from the moment this peer re-checked the op's aborts before its first kernel that touches other peers'
+    // buffers until those kernels completed (IpcArena::run); 0 otherwise. A peer stopped (SIGSTOP) outside that
+    // window will re-check on resume and never launch, so survivors need not wait for it (drain_peers).
+    std::atomic<uint64_t> launch;
     uint32_t vote;
     int32_t device;
     uint64_t bytes;
@@ -130,5 +134,7 @@ extern std::map<std::pair<const IpcArena *, uint64_t>, OpCtx> g_ctx;
 
 bool pid_alive(int pid);
 bool pid_quiesced(int pid);
+// every thread of the process is stopped (job control / ptrace stop) or gone: it runs no code until resumed
+bool pid_stopped(int pid);
 
 } // namespace pccl::client::ipc_detail

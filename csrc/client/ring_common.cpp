@@ -15,6 +15,10 @@ using namespace std::chrono_literals;
 namespace {
 std::atomic<uint64_t> g_pcie_h2d{0}, g_pcie_d2h{0};
 }
+OpWatch *&current_watch() {
+    thread_local OpWatch *w = nullptr;
+    return w;
+}
 void pcie_note(size_t h2d, size_t d2h) {
     if (h2d) g_pcie_h2d.fetch_add(h2d, std::memory_order_relaxed);
     if (d2h) g_pcie_d2h.fetch_add(d2h, std::memory_order_relaxed);
@@ -175,7 +179,7 @@ int recv_meta(const StepIo &io, proto::QuantMeta &theirs, std::atomic<uint64_t> 
             rx += proto::encode_with_id(*m).size() + kMetaFrameOverhead;
             return 0;
         }
-        if (!io.rx->is_open() || (failed && failed())) return 1;
+        if (!io.rx->is_open() || (failed && failed()) || watch_failed()) return 1;
         if (aborted()) return 2;
     }
 }
@@ -195,6 +199,26 @@ struct CountDown {
     void wait() {
         std::unique_lock l(m);
         cv.wait(l, [&] { return n == 0; });
+    }
+    // false once `stop` reports (polled every 20 ms) before every sender finished
+    bool wait_until_done(const std::function<bool()> &stop) {
+        std::unique_lock l(m);
+        while (!cv.wait_for(l, std::chrono::milliseconds(20), [&] { return n == 0; })) {
+            l.unlock();
+            const bool s = stop();
+            l.lock();
+            if (s && n != 0) return false;
+        }
+        return true;
+    }
+    // the senders of a failed step: a sender blocked in sendmsg on a peer that stopped reading is interrupted
+    void wait_failed(const Conns &txs) {
+        std::unique_lock l(m);
+        while (!cv.wait_for(l, std::chrono::milliseconds(100), [&] { return n == 0; })) {
+            l.unlock();
+            net::interrupt_blocked_senders(txs, net::sink_drain_grace());
+            l.lock();
+        }
     }
 };
 } // namespace
@@ -251,7 +275,7 @@ int striped_step(const Conns &txs, const Conns &rxs, uint64_t tag, uint64_t seq,
     if (before_rx) {
         if (const int brc = before_rx()) {
             send_rc.store(brc);
-            senders.wait();
+            senders.wait_failed(txs);
             remove_sinks();
             return brc;
         }
@@ -287,7 +311,7 @@ int striped_step(const Conns &txs, const Conns &rxs, uint64_t tag, uint64_t seq,
         while (done[k] >= rp.len[k] / elem) k = rr++ % rp.off.size();
         net::MuxConn *c = rx_conn(k);
         c->wait_sink(tag, std::min(rp.len[k], (done[k] + gran_el) * elem), 5ms);
-        if (!c->is_open() || send_rc.load() != 0) {
+        if (!c->is_open() || send_rc.load() != 0 || watch_failed()) {
             rc = 1;
             break;
         }
@@ -298,12 +322,19 @@ int striped_step(const Conns &txs, const Conns &rxs, uint64_t tag, uint64_t seq,
     }
     if (rc != 0) {
         send_rc.store(rc);
-        // senders stuck in send() on a dead peer return once the connection is torn down
-        senders.wait();
+        // senders stuck in send() on a peer that stopped reading are interrupted (wait_failed)
+        senders.wait_failed(txs);
         remove_sinks();
         return rc;
     }
-    senders.wait();
+    // every byte arrived; this step's own sends may still be blocked on a next peer that stopped reading: the wait
+    // ends on the op's abort / watchdog verdict as well
+    if (!senders.wait_until_done([&] { return watch_failed() || aborted(); })) {
+        send_rc.store(1);
+        senders.wait_failed(txs);
+        remove_sinks();
+        return aborted() ? 2 : 1;
+    }
     remove_sinks();
     if (send_rc.load() != 0) return 1;
     rx_ctr += rx_bytes;
@@ -334,6 +365,7 @@ int small_allgather_reduce(const Conns &txs, const Conns &rxs, uint64_t tag, uin
     uint8_t *v = all.data();
     std::memcpy(v + rank * bytes, src, bytes);
     for (size_t step = 0; step + 1 < ws; ++step) {
+        watch_step(step);
         const size_t send_idx = (rank + ws - step) % ws, recv_idx = (rank + ws - step - 1) % ws;
         const int rc = striped_step(txs, rxs, tag, seq, shape, v + send_idx * bytes, bytes, [](size_t) { return true; },
                                     v + recv_idx * bytes, bytes, es, std::max<size_t>(bytes, 1),
@@ -351,8 +383,10 @@ int run_lanes(const std::vector<size_t> &lo, const std::function<int(size_t, siz
     const size_t nl = lo.size() - 1;
     std::vector<int> rc(nl, 0);
     std::vector<std::thread> th;
-    for (size_t k = 1; k < nl; ++k) th.emplace_back([&, k] {
+    OpWatch *watch = current_watch();
+    for (size_t k = 1; k < nl; ++k) th.emplace_back([&, k, watch] {
         name_thread("pccl-ring-lane");
+        current_watch() = watch;
         rc[k] = fn(k, lo[k], lo[k + 1]);
     });
     rc[0] = fn(0, lo[0], lo[1]);
@@ -453,14 +487,30 @@ OpSenders::OpSenders(const Conns &txs, uint64_t tag, uint64_t seq, const Shape &
                      size_t max_stripes, DeviceBackend *be, std::atomic<uint64_t> &tx_ctr)
     : txs_(txs), tag_(tag), seq_(seq), shape_(shape), frame_(frame), be_(be), tx_ctr_(tx_ctr), steps_(nsteps),
       done_(nsteps) {
+    running_ = max_stripes;
     for (size_t k = 0; k < max_stripes; ++k) th_.emplace_back([this, k] {
         name_thread("pccl-stripe-tx");
         run(k);
+        {
+            std::lock_guard l(m_);
+            --running_;
+        }
+        cv_.notify_all();
     });
 }
 
 OpSenders::~OpSenders() {
     cancel();
+    // A stripe thread still blocked in sendmsg (its peer stopped reading: stopped, wedged, black-holed) would never
+    // return: interrupt such connections after a grace period instead of waiting for TCP to give up.
+    {
+        std::unique_lock l(m_);
+        while (!cv_.wait_for(l, std::chrono::milliseconds(100), [&] { return running_ == 0; })) {
+            l.unlock();
+            net::interrupt_blocked_senders(txs_, net::sink_drain_grace());
+            l.lock();
+        }
+    }
     for (auto &t : th_) t.join();
 }
 
@@ -488,22 +538,48 @@ bool OpSenders::sent(size_t g) {
     return published_ > g && done_[g] == 0;
 }
 
+bool OpSenders::should_stop() {
+    return watch_failed() || (abort_ && abort_());
+}
+
+// The op thread waits here for its own sends; a stripe blocked on a peer that stopped reading never finishes its
+// step, so the wait also ends on the op's abort / watchdog verdict (polled between short sleeps)
 bool OpSenders::wait(size_t g) {
     std::unique_lock l(m_);
-    cv_.wait(l, [&] { return rc_.load() != 0 || (published_ > g && done_[g] == 0); });
+    for (size_t polls = 1; !(rc_.load() != 0 || (published_ > g && done_[g] == 0)); ++polls) {
+        if (cv_.wait_for(l, std::chrono::milliseconds(5)) == std::cv_status::timeout && polls % 4 == 0) {
+            l.unlock();
+            const bool stop = should_stop();
+            l.lock();
+            if (stop) {
+                rc_.store(1);
+                cv_.notify_all();
+            }
+        }
+    }
     return rc_.load() == 0;
 }
 
 // (a stripe with no bytes in the last step may still be sending an earlier one)
 bool OpSenders::wait_all() {
-    std::unique_lock l(m_);
-    cv_.wait(l, [&] {
-        if (rc_.load() != 0) return true;
+    auto all_sent = [&] {
         if (published_ < steps_.size()) return false;
         for (size_t d : done_)
             if (d != 0) return false;
         return true;
-    });
+    };
+    std::unique_lock l(m_);
+    for (size_t polls = 1; !(rc_.load() != 0 || all_sent()); ++polls) {
+        if (cv_.wait_for(l, std::chrono::milliseconds(5)) == std::cv_status::timeout && polls % 4 == 0) {
+            l.unlock();
+            const bool stop = should_stop();
+            l.lock();
+            if (stop) {
+                rc_.store(1);
+                cv_.notify_all();
+            }
+        }
+    }
     return rc_.load() == 0;
 }
 
@@ -577,6 +653,7 @@ int RingRx::receive(size_t g, size_t unit, size_t gran, const std::function<void
     Step &r = steps_[g];
     const size_t gb = std::max(unit, gran / unit * unit);
     size_t idle = 0, rr = 0;
+    watch_step(g);
     while (r.remaining > 0) {
         bool progress = false;
         for (size_t k = 0; k < r.sinks.size(); ++k) {
@@ -601,7 +678,7 @@ int RingRx::receive(size_t g, size_t unit, size_t gran, const std::function<void
         while (!r.sinks[k] || r.done[k] >= r.rp.len[k]) k = rr++ % r.sinks.size();
         net::MuxConn *c = conn(k);
         c->wait_sink(r.sinks[k], std::min(r.rp.len[k], r.done[k] + gb), 5ms);
-        if (!c->is_open() || (failed && failed())) return 1;
+        if (!c->is_open() || (failed && failed()) || watch_failed()) return 1;
         if (++idle % 8 == 0 && aborted()) return 2;
     }
     return 0;

@@ -108,6 +108,23 @@ size_t stripe_count(size_t bytes, size_t conns, const Shape &shape);
 // group and the number of its sender threads; shape.stripes if op_max_step is unset)
 size_t op_stripes(const Shape &shape, size_t conns);
 
+// Progress watch of the op whose data path runs on this thread (Client::run_op installs it; run_lanes hands it to
+// its lane threads). The data paths publish the ring step they wait in; the client's liveness thread sets `failed`
+// when the op made no progress for PCCL_OP_STALL_MS and the master did not resolve the stall (or cannot: a reference
+// master), and every receive loop then returns an io failure.
+struct OpWatch {
+    std::atomic<uint32_t> step{0};
+    std::atomic<bool> failed{false};
+};
+OpWatch *&current_watch();
+inline void watch_step(size_t g) {
+    if (OpWatch *w = current_watch()) w->step.store(static_cast<uint32_t>(g), std::memory_order_relaxed);
+}
+inline bool watch_failed() {
+    const OpWatch *w = current_watch();
+    return w != nullptr && w->failed.load(std::memory_order_acquire);
+}
+
 // Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first
 // poll that sees it (Client::abort_received), so that poll records it here for every other thread of the op.
 class OpAbort {
@@ -277,9 +294,15 @@ public:
     bool wait_all();
     void cancel();
     bool failed() const { return rc_.load() != 0; }
+    // the op's abort poll: wait / wait_all also end (false) once it reports the master's abort or the op's watchdog
+    // failed it (a stripe blocked on a peer that stopped reading would otherwise never let them return). The caller
+    // must then report the op as aborted if the poll saw the abort (it consumed the master's only abort packet).
+    void set_abort(std::function<bool()> abort) { abort_ = std::move(abort); }
 
 private:
     void run(size_t k);
+    bool should_stop();
+    std::function<bool()> abort_;
     const Conns &txs_;
     const uint64_t tag_, seq_;
     const Shape shape_;
@@ -291,6 +314,7 @@ private:
     std::vector<Step> steps_;
     std::vector<size_t> done_;
     size_t published_ = 0;
+    size_t running_ = 0; // stripe threads that have not returned yet (guarded by m_)
     std::atomic<int> rc_{0};
     std::vector<std::thread> th_;
 };

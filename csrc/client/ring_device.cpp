@@ -138,9 +138,12 @@ int device_ring_pipeline(DevRing &R) {
     OpSenders senders(R.txs, R.tag, seq, shape, piece, nsteps, op_stripes(shape, R.txs.size()), be, R.tx);
     RingRx rx(R.rxs, R.tag, seq, shape, nsteps); // after the buffers its sinks point into
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, rx_bytes);
+    senders.set_abort(R.aborted);
     auto fail = [&](int code) {
         senders.cancel();
-        return code;
+        // a send wait that ended on the master's abort consumed its packet: report the abort (run_op must not wait
+        // for a second one)
+        return code == 1 && R.aborted() ? 2 : code;
     };
     // a segment's first payload: its own input chunk -> pinned, in pieces (from src: ready at call time, never
     // written by the op). Its slot was last read by the sends of step G - kNb.

@@ -167,10 +167,12 @@ int device_quant_lane(QLane &L) {
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);
 
+    senders.set_abort(L.aborted);
     auto fail = [&](int code) {
         senders.cancel();
         L.op_failed->store(true);
-        return code;
+        // a send wait that ended on the master's abort consumed its packet: report the abort
+        return code == 1 && L.aborted() ? 2 : code;
     };
     auto failed = [&] { return senders.failed() || L.op_failed->load(); };
 

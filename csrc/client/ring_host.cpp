@@ -37,6 +37,7 @@ int host_ring(const HostRingArgs &A) {
                         const std::function<void(size_t, size_t)> &consume,
                         const std::function<int()> &before_rx = {}) -> int {
         bool first = true;
+        watch_step(g);
         const int rc = striped_step(A.txs, A.rxs, A.tag, A.seq, A.shape, payload, tx_bytes, [](size_t) { return true; },
                                     sink, rx_bytes, qs, chunk, [&](size_t a, size_t b) {
                                         consume(a, b);

@@ -163,20 +163,28 @@ void fault_point(const char *point, uint64_t seq, size_t step, const char *phase
     if (!f.armed || f.seq != seq || f.point != point) return;
     if (f.step != SIZE_MAX && f.step != step) return;
     if (!f.phase.empty() && (phase == nullptr || f.phase != phase)) return;
+    // PCCL_FAULT_SIGNAL=STOP: the process stops instead of dying (SIGSTOP: sockets stay open, the kernel keeps
+    // ACKing; the harness resumes it with SIGCONT), the failure mode keepalive never detects
+    static const bool stop = [] {
+        const char *e = std::getenv("PCCL_FAULT_SIGNAL");
+        return e && (std::strcmp(e, "STOP") == 0 || std::strcmp(e, "SIGSTOP") == 0);
+    }();
+    const int sig = stop ? SIGSTOP : SIGKILL;
     // wall-clock time of the kill (harnesses time recovery from it: benchmarks/fault_tolerance.py)
     timespec now{};
     ::clock_gettime(CLOCK_REALTIME, &now);
-    std::fprintf(stderr, "[pccl] fault injection: SIGKILL at %s seq %llu step %lld phase %s t=%lld.%06ld\n", point,
-                 static_cast<unsigned long long>(seq), step == SIZE_MAX ? -1ll : static_cast<long long>(step),
-                 phase ? phase : "-", static_cast<long long>(now.tv_sec), now.tv_nsec / 1000);
+    std::fprintf(stderr, "[pccl] fault injection: %s at %s seq %llu step %lld phase %s t=%lld.%06ld\n",
+                 stop ? "SIGSTOP" : "SIGKILL", point, static_cast<unsigned long long>(seq),
+                 step == SIZE_MAX ? -1ll : static_cast<long long>(step), phase ? phase : "-",
+                 static_cast<long long>(now.tv_sec), now.tv_nsec / 1000);
     std::fflush(stderr);
     if (const char *d = std::getenv("PCCL_FAULT_INJECT_DELAY_MS")) // die a little later (the point's work goes on)
-        std::thread([ms = std::atol(d)] {
+        std::thread([ms = std::atol(d), sig] {
             ::usleep(static_cast<useconds_t>(ms) * 1000);
-            ::kill(::getpid(), SIGKILL);
+            ::kill(::getpid(), sig);
         }).detach();
     else
-        ::kill(::getpid(), SIGKILL);
+        ::kill(::getpid(), sig);
 }
 
 void fault_stall(const char *point, uint64_t seq) {

@@ -12,6 +12,15 @@ namespace pccl::master {
 using namespace proto;
 
 Master::Master(const SockAddr &listen_addr) : server_(listen_addr, false) {
+    peer_timeout_ms_ = static_cast<uint32_t>(env_size("PCCL_PEER_TIMEOUT_MS", 10000));
+    if (peer_timeout_ms_ > 0) {
+        heartbeat_ms_ = static_cast<uint32_t>(std::max<size_t>(20, env_size("PCCL_HEARTBEAT_MS", peer_timeout_ms_ / 5)));
+        op_stall_ms_ = static_cast<uint32_t>(env_size("PCCL_OP_STALL_MS", peer_timeout_ms_ + peer_timeout_ms_ / 2));
+    } else {
+        op_stall_ms_ = static_cast<uint32_t>(env_size("PCCL_OP_STALL_MS", 15000));
+    }
+    stall_window_ms_ = static_cast<uint32_t>(env_size("PCCL_STALL_WINDOW_MS", std::min<uint32_t>(1000, op_stall_ms_ / 4)));
+    vote_timeout_ms_ = static_cast<uint32_t>(env_size("PCCL_VOTE_TIMEOUT_MS", 0));
     server_.on_read([this](const SockAddr &a, uint16_t id, const uint8_t *p, size_t n) { on_packet(a, id, p, n); });
     server_.on_close([this](const SockAddr &a) { on_disconnect(a); });
     server_.on_tick([this] { on_tick(); });
@@ -266,7 +275,15 @@ void Master::on_packet(const SockAddr &addr, uint16_t id, const uint8_t *payload
         LOG(ERR) << "Master: malformed " << what << " from " << sockaddr_str(addr);
         kick(addr);
     };
+    if (ClientInfo *c = client_by_addr(addr)) c->last_seen = std::chrono::steady_clock::now(); // any packet is life
     switch (id) {
+        case C2M_HEARTBEAT: return;
+        case C2M_OP_STALLED: {
+            auto p = parse<C2MOpStalled>(payload, n);
+            if (!p) return bad("OpStalled");
+            handle_op_stalled(addr, *p);
+            return;
+        }
         case C2M_REQUEST_SESSION_REGISTRATION: {
             auto p = parse<C2MRequestSessionRegistration>(payload, n);
             if (!p) return bad("RequestSessionRegistration");
@@ -346,6 +363,13 @@ void Master::handle_join(const SockAddr &addr, const C2MRequestSessionRegistrati
         c.group = p.peer_group;
         c.host_token = p.host_token;
         c.xgmi = p.xgmi_capable;
+        c.liveness = p.liveness;
+        c.last_seen = std::chrono::steady_clock::now();
+        if (p.liveness) { // only a peer that announced the extension gets the appended fields
+            resp.heartbeat_ms = heartbeat_ms_;
+            resp.peer_timeout_ms = peer_timeout_ms_;
+            resp.op_stall_ms = op_stall_ms_;
+        }
         if (p.use_explicit_addresses) {
             c.p2p = p.advertised_p2p;
             c.ss = p.advertised_ss;
@@ -1099,12 +1123,176 @@ void Master::on_disconnect(const SockAddr &addr) {
 
 // PCCL_MASTER_DUMP_SEC=N: log the full consensus state every N seconds (diagnosing stuck runs)
 void Master::on_tick() {
+    check_liveness(std::chrono::steady_clock::now());
     static const size_t every = env_size("PCCL_MASTER_DUMP_SEC", 0);
     if (every == 0) return;
     const auto now = std::chrono::steady_clock::now();
     if (now - last_dump_ < std::chrono::seconds(every)) return;
     last_dump_ = now;
     LOG(WARN) << "Master state:\n" << dump_state();
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// liveness: heartbeats, stalled ops, vote timeouts
+//
+// The reference detects failures only by TCP close / RST and SO_KEEPALIVE (tinysockets multiplexed_socket.cpp:29-49,
+// server_socket.cpp). Neither fires for a peer that stops without closing its sockets (SIGSTOP, a wedged driver
+// call, a swapped-out host, a black-holed path): its kernel keeps ACKing, and keepalive never probes while data is
+// outstanding. Such a peer used to hang its whole group forever. Three bounded detectors act through the existing
+// disconnect path (unregister, abort the running tags, re-form the ring):
+//  * heartbeats: a liveness peer silent for PCCL_PEER_TIMEOUT_MS is dropped (the master sends M2CHeartbeat too, so
+//    peers detect a lost master);
+//  * stalled ops: peers report an op whose TCP data path made no progress (C2MOpStalled); the master collects the
+//    reports of the op for PCCL_STALL_WINDOW_MS, or until every performing participant reported, and drops the
+//    peer the evidence names;
+//  * vote timeout (PCCL_VOTE_TIMEOUT_MS, off by default: a slow peer cannot be told from a hung one): an idle peer
+//    that has not joined a consensus every other waiter of its group has waited in for that long is dropped.
+// ------------------------------------------------------------------------------------------------------------------
+void Master::check_liveness(std::chrono::steady_clock::time_point now) {
+    using std::chrono::milliseconds;
+    if (peer_timeout_ms_ > 0) {
+        if (now - last_heartbeat_ >= milliseconds(heartbeat_ms_)) {
+            last_heartbeat_ = now;
+            for (const auto &[_, c] : clients_)
+                if (c.liveness) server_.send_packet(c.addr, M2CHeartbeat{});
+        }
+        std::vector<SockAddr> silent;
+        for (const auto &[u, c] : clients_)
+            if (c.liveness && now - c.last_seen > milliseconds(peer_timeout_ms_)) silent.push_back(c.addr);
+        for (const auto &a : silent) {
+            const ClientInfo *c = client_by_addr(a);
+            LOG(WARN) << "Master: peer " << (c ? c->uuid.str() : std::string("?")) << " (" << sockaddr_str(a)
+                      << ") silent for more than " << peer_timeout_ms_ << " ms; dropping it";
+            live_silent_++;
+            kick(a);
+        }
+    }
+    std::vector<std::pair<uint32_t, uint64_t>> keys;
+    for (const auto &[k, _] : stalls_) keys.push_back(k);
+    for (const auto &k : keys) decide_stall(k.first, k.second, now);
+    if (vote_timeout_ms_ > 0) check_vote_timeouts(now);
+}
+
+void Master::handle_op_stalled(const SockAddr &addr, const C2MOpStalled &p) {
+    ClientInfo *c = client_by_addr(addr);
+    if (!c || c->phase != Phase::Accepted) return;
+    live_reports_++;
+    auto it = c->colls.find(p.tag);
+    if (it == c->colls.end() || it->second != CollState::Perform) return; // the op ended meanwhile
+    auto &v = stalls_[{c->group, p.tag}];
+    for (const auto &r : v)
+        if (r.reporter == c->uuid) return;
+    LOG(WARN) << "Master: op tag " << p.tag << " stalled at " << c->uuid.str() << " (step " << p.step << ", "
+              << (p.kind == kStallTxBlocked ? "send blocked to " : "nothing from ") << p.suspect.str() << ", "
+              << p.idle_ms << " ms)";
+    v.push_back(StallReport{c->uuid, p, std::chrono::steady_clock::now()});
+    decide_stall(c->group, p.tag, std::chrono::steady_clock::now());
+}
+
+bool Master::decide_stall(uint32_t group, uint64_t tag, std::chrono::steady_clock::time_point now) {
+    const auto key = std::make_pair(group, tag);
+    auto sit = stalls_.find(key);
+    if (sit == stalls_.end()) return false;
+    auto &v = sit->second;
+    size_t performing = 0, reported = 0;
+    for (const auto &[u, c] : clients_) {
+        if (c.group != group || c.phase != Phase::Accepted) continue;
+        auto it = c.colls.find(tag);
+        if (it == c.colls.end() || it->second != CollState::Perform) continue;
+        ++performing;
+        for (const auto &r : v)
+            if (r.reporter == u) ++reported;
+    }
+    if (performing == 0 || v.empty()) { // the op ended (aborted / completed) or its reporters left
+        stalls_.erase(sit);
+        return false;
+    }
+    if (reported < performing && now - v.front().at < std::chrono::milliseconds(stall_window_ms_)) return false;
+    // A blocked send is direct evidence against its receiver. Otherwise the ring stalled at one link: the peers
+    // behind it wait in later ring steps (each can finish the step it already has data for), so the report with the
+    // lowest step names the link's sender; ties go to the longest idle time.
+    const StallReport *best = nullptr;
+    for (const auto &r : v) {
+        const auto &a = r.report;
+        if (!best) {
+            best = &r;
+            continue;
+        }
+        const auto &b = best->report;
+        const bool a_tx = a.kind == kStallTxBlocked, b_tx = b.kind == kStallTxBlocked;
+        if (a_tx != b_tx) {
+            if (a_tx) best = &r;
+            continue;
+        }
+        if (a.step != b.step ? a.step < b.step : a.idle_ms > b.idle_ms) best = &r;
+    }
+    const Uuid suspect = best->report.suspect;
+    stalls_.erase(sit);
+    ClientInfo *s = client_by_uuid(suspect);
+    live_stalled_++;
+    if (s && s->group == group) {
+        LOG(WARN) << "Master: op tag " << tag << " of group " << group << " stalled (" << reported << " of "
+                  << performing << " participants reported); dropping peer " << suspect.str();
+        kick(s->addr); // the disconnect path aborts the op for everyone
+    } else {
+        LOG(WARN) << "Master: op tag " << tag << " stalled; the suspect already left: aborting the op";
+        auto &ab = groups_[group].aborted[tag];
+        if (!ab) {
+            ab = true;
+            send_abort(group, tag, true);
+        }
+    }
+    return true;
+}
+
+bool Master::is_waiting(const ClientInfo &c) {
+    switch (c.state) {
+        case State::VoteAcceptNewPeers:
+        case State::VoteNoNewPeersEstablishP2P:
+        case State::WaitingForOtherPeers:
+        case State::VoteOptimizeTopology:
+        case State::VoteCompleteTopologyOptimization:
+        case State::VoteSyncSharedState:
+        case State::VoteCompleteSharedStateSync: return true;
+        default: break;
+    }
+    if (c.voted_pending_query) return true;
+    for (const auto &[_, cs] : c.colls)
+        if (cs == CollState::VoteInitiate || cs == CollState::VoteComplete) return true;
+    return false;
+}
+
+// in application code: nothing pending at the master (a peer in a data phase - connecting, benchmarking, moving
+// shared state, running an op - is watched by the other detectors)
+bool Master::is_lagging(const ClientInfo &c) {
+    return c.phase == Phase::Accepted && c.state == State::Idle && c.colls.empty() && !c.voted_pending_query;
+}
+
+void Master::check_vote_timeouts(std::chrono::steady_clock::time_point now) {
+    std::map<uint32_t, std::chrono::steady_clock::time_point> oldest;
+    for (auto &[_, c] : clients_) {
+        if (c.phase != Phase::Accepted) continue;
+        const bool w = is_waiting(c);
+        if (w && !c.waiting) c.waiting_since = now;
+        c.waiting = w;
+        if (w) {
+            auto it = oldest.find(c.group);
+            if (it == oldest.end() || c.waiting_since < it->second) oldest[c.group] = c.waiting_since;
+        }
+    }
+    std::vector<SockAddr> late;
+    for (const auto &[u, c] : clients_) {
+        auto it = oldest.find(c.group);
+        if (it == oldest.end() || now - it->second < std::chrono::milliseconds(vote_timeout_ms_)) continue;
+        if (is_lagging(c)) late.push_back(c.addr);
+    }
+    for (const auto &a : late) {
+        const ClientInfo *c = client_by_addr(a);
+        LOG(WARN) << "Master: peer " << (c ? c->uuid.str() : std::string("?")) << " did not vote within "
+                  << vote_timeout_ms_ << " ms while its group waited; dropping it";
+        live_vote_++;
+        kick(a);
+    }
 }
 
 std::string Master::bandwidth_table() {

@@ -18,6 +18,7 @@
 
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -70,6 +71,20 @@ struct ClientInfo {
     uint64_t ss_revision = 0; // revision announced in the current shared-state round
     std::string host_token;   // registration extension; empty for reference clients
     bool xgmi = true;         // registration extension: may take the xGMI IPC path
+    // liveness extension (registration): the peer sends heartbeats; silent for PCCL_PEER_TIMEOUT_MS -> dropped.
+    // Reference peers (liveness = false) are exempt, as the reference master has no timeout at all.
+    bool liveness = false;
+    std::chrono::steady_clock::time_point last_seen{};
+    // vote timeout bookkeeping (PCCL_VOTE_TIMEOUT_MS): since when the peer waits in a consensus
+    bool waiting = false;
+    std::chrono::steady_clock::time_point waiting_since{};
+};
+
+// One C2MOpStalled report of a running op (collected per group and tag, decided by decide_stall)
+struct StallReport {
+    Uuid reporter;
+    proto::C2MOpStalled report;
+    std::chrono::steady_clock::time_point at;
 };
 
 struct GroupState {
@@ -128,6 +143,16 @@ private:
     void handle_dist_complete(const SockAddr &addr);
     void handle_coll_initiate(const SockAddr &addr, const proto::C2MCollectiveCommsInitiate &p);
     void handle_coll_complete(const SockAddr &addr, const proto::C2MCollectiveCommsComplete &p);
+    void handle_op_stalled(const SockAddr &addr, const proto::C2MOpStalled &p);
+
+    // liveness (on the loop thread; docs/ARCHITECTURE.md "Failure detection")
+    void check_liveness(std::chrono::steady_clock::time_point now);
+    // decides a stalled op once every performing participant reported or the decision window passed: kicks the peer
+    // the reports name (which aborts the op through the disconnect path); returns true if it decided
+    bool decide_stall(uint32_t group, uint64_t tag, std::chrono::steady_clock::time_point now);
+    void check_vote_timeouts(std::chrono::steady_clock::time_point now);
+    static bool is_waiting(const ClientInfo &c);
+    static bool is_lagging(const ClientInfo &c);
 
     // consensus checks
     void check_establish_consensus();
@@ -174,6 +199,13 @@ private:
     bool peer_dropped_ = false;
     bool running_ = false;
 
+    // liveness parameters (PCCL_PEER_TIMEOUT_MS default 10 s, 0 = off; PCCL_HEARTBEAT_MS default timeout / 5;
+    // PCCL_OP_STALL_MS default 1.5 x timeout; PCCL_STALL_WINDOW_MS default min(1 s, stall / 4); PCCL_VOTE_TIMEOUT_MS
+    // default 0 = off)
+    uint32_t peer_timeout_ms_ = 0, heartbeat_ms_ = 0, op_stall_ms_ = 0, stall_window_ms_ = 0, vote_timeout_ms_ = 0;
+    std::chrono::steady_clock::time_point last_heartbeat_{};
+    std::map<std::pair<uint32_t, uint64_t>, std::vector<StallReport>> stalls_;
+
     // async moonshot optimization
     std::mutex pending_mtx_;
     std::map<uint32_t, std::pair<std::vector<Uuid>, bool>> pending_rings_;
@@ -187,9 +219,15 @@ public:
     std::array<uint64_t, 4> topology_stats() const {
         return {topo_solves_.load(), topo_last_us_.load(), topo_changes_.load(), topo_moonshots_.load()};
     }
+    // liveness counters (pcclxMasterLivenessStats): [0] peers dropped for silence, [1] peers dropped on stall
+    // reports, [2] peers dropped for not voting (PCCL_VOTE_TIMEOUT_MS), [3] stall reports received
+    std::array<uint64_t, 4> liveness_stats() const {
+        return {live_silent_.load(), live_stalled_.load(), live_vote_.load(), live_reports_.load()};
+    }
 
 private:
     std::atomic<uint64_t> topo_solves_{0}, topo_last_us_{0}, topo_changes_{0}, topo_moonshots_{0};
+    std::atomic<uint64_t> live_silent_{0}, live_stalled_{0}, live_vote_{0}, live_reports_{0};
 };
 
 } // namespace pccl::master

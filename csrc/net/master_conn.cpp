@@ -10,6 +10,14 @@
 
 namespace pccl::net {
 
+namespace {
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+constexpr int64_t rx_spin_ns() { return 200 * 1000; }
+} // namespace
+
 MasterConnection::MasterConnection(const SockAddr &master) : master_(master) {}
 
 MasterConnection::~MasterConnection() {
@@ -26,6 +34,7 @@ bool MasterConnection::connect() {
     timeval tv{10, 0}; // bounded sends (reference: SO_SNDTIMEO 10 s)
     setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
     open_ = true;
+    last_rx_ns_.store(steady_ns(), std::memory_order_relaxed);
     rx_thread_ = std::thread([this] {
         name_thread("pccl-master-rx");
         rx_loop();
@@ -47,14 +56,6 @@ void MasterConnection::join() {
         fd_ = -1;
     }
 }
-
-namespace {
-int64_t steady_ns() {
-    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
-constexpr int64_t rx_spin_ns() { return 200 * 1000; }
-} // namespace
 
 bool MasterConnection::send_raw(uint16_t id, const std::vector<uint8_t> &payload) {
     if (!open_) return false;
@@ -79,6 +80,8 @@ void MasterConnection::rx_loop() {
         }
         auto pkt = recv_ltv(fd_);
         if (!pkt) break;
+        last_rx_ns_.store(steady_ns(), std::memory_order_relaxed);
+        if (pkt->id == proto::M2C_HEARTBEAT) continue; // a sign of life only (liveness extension): never queued
         {
             std::lock_guard lock(q_mtx_);
             queue_.push_back(Item{pkt->id, std::move(pkt->payload)});

@@ -28,6 +28,8 @@ public:
     void interrupt();
     void join();
     bool is_open() const { return open_.load(); }
+    // steady-clock ns of the last packet received from the master (any packet, M2CHeartbeat included; 0: none yet)
+    int64_t last_rx_ns() const { return last_rx_ns_.load(std::memory_order_relaxed); }
 
     template<typename P>
     bool send(const P &p) {
@@ -78,6 +80,7 @@ private:
     // (a request to the master is usually answered within tens of us, and waking a thread parked on an idle core
     // costs about as much: 200 us)
     std::atomic<int64_t> rx_hot_until_{0};
+    std::atomic<int64_t> last_rx_ns_{0};
 };
 
 } // namespace pccl::net

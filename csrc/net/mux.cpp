@@ -151,6 +151,11 @@ void MuxConn::tx_job_loop() {
     }
 }
 
+static int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n) {
     if (!is_open()) return false;
     uint8_t hdr[kMuxHeaderBytes];
@@ -160,11 +165,41 @@ bool MuxConn::send_frame(uint64_t tag, uint64_t ctr, const void *data, size_t n)
     if (wan_sim().enabled) wan_shape(n + 24, sim_next_free_, sim_last_send_);
     // bulk frames from pinned staging buffers may go out as MSG_ZEROCOPY (socket.cpp: sendv_all_zerocopy)
     const bool zc = zerocopy_ && n >= (256u << 10);
-    if (!(zc ? sendv_all_zerocopy(fd_, iov, n ? 2 : 1, zc_next_id_) : sendv_all(fd_, iov, n ? 2 : 1))) {
+    send_since_ns_.store(steady_ns(), std::memory_order_relaxed);
+    const bool ok = zc ? sendv_all_zerocopy(fd_, iov, n ? 2 : 1, zc_next_id_) : sendv_all(fd_, iov, n ? 2 : 1);
+    send_since_ns_.store(0, std::memory_order_relaxed);
+    if (!ok) {
         open_.store(false, std::memory_order_release);
         return false;
     }
+    tx_total_.fetch_add(n + kMuxHeaderBytes, std::memory_order_relaxed);
     return true;
+}
+
+std::chrono::nanoseconds MuxConn::send_blocked_for() const {
+    const int64_t t = send_since_ns_.load(std::memory_order_relaxed);
+    return std::chrono::nanoseconds(t == 0 ? 0 : std::max<int64_t>(0, steady_ns() - t));
+}
+
+size_t interrupt_blocked_senders(const std::vector<std::shared_ptr<MuxConn>> &conns, std::chrono::nanoseconds min_blocked) {
+    size_t n = 0;
+    for (const auto &c : conns) {
+        if (!c || !c->is_open()) continue;
+        const auto b = c->send_blocked_for();
+        if (b.count() > 0 && b >= min_blocked) {
+            LOG(WARN) << "MuxConn: send to " << sockaddr_str(c->peer_addr()) << " blocked for "
+                      << std::chrono::duration_cast<std::chrono::milliseconds>(b).count()
+                      << " ms in a failed op; interrupting the connection";
+            c->interrupt();
+            ++n;
+        }
+    }
+    return n;
+}
+
+std::chrono::milliseconds sink_drain_grace() {
+    static const auto v = std::chrono::milliseconds(env_size("PCCL_SINK_DRAIN_MS", 1000));
+    return v;
 }
 
 bool MuxConn::read_into(uint8_t *dst, size_t n, Sink *progress_sink) {
@@ -382,12 +417,13 @@ void MuxConn::remove_sink(uint64_t tag) {
 void MuxConn::remove_sink(uint64_t tag, const SinkRef &s) {
     if (!s) return;
     std::unique_lock l(mtx_);
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    const auto deadline = std::chrono::steady_clock::now() + sink_drain_grace();
     bool interrupted = false;
     while (s->busy) {
-        cv_.wait_for(l, std::chrono::milliseconds(50));
+        cv_.wait_for(l, std::chrono::milliseconds(20));
         if (std::chrono::steady_clock::now() > deadline && !interrupted) {
-            LOG(WARN) << "MuxConn: sink still being written after 10 s; interrupting connection";
+            LOG(WARN) << "MuxConn: sink still being written after " << sink_drain_grace().count()
+                      << " ms; interrupting connection";
             interrupted = true;
             if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
         }

@@ -95,6 +95,11 @@ public:
     void remove_sink(uint64_t tag);
 
     uint64_t rx_bytes_total() const { return rx_total_.load(std::memory_order_relaxed); }
+    uint64_t tx_bytes_total() const { return tx_total_.load(std::memory_order_relaxed); }
+    // How long the frame being sent right now has been inside send_frame (0: no send in progress). A send that does
+    // not finish means the peer does not drain its socket (stopped, wedged, or a black-holed path): the op watchdog
+    // names it, and aborting ops interrupt such a connection instead of joining a sender blocked in sendmsg.
+    std::chrono::nanoseconds send_blocked_for() const;
 
 private:
     struct Frame {
@@ -131,7 +136,17 @@ private:
     std::unordered_map<uint64_t, std::deque<SinkRef>> sinks_;
     std::unordered_map<uint64_t, std::deque<Frame>> queued_;
     std::atomic<uint64_t> rx_total_{0};
+    std::atomic<uint64_t> tx_total_{0};
+    std::atomic<int64_t> send_since_ns_{0}; // steady-clock ns at which the current send_frame started (0: none)
 };
+
+// Interrupts (shuts down) every connection of `conns` whose current send has been blocked for at least `min_blocked`:
+// the sender thread returns from sendmsg with an error. Used on failed ops, whose senders must not stay blocked on a
+// peer that stopped reading (the ring is re-established after a failed op anyway). Returns how many it interrupted.
+size_t interrupt_blocked_senders(const std::vector<std::shared_ptr<MuxConn>> &conns, std::chrono::nanoseconds min_blocked);
+// PCCL_SINK_DRAIN_MS (default 1000): how long removing a receive sink waits for a frame that is still being written
+// into it (the sender of a failed op is mid-frame) before it interrupts the connection.
+std::chrono::milliseconds sink_drain_grace();
 
 size_t multiplex_chunk_size();
 

@@ -77,6 +77,12 @@ void tune_socket(int fd, bool bulk) {
     setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &idle, sizeof(idle));
     setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl));
     setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt));
+    // Keepalive never fires while sent data is unacknowledged (retransmission governs, ~15 min) nor for a stopped
+    // peer (its kernel still ACKs, with a zero window once its buffer is full). TCP_USER_TIMEOUT bounds both: data
+    // unacknowledged, or unsent behind a zero window, for this long closes the connection (PCCL_TCP_USER_TIMEOUT_MS,
+    // default 30 s, 0 = the kernel's default). The liveness protocol usually acts first (PCCL_PEER_TIMEOUT_MS).
+    static const unsigned uto = static_cast<unsigned>(env_size("PCCL_TCP_USER_TIMEOUT_MS", 30000));
+    if (uto > 0) setsockopt(fd, IPPROTO_TCP, TCP_USER_TIMEOUT, &uto, sizeof(uto));
     if (bulk) {
         // Same-host data sockets get fixed 8 MiB buffers and MSG_ZEROCOPY sends (loopback: the receiver copies at
         // memory speed, and zero-copy saves the sender's copy, profiles/r3/zerocopy/). A socket to another host keeps
@@ -268,6 +274,9 @@ bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id) {
             LOG(WARN) << "MSG_ZEROCOPY: no send completion for 30 s; closing the connection";
             return false;
         }
+        // the socket was shut down (an aborted op interrupts a sender blocked on a peer that stopped reading) or
+        // failed: completions may never come, and poll would report the hang-up at once, forever
+        const bool hup = pr > 0 && (pfd.revents & (POLLHUP | POLLNVAL)) != 0;
         while (true) {
             char ctrl[128];
             msghdr msg{};
@@ -288,6 +297,7 @@ bool sendv_all_zerocopy(int fd, iovec *iov, int iovcnt, uint32_t &next_id) {
                 if (static_cast<int32_t>(se.ee_data + 1 - done_to) > 0) done_to = se.ee_data + 1;
             }
         }
+        if (hup && static_cast<int32_t>(next_id - done_to) > 0) return false;
     }
     return true;
 }

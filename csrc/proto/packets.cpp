@@ -19,6 +19,7 @@ void C2MRequestSessionRegistration::encode(WBuf &w) const {
     if (!host_token.empty()) {
         w.str(host_token);
         w.boolean(xgmi_capable);
+        if (liveness) w.u8(kLivenessVersion);
     }
 }
 
@@ -40,6 +41,7 @@ bool C2MRequestSessionRegistration::decode(RBuf &r) {
     if (r.ok() && r.remaining() > 0) host_token = r.str(); // absent when the peer is a reference implementation
     xgmi_capable = true;
     if (r.ok() && r.remaining() > 0) xgmi_capable = r.boolean();
+    liveness = r.ok() && r.remaining() > 0 && r.u8() >= 1;
     return r.ok();
 }
 

@@ -30,6 +30,9 @@ constexpr PacketId C2M_SYNC_SHARED_STATE = 8;
 constexpr PacketId C2M_DIST_SHARED_STATE_COMPLETE = 9;
 constexpr PacketId C2M_COLLECTIVE_COMMS_INITIATE = 10;
 constexpr PacketId C2M_COLLECTIVE_COMMS_COMPLETE = 11;
+// extensions (liveness, negotiated at registration: sent only to / by peers that announced it)
+constexpr PacketId C2M_HEARTBEAT = 12;
+constexpr PacketId C2M_OP_STALLED = 13;
 // ---- master -> client ----
 constexpr PacketId M2C_SESSION_REGISTRATION_RESPONSE = 1;
 constexpr PacketId M2C_P2P_CONNECTION_INFO = 2;
@@ -42,6 +45,7 @@ constexpr PacketId M2C_SYNC_SHARED_STATE_COMPLETE = 8;
 constexpr PacketId M2C_COLLECTIVE_COMMS_COMMENCE = 9;
 constexpr PacketId M2C_COLLECTIVE_COMMS_COMPLETE = 10;
 constexpr PacketId M2C_COLLECTIVE_COMMS_ABORT = 11;
+constexpr PacketId M2C_HEARTBEAT = 12; // extension (liveness)
 // ---- peer <-> peer ----
 constexpr PacketId P2P_HELLO = 1;
 constexpr PacketId P2P_HELLO_ACK = 2;
@@ -75,6 +79,11 @@ struct C2MRequestSessionRegistration {
     // no PCCL_DISABLE_IPC). Same-host pairs of which one cannot are benchmarked like remote pairs: their traffic
     // crosses loopback TCP, so a fixed xGMI-class cost would mislead the ring optimiser.
     bool xgmi_capable = true;
+    // extension after xgmi_capable (optional, u8 version): the peer runs the liveness protocol - it sends
+    // C2MHeartbeat at the interval the master answers with, reports stalled ops (C2MOpStalled) and watches the
+    // master's M2CHeartbeat. A reference peer sends none of it and the master exempts it from the peer timeout.
+    static constexpr uint8_t kLivenessVersion = 1;
+    bool liveness = false;
     void encode(WBuf &w) const;
     bool decode(RBuf &r);
 };
@@ -242,13 +251,67 @@ struct M2CSessionRegistrationResponse {
     static constexpr PacketId kId = M2C_SESSION_REGISTRATION_RESPONSE;
     bool accepted = false;
     Uuid assigned_uuid;
+    // extension (appended only for a peer that announced liveness): the master's liveness parameters. The peer sends
+    // C2MHeartbeat every heartbeat_ms and is dropped after peer_timeout_ms of silence; the master sends M2CHeartbeat
+    // at the same interval, and a peer treats peer_timeout_ms without any packet from the master as a lost master.
+    // op_stall_ms: an op's data path without progress for this long is reported (C2MOpStalled). 0 / absent: off.
+    uint32_t heartbeat_ms = 0, peer_timeout_ms = 0, op_stall_ms = 0;
     void encode(WBuf &w) const {
         w.boolean(accepted);
         w.uuid(assigned_uuid);
+        if (heartbeat_ms || peer_timeout_ms || op_stall_ms) {
+            w.u32(heartbeat_ms);
+            w.u32(peer_timeout_ms);
+            w.u32(op_stall_ms);
+        }
     }
     bool decode(RBuf &r) {
         accepted = r.boolean();
         assigned_uuid = r.uuid();
+        if (r.ok() && r.remaining() >= 12) {
+            heartbeat_ms = r.u32();
+            peer_timeout_ms = r.u32();
+            op_stall_ms = r.u32();
+        }
+        return r.ok();
+    }
+};
+
+// Liveness extension packets (C2M_HEARTBEAT / M2C_HEARTBEAT carry nothing; any packet counts as a sign of life).
+struct C2MHeartbeat : Empty {
+    static constexpr PacketId kId = C2M_HEARTBEAT;
+};
+struct M2CHeartbeat : Empty {
+    static constexpr PacketId kId = M2C_HEARTBEAT;
+};
+
+// A running op's data path made no progress (no byte received or sent on its connections) for op_stall_ms. The
+// reporter names the peer its evidence points at: the next peer if its own send to it has been blocked (the next
+// peer does not drain its socket), else the previous one (nothing arrives from it). `step` is the ring step the
+// reporter waits in; in a ring stalled at one link the peers behind the broken link wait in later steps, so the
+// report with the lowest step names the link. The master collects the reports of an op for a short window, kicks
+// the peer the evidence names and aborts the op (docs/ARCHITECTURE.md, failure detection).
+constexpr uint8_t kStallRxIdle = 0, kStallTxBlocked = 1;
+struct C2MOpStalled {
+    static constexpr PacketId kId = C2M_OP_STALLED;
+    uint64_t tag = 0;
+    Uuid suspect;
+    uint8_t kind = kStallRxIdle;
+    uint32_t step = 0;
+    uint64_t idle_ms = 0;
+    void encode(WBuf &w) const {
+        w.u64(tag);
+        w.uuid(suspect);
+        w.u8(kind);
+        w.u32(step);
+        w.u64(idle_ms);
+    }
+    bool decode(RBuf &r) {
+        tag = r.u64();
+        suspect = r.uuid();
+        kind = r.u8();
+        step = r.u32();
+        idle_ms = r.u64();
         return r.ok();
     }
 };

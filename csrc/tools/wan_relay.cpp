@@ -6,6 +6,12 @@
 // cannot influence.
 //
 //   pccl_wan_relay --delay-ms 50 --flow-mbit 1000 --link-mbit 25000 --map 40001:48149 [--map 40002:48152 ...]
+//                  [--blackhole-port 40001]
+//
+// Failure emulation: with --blackhole-port P, SIGUSR1 black-holes every connection of map P that exists at that
+// moment - both directions stop forwarding while the sockets stay open (the relay reads until its window is full,
+// then the sender's TCP sees a zero window), as a path that silently drops everything. Connections opened later
+// (the ring re-established without the link) are forwarded normally.
 //
 // Model: one-way delay d in both directions; a connection's bytes leave the relay no earlier than arrival + d and no
 // faster than flow_mbit (per direction); all bytes relayed towards one map target share link_mbit (in a ring, all
@@ -47,6 +53,8 @@ struct Config {
 Config g_cfg;
 std::atomic<uint64_t> g_bytes{0};
 volatile sig_atomic_t g_stop = 0;
+uint16_t g_blackhole_port = 0;
+std::atomic<int> g_blackhole_gen{0}; // bumped by SIGUSR1 (lock-free, async-signal-safe)
 
 // shared egress link of one map target (all connections relayed towards it)
 struct Link {
@@ -70,9 +78,11 @@ struct Chunk {
 // one direction of one connection: reader thread -> delay queue -> paced writer thread
 class Pump {
 public:
-    Pump(int src, int dst, Link *link) : src_(src), dst_(dst), link_(link) {
+    Pump(int src, int dst, Link *link, bool blackholable = false)
+        : src_(src), dst_(dst), link_(link), blackholable_(blackholable), born_gen_(g_blackhole_gen.load()) {
         window_ = std::max<size_t>(1 << 20, static_cast<size_t>(2 * g_cfg.delay_s * g_cfg.flow_Bps));
     }
+    bool blackholed() const { return blackholable_ && g_blackhole_gen.load() > born_gen_; }
     void run() {
         std::thread r([this] { reader(); });
         writer();
@@ -109,6 +119,10 @@ private:
                 q_.pop_front();
             }
             const size_t n = c.data.size();
+            if (blackholed()) { // forwards nothing from now on; the sockets stay open (the reader fills its window)
+                while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+                break;
+            }
             double t = std::max(c.arrival + g_cfg.delay_s, flow_next);
             flow_next = t + static_cast<double>(n) / g_cfg.flow_Bps;
             t = std::max(flow_next, link_ ? link_->reserve(n, t) : t);
@@ -141,6 +155,8 @@ private:
     }
     int src_, dst_;
     Link *link_;
+    const bool blackholable_;
+    const int born_gen_;
     size_t window_;
     std::mutex m_;
     std::condition_variable cv_;
@@ -191,7 +207,7 @@ void serve(uint16_t listen_port, uint16_t target) {
     while (true) {
         const int c = ::accept(ls, nullptr, nullptr);
         if (c < 0) continue;
-        std::thread([c, target, link] {
+        std::thread([c, target, link, listen_port] {
             const int t = connect_to(target);
             if (t < 0) {
                 ::close(c);
@@ -199,7 +215,8 @@ void serve(uint16_t listen_port, uint16_t target) {
             }
             tune(c);
             tune(t);
-            Pump up(c, t, link), down(t, c, nullptr); // towards the target: the predecessor's egress link
+            const bool bh = listen_port == g_blackhole_port;
+            Pump up(c, t, link, bh), down(t, c, nullptr, bh); // towards the target: the predecessor's egress link
             std::thread d([&] { down.run(); });
             up.run();
             d.join();
@@ -219,18 +236,20 @@ int main(int argc, char **argv) {
         if (k == "--delay-ms") g_cfg.delay_s = std::atof(v) / 1e3;
         else if (k == "--flow-mbit") g_cfg.flow_Bps = std::atof(v) * 1e6 / 8;
         else if (k == "--link-mbit") g_cfg.link_Bps = std::atof(v) * 1e6 / 8;
+        else if (k == "--blackhole-port") g_blackhole_port = static_cast<uint16_t>(std::atoi(v));
         else if (k == "--map") {
             unsigned a = 0, b = 0;
             if (std::sscanf(v, "%u:%u", &a, &b) != 2) return 2;
             maps.emplace_back(static_cast<uint16_t>(a), static_cast<uint16_t>(b));
         } else {
-            std::fprintf(stderr, "usage: %s --delay-ms D --flow-mbit F --link-mbit L --map LISTEN:TARGET ...\n", argv[0]);
+            std::fprintf(stderr, "usage: %s --delay-ms D --flow-mbit F --link-mbit L --map LISTEN:TARGET ... [--blackhole-port P]\n", argv[0]);
             return 2;
         }
     }
     if (maps.empty()) return 2;
     signal(SIGPIPE, SIG_IGN);
     signal(SIGTERM, [](int) { g_stop = 1; });
+    signal(SIGUSR1, [](int) { g_blackhole_gen.fetch_add(1); });
     for (auto [l, t] : maps) std::thread(serve, l, t).detach();
     std::printf("{\"relay\": \"ready\", \"maps\": %zu}\n", maps.size());
     std::fflush(stdout);

@@ -100,7 +100,11 @@ typedef enum pcclAttribute_t {
     /** [pccl-amd extension] wire framing of the last completed all-reduce: 0 none (no TCP data ring, e.g. xGMI/IPC),
      *  1 pccl-amd framing (agreed per op by every participant: striped connections, quantized lanes and metadata tag),
      *  2 reference framing (a participant without the extension, or PCCL_WIRE=reference) */
-    PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING = 68
+    PCCL_ATTRIBUTE_LAST_REDUCE_FRAMING = 68,
+    /** [pccl-amd extension] 1 while the connection to the master is open; 0 once it is gone (the master dropped this
+     *  peer - e.g. after it was stopped longer than PCCL_PEER_TIMEOUT_MS - or the master was lost). A peer at 0 can
+     *  only destroy the communicator and join again as a new peer. */
+    PCCL_ATTRIBUTE_MASTER_CONNECTED = 69
 } pcclAttribute_t;
 
 typedef enum pcclSharedStateSyncStrategy_t {

@@ -174,6 +174,8 @@ def _load() -> ctypes.CDLL:
         "pcclxPcieStats": ([p(c_uint64), c_size_t], c_size_t),
         "pcclxMasterBandwidthTable": ([c_void_p, c_char_p, c_size_t], c_size_t),
         "pcclxMasterTopologyStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),
+        "pcclxMasterLivenessStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),
+        "pcclxLivenessStats": ([c_void_p, p(c_uint64), c_size_t], c_size_t),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

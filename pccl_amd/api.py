@@ -99,6 +99,7 @@ class Attribute(Enum):
     LAST_REDUCE_PATH = 66
     COLLECTIVE_WORKER_THREADS = 67
     LAST_REDUCE_FRAMING = 68
+    MASTER_CONNECTED = 69
 
 
 class ReducePath(Enum):
@@ -472,6 +473,14 @@ class Communicator:
             C.pcclDestroyCommunicator(comm)
             self._comm = ctypes.c_void_p()
 
+    def liveness_stats(self):
+        """This peer's liveness counters: stalled-op reports sent to the master, ops failed by the local stall
+        watchdog, master declared lost (silent for 2 x PCCL_PEER_TIMEOUT_MS), heartbeats sent."""
+        out = (ctypes.c_uint64 * 4)()
+        C.pcclxLivenessStats(self._comm, out, 4)
+        return {"stall_reports": int(out[0]), "stall_fails": int(out[1]), "master_lost": int(out[2]),
+                "heartbeats": int(out[3])}
+
     def get_attribute(self, attribute: Attribute) -> int:
         v = ctypes.c_int()
         PCCLError.check(C.pcclGetAttribute(self._comm, attribute.value, ctypes.byref(v)), "pcclGetAttribute")
@@ -632,6 +641,14 @@ class MasterNode:
         C.pcclxMasterTopologyStats(self._master, out, 4)
         return {"solves": int(out[0]), "last_solve_us": int(out[1]), "ring_changes": int(out[2]),
                 "moonshot_solves": int(out[3])}
+
+    def liveness_stats(self):
+        """The master's liveness counters: peers dropped for silence (no heartbeat for PCCL_PEER_TIMEOUT_MS), peers
+        dropped on stalled-op reports, peers dropped for not voting (PCCL_VOTE_TIMEOUT_MS), stall reports received."""
+        out = (ctypes.c_uint64 * 4)()
+        C.pcclxMasterLivenessStats(self._master, out, 4)
+        return {"dropped_silent": int(out[0]), "dropped_stalled": int(out[1]), "dropped_vote_timeout": int(out[2]),
+                "stall_reports": int(out[3])}
 
     def await_termination(self):
         if self._running:

@@ -53,6 +53,11 @@ def main():
     ap.add_argument("--pool", type=int, default=0, help="P2P connection pool size (0: library default)")
     ap.add_argument("--max-failures", type=int, default=50, help="exit 3 after more failed ops than this")
     ap.add_argument("--report-mem", action="store_true", help="add the GPU's used bytes (all processes) to every line")
+    ap.add_argument("--rejoin", action="store_true",
+                    help="when the master drops this peer (MASTER_CONNECTED == 0, e.g. after it was stopped), print a "
+                         "'kicked' line, destroy the communicator and join again as a new peer")
+    ap.add_argument("--p2p-port", type=int, default=0, help="P2P listen port (0: library default)")
+    ap.add_argument("--adv-port", type=int, default=0, help="advertised P2P port (a relay in front of --p2p-port)")
     ap.add_argument("--verify-restore-ms", type=int, default=-1,
                     help="in-place: after a failed op wait this long, then require the buffer to be bit-exactly the "
                          "input again (the abort restore must not be overwritten by a late peer write)")
@@ -71,8 +76,17 @@ def main():
         else None
     dev = torch.device(a.device)
     t_start = time.perf_counter()
-    comm = pccl.Communicator(a.master, 0, **({"p2p_connection_pool_size": a.pool} if a.pool else {}))
-    comm.connect(n_attempts=30)
+    def make_comm():
+        kw = {"p2p_connection_pool_size": a.pool} if a.pool else {}
+        if a.p2p_port:
+            kw["p2p_listen_port"] = a.p2p_port
+        if a.adv_port:
+            kw["advertised_p2p_port"] = a.adv_port
+        c = pccl.Communicator(a.master, 0, **kw)
+        c.connect(n_attempts=30)
+        return c
+
+    comm = make_comm()
     if not a.no_wait:
         wait_for_world(comm, a.world, timeout=120)
     step, failures, first_ok = 0, 0, None
@@ -81,8 +95,20 @@ def main():
     while (step < a.steps) if a.duration <= 0 else (t_loop is None or time.perf_counter() - t_loop < a.duration):
         if t_loop is None:
             t_loop = time.perf_counter()
-        if it > 0 and comm.are_peers_pending():
-            comm.update_topology()
+        try:
+            if it > 0 and comm.are_peers_pending():
+                comm.update_topology()
+        except pccl.PCCLError:
+            if comm.get_attribute(pccl.Attribute.MASTER_CONNECTED) != 0:
+                raise
+            print(json.dumps({"rank": a.rank, "step": step, "error": "dropped", "kicked": True, "t": time.time()}),
+                  flush=True)
+            if not a.rejoin:
+                sys.exit(4)
+            comm.destroy()
+            comm = make_comm()
+            it = 0  # a newcomer's first vote is the all-reduce, as the admitting peers' next one (no pending query)
+            print(json.dumps({"rank": a.rank, "rejoined": True, "t": time.time()}), flush=True)
         it += 1
         ws = comm.get_attribute(pccl.Attribute.GLOBAL_WORLD_SIZE)
         if ws < 2:
@@ -101,7 +127,9 @@ def main():
         try:
             info = comm.all_reduce(x, y, op=op, tag=0 if a.const else step, quantization_options=qopt)
         except pccl.PCCLError as e:
-            rec = {"rank": a.rank, "step": step, "error": e.result.name}
+            rec = {"rank": a.rank, "step": step, "error": e.result.name, "t": time.time()}
+            if comm.get_attribute(pccl.Attribute.MASTER_CONNECTED) == 0:
+                rec["kicked"] = True
             if a.verify_restore_ms >= 0 and a.inplace:
                 time.sleep(a.verify_restore_ms / 1e3)
                 if dev.type == "cuda":
@@ -115,6 +143,13 @@ def main():
             failures += 1
             if failures > a.max_failures:
                 sys.exit(3)
+            if rec.get("kicked"):
+                if not a.rejoin:
+                    sys.exit(4)
+                comm.destroy()  # dropped by the master: join again as a new peer
+                comm = make_comm()
+                it = 0
+                print(json.dumps({"rank": a.rank, "rejoined": True, "t": time.time()}), flush=True)
             continue  # retry the step with the new world
         if dev.type == "cuda":
             torch.cuda.synchronize()
@@ -127,7 +162,7 @@ def main():
             lo = hi = float(info.local_world_size) if a.const else None
         rec = {"rank": a.rank, "step": step, "world": info.local_world_size, "lo": lo, "hi": hi,
                "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
-               "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4)}
+               "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4), "t": time.time()}
         rec["staging"] = pccl.memory.staging_pool_stats()
         if dev.type == "cuda":
             rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
