@@ -508,7 +508,7 @@ def _gpu_numa_node_child() -> int:
 # TCP 372 / 367 ms per op on the node vs 383 / 414 with the full mask (kill -> survivors' failed op 193 / 187 vs
 # 220 / 219 ms), config 3 uint8 1.09 / 1.11 vs 1.21 / 1.17 s; the collocated run (its relay moves 10 Gbit/s flows)
 # is faster with the full mask: 62.3 / 66.1 vs 60.3 / 57.3 Gbit/s.
-_NODE_MASKED = ("config5_kill_rejoin_tcp", "config3_wan_50ms")
+_NODE_MASKED = ("config5_kill_rejoin_tcp", "config5_stop_rejoin_tcp", "config3_wan_50ms")
 
 
 def _config_tcp_mask():
@@ -605,8 +605,11 @@ def baseline_configs(a, peers):
       * config 4 (benchmarks/shared_state_sync.py): a 1B-parameter fp32 shared state (8 tensors, 4 GB in HBM); a late
         joiner at revision 0 catches up from a trainer at revision 3, over loopback TCP (pinned staging) and over the
         same-host IPC hand-off; content and simplehash digests compared with the trainer's.
+      * config 5 with SIGSTOP instead of SIGKILL (--signal stop): the victim stops without closing a socket, so only
+        the liveness protocol (heartbeats, PCCL_PEER_TIMEOUT_MS = 2 s here) detects it; the stopped victim is then
+        SIGKILLed and a replacement joins as above (config5_stop_rejoin_tcp).
       * config 3 (benchmarks/wan_quantized.py, EMULATED WAN: pccl_wan_relay, a separate process delaying and pacing
-        every byte; tc-netem needs root): `peers` peer processes on cuda:0, 2 GiB fp32 AVG per peer, 50 ms one way,
+        every byte; tc-netem needs root; each format cold + warm, the warm repeat reported): `peers` peer processes on cuda:0, 2 GiB fp32 AVG per peer, 50 ms one way,
         1 Gbit/s flows, 25 Gbit/s links, 16 connections per neighbour; fp32 (8 ops in flight) and uint8 / int8
         zero-point-scale / fp8 (32 ops in flight, 512 KiB stripes: groups of 4 connections shared by 8 ops measured
         fastest, profiles/r5/b12/); seconds and the reference's metric (rx + tx Gbit/s per peer, its
@@ -615,17 +618,20 @@ def baseline_configs(a, peers):
     import subprocess
     runs = [("config5_kill_rejoin_tcp", ["fault_tolerance.py", "--transport", "tcp", "--peers", str(peers), "--mib",
                                          str(a.mib)], 240),
+            # the same with a peer that stops without closing a socket (SIGSTOP): only the liveness protocol detects it
+            ("config5_stop_rejoin_tcp", ["fault_tolerance.py", "--transport", "tcp", "--peers", str(peers), "--mib",
+                                         str(a.mib), "--signal", "stop", "--peer-timeout-ms", "2000"], 240),
             ("config5_kill_rejoin_ipc", ["fault_tolerance.py", "--transport", "ipc", "--peers", str(peers), "--mib",
                                          str(a.mib)], 180),
             ("config4_late_joiner_tcp", ["shared_state_sync.py", "--transport", "tcp", "--params", "1e9"], 180),
             ("config4_late_joiner_ipc", ["shared_state_sync.py", "--transport", "ipc", "--params", "1e9"], 120),
             ("config3_wan_50ms", ["wan_quantized.py", "--peers", str(peers), "--mib", "2048", "--latency-ms", "50",
                                   "--flow-mbit", "1000", "--link-mbit", "25000", "--pool", "16", "--concurrent", "8",
-                                  "--concurrent-quant", "32", "--stripe-min-kib", "512",
+                                  "--concurrent-quant", "32", "--stripe-min-kib", "512", "--repeat", "2",
                                   "--formats", "fp32,uint8,int8_zps,fp8"], 180),
             ("collocated_5ms_4peers", ["wan_quantized.py", "--peers", "4", "--mib", "2048", "--latency-ms", "5",
                                        "--flow-mbit", "10000", "--link-mbit", "50000", "--pool", "16",
-                                       "--concurrent", "8", "--formats", "fp32"], 120)]
+                                       "--concurrent", "8", "--repeat", "2", "--formats", "fp32"], 120)]
     only = os.environ.get("PCCL_BENCH_CONFIGS")
     if only:
         runs = [r for r in runs if r[0] in only.split(",")]
@@ -1067,6 +1073,12 @@ def main():
             extra["peer_rejoin_latency_source"] = ("BASELINE config 5, TCP device ring: replacement process's connect() "
                                                    "-> its first exact 1 GiB all-reduce at full world, after a peer was "
                                                    "SIGKILLed mid-op")
+            c5s = cfg.get("config5_stop_rejoin_tcp", {})
+            # a peer that stops without closing its sockets (SIGSTOP): detection by the liveness protocol alone
+            extra["stopped_peer_detection_ms"] = {
+                "peer_timeout_ms": c5s.get("peer_timeout_ms"),
+                "stop_to_survivors_failed_op_ms": c5s.get("stop_to_survivors_failed_op_ms"),
+                "stop_to_survivors_first_exact_op_ms": c5s.get("stop_to_survivors_first_exact_op_ms")}
         if "peer_curve" in extra:
             extra["peer_curve"].setdefault("DEVICE_RING", {})[str(P)] = _curve_point(nbytes, ring["t"], P)
     extra["sweep"] = sweep

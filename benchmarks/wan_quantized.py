@@ -163,8 +163,9 @@ def main():
                     help="PCCL_STRIPE_MIN_BYTES / 1024: smallest stripe of a ring step (>= 256)")
     ap.add_argument("--stripes", type=int, default=0, help="PCCL_RING_STRIPES (connections per ring step; 0 = default)")
     ap.add_argument("--device", default="cuda:0")
-    ap.add_argument("--repeat", type=int, default=1,
-                    help="run each format's multi-op this many times (the summary is the last one; 2 = cold + warm)")
+    ap.add_argument("--repeat", type=int, default=2,
+                    help="run each format's multi-op this many times: the summary is the last (warm) one, the first "
+                         "(cold: staging pools and connections' first use) is reported alongside")
     ap.add_argument("--formats", default=",".join(FORMATS))
     ap.add_argument("--emulator", default="relay", choices=["relay", "builtin"])
     ap.add_argument("--log-dir", default=None, help="keep every peer's stderr here")
@@ -240,7 +241,9 @@ def main():
         t = max(r[f]["seconds"] for r in res)
         wire = max((r[f]["tx"] + r[f]["rx"]) / r[f]["seconds"] for r in res)
         alg = nbytes / t
-        summary[f] = {"seconds": round(t, 4), "alg_GBps": round(alg / 1e9, 3),
+        cold = max(r[f]["reps"][0]["seconds"] for r in res)
+        summary[f] = {"seconds": round(t, 4), "repeat_reported": "warm (last of %d)" % a.repeat if a.repeat > 1
+                      else "cold (single run)", "seconds_cold": round(cold, 4), "alg_GBps": round(alg / 1e9, 3),
                       "bus_GBps": round(alg * 2 * (a.peers - 1) / a.peers / 1e9, 3),
                       "ref_metric_rx_plus_tx_Gbit_per_peer": round(wire * 8 / 1e9, 2),
                       "effective_fp32_Gbit_per_peer": round(2 * nbytes * (a.peers - 1) / a.peers * 2 / t * 8 / 1e9, 2),
@@ -255,8 +258,22 @@ def main():
                       # CPU cores the peer processes kept busy (sum over peers) while the multi-op ran
                       "peer_cpu_cores_per_repeat": [round(sum(r[f]["reps"][k]["cpu_cores"] for r in res), 2)
                                                     for k in range(a.repeat)]}
-    print(json.dumps({"metric": "quantized all-reduce over emulated WAN",
-                      "config": "int8-quantized all-reduce over tc-netem 50 ms simulated WAN, 8 peers",
+    emulator = ("userspace relay (pccl_wan_relay, a separate process)" if a.emulator == "relay"
+                else "in-library pacing (PCCL_SIM_WAN)")
+    quant = [f for f in a.formats.split(",") if f != "fp32"]
+    cq = a.concurrent_quant or a.concurrent
+    if not quant:
+        ops = f"{a.concurrent} ops in flight"
+    elif "fp32" not in a.formats.split(","):
+        ops = f"{cq} ops in flight"
+    else:
+        ops = f"{a.concurrent} ops in flight (fp32), {cq} (quantized)"
+    config = (f"{'/'.join(a.formats.split(','))} AVG all-reduce of {a.mib} MiB fp32 per peer, {a.peers} peers "
+              f"({a.device}, one process each, TCP ring), {ops}, {a.pool} connections per neighbour, emulated WAN: "
+              f"{emulator}, {a.latency_ms:g} ms one way, {a.flow_mbit:g} Mbit/s per flow, {a.link_mbit:g} Mbit/s "
+              f"per link; warm repeat of {a.repeat}")
+    print(json.dumps({"metric": "all-reduce over emulated WAN" + (" (quantized formats)" if quant else ""),
+                      "config": config,
                       "peers": a.peers, "mib_per_peer": a.mib, "device": a.device,
                       "wan": {"emulator": "pccl_wan_relay (separate process)" if a.emulator == "relay"
                               else "PCCL_SIM_WAN (inside the library)",

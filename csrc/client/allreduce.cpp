@@ -222,6 +222,12 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
                 r = hier_reduce(*op, *rv, seq, di.device);
                 done = true;
                 if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::Hierarchical);
+            } else if (rv->arena && device && op->req.count * dtype_size(op->req.dtype) > kIpcMaxOpBytes) {
+                // above one arena op's staged size: consecutive xGMI sub-ops (every peer derives the same split)
+                bool use_ring = false;
+                r = ipc_reduce_segmented(*op, *rv, seq, di.device, use_ring);
+                done = !use_ring;
+                if (r.first && !r.second) last_path_ = static_cast<int>(ReducePath::DeviceIpc);
             } else if (rv->arena) {
                 // every peer of an intra-node ring votes; the xGMI path runs only if all buffers are on GPUs
                 const int decision = rv->arena->vote(*this, *op, seq, device, device ? di.device : -1);

@@ -247,6 +247,10 @@ private:
     std::pair<bool, bool> ring_reduce_device_quant(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> device_quant_reference_framing(OpState &op, const RingView &rv, uint64_t seq, int device);
     std::pair<bool, bool> ipc_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
+    // An xGMI op above the arena's staged size (kIpcMaxOpBytes) as consecutive sub-ops; `use_ring` is set when the
+    // first sub-op's vote chose the TCP ring (the whole op then takes it)
+    std::pair<bool, bool> ipc_reduce_segmented(OpState &op, const RingView &rv, uint64_t seq, int device,
+                                               bool &use_ring);
     std::pair<bool, bool> hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
     bool abort_received(uint64_t tag);
 

@@ -51,7 +51,11 @@ namespace pccl::client {
 
 constexpr size_t kIpcSegBytes = size_t{1} << 30;                 // staged comm buffer segment
 constexpr size_t kIpcMaxExport = (size_t{2} << 30) - (size_t{2} << 20); // largest user allocation exported as is
-constexpr uint32_t kIpcMaxSegs = 16;                              // => ops of up to 16 GiB take the xGMI path
+constexpr uint32_t kIpcMaxSegs = 16;                              // staged segments of one arena op
+// Largest xGMI op handled in one arena op (16 GiB); larger ones run as consecutive sub-ops of at most this size
+// (Client::ipc_reduce_segmented), sub-op i under arena sequence number seq + (i << kIpcSubSeqShift) in the op's slot
+constexpr size_t kIpcMaxOpBytes = kIpcSegBytes * kIpcMaxSegs;
+constexpr unsigned kIpcSubSeqShift = 40;
 
 class Client;
 struct ArenaShm;

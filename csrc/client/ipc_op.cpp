@@ -520,6 +520,59 @@ std::pair<bool, bool> Client::ipc_reduce(OpState &op, const RingView &rv, uint64
                          op.tx, op.rx, nullptr, 0, &op.settle);
 }
 
+// xGMI ops above kIpcMaxOpBytes (one arena op publishes at most kIpcMaxSegs staged 1 GiB segments per buffer): the
+// op runs as consecutive sub-ops over element ranges of at most that size, each a complete arena op (vote, kernels,
+// barriers) under its own sequence number seq + (i << kIpcSubSeqShift) in the op's slot - every peer derives the same
+// split from the op's count, and a sub-op reuses the slot only after every peer released the previous one
+// (wait_slot_free), so phase words stay ordered. MI355X holds 288 GB of HBM: such tensors used to drop to the TCP ring
+// (~100x slower on one node). In place, each finished sub-op keeps its input backup until the master's verdict, and a
+// sub-op that fails restores the ranges of the ones before it.
+std::pair<bool, bool> Client::ipc_reduce_segmented(OpState &op, const RingView &rv, uint64_t seq, int device,
+                                                   bool &use_ring) {
+    use_ring = false;
+    const size_t es = dtype_size(op.req.dtype);
+    const size_t per = kIpcMaxOpBytes / es / 4096 * 4096; // elements per sub-op
+    const size_t nsub = (op.req.count + per - 1) / per;
+    std::vector<std::function<void(bool)>> settles;
+    auto restore_done = [&] {
+        for (auto &s : settles)
+            if (s) s(true);
+        settles.clear();
+    };
+    for (size_t i = 0; i < nsub; ++i) {
+        const size_t lo = i * per, n = std::min(per, op.req.count - lo);
+        OpState sub;
+        sub.req = op.req;
+        sub.req.src = static_cast<const uint8_t *>(op.req.src) + lo * es;
+        sub.req.dst = static_cast<uint8_t *>(op.req.dst) + lo * es;
+        sub.req.count = n;
+        const uint64_t aseq = seq + (static_cast<uint64_t>(i) << kIpcSubSeqShift);
+        const int decision = rv.arena->vote(*this, sub, aseq, true, device);
+        if (decision == IpcArena::kUseRing && i == 0) {
+            use_ring = true;
+            return {false, false};
+        }
+        if (decision != IpcArena::kUseIpc) {
+            LOG(WARN) << "IPC: sub-op " << i << " of " << nsub << " of op seq " << seq << " not run (decision "
+                      << decision << ")";
+            restore_done();
+            return {false, decision == IpcArena::kAbortedByMaster || abort_received(op.req.tag)};
+        }
+        const auto r = rv.arena->run(*this, op.req.tag, aseq, sub.req.src, sub.req.dst, n, op.req.dtype, op.req.op,
+                                     device, op.tx, op.rx, nullptr, 0, &sub.settle);
+        if (!r.first || r.second) {
+            restore_done();
+            return r;
+        }
+        settles.push_back(std::move(sub.settle));
+    }
+    op.settle = [settles = std::move(settles)](bool restore) mutable {
+        for (auto &s : settles)
+            if (s) s(restore);
+    };
+    return {true, false};
+}
+
 // Hierarchical all-reduce (ring spans several hosts with L peers each): reduce-scatter inside each host over xGMI,
 // one TCP device ring per local rank across hosts on the 1/L shard, all-gather inside the host over xGMI. Every byte
 // crosses the network once per host instead of once per GPU.

@@ -49,9 +49,12 @@ public:
     uint64_t allocs() const { return allocs_.load(std::memory_order_relaxed); }
     uint64_t alloc_us() const { return alloc_us_.load(std::memory_order_relaxed); }
 
-    static constexpr size_t kSlabBytes = 128u << 20;
-    static constexpr size_t kSlabMaxRequest = 32u << 20;
+    // A ring step's staging lease is its chunk plus a few bytes of vector-phase slack (ring_device.cpp: chunk + 64):
+    // the request limit and the slab leave room for that, so four leases of an exactly 32 MiB chunk (8 peers x 256 MiB
+    // fp32, config 3's ops) still share one slab instead of each becoming a whole pinned allocation.
     static constexpr size_t kGranule = 4096;
+    static constexpr size_t kSlabMaxRequest = (32u << 20) + 16 * kGranule;
+    static constexpr size_t kSlabBytes = 4 * kSlabMaxRequest;
 
     struct Slab {
         uint8_t *base = nullptr;

@@ -166,7 +166,7 @@ int send_meta(const StepIo &io, const proto::QuantMeta &mine, std::atomic<uint64
     pkt.meta = mine;
     auto bytes = proto::encode_with_id(pkt);
     if (!io.tx->send_frame(io.tag, io.seq, bytes.data(), bytes.size())) return 1;
-    tx += bytes.size() + kMetaFrameOverhead;
+    tx += meta_accounting_bytes(mine);
     return 0;
 }
 
@@ -176,7 +176,7 @@ int recv_meta(const StepIo &io, proto::QuantMeta &theirs, std::atomic<uint64_t> 
         auto m = io.rx->recv_packet<proto::P2PDequantizationMeta>(io.tag, io.seq, 20ms);
         if (m) {
             theirs = m->meta;
-            rx += proto::encode_with_id(*m).size() + kMetaFrameOverhead;
+            rx += meta_accounting_bytes(m->meta);
             return 0;
         }
         if (!io.rx->is_open() || (failed && failed()) || watch_failed()) return 1;

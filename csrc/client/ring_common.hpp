@@ -155,9 +155,14 @@ struct StepIo {
     uint64_t pkt_tag; // P2PDequantizationMeta::tag (the lane's data tag)
 };
 StepIo step_io(const Conns &txs, const Conns &rxs, uint64_t data_tag, uint64_t seq, const Shape &shape);
-// tx / rx byte accounting of a metadata packet: the encoded packet (id + payload) plus 8, as the reference counts it
-// (its LTV header u64 length + u16 id + payload, reduce.cpp:162-165,186-187; frame preambles are not counted)
-constexpr size_t kMetaFrameOverhead = 8;
+// tx / rx byte accounting of a metadata packet, exactly as the reference counts it (reduce.cpp:162-165,186-189): its
+// LTV header (u64 length + u16 id = 10 bytes) plus P2PPacketDequantizationMeta::serializedSize() = tag 8 + meta type 1
+// + 4 + |min value| + 4 + |max value| (ccoip_packets.cpp:543-548; both value vectors are empty for zero-point-scale):
+// 35 bytes for a float min-max packet, 27 for zero-point-scale, whatever the encoded size. Frame preambles are not
+// counted (reduce.cpp:212).
+inline size_t meta_accounting_bytes(const proto::QuantMeta &m) {
+    return 10 + 8 + 1 + 4 + 4 + (m.algo == QuantAlgo::MinMax ? 2 * dtype_size(m.value_type) : 0);
+}
 // Returns 0 ok, 1 io failure.
 int send_meta(const StepIo &io, const proto::QuantMeta &mine, std::atomic<uint64_t> &tx);
 // Waits for the peer's metadata of the next step (the packets of a lane arrive in step order). Returns 0 ok, 1 io

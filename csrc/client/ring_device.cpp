@@ -247,6 +247,211 @@ int device_ring_pipeline(DevRing &R) {
     return 0; // complete once its last received bytes landed in HBM (the Drain waits for them)
 }
 
+// The device ring in the reference framing (a participant without the pccl-amd extension, Shape::reference): every
+// ring step carries its whole chunk on one connection (reference reduce.cpp:149-151, 528-784), so the op cannot be
+// split into segments as device_ring_pipeline does, and that pipeline's per-step staging (3 slots x pinned TX, pinned
+// RX and HBM, each a whole chunk) would grow with the tensor: 2 peers x 16 GiB bf16 leased 48 GiB of pinned memory.
+// Here a step is moved in pieces of PCCL_REF_PIECE_BYTES (64 MiB, the reference's frame size) through fixed rings of
+// pinned and HBM slots: received pieces land in posted piece sinks (the tag's byte stream fills them in order, a
+// sender's frames may straddle them), are copied to HBM and reduced into the output in place (reduce-scatter) or
+// copied there (all-gather); a sender thread stages each piece of the next step's payload from HBM into pinned memory
+// (device->host copy once the piece it depends on was reduced) and sends it. The wire is byte-identical to the
+// unsegmented pipeline's; staging is 3 + 3 pinned and 3 HBM slots of one piece, whatever the tensor. Costs one extra
+// device->host copy per reduce-scatter byte (the pipeline streams the next payload out of the reduce kernel).
+int device_ring_reference_pieces(DevRing &R) {
+    DeviceBackend *be = R.be;
+    const PcieQueues pq = R.pq;
+    DevStream st = R.st;
+    const size_t ws = R.ws, rank = R.rank, es = R.es, nsteps = 2 * (ws - 1);
+    const uint64_t seq = R.seq;
+    const size_t P = std::max<size_t>(1 << 20, env_size("PCCL_REF_PIECE_BYTES", 64u << 20)) / es * es;
+    const auto bounds = chunk_bounds(R.count, ws);
+    net::MuxConn *txc = R.txs[stripe_conn(seq, R.tag, 0, R.txs.size(), R.shape)].get();
+    net::MuxConn *rxc = R.rxs[stripe_conn(seq, R.tag, 0, R.rxs.size(), R.shape)].get();
+
+    std::mutex ev_m;
+    std::condition_variable ev_cv;
+    std::vector<DevEvent> owned;
+    auto record = [&](DevStream s) {
+        DevEvent e = event_pool().get();
+        be->event_record(e, s);
+        std::lock_guard l(ev_m);
+        owned.push_back(e);
+        return e;
+    };
+    // one unit per (step, piece) in wire order; done[u]: the event after the unit's consume (its bytes in HBM)
+    struct Unit {
+        size_t g, off, n; // step, byte offset in the step's chunk, bytes
+    };
+    std::vector<Unit> units;
+    std::vector<std::vector<size_t>> unit_of(nsteps); // unit index of (step, piece)
+    for (size_t g = 0; g < nsteps; ++g) {
+        const auto [rs, re] = bounds[chunk_rx(g, rank, ws)];
+        for (size_t off = 0; off < (re - rs) * es; off += P) {
+            unit_of[g].push_back(units.size());
+            units.push_back(Unit{g, off, std::min(P, (re - rs) * es - off)});
+        }
+    }
+    std::vector<DevEvent> done(units.size(), nullptr);
+    constexpr size_t K = 3;
+    Lease rxl[K], stl[K], txl[2];
+    for (size_t i = 0; i < K; ++i) {
+        rxl[i] = Lease(pinned_pool(), P);
+        stl[i] = Lease(device_pool(), P, R.device);
+        if (!rxl[i].ok() || !stl[i].ok()) return 1;
+    }
+    for (auto &t : txl) {
+        t = Lease(pinned_pool(), P);
+        if (!t.ok()) return 1;
+    }
+    const DevEvent input_ready = record(st); // dst holds the input once the op stream gets here
+    std::atomic<int> cancel{0}, send_rc{0};
+    std::atomic<bool> sender_done{false};
+
+    // ---- sender: step g's payload is chunk_tx(g) of dst, which step g-1 received (g = 0: the own input chunk)
+    std::thread sender([&] {
+        name_thread("pccl-ref-tx");
+        struct Done {
+            std::atomic<bool> &f;
+            ~Done() { f.store(true); }
+        } mark{sender_done};
+        struct Staged {
+            size_t slot = 0, n = 0;
+            DevEvent copied = nullptr;
+        };
+        std::vector<std::pair<size_t, size_t>> plan; // (step, byte offset) of every piece sent, in order
+        for (size_t g = 0; g < nsteps; ++g) {
+            const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
+            for (size_t off = 0; off < (te - ts) * es; off += P) plan.emplace_back(g, off);
+        }
+        auto stage = [&](size_t k) -> Staged {
+            const auto [g, off] = plan[k];
+            const auto [ts, te] = bounds[chunk_tx(g, rank, ws)];
+            DevEvent dep = input_ready;
+            if (g > 0) { // the piece of step g-1 that received these bytes (same chunk, same offsets)
+                const size_t u = unit_of[g - 1][off / P];
+                std::unique_lock l(ev_m);
+                ev_cv.wait(l, [&] { return done[u] != nullptr || cancel.load() != 0; });
+                if (cancel.load() != 0) return {};
+                dep = done[u];
+            }
+            if (!event_wait_polling(be, dep)) return {};
+            Staged s{k % 2, std::min(P, (te - ts) * es - off), nullptr};
+            be->memcpy_async(txl[s.slot].data(), R.dst + ts * es + off, s.n, pq.d2h);
+            pcie_note(0, s.n);
+            s.copied = record(pq.d2h);
+            return s;
+        };
+        Staged cur = plan.empty() ? Staged{} : stage(0);
+        for (size_t k = 0; k < plan.size(); ++k) {
+            if (!cur.copied) {
+                send_rc.store(1);
+                return;
+            }
+            const Staged next = k + 1 < plan.size() ? stage(k + 1) : Staged{}; // its copy overlaps this send
+            if (!event_wait_polling(be, cur.copied) || cancel.load() != 0 ||
+                !txc->send_frame(R.tag, seq, txl[cur.slot].data(), cur.n)) {
+                send_rc.store(1);
+                return;
+            }
+            R.tx += cur.n;
+            cur = next;
+        }
+    });
+    auto stop_sender = [&] {
+        cancel.store(1);
+        {
+            std::lock_guard l(ev_m);
+        }
+        ev_cv.notify_all();
+        // a send blocked on a peer that stopped reading is interrupted after a grace period, not waited for
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!sender_done.load()) {
+            if (std::chrono::steady_clock::now() - t0 > net::sink_drain_grace())
+                net::interrupt_blocked_senders(R.txs, std::chrono::nanoseconds(1));
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        }
+        sender.join();
+    };
+
+    // ---- receiver (this thread): unit u lands in rx slot u % K, whose previous unit's consume must be complete
+    std::vector<net::MuxConn::SinkRef> sinks(units.size());
+    size_t posted = 0;
+    // sinks of the next units (at most K ahead of the one consumed, u): unit v reuses slot v % K once unit v - K's
+    // copy / reduce out of it completed
+    auto post_ready = [&](size_t u) {
+        while (posted < units.size() && posted < u + K) {
+            if (posted >= K && be->event_query(done[posted - K]) == 0) return;
+            sinks[posted] = rxc->post_sink(R.tag, seq, rxl[posted % K].data(), units[posted].n);
+            ++posted;
+        }
+    };
+    int rc = 0;
+    for (size_t u = 0; u < units.size() && rc == 0; ++u) {
+        const Unit &un = units[u];
+        watch_step(un.g);
+        size_t idle = 0;
+        while (true) {
+            post_ready(u);
+            if (u < posted && net::MuxConn::sink_progress(sinks[u]) >= un.n) break;
+            if (u < posted) rxc->wait_sink(sinks[u], un.n, std::chrono::milliseconds(5));
+            else std::this_thread::sleep_for(std::chrono::microseconds(50));
+            if (!rxc->is_open() || send_rc.load() != 0 || watch_failed()) {
+                rc = 1;
+                break;
+            }
+            if (++idle % 8 == 0 && R.aborted()) {
+                rc = 2;
+                break;
+            }
+        }
+        if (rc) break;
+        const size_t s = u % K;
+        const auto [rs0, re0] = bounds[chunk_rx(un.g, rank, ws)];
+        uint8_t *region = R.dst + rs0 * es + un.off;
+        DevEvent e;
+        if (un.g + 1 < ws) { // reduce-scatter: pinned -> HBM stage (copy engine), reduce into the output in place
+            be->memcpy_async(stl[s].data(), rxl[s].data(), un.n, pq.h2d);
+            be->stream_wait_event(st, record(pq.h2d));
+            be->reduce(region, stl[s].data(), un.n / es, R.dtype, R.rop, st);
+            e = record(st);
+        } else { // all-gather: the owner's reduced bytes straight into the output
+            be->memcpy_async(region, rxl[s].data(), un.n, st);
+            e = record(st);
+        }
+        pcie_note(un.n, 0);
+        rxc->remove_sink(R.tag, sinks[u]);
+        sinks[u] = nullptr;
+        {
+            std::lock_guard l(ev_m);
+            done[u] = e;
+        }
+        ev_cv.notify_all();
+        R.rx += un.n;
+        if (u + 1 == units.size() || units[u + 1].g != un.g) {
+            const size_t g = un.g;
+            step_mark(g + 1 < ws, g + 1 < ws ? g : g - (ws - 1));
+            if (g + 2 == ws) trace_mark("reduce_scatter");
+        }
+    }
+    // every piece arrived; the last step's sends may still be in flight (ended by the op's abort / watchdog too)
+    for (size_t polls = 1; rc == 0 && !sender_done.load(); ++polls) {
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        if (polls % 25 == 0 && (watch_failed() || R.aborted())) rc = R.aborted() ? 2 : 1;
+    }
+    if (rc != 0) stop_sender();
+    else sender.join();
+    if (rc == 0 && send_rc.load() != 0) rc = R.aborted() ? 2 : 1;
+    for (auto &sk : sinks)
+        if (sk) rxc->remove_sink(R.tag, sk);
+    // nothing of the op may still read or write its buffers when they go back to the pools
+    stream_wait_polling(be, pq.h2d);
+    stream_wait_polling(be, pq.d2h);
+    stream_wait_polling(be, st);
+    for (auto e : owned) event_pool().put(e);
+    return rc;
+}
+
 } // namespace
 
 std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv, uint64_t seq, int device) {
@@ -299,7 +504,10 @@ std::pair<bool, bool> Client::ring_reduce_device(OpState &op, const RingView &rv
     OpAbort aborted([this, t = q.tag] { return abort_received(t); });
     DevRing R{rv.tx, rv.rx, ws, rank, q.tag, seq, op.shape, be, pq, st, static_cast<const uint8_t *>(q.src), dst,
               q.count, es, piece, q.dtype, q.op, device, [&] { return aborted(); }, op.tx, op.rx};
-    const int rc = device_ring_pipeline(R);
+    // reference framing cannot be segmented: ring chunks above the segment bound move in pieces instead
+    const size_t ref_bound = std::max<size_t>(1, env_size("PCCL_SEGMENT_CHUNK_MIB", 128)) << 20;
+    const int rc = op.shape.reference && (q.count + ws - 1) / ws * es > ref_bound ? device_ring_reference_pieces(R)
+                                                                                 : device_ring_pipeline(R);
     if (rc != 0) {
         // the pipeline drained every copy and kernel of the op and no sink of it is posted any more: restore
         be->stream_sync(st);

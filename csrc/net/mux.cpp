@@ -241,39 +241,46 @@ void MuxConn::rx_loop() {
             LOG(WARN) << "MuxConn: invalid frame header from " << sockaddr_str(peer_addr_) << "; closing";
             break;
         }
-        const size_t n = len;
-        Sink *sink = nullptr;
-        size_t offset = 0;
-        {
-            std::lock_guard l(mtx_);
-            // deliver directly only if nothing for this tag/ctr is still queued ahead of this frame (FIFO)
-            auto qit = queued_.find(tag);
-            bool queued_ahead = false;
-            if (qit != queued_.end())
-                for (const auto &f : qit->second)
-                    if (f.ctr == ctr) queued_ahead = true;
-            if (!queued_ahead) sink = sink_for_locked(tag, ctr, n);
-            if (sink != nullptr) {
-                sink->busy = true;
-                offset = sink->received.load(std::memory_order_relaxed);
+        // The frame's payload is a run of the tag's byte stream: it fills the tag's oldest sinks with room in FIFO
+        // order and may straddle several of them (a sender's frame size need not match the receiver's sinks: a
+        // reference peer frames a ring step in PCCL_MULTIPLEX_CHUNK_SIZE pieces of its own choosing). Whatever finds
+        // no sink is queued and copied into the sinks posted later.
+        size_t left = len;
+        bool ok = true;
+        while (ok && left > 0) {
+            Sink *sink = nullptr;
+            size_t offset = 0, take = 0;
+            {
+                std::lock_guard l(mtx_);
+                // deliver directly only if nothing for this tag/ctr is still queued ahead of these bytes (FIFO)
+                auto qit = queued_.find(tag);
+                bool queued_ahead = false;
+                if (qit != queued_.end())
+                    for (const auto &f : qit->second)
+                        if (f.ctr == ctr) queued_ahead = true;
+                if (!queued_ahead) sink = sink_for_locked(tag, ctr);
+                if (sink != nullptr) {
+                    sink->busy = true;
+                    offset = sink->received.load(std::memory_order_relaxed);
+                    take = std::min(left, sink->capacity - offset);
+                }
             }
-        }
-        if (sink != nullptr) {
-            bool ok;
+            if (sink == nullptr) break;
             {
                 RoctxIoRange io("recv");
-                ok = read_into(sink->dst + offset, n, sink);
+                ok = read_into(sink->dst + offset, take, sink);
             }
             {
                 std::lock_guard l(mtx_);
                 sink->busy = false;
             }
             cv_.notify_all();
-            if (!ok) break;
-            continue;
+            left -= take;
         }
-        std::vector<uint8_t> buf(n);
-        if (n > 0 && !read_into(buf.data(), n, nullptr)) break;
+        if (!ok) break;
+        if (left == 0) continue;
+        std::vector<uint8_t> buf(left);
+        if (!read_into(buf.data(), left, nullptr)) break;
         {
             std::lock_guard l(mtx_);
             auto it = sinks_.find(tag);
@@ -303,6 +310,7 @@ std::optional<std::vector<uint8_t>> MuxConn::recv_frame(uint64_t tag, uint64_t c
             while (!q.empty() && q.front().ctr < ctr) q.pop_front();
             if (!q.empty() && q.front().ctr == ctr) {
                 auto data = std::move(q.front().data);
+                if (q.front().off > 0) data.erase(data.begin(), data.begin() + static_cast<long>(q.front().off));
                 q.pop_front();
                 if (q.empty()) queued_.erase(it);
                 return data;
@@ -318,14 +326,14 @@ std::optional<std::vector<uint8_t>> MuxConn::recv_frame(uint64_t tag, uint64_t c
     }
 }
 
-MuxConn::Sink *MuxConn::sink_for_locked(uint64_t tag, uint64_t ctr, size_t n) {
+MuxConn::Sink *MuxConn::sink_for_locked(uint64_t tag, uint64_t ctr) {
     auto it = sinks_.find(tag);
     if (it == sinks_.end()) return nullptr;
     for (auto &s : it->second) {
         if (s->ctr != ctr) continue;
         const size_t have = s->received.load(std::memory_order_relaxed);
-        if (have >= s->capacity) continue; // full: the frame belongs to a later sink
-        return have + n <= s->capacity && !s->busy ? s.get() : nullptr;
+        if (have >= s->capacity) continue; // full: the bytes belong to a later sink
+        return s->busy ? nullptr : s.get();
     }
     return nullptr;
 }
@@ -340,13 +348,15 @@ void MuxConn::drain_queued_locked(uint64_t tag, uint64_t ctr) {
         while (!q.empty() && q.front().ctr < cur) q.pop_front(); // stale frames of an aborted earlier op
     }
     while (!q.empty() && q.front().ctr == ctr) {
-        Sink *s = sink_for_locked(tag, ctr, q.front().data.size());
+        Sink *s = sink_for_locked(tag, ctr);
         if (s == nullptr) break;
-        const auto &f = q.front().data;
+        Frame &f = q.front();
         const size_t have = s->received.load(std::memory_order_relaxed);
-        std::memcpy(s->dst + have, f.data(), f.size());
-        s->received.store(have + f.size(), std::memory_order_release);
-        q.pop_front();
+        const size_t take = std::min(f.data.size() - f.off, s->capacity - have);
+        std::memcpy(s->dst + have, f.data.data() + f.off, take);
+        s->received.store(have + take, std::memory_order_release);
+        f.off += take;
+        if (f.off == f.data.size()) q.pop_front();
     }
     if (q.empty()) queued_.erase(it);
 }

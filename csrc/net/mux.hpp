@@ -68,7 +68,8 @@ public:
     }
 
     // Posts a sink of exactly `n` bytes at `dst` for (tag, ctr). Already-queued matching frames are copied in.
-    // Sinks of one tag form a FIFO: frames fill the oldest sink that still has room, so a ring op can post the next
+    // Sinks of one tag form a FIFO over the tag's byte stream: bytes fill the oldest sink that still has room (a
+    // frame may straddle sinks, so sink sizes need not match the sender's frames), so a ring op can post the next
     // step's sinks while the current step is still receiving (the sender streams both steps back to back on this
     // connection) and early frames land in place instead of being queued and copied once more.
     struct Sink {
@@ -105,6 +106,7 @@ private:
     struct Frame {
         uint64_t ctr;
         std::vector<uint8_t> data;
+        size_t off = 0; // bytes already copied into sinks (a frame may straddle sinks)
     };
     void rx_loop();
     bool read_into(uint8_t *dst, size_t n, Sink *progress_sink);
@@ -129,9 +131,9 @@ private:
 
     std::mutex mtx_;
     std::condition_variable cv_;
-    // oldest sink of `tag` with room for `n` more bytes (full ones are skipped; a partly filled one without room for
-    // the whole frame stops the search: frames never straddle sinks); nullptr if none. Caller holds mtx_.
-    Sink *sink_for_locked(uint64_t tag, uint64_t ctr, size_t n);
+    // oldest sink of (`tag`, `ctr`) that is not full (the next bytes of the tag's stream go there; a frame may
+    // straddle sinks); nullptr if none or it is being written. Caller holds mtx_.
+    Sink *sink_for_locked(uint64_t tag, uint64_t ctr);
     void drain_queued_locked(uint64_t tag, uint64_t ctr);
     std::unordered_map<uint64_t, std::deque<SinkRef>> sinks_;
     std::unordered_map<uint64_t, std::deque<Frame>> queued_;

@@ -8,6 +8,8 @@
 //   record     - Q threads: hipEventRecord(e, 0) + hipEventQuery (the path that remains in the library)
 //   query_own  - Q threads: hipStreamQuery on a stream each thread created (the shortcut on a non-default stream)
 //   query_null - Q threads: hipStreamQuery(0) (the shortcut on torch's default stream, as in the crashed test)
+//   mixed_null - Q threads: a kernel on stream 0 (torch's default stream, where the test's backward ran), then
+//                hipStreamQuery(0), hipEventRecord(e, 0) and hipEventQuery(e) - every call of the crashed path at once
 // Every mode also runs C churn threads: hipStreamCreate, a small kernel, hipEventCreate / Record / Synchronize,
 // hipEventDestroy, hipStreamDestroy in a loop. Prints one JSON line; a crash shows as the process's signal.
 #include <hip/hip_runtime.h>
@@ -39,17 +41,18 @@ int main(int argc, char **argv) {
     const double seconds = argc > 2 ? std::atof(argv[2]) : 10.0;
     const int nq = argc > 3 ? std::atoi(argv[3]) : 8, nc = argc > 4 ? std::atoi(argv[4]) : 8;
     const bool record = std::strcmp(mode, "record") == 0, own = std::strcmp(mode, "query_own") == 0,
-               null_q = std::strcmp(mode, "query_null") == 0;
-    if (!record && !own && !null_q) {
-        std::fprintf(stderr, "usage: %s record|query_own|query_null [seconds] [query threads] [churn threads]\n",
+               null_q = std::strcmp(mode, "query_null") == 0, mixed = std::strcmp(mode, "mixed_null") == 0;
+    if (!record && !own && !null_q && !mixed) {
+        std::fprintf(stderr,
+                     "usage: %s record|query_own|query_null|mixed_null [seconds] [query threads] [churn threads]\n",
                      argv[0]);
         return 1;
     }
     CHECK(hipSetDevice(0));
     float *buf = nullptr;
     const int n = 1 << 16;
-    CHECK(hipMalloc(&buf, sizeof(float) * n * (nc + 1)));
-    CHECK(hipMemset(buf, 0, sizeof(float) * n * (nc + 1)));
+    CHECK(hipMalloc(&buf, sizeof(float) * n * (nc + nq + 1)));
+    CHECK(hipMemset(buf, 0, sizeof(float) * n * (nc + nq + 1)));
     CHECK(hipDeviceSynchronize());
     std::atomic<bool> stop{false};
     std::atomic<unsigned long long> q_iters{0}, c_iters{0};
@@ -67,6 +70,12 @@ int main(int argc, char **argv) {
                     CHECK(hipEventRecord(e, nullptr));
                     while (hipEventQuery(e) == hipErrorNotReady) {
                     }
+                } else if (mixed) {
+                    float *p = buf + static_cast<size_t>(nc + 1 + t) * n;
+                    hipLaunchKernelGGL(k_touch, dim3(n / 256), dim3(256), 0, nullptr, p, n);
+                    CHECK(hipStreamQuery(nullptr));
+                    CHECK(hipEventRecord(e, nullptr));
+                    CHECK(hipEventQuery(e));
                 } else if (own) {
                     if (it % 64 == 0) hipLaunchKernelGGL(k_touch, dim3(n / 256), dim3(256), 0, mine, buf, n);
                     CHECK(hipStreamQuery(mine));

@@ -609,16 +609,26 @@ TEST(mux_oversized_frame_closes_connection) { // reference pops and silently dro
     delete rx;
 }
 
-TEST(mux_frame_larger_than_sink_is_queued_not_truncated) {
+TEST(mux_frame_straddles_sinks_in_fifo_order) {
+    // a frame larger than the oldest sink fills it and continues in the next sinks of the tag (posted before or after
+    // it arrived); nothing is written past a sink (guard bytes stay untouched)
     auto [tx, rx] = mux_pair2();
-    std::vector<uint8_t> big(200, 7), small_sink(100, 0);
-    rx->post_sink(3, 1, small_sink.data(), small_sink.size());
+    std::vector<uint8_t> big(250);
+    for (size_t i = 0; i < big.size(); ++i) big[i] = static_cast<uint8_t>(i);
+    std::vector<uint8_t> a(100 + 8, 0xee), b(100 + 8, 0xee), c(100 + 8, 0xee);
+    auto sa = rx->post_sink(3, 1, a.data(), 100);
     EXPECT(tx->send_frame(3, 1, big.data(), big.size()));
-    std::this_thread::sleep_for(50ms);
-    EXPECT(rx->sink_progress(3) == 0); // never written past the sink
-    rx->remove_sink(3);
-    auto f = rx->recv_frame(3, 1, 1000ms);
-    EXPECT(f && *f == big);
+    EXPECT(eventually([&] { return net::MuxConn::sink_progress(sa) == 100; }, 2000ms));
+    auto sb = rx->post_sink(3, 1, b.data(), 100);
+    auto sc = rx->post_sink(3, 1, c.data(), 100);
+    EXPECT(eventually([&] { return net::MuxConn::sink_progress(sc) == 50; }, 2000ms));
+    EXPECT(net::MuxConn::sink_progress(sb) == 100);
+    EXPECT(std::equal(a.begin(), a.begin() + 100, big.begin()) && a[100] == 0xee);
+    EXPECT(std::equal(b.begin(), b.begin() + 100, big.begin() + 100) && b[100] == 0xee);
+    EXPECT(std::equal(c.begin(), c.begin() + 50, big.begin() + 200) && c[50] == 0xee);
+    rx->remove_sink(3, sa);
+    rx->remove_sink(3, sb);
+    rx->remove_sink(3, sc);
     delete tx;
     delete rx;
 }

@@ -719,6 +719,14 @@ TEST(pool_slabs_carve_coalesce_and_reuse) {
     EXPECT(huge2.p == huge.p && pool.allocs() == 3);
     pool.put(huge2);
     EXPECT(pool.in_use() == 0 && pool.peak() >= 64u * (3u << 20));
+    // four ring-step leases of an exactly 32 MiB chunk plus the 64-byte vector-phase slack (ring_device.cpp) share
+    // one slab: config 3's fp32 ops (8 peers x 256 MiB) used to make each of them a whole pinned allocation
+    BufferPool p4(BufferPool::Kind::Host);
+    std::vector<BufferPool::Buf> step;
+    for (int i = 0; i < 4; ++i) step.push_back(p4.get((32u << 20) + 64));
+    EXPECT(p4.allocs() == 1);
+    for (auto &b : step) EXPECT(b.p != nullptr && b.slab != nullptr);
+    for (auto &b : step) p4.put(b);
 }
 
 TEST(pool_concurrent_leases_stay_disjoint) {

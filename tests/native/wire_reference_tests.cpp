@@ -119,9 +119,10 @@ TEST(reference_framed_quantized_ring_golden_bytes) {
     EXPECT(rc == 0);
     const std::vector<float> want = {5, 6, 7, 8, 30, 33, 30, 33};
     EXPECT(data == want);
-    // byte counters as the reference keeps them: a metadata packet counts its LTV header (u64 length + u16 id) and
-    // payload, 28 bytes (reduce.cpp:162-165,186-187), data its raw bytes: 2 x 28 + 2 x 4 each way
-    EXPECT(txc.load() == 2 * 28 + 8 && rxc.load() == 2 * 28 + 8);
+    // byte counters as the reference keeps them: a metadata packet counts its LTV header (u64 length + u16 id, 10)
+    // plus serializedSize() = 8 + 1 + (4 + 4) + (4 + 4) = 25 for float min / max, 35 bytes (reduce.cpp:162-165,
+    // 186-187, ccoip_packets.cpp:543-548), data its raw bytes: 2 x 35 + 2 x 4 each way
+    EXPECT(txc.load() == 2 * 35 + 8 && rxc.load() == 2 * 35 + 8);
     EXPECT(!readable_within(ref_in, 50)); // nothing else on the wire
     tx->interrupt();
     rx->interrupt();

@@ -602,6 +602,62 @@ def test_device_ring_staging_bounded_by_segment(hip):
         assert pinned_peak <= (1 << 30), lines[-1]["staging"]
 
 
+def test_ipc_op_above_arena_size_runs_as_sub_ops(hip):
+    """2 threaded peers x 20 GiB bf16 (above one arena op's 16 GiB of staged segments): the op runs on the xGMI path
+    as consecutive sub-ops (Client::ipc_reduce_segmented) instead of dropping to the TCP ring; exact sums, path IPC.
+    Then a second op in place with a non-uniform input: every element is restored or reduced correctly across the
+    sub-op boundary."""
+    n = 10 << 30  # bf16 elements: 20 GiB per buffer
+
+    def fn(rank, comm):
+        x = torch.full((n,), float(rank + 1), device=hip, dtype=torch.bfloat16)
+        y = torch.empty_like(x)
+        comm.all_reduce(x, y, op=pccl.ReduceOp.SUM, tag=0)
+        torch.cuda.synchronize()
+        p1 = comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH)
+        ok1 = bool((y == 3.0).all())
+        del y
+        # in place, values that differ per 1 Mi block (the sub-op boundary at 8 Gi elements is not block aligned)
+        rows = x.view(-1, 1 << 20)
+        pat = (torch.arange(rows.shape[0], device=hip) % 7).to(torch.bfloat16)
+        rows.copy_(pat.unsqueeze(1).expand_as(rows))
+        comm.all_reduce(x, x, op=pccl.ReduceOp.SUM, tag=1)
+        torch.cuda.synchronize()
+        want = (pat.float() * 2).to(torch.bfloat16).unsqueeze(1)
+        ok2 = all(bool((rows[k:k + 1024] == want[k:k + 1024]).all()) for k in range(0, rows.shape[0], 1024))
+        return p1, ok1, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), ok2
+
+    res = _run(2, fn)
+    for p1, ok1, p2, ok2 in res:
+        assert ok1 and ok2, res
+        assert p1 == p2 == pccl.ReducePath.DEVICE_IPC.value, res
+
+
+@pytest.mark.gpu
+def test_device_ring_reference_framing_staging_bounded(hip):
+    """The same 2 x 8 GiB bf16 in-place op with one peer speaking the reference protocol (PCCL_WIRE=reference): the
+    op runs in the reference framing, which cannot be segmented (every ring step carries its whole 4 GiB chunk on one
+    connection), so the device ring moves each step in 64 MiB pieces through fixed staging rings
+    (device_ring_reference_pieces): exact sums, framing 2 (reference) reported, pinned staging <= 1 GiB per peer
+    (was 6 x 4 GiB)."""
+    worker = os.path.join(HERE, "workers", "allreduce_peer.py")
+    n = 4 << 30  # bf16 elements: 8 GiB per peer
+    with local_master() as addr:
+        ps = [spawn_python([worker, addr, "2", str(r), "--device", "cuda:0", "--dtype", "bf16", "--n", str(n),
+                            "--const", "--inplace", "--steps", "2", "--pool", "2", "--report-framing"],
+                           env=dict({"PCCL_DISABLE_IPC": "1"}, **({"PCCL_WIRE": "reference"} if r == 0 else {})),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+              for r in range(2)]
+        outs = communicate_all(ps, 280, DIAG_SIGNALS)
+    for p, (o, e) in zip(ps, outs):
+        assert p.returncode == 0, e[-3000:]
+        lines = [json.loads(ln) for ln in o.splitlines() if ln.startswith("{")]
+        assert len(lines) == 2 and not any(ln.get("bad") for ln in lines), lines
+        assert all(ln["path"] == pccl.ReducePath.DEVICE_RING.value and ln["framing"] == 2 for ln in lines), lines
+        pinned_peak = max(ln["staging"]["pinned"]["peak"] for ln in lines)
+        assert pinned_peak <= (1 << 30), lines[-1]["staging"]
+
+
 def test_device_ring_pcie_bytes_match_model(hip, monkeypatch):
     """pcclxPcieStats (bench.py extra.per_rank): a device-ring op queues exactly the ring's staging traffic - per peer
     S device->host (the step-0 payload and every reduced next payload) and 2(W-1)/W S host->device (every received

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--pool", type=int, default=0, help="P2P connection pool size (0: library default)")
     ap.add_argument("--max-failures", type=int, default=50, help="exit 3 after more failed ops than this")
     ap.add_argument("--report-mem", action="store_true", help="add the GPU's used bytes (all processes) to every line")
+    ap.add_argument("--report-framing", action="store_true", help="add LAST_REDUCE_FRAMING to every line")
     ap.add_argument("--rejoin", action="store_true",
                     help="when the master drops this peer (MASTER_CONNECTED == 0, e.g. after it was stopped), print a "
                          "'kicked' line, destroy the communicator and join again as a new peer")
@@ -164,6 +165,8 @@ def main():
                "path": comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), "sec": dt, "tx": info.tx_bytes,
                "rx": info.rx_bytes, "first_ok_s": round(first_ok, 4), "t": time.time()}
         rec["staging"] = pccl.memory.staging_pool_stats()
+        if a.report_framing:
+            rec["framing"] = comm.get_attribute(pccl.Attribute.LAST_REDUCE_FRAMING)
         if dev.type == "cuda":
             rec["ipc_bufs"] = pccl.memory.ipc_buffer_stats()
             if a.report_mem:
