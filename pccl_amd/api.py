@@ -440,10 +440,10 @@ class Communicator:
     def __init__(self, address: str, peer_group: int = 0, p2p_connection_pool_size: int = 0,
                  public_advertise_ip: Optional[str] = None, p2p_listen_port: int = 48149,
                  shared_state_listen_port: int = 48150, benchmark_listen_port: int = 48151,
-                 advertised_p2p_port: Optional[int] = None):
-        """``advertised_p2p_port``: the P2P port announced to the other peers when it differs from the listen port
-        (behind NAT / port forwarding, or a relay such as ``pccl_wan_relay``); implies advertising
-        ``public_advertise_ip`` (default 127.0.0.1)."""
+                 advertised_p2p_port: Optional[int] = None, advertised_shared_state_port: Optional[int] = None):
+        """``advertised_p2p_port`` / ``advertised_shared_state_port``: the port announced to the other peers when it
+        differs from the listen port (behind NAT / port forwarding, or a relay such as ``pccl_wan_relay``); implies
+        advertising ``public_advertise_ip`` (default 127.0.0.1)."""
         ip, port = _parse_host_port(address)
         params = _native.CommCreateParams()
         params.master_address = _socket_address(ip, port)
@@ -452,13 +452,14 @@ class Communicator:
         params.internal_p2p_listen_port = p2p_listen_port
         params.internal_shared_state_listen_port = shared_state_listen_port
         params.internal_benchmark_listen_port = benchmark_listen_port
-        if advertised_p2p_port is not None and not public_advertise_ip:
+        if (advertised_p2p_port is not None or advertised_shared_state_port is not None) and not public_advertise_ip:
             public_advertise_ip = "127.0.0.1"
         if public_advertise_ip:
             adv = ip_address(public_advertise_ip)
             params.use_explicit_p2p_addresses = True
             params.advertised_p2p_address = _socket_address(adv, advertised_p2p_port or p2p_listen_port)
-            params.advertised_shared_state_address = _socket_address(adv, shared_state_listen_port)
+            params.advertised_shared_state_address = _socket_address(adv, advertised_shared_state_port or
+                                                                     shared_state_listen_port)
             params.advertised_benchmark_address = _socket_address(adv, benchmark_listen_port)
         self._comm = ctypes.c_void_p()
         PCCLError.check(C.pcclCreateCommunicator(ctypes.byref(params), ctypes.byref(self._comm)),

@@ -254,3 +254,172 @@ TEST(wire_shape_roundtrip_and_clamp) {
     const Shape s = Shape::from_wire(a.shape);
     EXPECT(!s.reference && s.stripes == 8 && s.quant_lanes == 3 && s.stripe_min == (size_t{16} << 20));
 }
+
+namespace {
+// the reference's P2PPacketDequantizationMeta (id 3) for a ZERO_POINT_SCALE chunk: u8 1 | u8 zero point type (int64)
+// | zero point big-endian (an integer: network order, reference quantize.hpp MakeZeroPointScale) | u8 scale type
+// (float) | scale in host order (floats are not swapped)
+std::vector<uint8_t> zps_packet(uint64_t tag, int64_t zp, float scale) {
+    std::vector<uint8_t> p = {0x00, 0x03};
+    put_be64(p, tag);
+    p.push_back(0x01); // ZERO_POINT_SCALE
+    p.push_back(7);    // ccoipInt64
+    put_be64(p, static_cast<uint64_t>(zp));
+    p.push_back(10); // ccoipFloat
+    uint8_t b[4];
+    std::memcpy(b, &scale, 4);
+    p.insert(p.end(), b, b + 4);
+    return p;
+}
+} // namespace
+
+// A zero-point-scale (int8) quantized 2-peer ring in the reference framing, byte for byte: metadata packet on the
+// data tag, the step's data only after the peer's packet, de-quantization of exactly what the peer sent.
+TEST(reference_framed_zps_ring_golden_bytes) {
+    int txsv[2], rxsv[2];
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, txsv) == 0);
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, rxsv) == 0);
+    auto tx = std::make_shared<net::MuxConn>(txsv[0], net::MuxConn::Mode::Tx, SockAddr{});
+    auto rx = std::make_shared<net::MuxConn>(rxsv[1], net::MuxConn::Mode::Rx, SockAddr{});
+    EXPECT(tx->start() && rx->start());
+    const Conns txs{tx}, rxs{rx};
+    const int ref_in = txsv[1], ref_out = rxsv[0];
+    // rank 0 of 2: chunk 0 = [-1, 0, 1, 2] is its reduce-scatter payload, chunk 1 = [10] * 4 receives the peer's
+    std::vector<float> data = {-1, 0, 1, 2, 10, 10, 10, 10};
+    const uint64_t tag = 0x77, seq = 3;
+    std::atomic<uint64_t> txc{0}, rxc{0};
+    int rc = -1;
+    std::thread lib([&] {
+        HostRingArgs A{txs, rxs, 2, 0, tag, seq, Shape::reference_framing(), reinterpret_cast<uint8_t *>(data.data()),
+                       data.size(), DType::F32, DType::I8, QuantAlgo::ZeroPointScale, ReduceOp::Sum, true,
+                       [] { return false; }, txc, rxc};
+        rc = host_ring(A);
+    });
+    float s3;
+    const uint8_t s3b[4] = {0xc1, 0xc0, 0x40, 0x3c}; // float(3 / 255)
+    std::memcpy(&s3, s3b, 4);
+    // reduce-scatter: scale (2 - -1) / 255, zero point rint(-128 + 1 / scale) = -43; q = rint(x / scale) - 43
+    const auto m0 = frame(tag, seq, zps_packet(tag, -43, s3));
+    EXPECT(read_exact(ref_in, m0.size()) == m0);
+    EXPECT(!readable_within(ref_in, 150));
+    const auto pm0 = frame(tag, seq, zps_packet(tag, 0, 0.5f));
+    EXPECT(net::send_all(ref_out, pm0.data(), pm0.size()));
+    const auto d0 = frame(tag, seq, {0x80, 0xd5, 0x2a, 0x7f}); // -128, -43, 42, 127
+    EXPECT(read_exact(ref_in, d0.size()) == d0);
+    const auto pd0 = frame(tag, seq, {0xec, 0xf2, 0xec, 0xf2}); // (-20, -14) x 0.5: the peer's -10, -7, -10, -7
+    EXPECT(net::send_all(ref_out, pd0.data(), pd0.size()));
+    // all-gather: the library owns chunk 1 = [0, 3, 0, 3]: scale 3 / 255, zero point -128, its copy := D(Q(x))
+    const auto m1 = frame(tag, seq, zps_packet(tag, -128, s3));
+    EXPECT(read_exact(ref_in, m1.size()) == m1);
+    EXPECT(!readable_within(ref_in, 150));
+    const auto pm1 = frame(tag, seq, zps_packet(tag, -100, 0.25f));
+    EXPECT(net::send_all(ref_out, pm1.data(), pm1.size()));
+    const auto d1 = frame(tag, seq, {0x80, 0x7f, 0x80, 0x7f});
+    EXPECT(read_exact(ref_in, d1.size()) == d1);
+    const auto pd1 = frame(tag, seq, {0xa0, 0xa4, 0xa8, 0xac}); // (q + 100) x 0.25: the peer's chunk 0 = 1, 2, 3, 4
+    EXPECT(net::send_all(ref_out, pd1.data(), pd1.size()));
+    lib.join();
+    EXPECT(rc == 0);
+    const std::vector<float> want = {1, 2, 3, 4, 0, 255 * s3, 0, 255 * s3};
+    EXPECT(data == want);
+    // a zero-point-scale packet counts 10 + serializedSize() = 10 + 8 + 1 + 4 + 4 (its min / max vectors are empty)
+    EXPECT(txc.load() == 2 * 27 + 8 && rxc.load() == 2 * 27 + 8);
+    EXPECT(!readable_within(ref_in, 50));
+    tx->interrupt();
+    rx->interrupt();
+    ::close(ref_in);
+    ::close(ref_out);
+}
+
+// An unquantized reference-framed ring step larger than the reference's 64 MiB frame (PCCL_MULTIPLEX_CHUNK_SIZE,
+// reduce.cpp:20): rank 1 of a 3-peer ring, ring chunks of 64 MiB + 4 KiB. The emulated reference neighbours send each
+// step as a 64 MiB frame plus a 4 KiB one on the op's data tag and stream counter (reference reduce.cpp:201-274); the
+// library's frames carry the same tag / counter, every byte of every step is the ring algorithm's (reduce-scatter
+// sends the own chunk, then the reduced one; all-gather forwards), and the byte counters hold the data bytes only.
+TEST(reference_framed_plain_ring_frames_above_64mib) {
+    int txsv[2], rxsv[2];
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, txsv) == 0);
+    EXPECT(socketpair(AF_UNIX, SOCK_STREAM, 0, rxsv) == 0);
+    auto tx = std::make_shared<net::MuxConn>(txsv[0], net::MuxConn::Mode::Tx, SockAddr{});
+    auto rx = std::make_shared<net::MuxConn>(rxsv[1], net::MuxConn::Mode::Rx, SockAddr{});
+    EXPECT(tx->start() && rx->start());
+    const Conns txs{tx}, rxs{rx};
+    const int ref_in = txsv[1], ref_out = rxsv[0];
+    constexpr size_t C = (size_t{16} << 20) + 1024; // floats per ring chunk: 64 MiB + 4 KiB
+    std::vector<float> data(3 * C);
+    for (size_t i = 0; i < data.size(); ++i) data[i] = static_cast<float>(i % 7);
+    const std::vector<float> x = data;
+    const uint64_t tag = 0xabc, seq = 41;
+    std::atomic<uint64_t> txc{0}, rxc{0};
+    int rc = -1;
+    std::thread lib([&] {
+        HostRingArgs A{txs, rxs, 3, 1, tag, seq, Shape::reference_framing(), reinterpret_cast<uint8_t *>(data.data()),
+                       data.size(), DType::F32, DType::F32, QuantAlgo::None, ReduceOp::Sum, false,
+                       [] { return false; }, txc, rxc};
+        rc = host_ring(A);
+    });
+    // the previous peer's four steps (reduce-scatter 0, 1, all-gather 0, 1): constant chunks 1, 2, 3, 4
+    std::thread prev([&] {
+        std::vector<float> chunk(C);
+        for (int g = 0; g < 4; ++g) {
+            std::fill(chunk.begin(), chunk.end(), static_cast<float>(g + 1));
+            const auto *b = reinterpret_cast<const uint8_t *>(chunk.data());
+            for (size_t off = 0; off < C * 4;) {
+                const size_t n = std::min<size_t>(size_t{64} << 20, C * 4 - off);
+                uint8_t h[net::kMuxHeaderBytes];
+                net::mux_frame_header(h, n, tag, seq);
+                if (!net::send_all(ref_out, h, sizeof(h)) || !net::send_all(ref_out, b + off, n)) return;
+                off += n;
+            }
+        }
+    });
+    // what the library must send per step, as a function of the element index inside the chunk
+    auto expect_tx = [&](int g, size_t i) -> float {
+        switch (g) {
+            case 0: return x[C + i];         // its own chunk 1
+            case 1: return x[i] + 1.0f;      // chunk 0 reduced with the peer's part
+            case 2: return x[2 * C + i] + 2.0f; // chunk 2, fully reduced: it owns it
+            default: return 3.0f;            // chunk 1 as received (forwarded)
+        }
+    };
+    bool headers_ok = true, bytes_ok = true;
+    size_t frames = 0;
+    std::vector<uint8_t> buf;
+    for (int g = 0; g < 4; ++g) {
+        for (size_t got = 0; got < C * 4;) {
+            const auto h = read_exact(ref_in, net::kMuxHeaderBytes);
+            uint64_t n = 0, t = 0, c = 0;
+            if (h.size() != net::kMuxHeaderBytes || !net::mux_parse_header(h.data(), n, t, c)) {
+                headers_ok = false;
+                break;
+            }
+            headers_ok = headers_ok && t == tag && c == seq && n > 0 && got + n <= C * 4 && n % 4 == 0;
+            buf = read_exact(ref_in, n);
+            if (buf.size() != n) {
+                headers_ok = false;
+                break;
+            }
+            const size_t e0 = got / 4;
+            for (size_t k = 0; k < n / 4; ++k) {
+                float v;
+                std::memcpy(&v, buf.data() + 4 * k, 4);
+                bytes_ok = bytes_ok && v == expect_tx(g, e0 + k);
+            }
+            got += n;
+            ++frames;
+        }
+    }
+    prev.join();
+    lib.join();
+    EXPECT(rc == 0 && headers_ok && bytes_ok && frames >= 8);
+    bool result_ok = true;
+    for (size_t i = 0; i < C; ++i)
+        result_ok = result_ok && data[i] == 4.0f && data[C + i] == 3.0f && data[2 * C + i] == x[2 * C + i] + 2.0f;
+    EXPECT(result_ok);
+    EXPECT(txc.load() == 4 * C * 4 && rxc.load() == 4 * C * 4);
+    EXPECT(!readable_within(ref_in, 50));
+    tx->interrupt();
+    rx->interrupt();
+    ::close(ref_in);
+    ::close(ref_out);
+}
