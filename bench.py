@@ -493,12 +493,13 @@ class _cpu_mask:
         return False
 
 
-def _gpu_numa_node_child() -> int:
-    """_gpu_numa_node(0) read by a child process, so this process's GPU runtime stays uninitialised; -1 if unknown."""
+def _gpu_numa_node_child(local_rank: int = 0) -> int:
+    """_gpu_numa_node(local_rank) read by a child process, so this process's GPU runtime stays uninitialised (its
+    threads would keep the CPU mask from before a later sched_setaffinity); -1 if unknown."""
     import subprocess
     try:
-        r = subprocess.run([sys.executable, "-c", "import bench; print(bench._gpu_numa_node(0))"], cwd=ROOT,
-                           capture_output=True, text=True, timeout=180)
+        r = subprocess.run([sys.executable, "-c", f"import bench; print(bench._gpu_numa_node({int(local_rank)}))"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=180)
         return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else -1
     except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
         return -1
@@ -910,7 +911,9 @@ def _numa_bind():
     if os.environ.get("PCCL_BENCH_NUMA_BIND", "1") != "1":
         return None
     try:
-        node = _gpu_numa_node(int(os.environ.get("LOCAL_RANK", "0")))
+        # looked up in a child: this process must not initialise the GPU runtime (and start its threads) before the
+        # binding, or those threads keep the old mask (sched_setaffinity changes the calling thread only)
+        node = _gpu_numa_node_child(int(os.environ.get("LOCAL_RANK", "0")))
         if node < 0:
             return {"numa_bind": "no node"}
         with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
@@ -1013,7 +1016,7 @@ def main():
     pre = {}
     if not a.extras_child and not a.quick and not several:
         pre = pre_gpu_measurements(a)
-    if not several:  # reading the GPU's PCI address initialises this process's GPU runtime
+    if not several:  # (bound after the multi-process measurements, which keep the full mask)
         numa = _numa_bind()
     job = Job(a)
     nbytes = a.mib << 20

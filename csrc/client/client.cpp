@@ -480,15 +480,22 @@ bool Client::optimize_topology() {
         auto resp = master_.receive<M2COptimizeTopologyResponse>();
         if (!resp) return false;
         // The master orders the probes as a round-robin schedule (every peer sends to one peer and receives from one
-        // per round): probe them in that order; a target still serving the previous round's sender is retried
-        // shortly, and only moved behind the others after repeated refusals.
+        // per round): probe them in that order. A target still serving the previous round's sender (one probe holds
+        // it for PCCL_BENCHMARK_MILLIS) is retried with a back-off from 20 ms up to 1/8 of a probe, and moved behind
+        // the other targets once it has refused for half a probe's length, so a busy server sees a few connection
+        // attempts per probe instead of fifty per second.
         std::list<BenchmarkRequest> todo(resp->requests.begin(), resp->requests.end());
         std::map<Uuid, int> refusals;
+        std::map<Uuid, std::chrono::steady_clock::time_point> busy_since;
+        const auto probe = std::chrono::milliseconds(env_size("PCCL_BENCHMARK_MILLIS", 10000));
+        auto delay = std::chrono::milliseconds(20);
         while (!todo.empty()) {
             auto it = todo.begin();
             double mbps = 0;
             const BenchResult r = benchmark_send(uuid_, it->to_peer_endpoint, mbps);
             if (r == BenchResult::Success) {
+                delay = std::chrono::milliseconds(20);
+                busy_since.erase(it->to_peer);
                 C2MReportPeerBandwidth rep;
                 rep.to_peer = it->to_peer;
                 rep.bandwidth_mbps = mbps;
@@ -496,8 +503,17 @@ bool Client::optimize_topology() {
                 LOG(INFO) << "Bandwidth to " << it->to_peer.str() << ": " << mbps << " Mbit/s";
                 todo.erase(it);
             } else if (r == BenchResult::Busy || r == BenchResult::SendFailure) {
-                if (++refusals[it->to_peer] % 10 == 0 && todo.size() > 1) todo.splice(todo.end(), todo, it);
-                std::this_thread::sleep_for(20ms);
+                const auto now = std::chrono::steady_clock::now();
+                auto since = busy_since.emplace(it->to_peer, now).first;
+                ++refusals[it->to_peer];
+                if (now - since->second >= probe / 2 && todo.size() > 1) {
+                    busy_since.erase(since);
+                    todo.splice(todo.end(), todo, it);
+                    delay = std::chrono::milliseconds(20);
+                    continue;
+                }
+                std::this_thread::sleep_for(delay);
+                delay = std::min<std::chrono::milliseconds>(delay * 2, std::max<std::chrono::milliseconds>(20ms, probe / 8));
             } else {
                 LOG(WARN) << "Benchmark to " << sockaddr_str(it->to_peer_endpoint) << " failed; skipping";
                 todo.erase(it);

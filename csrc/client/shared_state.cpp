@@ -484,15 +484,40 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
             for (auto &b : bins) std::sort(b.begin(), b.end());
         }
         std::atomic<uint64_t> rx{0}, revision{0};
+        // the first stream that fails ends the others at once (shut down their sockets): the next distributor is
+        // tried as soon as one stream of this one failed, not after every other stream's own timeouts
+        std::mutex fds_m;
+        std::vector<int> fds;
+        std::atomic<bool> failed{false};
+        auto fail_all = [&] {
+            failed.store(true);
+            std::lock_guard l(fds_m);
+            for (int f : fds) ::shutdown(f, SHUT_RDWR);
+        };
         // one connection: the keys of `idx` (indices into the master's outdated-key list), received in that order
         // (no key at all: the request still runs, its response carries the revision)
         auto fetch_keys = [&](const std::vector<size_t> &idx) -> bool {
+            if (failed.load()) return false;
             const int fd = net::connect_tcp(distributor, 10000);
             if (fd < 0) {
                 LOG(WARN) << "Shared state sync: cannot reach distributor " << sockaddr_str(distributor);
                 return false;
             }
             FdGuard fdg{fd};
+            {
+                std::lock_guard l(fds_m);
+                if (failed.load()) return false;
+                fds.push_back(fd);
+            }
+            struct Unlist {
+                std::mutex &m;
+                std::vector<int> &v;
+                int fd;
+                ~Unlist() {
+                    std::lock_guard l(m);
+                    v.erase(std::remove(v.begin(), v.end(), fd), v.end());
+                }
+            } unlist{fds_m, fds, fd};
             C2SRequestSharedState req;
             for (size_t i : idx) req.keys.push_back(resp->outdated_keys[i]);
             if (!net::send_packet(fd, req)) return false;
@@ -518,8 +543,12 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
         };
         std::vector<char> ok(streams, 0);
         std::vector<std::thread> ts;
-        for (size_t k = 1; k < streams; ++k) ts.emplace_back([&, k] { ok[k] = fetch_keys(bins[k]); });
-        ok[0] = fetch_keys(bins[0]);
+        auto run = [&](size_t k) {
+            ok[k] = fetch_keys(bins[k]);
+            if (!ok[k]) fail_all();
+        };
+        for (size_t k = 1; k < streams; ++k) ts.emplace_back(run, k);
+        run(0);
         for (auto &t : ts) t.join();
         info.rx_bytes += rx.load();
         if (std::find(ok.begin(), ok.end(), 0) != ok.end()) return false;
