@@ -209,7 +209,10 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
             if (!spin_until([&] { return be->event_query(op->req.ready) != 0; })) event_wait_polling(be, op->req.ready);
             trace_mark("input_ready");
         }
-        event_pool().put(op->req.ready);
+        // a pooled event is never pending: one still in flight (an op that did not commence) is released instead
+        DeviceBackend *be = device_backend();
+        if (commenced || be->event_query(op->req.ready) != 0) event_pool().put(op->req.ready);
+        else be->destroy_event(op->req.ready);
         op->req.ready = nullptr;
     }
     if (commenced) {

@@ -13,11 +13,13 @@ from pccl_amd.utils import DIAG_SIGNALS, communicate_all, free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "build")
 MASTER = os.path.join(ROOT, "pccl_amd", "lib", "ccoip_master")
+STREAM_PEERS = os.path.join(BUILD, "tests", "pccl_stream_ordered_peers")
+HOSTDEV = os.path.join(ROOT, "pccl_amd", "lib", "libpccl_hostdev.so")
 
 
 def _ensure_built():
     need = [os.path.join(BUILD, "tests", "pccl_unit_tests"), os.path.join(BUILD, "tests", "pccl_reduce_peer"), MASTER]
-    if not all(os.path.exists(p) for p in need):
+    if not all(os.path.exists(p) for p in need + [STREAM_PEERS, HOSTDEV]):
         import __graft_entry__
         __graft_entry__.build()
     return need
@@ -49,6 +51,24 @@ def test_c_api_peers_with_standalone_master(world, num_ops, n, pool, inflight):
         m.terminate()
         m.wait(timeout=30)
     assert m.returncode == 0  # SIGTERM -> clean interrupt + await termination
+
+
+def _hostdev_env(plugin, **extra):
+    # the host-emulated device backend: every pointer is "device" memory, streams are worker threads, no xGMI
+    return dict(os.environ, PCCL_HIP_PLUGIN=plugin, PCCL_HOSTDEV_ALL_DEVICE="1", PCCL_DISABLE_IPC="1", **extra)
+
+
+@pytest.mark.parametrize("peers,ops,n", [(2, 20, 1 << 20), (3, 12, 100_003)])
+def test_stream_ordered_threaded_peers_hostdev(peers, ops, n):
+    """Threaded peers of one process in the stream-ordered start path (pcclxAllReduce[Async]OnStream; the shared
+    null stream and per-peer streams, producers that finish after the call returned) on the host-emulated device
+    backend: exact sums on the device ring (docs/STREAM_QUERY_CRASH.md)."""
+    _ensure_built()
+    r = subprocess.run([STREAM_PEERS, str(peers), str(ops), str(n)], capture_output=True, text=True, timeout=300,
+                       env=_hostdev_env(HOSTDEV))
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res == {"peers": peers, "ops": ops, "elements": n, "bad": 0}
 
 
 def test_c99_header_compat(tmp_path):
@@ -123,6 +143,11 @@ def test_tsan_build_unit_and_peers(tmp_path):
     finally:
         m.terminate()
         m.wait(timeout=60)
+    # two threaded peers in the stream-ordered start path on the host-emulated device backend (round-5 crash setup)
+    r = subprocess.run([os.path.join(bdir, "tests", "pccl_stream_ordered_peers"), "2", "16", "262147"],
+                       capture_output=True, text=True, timeout=900,
+                       env=_hostdev_env(os.path.join(out, "libpccl_hostdev.so"), TSAN_OPTIONS=env["TSAN_OPTIONS"]))
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     # the Python-level scenarios (threaded peers in one process: all-reduce matrix, shared-state protocol) against
     # the TSan library, with the clang TSan runtime preloaded into the (uninstrumented) interpreter
     import glob
