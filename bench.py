@@ -83,6 +83,7 @@ class Job:
         self.a = a
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
+        self.phase_log = []  # per-rank record of every measured phase (measure -> _phase_ranks)
         self.dist = None
         local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
         same_gpu = os.environ.get("PCCL_BENCH_SAME_GPU") == "1"  # rehearsal of the N>1 path on a 1-GPU box
@@ -249,11 +250,12 @@ def _timed(job, i, comm, x, y, steps, warmup, tag0=0, ops=None, qopt=None):
     # CPU seconds of the whole process (every peer thread of this rank) over the timed ops: the loopback-TCP ring is
     # CPU work (kernel socket copies), so cpu_s / dt shows how many cores it kept busy
     cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    sys_s = ru1.ru_stime - ru0.ru_stime  # kernel time: on the TCP rings mostly socket copies
     if tc0 is not None:
         job.cpu_by_thread = _cpu_by_thread(tc0, _task_cpu(), cpu, dt)
         pc1 = pccl.memory.pcie_stats()
         job.pcie = {k: (pc1[k] - pc0[k]) / steps for k in pc1}  # this process's (= GPU's) staging bytes per op
-    return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), cpu
+    return dt, tx, rx, comm.get_attribute(pccl.Attribute.LAST_REDUCE_PATH), cpu, sys_s
 
 
 def _task_cpu():
@@ -331,11 +333,14 @@ def _curve_point(nbytes, t, n):
     return {"ms": round(t * 1e3, 4), "bus_bw_per_peer_GBps": round(_bw(nbytes, t, n)[1], 3)}
 
 
-def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, windows=1, quant=False):
+def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, windows=1, quant=False, label=None):
     """Runs one phase; returns {"t": s/op (max over the job), "tx", "rx", "path", "sweep": {bytes: s/op}, "ok",
-    "windows": [s/op of each timed window (the first is "t")], "op_ms": per-op wall times of peer 0 in window 1}."""
+    "windows": [s/op of each timed window (the first is "t")], "op_ms": per-op wall times of peer 0 in window 1}.
+    Every phase also appends its per-rank record to ``job.phase_log`` (``_phase_ranks``)."""
+    import pccl_amd as pccl
     torch = job.torch
     total = peers or job.total
+    ipc0 = pccl.memory.ipc_buffer_stats()
 
     def fn(i, comm):
         import contextlib
@@ -381,6 +386,7 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, 
                                   "cpu_by_thread": getattr(job, "cpu_by_thread", None)})
     for b in sweep:
         out["sweep"][b] = job.max_over_job([r[b] for r in res])
+    job.phase_log.append(_phase_ranks(job, label or ("ipc" if ipc else "device_ring"), res, dt / steps, ipc0))
     if check:
         ok = all(r["ok"] for r in res)
         if job.dist is not None:
@@ -389,6 +395,29 @@ def measure(job, *, ipc, nbytes, steps, warmup, sweep=(), peers=0, check=False, 
             ok = t.item() == 0.0
         out["ok"] = ok
     return out
+
+
+def _phase_ranks(job, label, res, t, ipc0):
+    """One phase, per rank (= per GPU at N > 1): the reduce path its peers' ops took, the cross-GPU pre-flight probes
+    that ran in it (passed / failed: the xGMI path's first op of an arena spanning GPUs writes a probe into every
+    peer's buffer; a failure moves the ring to TCP), and the kernel CPU time per socket throughput - what the TCP
+    ring's host-bound scaling model (docs/PERFORMANCE.md) depends on, measured on every rank."""
+    import pccl_amd as pccl
+    ipc1 = pccl.memory.ipc_buffer_stats()
+    main = res[0]["main"]
+    tx = sum(r["main"][1] for r in res)  # this rank's peers, over the main window
+    rx = sum(r["main"][2] for r in res)
+    wall = max(main[0], 1e-9)
+    sys_cores = main[5] / wall
+    tx_gbps = tx / wall / 1e9
+    rec = {"rank": job.rank, "gpu": job.gpu, "peers": len(res),
+           "paths": sorted({pccl.ReducePath(r["main"][3]).name for r in res}),
+           "preflight_passed": ipc1.get("preflight_passed", 0) - ipc0.get("preflight_passed", 0),
+           "preflight_failed": ipc1.get("preflight_failed", 0) - ipc0.get("preflight_failed", 0),
+           "socket_tx_GBps": round(tx_gbps, 3), "socket_rx_GBps": round(rx / wall / 1e9, 3),
+           "sys_cores": round(sys_cores, 2),
+           "sys_cores_per_socket_GBps": round(sys_cores / tx_gbps, 3) if tx_gbps > 0.01 else None}
+    return {"phase": label, "ms_per_op": round(t * 1e3, 3), "per_rank": job.gather(rec)}
 
 
 def _per_rank_diag(ring, nbytes, P):
@@ -721,7 +750,7 @@ def run_extras(job, a, nbytes):
     extra, sweep, curve = {}, {}, {}
     if not a.no_ipc_extra:
         ipc = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
-                      sweep=(1 << 20, 16 << 20, 256 << 20))
+                      sweep=(1 << 20, 16 << 20, 256 << 20), label="ipc_same_peers")
         ialg, ibus = _bw(nbytes, ipc["t"], P)
         extra["ipc_same_peers"] = {"ms_per_op": round(ipc["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(ibus, 3),
                                    "aggregate_bus_bw_GBps": round(ibus * P, 3),
@@ -735,7 +764,7 @@ def run_extras(job, a, nbytes):
         # how this rank's IPC ops handed buffers over, incl. the cross-GPU pre-flight result (pccl_amd.memory)
         extra["ipc_buffer_stats_rank0"] = pccl.memory.ipc_buffer_stats()
         if job.world == 1:
-            two = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=2)
+            two = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=2, label="ipc_2_peers")
             talg, tbus = _bw(nbytes, two["t"], 2)
             extra["ipc_2_peers_1gpu"] = {"ms_per_op": round(two["t"] * 1e3, 4), "bus_bw_per_peer_GBps": round(tbus, 3),
                                          "reduce_path": pccl.ReducePath(two["path"]).name}
@@ -744,7 +773,8 @@ def run_extras(job, a, nbytes):
     if not a.no_quant_extra:
         # the quantized wire format on the same device ring (uint8 min-max: bf16 -> u8 on the GPU, 2x fewer bytes on
         # the wire; BASELINE config 3's format without the WAN)
-        qr = measure(job, ipc=False, nbytes=nbytes, steps=max(3, a.steps // 2), warmup=2, quant=True)
+        qr = measure(job, ipc=False, nbytes=nbytes, steps=max(3, a.steps // 2), warmup=2, quant=True,
+                     label="ring_quant_u8")
         extra["ring_quant_u8_same_peers"] = {"ms_per_op": round(qr["t"] * 1e3, 3),
                                              "bus_bw_per_peer_GBps": round(_bw(nbytes, qr["t"], P)[1], 3),
                                              "wire_tx_bytes_per_op_rank0": qr["tx"],
@@ -754,10 +784,10 @@ def run_extras(job, a, nbytes):
         for p in (2, 4):
             if p >= P:
                 continue
-            r = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p)
+            r = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p, label=f"device_ring_{p}")
             curve.setdefault("DEVICE_RING", {})[str(p)] = _curve_point(nbytes, r["t"], p)
             if not a.no_ipc_extra and p != 2:
-                r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p)
+                r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, peers=p, label=f"ipc_{p}")
                 curve.setdefault("DEVICE_IPC", {})[str(p)] = _curve_point(nbytes, r["t"], p)
     if curve:
         extra["peer_curve"] = curve
@@ -775,6 +805,7 @@ def run_extras(job, a, nbytes):
             extra["peer_rejoin_latency_source"] = "2 threaded peers, xGMI path, connect -> first op (no kill)"
     else:
         extra["multi_gpu_table"] = multi_gpu_table(job, a, nbytes)
+    extra["per_rank_phases"] = job.phase_log
     return extra, sweep
 
 
@@ -805,7 +836,7 @@ def multi_gpu_table(job, a, nbytes):
         try:
             os.environ.update(env)  # read per op by the library; every rank switches at the same phase boundary
             r = measure(job, ipc=True, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=True,
-                        sweep=tuple(m << 20 for m in SIZES_MIB if (m << 20) < nbytes))
+                        sweep=tuple(m << 20 for m in SIZES_MIB if (m << 20) < nbytes), label=name)
             ts = {m: r["sweep"][m << 20] for m in SIZES_MIB if (m << 20) < nbytes}
             ts[nbytes >> 20] = r["t"]
             table[name] = {"sizes": _size_row(job, P, ts), "result_exact": r.get("ok"),
@@ -1034,7 +1065,8 @@ def main():
 
     # ---- headline: TCP device ring, P peers x 1 GiB bf16
     ring = measure(job, ipc=False, nbytes=nbytes, steps=a.steps, warmup=a.warmup, check=not a.quick,
-                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20), windows=max(1, a.windows))
+                   sweep=() if a.quick else (1 << 20, 16 << 20, 256 << 20), windows=max(1, a.windows),
+                   label="headline_device_ring")
     import pccl_amd as pccl
     alg, bus = _bw(nbytes, ring["t"], P)
     path_name = pccl.ReducePath(ring["path"]).name
@@ -1051,6 +1083,7 @@ def main():
                   "cpu_by_thread_rank0": getattr(job, "cpu_by_thread", None),
                   "result_exact": ring.get("ok")})
     extra["per_rank"] = _per_rank_diag(ring, nbytes, P)
+    extra["per_rank_phases"] = list(job.phase_log)
     sweep = {"DEVICE_RING": {str(b >> 20) + "MiB": {"ms": round(t * 1e3, 3),
                                                     "bus_bw_per_peer_GBps": round(_bw(b, t, P)[1], 3)}
                              for b, t in ring["sweep"].items()}}
@@ -1062,7 +1095,9 @@ def main():
             x_extra, x_sweep = run_extras(job, a, nbytes)
         else:
             x_extra, x_sweep = extras_in_child(job, a)
+        headline_phases = job.phase_log[:1] if os.environ.get("PCCL_BENCH_EXTRAS_INPROC") != "1" else []
         extra.update(x_extra)
+        extra["per_rank_phases"] = headline_phases + x_extra.get("per_rank_phases", [])
         sweep.update(x_sweep)
         if "latency_1MiB_ipc_python_processes" in pre:
             extra["latency_1MiB_ipc_python_processes"] = pre["latency_1MiB_ipc_python_processes"]

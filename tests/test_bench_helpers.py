@@ -98,7 +98,7 @@ def test_numa_bind_to_the_gpus_node(monkeypatch):
     if not os.path.exists("/sys/devices/system/node/node0/cpulist"):
         return
     own = os.sched_getaffinity(0)
-    monkeypatch.setattr(bench, "_gpu_numa_node", lambda local_rank: 0)
+    monkeypatch.setattr(bench, "_gpu_numa_node_child", lambda local_rank=0: 0)
     monkeypatch.delenv("PCCL_BENCH_NUMA_BIND", raising=False)
     try:
         with open("/sys/devices/system/node/node0/cpulist") as f:
@@ -136,3 +136,25 @@ def test_config_tcp_mask_modes(monkeypatch):
 def test_pool_reserve_nothing_is_a_no_op():
     import pccl_amd as pccl
     pccl.memory.reserve_staging()  # zero counts: nothing leased, success
+
+
+def test_phase_ranks_path_preflight_and_sys_cores(monkeypatch):
+    """extra.per_rank_phases: per rank and phase, the reduce paths its peers took, the pre-flight probes that ran in the
+    phase (counter deltas) and the kernel CPU per socket throughput."""
+    import pccl_amd as pccl
+    monkeypatch.setattr(pccl.memory, "ipc_buffer_stats", lambda: {"preflight_passed": 3, "preflight_failed": 1})
+    j = bench.Job.__new__(bench.Job)
+    j.rank, j.gpu, j.dist = 0, 0, None
+    ring = pccl.ReducePath.DEVICE_RING.value
+    # two peers of this rank: 2 s window, 4 GB sent each, 3 s of kernel CPU in the process
+    res = [{"main": (2.0, 4e9, 4e9, ring, 5.0, 3.0)}, {"main": (2.0, 4e9, 4e9, ring, 5.0, 3.0)}]
+    rec = bench._phase_ranks(j, "device_ring", res, 0.25, {"preflight_passed": 2, "preflight_failed": 1})
+    assert rec["phase"] == "device_ring" and rec["ms_per_op"] == 250.0
+    (r,) = rec["per_rank"]
+    assert r["paths"] == ["DEVICE_RING"] and r["peers"] == 2
+    assert r["preflight_passed"] == 1 and r["preflight_failed"] == 0
+    assert r["socket_tx_GBps"] == 4.0 and r["sys_cores"] == 1.5
+    assert r["sys_cores_per_socket_GBps"] == round(1.5 / 4.0, 3)
+    # no socket traffic (xGMI): no ratio
+    res = [{"main": (2.0, 0, 0, pccl.ReducePath.DEVICE_IPC.value, 1.0, 0.1)}]
+    assert bench._phase_ranks(j, "ipc", res, 0.01, {})["per_rank"][0]["sys_cores_per_socket_GBps"] is None
