@@ -409,12 +409,15 @@ def _phase_ranks(job, label, res, t, ipc0):
     rx = sum(r["main"][2] for r in res)
     wall = max(main[0], 1e-9)
     sys_cores = main[5] / wall
-    tx_gbps = tx / wall / 1e9
-    rec = {"rank": job.rank, "gpu": job.gpu, "peers": len(res),
-           "paths": sorted({pccl.ReducePath(r["main"][3]).name for r in res}),
+    paths = sorted({pccl.ReducePath(r["main"][3]).name for r in res})
+    # (the op counters count an xGMI op's bytes too: socket rates only where a TCP ring ran)
+    tcp = any(p in ("HOST_RING", "DEVICE_RING", "HIERARCHICAL") for p in paths)
+    tx_gbps = tx / wall / 1e9 if tcp else 0.0
+    rec = {"rank": job.rank, "gpu": job.gpu, "peers": len(res), "paths": paths,
            "preflight_passed": ipc1.get("preflight_passed", 0) - ipc0.get("preflight_passed", 0),
            "preflight_failed": ipc1.get("preflight_failed", 0) - ipc0.get("preflight_failed", 0),
-           "socket_tx_GBps": round(tx_gbps, 3), "socket_rx_GBps": round(rx / wall / 1e9, 3),
+           "socket_tx_GBps": round(tx_gbps, 3) if tcp else None,
+           "socket_rx_GBps": round(rx / wall / 1e9, 3) if tcp else None,
            "sys_cores": round(sys_cores, 2),
            "sys_cores_per_socket_GBps": round(sys_cores / tx_gbps, 3) if tx_gbps > 0.01 else None}
     return {"phase": label, "ms_per_op": round(t * 1e3, 3), "per_rank": job.gather(rec)}

@@ -128,7 +128,8 @@ void Client::arm_ready(OpState &op) {
     if (!op.req.stream_ordered || op.req.ready) return;
     op.req.stream_ordered = false;
     DeviceBackend *be = device_backend();
-    DevEvent e = be ? event_pool().get() : nullptr;
+    // (an event of the buffers' device: the caller's stream is that device's, whatever the thread's current device)
+    DevEvent e = be ? event_pool().get(op.si.is_device ? op.si.device : -1) : nullptr;
     if (e && be->event_record(e, op.req.ready_stream)) {
         op.req.ready = e;
         return;
@@ -211,8 +212,12 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
         }
         // a pooled event is never pending: one still in flight (an op that did not commence) is released instead
         DeviceBackend *be = device_backend();
-        if (commenced || be->event_query(op->req.ready) != 0) event_pool().put(op->req.ready);
-        else be->destroy_event(op->req.ready);
+        if (commenced || be->event_query(op->req.ready) != 0) {
+            event_pool().put(op->req.ready);
+        } else {
+            be->destroy_event(op->req.ready);
+            event_pool().forget(op->req.ready);
+        }
         op->req.ready = nullptr;
     }
     if (commenced) {

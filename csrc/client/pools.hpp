@@ -143,29 +143,49 @@ private:
     std::map<int, std::vector<DevStream>> free_;
 };
 
+// Events are bound to the device current at their creation, and recording one on another device's stream is an
+// error: the pool keeps one free list per device and hands out only events of the device asked for (default: the
+// calling thread's current device).
 class EventPool {
 public:
-    DevEvent get() {
+    DevEvent get(int device = -1) {
+        DeviceBackend *be = device_backend();
+        if (!be) return nullptr;
+        if (device < 0) device = be->current_device();
         {
             std::lock_guard l(mtx_);
-            if (!free_.empty()) {
-                DevEvent e = free_.back();
-                free_.pop_back();
+            auto &f = free_[device];
+            if (!f.empty()) {
+                DevEvent e = f.back();
+                f.pop_back();
                 return e;
             }
         }
-        DeviceBackend *be = device_backend();
-        return be ? be->create_event() : nullptr;
+        const int cur = be->current_device();
+        if (cur != device) be->set_device(device);
+        DevEvent e = be->create_event();
+        if (cur != device) be->set_device(cur);
+        if (e) {
+            std::lock_guard l(mtx_);
+            device_of_[e] = device;
+        }
+        return e;
     }
     void put(DevEvent e) {
         if (!e) return;
         std::lock_guard l(mtx_);
-        free_.push_back(e);
+        auto it = device_of_.find(e);
+        free_[it != device_of_.end() ? it->second : 0].push_back(e);
+    }
+    void forget(DevEvent e) { // a destroyed event (its handle may be reused by the runtime)
+        std::lock_guard l(mtx_);
+        device_of_.erase(e);
     }
 
 private:
     std::mutex mtx_;
-    std::vector<DevEvent> free_;
+    std::map<int, std::vector<DevEvent>> free_;
+    std::map<DevEvent, int> device_of_;
 };
 
 StreamPool &stream_pool();

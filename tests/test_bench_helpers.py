@@ -157,4 +157,5 @@ def test_phase_ranks_path_preflight_and_sys_cores(monkeypatch):
     assert r["sys_cores_per_socket_GBps"] == round(1.5 / 4.0, 3)
     # no socket traffic (xGMI): no ratio
     res = [{"main": (2.0, 0, 0, pccl.ReducePath.DEVICE_IPC.value, 1.0, 0.1)}]
-    assert bench._phase_ranks(j, "ipc", res, 0.01, {})["per_rank"][0]["sys_cores_per_socket_GBps"] is None
+    r = bench._phase_ranks(j, "ipc", res, 0.01, {})["per_rank"][0]
+    assert r["sys_cores_per_socket_GBps"] is None and r["socket_tx_GBps"] is None
