@@ -148,7 +148,8 @@ def test_tsan_build_unit_and_peers(tmp_path):
                        capture_output=True, text=True, timeout=900,
                        env=_hostdev_env(os.path.join(out, "libpccl_hostdev.so"), TSAN_OPTIONS=env["TSAN_OPTIONS"]))
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
-    # the Python-level scenarios (threaded peers in one process: all-reduce matrix, shared-state protocol) against
+    # the Python-level scenarios (threaded peers in one process: all-reduce matrix, shared-state protocol; peer
+    # processes stopped / black-holed mid-op: the liveness protocol's heartbeats, watchdog and teardown) against
     # the TSan library, with the clang TSan runtime preloaded into the (uninstrumented) interpreter
     import glob
     rt = sorted(glob.glob("/opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.tsan-x86_64.so"))[-1]
@@ -156,7 +157,8 @@ def test_tsan_build_unit_and_peers(tmp_path):
                   TSAN_OPTIONS=env["TSAN_OPTIONS"] + " ignore_noninstrumented_modules=1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
                         os.path.join(ROOT, "tests", "test_allreduce.py"),
-                        os.path.join(ROOT, "tests", "test_shared_state_scenarios.py")],
+                        os.path.join(ROOT, "tests", "test_shared_state_scenarios.py"),
+                        os.path.join(ROOT, "tests", "test_liveness.py")],
                        capture_output=True, text=True, env=py_env, timeout=900, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reports = [f.read_text() for f in tmp_path.glob("tsan*")]
