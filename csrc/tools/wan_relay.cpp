@@ -18,9 +18,16 @@
 // of them come from the target's predecessor, so this is that peer's egress link). The relay reads at most
 // 2 x d x flow_rate bytes ahead per direction (the bandwidth-delay product of the flow: the window a real WAN TCP
 // connection would have in flight), so senders feel back-pressure as on a real long fat pipe.
+//
+// CPU: a real WAN path costs the hosts nothing, so the relay keeps its own share small. Chunks are recycled buffers
+// (no allocation or zero-fill per chunk) and leave with MSG_ZEROCOPY sends: the kernel hands the relay's pages to
+// the receiving peer, whose receive copy happens anyway, instead of copying them into socket buffers first. A chunk's
+// buffer returns to the pool once the kernel reports its send complete.
 #include <arpa/inet.h>
+#include <linux/errqueue.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -70,9 +77,12 @@ struct Link {
     }
 };
 
+constexpr size_t kChunk = 256 << 10;
+
 struct Chunk {
-    double arrival;
-    std::vector<char> data;
+    double arrival = 0;
+    std::unique_ptr<char[]> data;
+    size_t n = 0;
 };
 
 // one direction of one connection: reader thread -> delay queue -> paced writer thread
@@ -90,24 +100,62 @@ public:
     }
 
 private:
+    std::unique_ptr<char[]> take_buffer() {
+        {
+            std::lock_guard l(m_);
+            if (!free_.empty()) {
+                auto b = std::move(free_.back());
+                free_.pop_back();
+                return b;
+            }
+        }
+        return std::unique_ptr<char[]>(new char[kChunk]); // (not zero-filled)
+    }
     void reader() {
         while (true) {
-            std::vector<char> buf(256 << 10);
-            const ssize_t k = ::recv(src_, buf.data(), buf.size(), 0);
+            auto buf = take_buffer();
+            const ssize_t k = ::recv(src_, buf.get(), kChunk, 0);
             if (k <= 0) break;
-            buf.resize(static_cast<size_t>(k));
             std::unique_lock l(m_);
             cv_.wait(l, [&] { return queued_ < window_ || closed_; });
             if (closed_) break;
-            queued_ += buf.size();
-            q_.push_back({now_s(), std::move(buf)});
+            queued_ += static_cast<size_t>(k);
+            q_.push_back({now_s(), std::move(buf), static_cast<size_t>(k)});
             cv_.notify_all();
         }
         std::lock_guard l(m_);
         eof_ = true;
         cv_.notify_all();
     }
+    // MSG_ZEROCOPY completions: the ids in [ee_info, ee_data] are done (in order on one socket); their buffers are
+    // recycled. With `wait_ms` > 0, waits that long for completions to arrive.
+    void reap(int wait_ms) {
+        if (pending_.empty()) return;
+        if (wait_ms > 0) {
+            pollfd pfd{dst_, 0, 0}; // (POLLERR is always reported)
+            ::poll(&pfd, 1, wait_ms);
+        }
+        while (true) {
+            char ctrl[128];
+            msghdr msg{};
+            msg.msg_control = ctrl;
+            msg.msg_controllen = sizeof(ctrl);
+            if (::recvmsg(dst_, &msg, MSG_ERRQUEUE | MSG_DONTWAIT) < 0) break;
+            for (cmsghdr *cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
+                auto *se = reinterpret_cast<sock_extended_err *>(CMSG_DATA(cm));
+                if (se->ee_errno != 0 || se->ee_origin != SO_EE_ORIGIN_ZEROCOPY) continue;
+                if (static_cast<int32_t>(se->ee_data + 1 - done_to_) > 0) done_to_ = se->ee_data + 1;
+            }
+        }
+        std::lock_guard l(m_);
+        while (!pending_.empty() && static_cast<int32_t>(done_to_ - pending_.front().first) >= 0) {
+            free_.push_back(std::move(pending_.front().second));
+            pending_.pop_front();
+        }
+    }
     void writer() {
+        int one = 1;
+        const bool zc = ::setsockopt(dst_, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one)) == 0;
         double flow_next = 0;
         while (true) {
             Chunk c;
@@ -118,7 +166,7 @@ private:
                 c = std::move(q_.front());
                 q_.pop_front();
             }
-            const size_t n = c.data.size();
+            const size_t n = c.n;
             if (blackholed()) { // forwards nothing from now on; the sockets stay open (the reader fills its window)
                 while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(50));
                 break;
@@ -130,21 +178,29 @@ private:
             size_t off = 0;
             bool ok = true;
             while (off < n) {
-                const ssize_t k = ::send(dst_, c.data.data() + off, n - off, MSG_NOSIGNAL);
+                const ssize_t k = ::send(dst_, c.data.get() + off, n - off, MSG_NOSIGNAL | (zc ? MSG_ZEROCOPY : 0));
                 if (k <= 0) {
                     ok = false;
                     break;
                 }
+                if (zc) ++next_id_;
                 off += static_cast<size_t>(k);
             }
             g_bytes += off;
             {
                 std::lock_guard l(m_);
                 queued_ -= n;
+                // the kernel may still read this buffer (zero-copy): it is recycled on its completion
+                if (zc) pending_.emplace_back(next_id_, std::move(c.data));
+                else free_.push_back(std::move(c.data));
                 cv_.notify_all();
             }
+            if (zc) reap(0);
             if (!ok) break;
         }
+        // buffers the kernel may still read are not freed: wait for their completions, else leave them allocated
+        for (int i = 0; i < 20 && !pending_.empty(); ++i) reap(100);
+        for (auto &p : pending_) (void)p.second.release();
         {
             std::lock_guard l(m_);
             closed_ = true;
@@ -161,6 +217,9 @@ private:
     std::mutex m_;
     std::condition_variable cv_;
     std::deque<Chunk> q_;
+    std::vector<std::unique_ptr<char[]>> free_;
+    std::deque<std::pair<uint32_t, std::unique_ptr<char[]>>> pending_; // (id after its last send, buffer)
+    uint32_t next_id_ = 0, done_to_ = 0;
     size_t queued_ = 0;
     bool eof_ = false, closed_ = false;
 };
