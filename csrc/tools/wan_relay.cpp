@@ -21,10 +21,13 @@
 //
 // CPU: a real WAN path costs the hosts nothing, so the relay keeps its own share small. Chunks are recycled buffers
 // (no allocation or zero-fill per chunk) and leave with MSG_ZEROCOPY sends: the kernel hands the relay's pages to
-// the receiving peer, whose receive copy happens anyway, instead of copying them into socket buffers first. A chunk's
-// buffer returns to the pool once the kernel reports its send complete.
+// the receiving peer, whose receive copy happens anyway, instead of copying them into socket buffers first
+// (PCCL_RELAY_ZEROCOPY=0: plain sends). A chunk's buffer returns to the pool once the kernel reports its send complete.
+// Collocated emulation, interleaved against the previous relay (profiles/r6/collocated_relay_ab/): warm repeats
+// 0.60-0.76 s vs 0.83-1.03 s; the emulation's run-to-run spread on a 16-CPU share stays large.
 #include <arpa/inet.h>
 #include <linux/errqueue.h>
+#include <malloc.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -155,7 +158,9 @@ private:
     }
     void writer() {
         int one = 1;
-        const bool zc = ::setsockopt(dst_, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one)) == 0;
+        const char *zenv = std::getenv("PCCL_RELAY_ZEROCOPY"); // 0: plain sends (A/B)
+        const bool zc = !(zenv && std::strcmp(zenv, "0") == 0) &&
+                        ::setsockopt(dst_, SOL_SOCKET, SO_ZEROCOPY, &one, sizeof(one)) == 0;
         double flow_next = 0;
         while (true) {
             Chunk c;
@@ -306,6 +311,8 @@ int main(int argc, char **argv) {
         }
     }
     if (maps.empty()) return 2;
+    // chunk buffers from the heap, not one mmap (and its page faults) per buffer: the pools only grow
+    mallopt(M_MMAP_THRESHOLD, 64 << 20);
     signal(SIGPIPE, SIG_IGN);
     signal(SIGTERM, [](int) { g_stop = 1; });
     signal(SIGUSR1, [](int) { g_blackhole_gen.fetch_add(1); });
