@@ -207,6 +207,7 @@ void Master::send_connection_info(bool include_registered) {
         info.num_distinct_peer_groups = num_groups(include_registered);
         info.largest_peer_group_world_size = largest_group(include_registered);
         const auto ring = ring_of(c.group, include_registered);
+        c.ring_members = ring;
         std::vector<Uuid> neighbors;
         if (ring.size() > 1) {
             const size_t pos = std::find(ring.begin(), ring.end(), u) - ring.begin();
@@ -992,10 +993,21 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
             seg_any = true;
         }
     }
+    bool stale = false;
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
         c.colls[tag] = CollState::Perform;
         server_.send_packet(c.addr, pkt);
+        for (const Uuid &m : c.ring_members)
+            if (!clients_.count(m)) stale = true;
+    }
+    // A participant's ring still holds a peer that has left (dropped by the liveness protocol while the others were
+    // between ops: no op of theirs was running to abort, and a stopped peer's connections stay open). The op would wait
+    // on that peer until the stall watchdog fires; it is aborted right away instead, and the peers re-establish.
+    if (stale) {
+        LOG(WARN) << "Master: op tag " << tag << " commenced on a ring with a departed peer; aborting it";
+        groups_[group].aborted[tag] = true;
+        send_abort(group, tag, true);
     }
 }
 

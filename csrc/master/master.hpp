@@ -64,6 +64,9 @@ struct ClientInfo {
     State state = State::Idle;
     bool voted_pending_query = false;
     std::map<uint64_t, CollState> colls;
+    // the ring members of this peer's last P2P establishment: an op whose participants' rings still hold a peer that
+    // has left cannot complete (a stopped peer's connections stay open, so nothing on the data plane fails)
+    std::vector<Uuid> ring_members;
     std::map<uint64_t, uint8_t> coll_flags; // initiate capability bits per running tag
     std::map<uint64_t, proto::WireShape> coll_shapes; // proposed data-plane shape per running tag (kCollFlagExtWire)
     uint32_t group = 0;

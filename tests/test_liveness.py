@@ -175,6 +175,39 @@ def test_blackholed_link_host_ring(monkeypatch):
         assert any(x["world"] == 3 for x in after), "the dropped peer did not rejoin"
 
 
+def test_sigstopped_idle_peer_consensus(monkeypatch):
+    """A peer stopped between collectives (SIGSTOP from outside while it idles) holds no op the watchdog could see;
+    the consensus rounds that need its vote - the shared-state sync (every accepted peer must vote) and the next
+    all-reduce - would wait for it forever without heartbeats. The master drops it after PCCL_PEER_TIMEOUT_MS, and
+    the survivors complete a round at W = 2 within the timeout + 2 s of the stop; once resumed, the stopped peer
+    finds itself dropped (MASTER_CONNECTED == 0)."""
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", str(int(PEER_TIMEOUT_S * 1000)))
+    worker = os.path.join(HERE, "workers", "consensus_peer.py")
+    with local_master() as addr:
+        ps = [spawn_python([worker, addr, "3", str(r), "--duration", "14", "--step-sleep", "0.3"],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
+        run = _Run(ps, 120)
+        time.sleep(6.0)  # import, connect, admit, some rounds
+        t_stop = time.time()
+        os.kill(ps[0].pid, signal.SIGSTOP)
+        time.sleep(5.0)
+        os.kill(ps[0].pid, signal.SIGCONT)
+        outs = run.join()
+    for r in range(3):
+        assert ps[r].returncode == 0, (r, outs[r][1][-3000:])
+    for r in (1, 2):
+        lines = _lines(outs[r][0])
+        before = [x for x in lines if x["t"] < t_stop and x.get("world") == 3]
+        assert len(before) >= 2, lines[:5]
+        after = [x for x in lines if x["t"] > t_stop and x.get("world") == 2 and x.get("ar")]
+        assert after, lines[-5:]
+        # a round that started before the drop ends once the master dropped the peer (+ its own duration)
+        done = min(x["t"] for x in after) - t_stop
+        assert done <= PEER_TIMEOUT_S + 2.0 + 0.5, f"first W = 2 round {done:.2f} s after the stop"
+        print(f"peer {r}: first round at W = 2 {done:.2f} s after the stop")
+    assert any(x.get("kicked") for x in _lines(outs[0][0])), outs[0][0][-1000:]
+
+
 def test_reference_wire_peer_is_exempt_from_heartbeats(monkeypatch):
     """A peer speaking the reference protocol (PCCL_WIRE=reference) sends no heartbeats and must not be dropped for
     it: with a 1 s peer timeout, a mixed pair keeps all-reducing for 4 s without an error."""
