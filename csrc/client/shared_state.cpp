@@ -294,11 +294,20 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
 
     // Same-host distributor: HBM entries are handed over as HIP IPC handles and copied device-to-device (over xGMI
     // between GPUs) instead of D2H -> TCP -> H2D. `fallback` is set if the distributor does not speak the extension.
+    // A distributor that stops without closing its socket (SIGSTOP, a wedged host) keeps the connection alive: its
+    // kernel still ACKs, so neither keepalive nor TCP_USER_TIMEOUT ends a receive from it. A fetch receive that gets
+    // no byte for the op-stall timeout (PCCL_OP_STALL_MS) fails instead, and the next distributor is tried.
+    auto stall_guard = [this](int fd) {
+        if (stall_ms_ == 0) return;
+        timeval tv{static_cast<time_t>(stall_ms_ / 1000), static_cast<suseconds_t>(stall_ms_ % 1000) * 1000};
+        setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    };
     auto fetch_ipc = [&](const SockAddr &distributor, bool &fallback) -> bool {
         fallback = false;
         const int fd = net::connect_tcp(distributor, 10000);
         if (fd < 0) return false;
         FdGuard fdg{fd};
+        stall_guard(fd);
         C2SRequestSharedStateIpc req;
         req.keys = resp->outdated_keys;
         req.host_token = net::host_token();
@@ -504,6 +513,7 @@ bool Client::sync_shared_state(SharedState &ss, SSInfo &info) {
                 return false;
             }
             FdGuard fdg{fd};
+            stall_guard(fd);
             {
                 std::lock_guard l(fds_m);
                 if (failed.load()) return false;
@@ -692,6 +702,7 @@ void Client::serve_shared_state(int fd, SockAddr peer) {
         resp.revision = revision;
         for (const auto &e : to_send) resp.entries.push_back(SharedStateEntryInfo{e.key, e.bytes});
         if (!net::send_packet(fd, resp)) return;
+        fault_point("ss_serve", revision); // tests: fail after the response, before the entries
         for (const auto &e : to_send) {
             if (!stream_entry(e)) {
                 LOG(WARN) << "Shared state: streaming " << e.key << " to " << sockaddr_str(peer) << " failed";

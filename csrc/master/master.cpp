@@ -706,6 +706,15 @@ SSStatus Master::revision_status(ClientInfo &c, uint64_t revision) {
         else if (revision > gs.next_revision) st = SSStatus::RevisionIncrementViolation;
     } else if (revision > 0) {
         gs.next_revision = revision; // resume: adopt the first non-zero revision
+        // Peers of this round that voted before with an older revision (e.g. a fresh peer at 0 ahead of a resuming
+        // one) are outdated, not matching: they receive the state instead of competing for the election by
+        // popularity (the reference keeps their early "match", so a 1:1 tie could hand the fresh state to the
+        // resuming peer)
+        for (auto &[u, prev] : gs.statuses) {
+            const ClientInfo *o = client_by_uuid(u);
+            if (o && o->state == State::VoteSyncSharedState && o->ss_revision < revision && prev == SSStatus::Match)
+                prev = SSStatus::RevisionOutdated;
+        }
     }
     gs.statuses[c.uuid] = st;
     c.ss_revision = revision;

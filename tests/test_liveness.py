@@ -208,6 +208,37 @@ def test_sigstopped_idle_peer_consensus(monkeypatch):
     assert any(x.get("kicked") for x in _lines(outs[0][0])), outs[0][0][-1000:]
 
 
+def test_sigstopped_shared_state_distributor(monkeypatch):
+    """The shared-state distributor stops (SIGSTOP at the ss_serve fault point: response sent, entries not yet
+    streamed) while a late joiner fetches 256 MiB from it over TCP. Its kernel keeps the connections alive, so
+    neither keepalive nor TCP_USER_TIMEOUT would end the joiner's receives: the fetch sockets time out after
+    PCCL_OP_STALL_MS without a byte, and the joiner's sync fails within that + 2 s of the stop instead of hanging."""
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", str(int(PEER_TIMEOUT_S * 1000)))
+    stall_s = 1.5 * PEER_TIMEOUT_S
+    worker = os.path.join(HERE, "workers", "ss_peer.py")
+    extra = ["--device", "cpu", "--n", str(1 << 26), "--world", "2", "--no-all-reduce"]
+    stop = {"PCCL_FAULT_INJECT": "ss_serve:5", "PCCL_FAULT_SIGNAL": "STOP"}
+    with local_master() as addr:
+        d = spawn_python([worker, addr, "dist", *extra], env=stop, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+        time.sleep(1.0)
+        j = spawn_python([worker, addr, "join", *extra], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        run = _Run([j], 120)
+        try:
+            _wait_until(lambda: _proc_state(d.pid) == "T" or d.poll() is not None, 60, "the distributor to stop")
+            t_stop = time.time()
+            (jo, je), = run.join()
+        finally:
+            d.kill()
+            d.communicate(timeout=30)
+    assert j.returncode == 0, je[-3000:]
+    sync = next(x for x in _lines(jo) if x["phase"] == "sync")
+    assert "error" in sync, (sync, je[-3000:])
+    detect = sync["t"] - t_stop
+    assert detect <= stall_s + 2.0, f"sync failed {detect:.2f} s after the stop"
+    print(f"joiner: sync failed {detect:.2f} s after the distributor stopped")
+
+
 def test_reference_wire_peer_is_exempt_from_heartbeats(monkeypatch):
     """A peer speaking the reference protocol (PCCL_WIRE=reference) sends no heartbeats and must not be dropped for
     it: with a 1 s peer timeout, a mixed pair keeps all-reducing for 4 s without an error."""
