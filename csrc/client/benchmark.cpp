@@ -33,6 +33,10 @@ BenchResult benchmark_send(const Uuid &self, const SockAddr &endpoint, double &m
         hello.peer_uuid = self;
         timeval tv{5, 0};
         setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+        // a target that stops reading (stopped, wedged) keeps the connection alive with a zero window: a send that
+        // moves no byte for 2 s ends the probe instead of blocking until TCP_USER_TIMEOUT
+        timeval stv{2, 0};
+        setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &stv, sizeof(stv));
         if (!net::send_packet(fd, hello)) {
             ::close(fd);
             for (int f : fds) ::close(f);
