@@ -30,7 +30,7 @@ _pools: dict = {}
 
 
 def _immortal(obj) -> None:
-    """Keeps `obj` alive until the process exits. Measured on MI355X (scripts/probes/shareable_exit_probe.py): when
+    """Keeps `obj` alive until the process exits. Measured on MI355X (profiles/r2/shareable/shareable_exit_probe.py): when
     the interpreter's final garbage collection destroys a MemPool backed by a pluggable allocator, the process dies
     with SIGSEGV; deleting it earlier or never is fine. The OS reclaims the memory at exit."""
     ctypes.pythonapi.Py_IncRef(ctypes.py_object(obj))
