@@ -1,4 +1,5 @@
-// Golden wire-format tests: every CCoIP packet (29 ids) and both framings, against byte arrays
+// Golden wire-format tests: every CCoIP packet (29 ids), both framings, and the pccl-amd liveness
+// extension (registration suffixes, heartbeat and op-stalled packets), against byte arrays
 // written down from the reference's serialize() order (ccoip/src/cpp/ccoip_packets.cpp:6-625,
 // tinysockets multiplexed_socket.cpp:406-411, queued_client_socket.cpp:299-305) - NOT produced by our encoder.
 // Each case checks (1) our encoder emits exactly the golden bytes for a packet whose pccl-amd extension fields are
@@ -396,4 +397,55 @@ TEST(golden_extensions_are_suffixes) {
     i.flags = proto::kCollFlagHierarchical;
     const auto ib = proto::encode_with_id(i);
     EXPECT(ib.size() == 21 && ib.back() == proto::kCollFlagHierarchical);
+}
+
+// Liveness extension (pccl-amd only, docs/WIRE_DIVERGENCES.md): appended to the registration request after the
+// xGMI byte, appended to the registration response only when the master runs it, and three packets of its own.
+TEST(golden_liveness_registration_suffixes) {
+    proto::C2MRequestSessionRegistration p;
+    p.peer_group = 0;
+    p.p2p_port = 1;
+    p.ss_port = 2;
+    p.bm_port = 3;
+    p.host_token = "h";
+    p.xgmi_capable = true;
+    p.liveness = true;
+    const auto g = G(1).u32(0).boolean(false).u16(1).u16(2).u16(3).str("h").boolean(true).u8(1).b;
+    check(p, g, "registration + liveness");
+    auto q = parse<proto::C2MRequestSessionRegistration>(g);
+    EXPECT(q && q->liveness && q->xgmi_capable && q->host_token == "h");
+    // without the liveness byte (an older pccl-amd peer): no liveness
+    auto o = parse<proto::C2MRequestSessionRegistration>(G(1).u32(0).boolean(false).u16(1).u16(2).u16(3).str("h")
+                                                             .boolean(true).b);
+    EXPECT(o && !o->liveness);
+
+    proto::M2CSessionRegistrationResponse r;
+    r.accepted = true;
+    r.assigned_uuid = uuid_of(0x40);
+    r.heartbeat_ms = 400;
+    r.peer_timeout_ms = 2000;
+    r.op_stall_ms = 3000;
+    const auto gr = G(1).boolean(true).uuid(uuid_of(0x40)).u32(400).u32(2000).u32(3000).b;
+    check(r, gr, "registration response + liveness");
+    auto rr = parse<proto::M2CSessionRegistrationResponse>(gr);
+    EXPECT(rr && rr->heartbeat_ms == 400 && rr->peer_timeout_ms == 2000 && rr->op_stall_ms == 3000);
+    // a reference master's response: no liveness parameters (everything off)
+    auto rref = parse<proto::M2CSessionRegistrationResponse>(G(1).boolean(true).uuid(uuid_of(0x40)).b);
+    EXPECT(rref && rref->heartbeat_ms == 0 && rref->peer_timeout_ms == 0 && rref->op_stall_ms == 0);
+}
+
+TEST(golden_liveness_packets) { // C2M 12 / M2C 12: id only; C2M 13: u64 tag, uuid, u8 kind, u32 step, u64 idle_ms
+    check(proto::C2MHeartbeat{}, {0x00, 0x0C}, "C2MHeartbeat");
+    check(proto::M2CHeartbeat{}, {0x00, 0x0C}, "M2CHeartbeat");
+    proto::C2MOpStalled s;
+    s.tag = 20;
+    s.suspect = uuid_of(0x50);
+    s.kind = proto::kStallTxBlocked;
+    s.step = 3;
+    s.idle_ms = 3011;
+    const auto g = G(13).u64(20).uuid(uuid_of(0x50)).u8(1).u32(3).u64(3011).b;
+    check(s, g, "C2MOpStalled");
+    auto q = parse<proto::C2MOpStalled>(g);
+    EXPECT(q && q->tag == 20 && q->suspect == uuid_of(0x50) && q->kind == proto::kStallTxBlocked && q->step == 3 &&
+           q->idle_ms == 3011);
 }
