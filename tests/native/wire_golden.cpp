@@ -1,5 +1,5 @@
 // Golden wire-format tests: every CCoIP packet (29 ids), both framings, and the pccl-amd liveness
-// extension (registration suffixes, heartbeat and op-stalled packets), against byte arrays
+// extension (registration suffixes, heartbeat and op-stalled packets, as docs/WIRE_DIVERGENCES.md specifies them), against byte arrays
 // written down from the reference's serialize() order (ccoip/src/cpp/ccoip_packets.cpp:6-625,
 // tinysockets multiplexed_socket.cpp:406-411, queued_client_socket.cpp:299-305) - NOT produced by our encoder.
 // Each case checks (1) our encoder emits exactly the golden bytes for a packet whose pccl-amd extension fields are
