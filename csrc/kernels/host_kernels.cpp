@@ -282,19 +282,21 @@ static bool quantize_v(void *dst_q, const void *src, size_t n, DType qtype, cons
     return false;
 }
 
+bool host_quantize_params(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, const QuantParams &p) {
+    switch (vtype) {
+        case DType::F32: return quantize_v<EF32>(dst_q, src, count, qtype, p);
+        case DType::F64: return quantize_v<EF64>(dst_q, src, count, qtype, p);
+        case DType::BF16: return quantize_v<EBF16>(dst_q, src, count, qtype, p);
+        case DType::F16: return quantize_v<EF16>(dst_q, src, count, qtype, p);
+        default: return false;
+    }
+}
+
 proto::QuantMeta host_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, QuantAlgo algo) {
     double mn = 0, mx = 0;
     host_minmax(src, count, vtype, mn, mx);
     proto::QuantMeta meta = make_meta(algo, vtype, qtype, mn, mx);
-    const QuantParams p = make_params(meta, qtype);
-    bool ok = false;
-    switch (vtype) {
-        case DType::F32: ok = quantize_v<EF32>(dst_q, src, count, qtype, p); break;
-        case DType::F64: ok = quantize_v<EF64>(dst_q, src, count, qtype, p); break;
-        case DType::BF16: ok = quantize_v<EBF16>(dst_q, src, count, qtype, p); break;
-        case DType::F16: ok = quantize_v<EF16>(dst_q, src, count, qtype, p); break;
-        default: break;
-    }
+    const bool ok = host_quantize_params(dst_q, src, count, vtype, qtype, make_params(meta, qtype));
     if (!ok) {
         LOG(ERR) << "host_quantize: unsupported combination " << dtype_name(vtype) << " -> " << dtype_name(qtype);
     }
@@ -349,7 +351,11 @@ static bool dequant_op(void *dst, const void *src_q, size_t n, DType qtype, Redu
 
 bool host_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                          const proto::QuantMeta &meta) {
-    const QuantParams p = make_params(meta, qtype);
+    return host_dequant_reduce_params(dst, src_q, count, vtype, qtype, op, make_params(meta, qtype));
+}
+
+bool host_dequant_reduce_params(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                                const QuantParams &p) {
     switch (vtype) {
         case DType::F32: return dequant_op<EF32>(dst, src_q, count, qtype, op, p);
         case DType::F64: return dequant_op<EF64>(dst, src_q, count, qtype, op, p);

@@ -22,6 +22,11 @@ bool host_reduce3(void *out, const void *a, const void *b, size_t count, DType t
 bool host_dequant_reduce(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
                          const proto::QuantMeta &meta);
 
+// The same with given parameters (make_params of a metadata packet): what the device kernels compute.
+bool host_dequant_reduce_params(void *dst, const void *src_q, size_t count, DType vtype, DType qtype, ReduceOp op,
+                                const QuantParams &p);
+bool host_quantize_params(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, const QuantParams &p);
+
 // Computes metadata over src and quantizes into dst_q.
 proto::QuantMeta host_quantize(void *dst_q, const void *src, size_t count, DType vtype, DType qtype, QuantAlgo algo);
 

@@ -8,8 +8,8 @@
 // stream_wait_event makes a stream wait for an event of another stream; the null stream (nullptr) is one process-wide
 // stream. Device memory is host memory: allocations of this backend are "device" pointers, and with
 // PCCL_HOSTDEV_ALL_DEVICE=1 every pointer is (a test's own buffers then take the device paths). Copies and the
-// reduce kernels run on the stream's thread with the host kernels (bit-identical to the HIP kernels). The xGMI / IPC
-// and VMM entry points report failure, so the library uses the TCP rings.
+// reduce, quantize and de-quantize kernels run on the stream's thread with the host kernels (bit-identical to the HIP
+// kernels). The xGMI / IPC and VMM entry points report failure, so the library uses the TCP rings.
 //
 // Extra entry points for tests (dlsym): pccl_hostdev_fill(stream, ptr, n_floats, value, delay_us) queues a "producer
 // kernel" that sleeps delay_us, then writes `value` into n fp32 elements - input the stream-ordered ops must wait for;
@@ -234,24 +234,57 @@ public:
         stream_of(s)->push([=] { kernels::host_finalize_avg(dst, count, t, world); });
         return true;
     }
-    // quantized paths, hashes, xGMI kernels and the optimizer are not emulated: the device ring quantizes through
-    // them, so quantized device ops fail here (the tests of this backend use the plain rings)
-    bool dequant_reduce(void *, const void *, size_t, DType, DType, ReduceOp, const kernels::QuantParams &,
-                        DevStream) override {
-        return false;
+    // quantized paths: the host twins of the device kernels (bit-identical), run on the stream's thread
+    bool dequant_reduce(void *dst, const void *src_q, size_t n, DType vt, DType qt, ReduceOp op,
+                        const kernels::QuantParams &p, DevStream s) override {
+        stream_of(s)->push([=] { kernels::host_dequant_reduce_params(dst, src_q, n, vt, qt, op, p); });
+        return true;
     }
-    bool dequant_reduce_minmax(void *, const void *, size_t, DType, DType, ReduceOp, const kernels::QuantParams &,
-                               double *, int, int *, DevStream) override {
-        return false;
+    // one (min, max) partial of the values stored (the device kernels emit one per workgroup)
+    bool dequant_reduce_minmax(void *dst, const void *src_q, size_t n, DType vt, DType qt, ReduceOp op,
+                               const kernels::QuantParams &p, double *partials, int max_blocks, int *blocks,
+                               DevStream s) override {
+        if (max_blocks < 1) return false;
+        *blocks = 1;
+        stream_of(s)->push([=] {
+            kernels::host_dequant_reduce_params(dst, src_q, n, vt, qt, op, p);
+            kernels::host_minmax(dst, n, vt, partials[0], partials[1]);
+        });
+        return true;
     }
-    bool quantize(void *, const void *, size_t, DType, DType, const kernels::QuantParams &, DevStream) override {
-        return false;
+    bool quantize(void *dst_q, const void *src, size_t n, DType vt, DType qt, const kernels::QuantParams &p,
+                  DevStream s) override {
+        stream_of(s)->push([=] { kernels::host_quantize_params(dst_q, src, n, vt, qt, p); });
+        return true;
     }
-    bool quantize_setback(void *, void *, size_t, DType, DType, const kernels::QuantParams &, DevStream) override {
-        return false;
+    // own chunk := D(Q(x)) (what every other peer de-quantizes)
+    bool quantize_setback(void *dst_q, void *src, size_t n, DType vt, DType qt, const kernels::QuantParams &p,
+                          DevStream s) override {
+        stream_of(s)->push([=] {
+            kernels::host_quantize_params(dst_q, src, n, vt, qt, p);
+            kernels::host_dequant_reduce_params(src, dst_q, n, vt, qt, ReduceOp::Set, p);
+        });
+        return true;
     }
-    bool minmax(const void *, size_t, DType, double *, DevStream) override { return false; }
-    bool minmax_fold(const double *, int, size_t, double *, DevStream) override { return false; }
+    bool minmax(const void *src, size_t n, DType vt, double *out2, DevStream s) override {
+        stream_of(s)->push([=] {
+            kernels::host_minmax(src, n, vt, out2[0], out2[1]);
+            if (n == 0) out2[0] = out2[1] = 0.0;
+        });
+        return true;
+    }
+    bool minmax_fold(const double *partials, int nparts, size_t n, double *out2, DevStream s) override {
+        stream_of(s)->push([=] {
+            double lo = __builtin_inf(), hi = -__builtin_inf();
+            for (int i = 0; i < nparts; ++i) {
+                lo = partials[2 * i] < lo ? partials[2 * i] : lo;
+                hi = partials[2 * i + 1] > hi ? partials[2 * i + 1] : hi;
+            }
+            out2[0] = n ? lo : 0.0;
+            out2[1] = n ? hi : 0.0;
+        });
+        return true;
+    }
     bool multi_reduce(void *const *, int, const void *const *, int, size_t, DType, ReduceOp, DevStream, int,
                       bool) override {
         return false;

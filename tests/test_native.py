@@ -55,7 +55,11 @@ def test_c_api_peers_with_standalone_master(world, num_ops, n, pool, inflight):
 
 def _hostdev_env(plugin, **extra):
     # the host-emulated device backend: every pointer is "device" memory, streams are worker threads, no xGMI
-    return dict(os.environ, PCCL_HIP_PLUGIN=plugin, PCCL_HOSTDEV_ALL_DEVICE="1", PCCL_DISABLE_IPC="1", **extra)
+    env = dict(os.environ)
+    env.update(extra)
+    env.update(PCCL_HIP_PLUGIN=plugin, PCCL_HOSTDEV_ALL_DEVICE="1", PCCL_DISABLE_IPC="1")
+    env.pop("PCCL_DISABLE_HIP", None)
+    return env
 
 
 @pytest.mark.parametrize("peers,ops,n", [(2, 20, 1 << 20), (3, 12, 100_003)])
@@ -69,6 +73,21 @@ def test_stream_ordered_threaded_peers_hostdev(peers, ops, n):
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res == {"peers": peers, "ops": ops, "elements": n, "bad": 0}
+
+
+EMULATED_DEVICE_SUITES = ["test_allreduce.py", "test_allreduce_matrix.py", "test_shared_state.py",
+                          "test_shared_state_scenarios.py", "test_ddp_overlap.py", "test_diloco.py"]
+
+
+def test_cpu_suites_on_emulated_device_rings():
+    """The CPU all-reduce matrix, shared-state and DDP / DiLoCo suites with every buffer taken for device memory on
+    the host-emulated backend: the same scenarios then run through the device rings (plain and quantized pipelines,
+    OpSenders / RingRx / step slots, staging, the shared-state device paths) instead of the host ring."""
+    _ensure_built()
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
+                        *[os.path.join(ROOT, "tests", t) for t in EMULATED_DEVICE_SUITES]],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT, env=_hostdev_env(HOSTDEV))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
 
 def test_c99_header_compat(tmp_path):
@@ -160,6 +179,12 @@ def test_tsan_build_unit_and_peers(tmp_path):
                         os.path.join(ROOT, "tests", "test_shared_state_scenarios.py"),
                         os.path.join(ROOT, "tests", "test_liveness.py")],
                        capture_output=True, text=True, env=py_env, timeout=900, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    # the same Python suites through the device rings of the host-emulated backend (TSan build of it)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
+                        *[os.path.join(ROOT, "tests", t) for t in EMULATED_DEVICE_SUITES]],
+                       capture_output=True, text=True, timeout=1200, cwd=ROOT,
+                       env=_hostdev_env(os.path.join(out, "libpccl_hostdev.so"), **py_env))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reports = [f.read_text() for f in tmp_path.glob("tsan*")]
     assert not any("WARNING: ThreadSanitizer" in t for t in reports), "\n".join(reports)[:5000]
