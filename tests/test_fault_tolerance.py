@@ -305,6 +305,39 @@ HRING_KILLS = [(0, "rx", True, False), (1, "end", False, False), (2, "rx", True,
                (None, "op_end", True, False), (None, "op_end", True, True)]
 
 
+HOSTDEV = os.path.join(os.path.dirname(HERE), "pccl_amd", "lib", "libpccl_hostdev.so")
+
+
+@pytest.mark.parametrize("point,step,phase,inplace", RING_KILLS)
+def test_emulated_device_ring_sigkill_mid_op(point, step, phase, inplace):
+    """The device ring's kill matrix (RING_KILLS) on CPU: 3 peer processes on the host-emulated device backend
+    (csrc/testing/hostdev_backend.cpp: every buffer taken for device memory, streams as worker threads, the host twins
+    of the kernels) run the plain and quantized device rings; the victim SIGKILLs itself at the point of op 8. The
+    survivors fail that op, drain every copy / kernel of it before the in-place input is restored (re-read 100 ms
+    later, bit-exact), re-form the ring and finish every step exactly in the smaller world, on the device ring."""
+    if not os.path.exists(HOSTDEV):
+        pytest.skip("libpccl_hostdev.so not built")
+    quant = point == "qring" or phase == "q"
+    inject = "op_end:8" if point == "op_end" else f"{point}:8:{step}:{phase}"
+    dev = {"PCCL_HIP_PLUGIN": HOSTDEV, "PCCL_HOSTDEV_ALL_DEVICE": "1", "PCCL_DISABLE_IPC": "1"}
+    extra = (["--inplace"] if inplace else []) + (["--quant", "u8"] if quant else [])
+    with local_master() as addr:
+        ps = [spawn_python([WORKER, addr, "3", str(r), "--device", "cpu", "--const", "--n", str(1 << 22), "--steps",
+                            "30", "--pool", "2", *extra, *(["--verify-restore-ms", "100"] if r else [])],
+                           env=dict(dev, PCCL_FAULT_INJECT=inject) if r == 0 else dev,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
+        outs = communicate_all(ps, 240, DIAG_SIGNALS)
+    assert ps[0].returncode == -9, outs[0][1][-2000:]
+    for r in (1, 2):
+        assert ps[r].returncode == 0, outs[r][1][-3000:]
+        lines = _lines(outs[r][0])
+        oks = _check_ok(lines)
+        errs = [x for x in lines if "error" in x]
+        assert len(oks) == 30 and oks[0]["world"] == 3 and oks[-1]["world"] == 2, (len(oks), oks[-1])
+        assert all(x["path"] == 2 for x in oks), oks[-1]
+        assert errs and not any(x.get("restore_bad") for x in errs), errs
+
+
 @pytest.mark.parametrize("step,phase,inplace,quant", HRING_KILLS)
 def test_host_ring_sigkill_mid_op(step, phase, inplace, quant):
     """Abort safety of the host ring (the reference's data path, reduce.cpp:551-580,657-660): survivors of a peer

@@ -315,6 +315,42 @@ def _gpu_stop_run(monkeypatch, inject, extra_env, n, extra_args=()):
     return t_stop, outs
 
 
+HOSTDEV = os.path.join(os.path.dirname(HERE), "pccl_amd", "lib", "libpccl_hostdev.so")
+
+
+@pytest.mark.parametrize("point", ["ring:20:1:rx", "qring:20:1:meta"])
+def test_sigstopped_peer_emulated_device_ring(monkeypatch, point):
+    """The device ring's stop points on CPU: peers on the host-emulated device backend (every buffer taken for device
+    memory, streams as worker threads; csrc/testing/hostdev_backend.cpp) run the plain and quantized device rings, and
+    peer 0 stops inside a ring step; survivors fail within the peer timeout + 2 s, drain, restore their in-place input
+    and continue at W = 2 on the device ring; the resumed peer rejoins."""
+    if not os.path.exists(HOSTDEV):
+        pytest.skip("libpccl_hostdev.so not built")
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", str(int(PEER_TIMEOUT_S * 1000)))
+    dev = {"PCCL_HIP_PLUGIN": HOSTDEV, "PCCL_HOSTDEV_ALL_DEVICE": "1", "PCCL_DISABLE_IPC": "1"}
+    extra = ["--const", "--inplace", "--verify-restore-ms", "100", "--n", str(1 << 20), "--pool", "2", "--duration",
+             "16", "--rejoin", "--max-failures", "30"] + (["--quant", "u8"] if point.startswith("qring") else [])
+    stop = dict(dev, PCCL_FAULT_INJECT=point, PCCL_FAULT_SIGNAL="STOP")
+    with local_master() as addr:
+        ps = [spawn_python([WORKER, addr, "3", str(r), "--device", "cpu", *extra], env=stop if r == 0 else dev,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
+        run = _Run(ps, 150)
+        _wait_until(lambda: _proc_state(ps[0].pid) == "T" or ps[0].poll() is not None, 60, "the victim to stop")
+        t_stop = time.time()
+        assert ps[0].poll() is None
+        time.sleep(5.0)
+        os.kill(ps[0].pid, signal.SIGCONT)
+        outs = run.join()
+    for r in range(3):
+        assert ps[r].returncode == 0, (r, outs[r][1][-3000:])
+    for r in (1, 2):
+        lines = _lines(outs[r][0])
+        assert all(x["path"] == 2 for x in lines if "path" in x), lines[-3:]
+        detect, after = _check_survivor(lines, t_stop, PEER_TIMEOUT_S + 2.0)
+        print(f"peer {r}: failed op {detect:.2f} s after the stop")
+        assert any(x["world"] == 3 for x in after), "the resumed peer did not rejoin"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("point", ["ring:20:1:rx", "ring:20:2:publish", "qring:20:1:meta"])
 def test_gpu_sigstopped_peer_device_ring(hip, monkeypatch, point):
