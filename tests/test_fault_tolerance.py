@@ -305,7 +305,9 @@ HRING_KILLS = [(0, "rx", True, False), (1, "end", False, False), (2, "rx", True,
                (None, "op_end", True, False), (None, "op_end", True, True)]
 
 
-HOSTDEV = os.path.join(os.path.dirname(HERE), "pccl_amd", "lib", "libpccl_hostdev.so")
+# the host-emulated device backend (PCCL_TEST_HOSTDEV: another build of it, e.g. the TSan one)
+HOSTDEV = os.environ.get("PCCL_TEST_HOSTDEV") or os.path.join(os.path.dirname(HERE), "pccl_amd", "lib",
+                                                              "libpccl_hostdev.so")
 
 
 @pytest.mark.parametrize("point,step,phase,inplace", RING_KILLS)

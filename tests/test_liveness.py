@@ -315,7 +315,9 @@ def _gpu_stop_run(monkeypatch, inject, extra_env, n, extra_args=()):
     return t_stop, outs
 
 
-HOSTDEV = os.path.join(os.path.dirname(HERE), "pccl_amd", "lib", "libpccl_hostdev.so")
+# the host-emulated device backend (PCCL_TEST_HOSTDEV: another build of it, e.g. the TSan one)
+HOSTDEV = os.environ.get("PCCL_TEST_HOSTDEV") or os.path.join(os.path.dirname(HERE), "pccl_amd", "lib",
+                                                              "libpccl_hostdev.so")
 
 
 @pytest.mark.parametrize("point", ["ring:20:1:rx", "qring:20:1:meta"])

@@ -186,5 +186,13 @@ def test_tsan_build_unit_and_peers(tmp_path):
                        capture_output=True, text=True, timeout=1200, cwd=ROOT,
                        env=_hostdev_env(os.path.join(out, "libpccl_hostdev.so"), **py_env))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    # peer processes stopped / killed inside device ring steps on the emulated backend: the abort, drain and restore
+    # paths of the plain and quantized device rings
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu", "-k",
+                        "emulated", os.path.join(ROOT, "tests", "test_fault_tolerance.py"),
+                        os.path.join(ROOT, "tests", "test_liveness.py")],
+                       capture_output=True, text=True, timeout=1800, cwd=ROOT,
+                       env=dict(py_env, PCCL_TEST_HOSTDEV=os.path.join(out, "libpccl_hostdev.so")))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reports = [f.read_text() for f in tmp_path.glob("tsan*")]
     assert not any("WARNING: ThreadSanitizer" in t for t in reports), "\n".join(reports)[:5000]
