@@ -317,8 +317,8 @@ def test_emulated_device_ring_sigkill_mid_op(point, step, phase, inplace):
     of the kernels) run the plain and quantized device rings; the victim SIGKILLs itself at the point of op 8. The
     survivors fail that op, drain every copy / kernel of it before the in-place input is restored (re-read 100 ms
     later, bit-exact), re-form the ring and finish every step exactly in the smaller world, on the device ring."""
-    if not os.path.exists(HOSTDEV):
-        pytest.skip("libpccl_hostdev.so not built")
+    if not os.path.exists(HOSTDEV) or os.environ.get("PCCL_DISABLE_HIP") == "1":
+        pytest.skip("libpccl_hostdev.so not built, or device plugins disabled (PCCL_DISABLE_HIP)")
     quant = point == "qring" or phase == "q"
     inject = "op_end:8" if point == "op_end" else f"{point}:8:{step}:{phase}"
     dev = {"PCCL_HIP_PLUGIN": HOSTDEV, "PCCL_HOSTDEV_ALL_DEVICE": "1", "PCCL_DISABLE_IPC": "1"}

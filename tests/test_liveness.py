@@ -320,24 +320,26 @@ HOSTDEV = os.environ.get("PCCL_TEST_HOSTDEV") or os.path.join(os.path.dirname(HE
                                                               "libpccl_hostdev.so")
 
 
-@pytest.mark.parametrize("point", ["ring:20:1:rx", "qring:20:1:meta"])
+@pytest.mark.parametrize("point", ["ring:8:1:rx", "qring:8:1:meta"])  # (op 8: reached early under TSan too)
 def test_sigstopped_peer_emulated_device_ring(monkeypatch, point):
     """The device ring's stop points on CPU: peers on the host-emulated device backend (every buffer taken for device
     memory, streams as worker threads; csrc/testing/hostdev_backend.cpp) run the plain and quantized device rings, and
     peer 0 stops inside a ring step; survivors fail within the peer timeout + 2 s, drain, restore their in-place input
     and continue at W = 2 on the device ring; the resumed peer rejoins."""
-    if not os.path.exists(HOSTDEV):
-        pytest.skip("libpccl_hostdev.so not built")
+    if not os.path.exists(HOSTDEV) or os.environ.get("PCCL_DISABLE_HIP") == "1":
+        pytest.skip("libpccl_hostdev.so not built, or device plugins disabled (PCCL_DISABLE_HIP)")
     monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", str(int(PEER_TIMEOUT_S * 1000)))
     dev = {"PCCL_HIP_PLUGIN": HOSTDEV, "PCCL_HOSTDEV_ALL_DEVICE": "1", "PCCL_DISABLE_IPC": "1"}
-    extra = ["--const", "--inplace", "--verify-restore-ms", "100", "--n", str(1 << 20), "--pool", "2", "--duration",
-             "16", "--rejoin", "--max-failures", "30"] + (["--quant", "u8"] if point.startswith("qring") else [])
+    scale = float(os.environ.get("PCCL_TEST_TIME_SCALE", "1"))  # (sanitizer builds run slower)
+    extra = ["--const", "--inplace", "--verify-restore-ms", "100", "--n", str(1 << 19), "--pool", "2", "--duration",
+             str(16 * scale), "--rejoin", "--max-failures", "30"] + (["--quant", "u8"] if point.startswith("qring") else [])
     stop = dict(dev, PCCL_FAULT_INJECT=point, PCCL_FAULT_SIGNAL="STOP")
     with local_master() as addr:
         ps = [spawn_python([WORKER, addr, "3", str(r), "--device", "cpu", *extra], env=stop if r == 0 else dev,
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(3)]
-        run = _Run(ps, 150)
-        _wait_until(lambda: _proc_state(ps[0].pid) == "T" or ps[0].poll() is not None, 60, "the victim to stop")
+        run = _Run(ps, 150 * scale)
+        _wait_until(lambda: _proc_state(ps[0].pid) == "T" or ps[0].poll() is not None, 60 * scale,
+                    "the victim to stop")
         t_stop = time.time()
         assert ps[0].poll() is None
         time.sleep(5.0)

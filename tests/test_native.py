@@ -193,7 +193,7 @@ def test_tsan_build_unit_and_peers(tmp_path):
                         os.path.join(ROOT, "tests", "test_liveness.py")],
                        capture_output=True, text=True, timeout=1800, cwd=ROOT,
                        env=dict({k: v for k, v in py_env.items() if k != "PCCL_DISABLE_HIP"},
-                                PCCL_TEST_HOSTDEV=os.path.join(out, "libpccl_hostdev.so")))
+                                PCCL_TEST_HOSTDEV=os.path.join(out, "libpccl_hostdev.so"), PCCL_TEST_TIME_SCALE="3"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     reports = [f.read_text() for f in tmp_path.glob("tsan*")]
     assert not any("WARNING: ThreadSanitizer" in t for t in reports), "\n".join(reports)[:5000]
