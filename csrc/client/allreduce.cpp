@@ -164,7 +164,6 @@ void Client::initiate_op(OpState &op) {
     } else {
         init.flags |= kCollFlagExtWire; // pccl-amd framing, with this peer's proposed shape
         init.shape = ring::local_wire_shape();
-        if (!op.device) init.shape.quant_piece_kib = 0; // (per-piece metadata: device rings only)
     }
     op.init_sent = master_.send(init);
 }

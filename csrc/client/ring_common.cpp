@@ -49,7 +49,6 @@ Shape Shape::from_wire(const proto::WireShape &w) {
     s.quant_lanes = std::max<size_t>(1, std::min<size_t>(4, w.quant_lanes));
     s.stripe_min = std::max<size_t>(256, w.stripe_min_kib) << 10;
     s.segment_chunk = static_cast<size_t>(w.segment_chunk_mib) << 20;
-    s.quant_piece = static_cast<size_t>(w.quant_piece_kib) << 10;
     return s;
 }
 
@@ -69,7 +68,6 @@ proto::WireShape local_wire_shape() {
     const size_t min_bytes = std::max<size_t>(256 << 10, env_size("PCCL_STRIPE_MIN_BYTES", 8u << 20));
     w.stripe_min_kib = static_cast<uint16_t>(std::min<size_t>(65535, min_bytes >> 10));
     w.segment_chunk_mib = static_cast<uint16_t>(std::min<size_t>(65535, env_size("PCCL_SEGMENT_CHUNK_MIB", 128)));
-    w.quant_piece_kib = static_cast<uint16_t>(std::min<size_t>(65535, env_size("PCCL_QUANT_PIECE_META_KIB", 256)));
     return w;
 }
 

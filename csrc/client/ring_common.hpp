@@ -53,7 +53,6 @@ struct Shape {
     size_t stripe_min = 8u << 20;   // smallest stripe (bytes)
     size_t quant_lanes = 2;         // lanes of a quantized op
     size_t segment_chunk = 128u << 20; // largest ring chunk of one segment, value bytes (0: the op is one segment)
-    size_t quant_piece = 0; // wire bytes per separately quantized piece of a small quantized device op (0: per step)
     // bytes of the op's largest ring step (op_shape; 0: not derived, stripe_conn assumes `stripes`): every peer
     // derives it from the op's agreed values; with the size of a connection pool it gives the op's stripe count on
     // that pool (stripe_count), the same at both of its ends even when neighbours' pools differ in size

@@ -9,13 +9,8 @@
 //   * all-gather: the owner quantizes its finished chunk once and overwrites its own copy with D(Q(x)) (every peer
 //     ends bit-identical); received quantized chunks are forwarded cut-through (the next step's metadata and sends
 //     start when this step's metadata arrives; every piece leaves as it lands) and de-quantized.
-// The per-step serialisation of the reduce-scatter is inherent to one metadata packet per step; lanes overlap it (one
-// lane's fill and drain runs while another lane's data moves). Small ops (a lane's chunk of at most kPieceMetaMaxChunk
-// wire bytes: many concurrent ops over a long-latency link) run with per-piece metadata instead when every participant
-// agreed to it (Shape::quant_piece): each piece of a payload is quantized with its own min / max and its own metadata
-// packet, so the reduce-scatter forwards piece by piece - a reduced piece leaves as soon as it is complete, instead of
-// after the whole chunk - and a WAN hop costs one latency plus one piece, not one latency plus one chunk.
-// Reference (host memory, one lane): ccoip/src/cpp/reduce.cpp:609-774.
+// The per-step serialisation of the reduce-scatter is inherent to the protocol; lanes overlap it (one lane's fill and
+// drain runs while another lane's data moves). Reference (host memory, one lane): ccoip/src/cpp/reduce.cpp:609-774.
 // In the reference framing (a reference peer in the ring, or PCCL_WIRE=reference) the op runs the host ring's
 // step-synchronous protocol on a pinned bounce buffer instead (device_quant_reference_framing).
 #include <cstring>
@@ -34,10 +29,6 @@ namespace {
 
 using namespace ring;
 using proto::QuantMeta;
-
-// largest lane chunk (wire bytes) that runs with per-piece metadata when agreed (the small ops of a WAN run; larger
-// chunks keep one metadata packet per step, whose fused min / max folds and larger launches serve them better)
-constexpr size_t kPieceMetaMaxChunk = 8u << 20;
 
 // Start order of the lanes of one quantized op: lane k+1 starts once lane k's first payload is quantized. The lanes
 // then run half a phase apart: one lane's reduce-scatter step quantizes (device->host writes) while the other's data
@@ -129,11 +120,6 @@ int device_quant_lane(QLane &L) {
     auto nrx = [&](size_t G) { return rx_range(G).second - rx_range(G).first; };
     const size_t qbytes = max_chunk * qs + 64;
     const Shape shape = op_shape(agreed, max_chunk * qs); // the lane's connection groups
-    // per-piece metadata (see the top): one segment, a small chunk, agreed by every participant
-    const bool pm = agreed.quant_piece > 0 && nseg == 1 && max_chunk * qs <= kPieceMetaMaxChunk && ws >= 2;
-    const size_t pel = pm ? std::max<size_t>(256, agreed.quant_piece / qs / 64 * 64) : piece_el; // elements per piece
-    auto npieces = [&](size_t n) { return (n + pel - 1) / pel; };
-    const size_t ntxq = pm ? 3 : 2; // payload buffers (piece metadata: step g+1's payload fills while g-1's drains)
     // receive slots (3, 6 and 8 slots for the small steps of 32 / 64 concurrent WAN ops measured the same:
     // profiles/r5/b10/)
     constexpr size_t kNb = StepSlots::kDefaultSlots;
@@ -142,10 +128,10 @@ int device_quant_lane(QLane &L) {
     // all-gather's first payload), so its min / max is one fold of those partials instead of a second pass. A step
     // whose launches do not fit the partials buffer falls back to a separate min / max pass.
     constexpr int kMmSlots = 65536, kMmMinRoom = 64; // 1 MiB of partials: ~1 GiB bf16 chunks
-    Lease txl[3], rxl[StepSlots::kMaxSlots], dvl[StepSlots::kMaxSlots], mml, mmp;
-    uint8_t *txq[3], *rxbuf[StepSlots::kMaxSlots], *rxdev[StepSlots::kMaxSlots];
+    Lease txl[2], rxl[StepSlots::kMaxSlots], dvl[StepSlots::kMaxSlots], mml, mmp;
+    uint8_t *txq[2], *rxbuf[StepSlots::kMaxSlots], *rxdev[StepSlots::kMaxSlots];
     for (size_t i = 0; i < kNb; ++i) {
-        if (i < ntxq) {
+        if (i < 2) {
             txl[i] = Lease(pinned_pool(), qbytes);
             if (!txl[i].ok()) return 1;
             txq[i] = txl[i].data();
@@ -172,11 +158,11 @@ int device_quant_lane(QLane &L) {
         }
     } drain{be, st, &owned};
 
-    ReadyRanges txready[3];
+    ReadyRanges txready[2];
     const size_t nsteps = nseg * nps;
     auto is_rs = [&](size_t G) { return G % nps + 1 < ws; };
 
-    OpSenders senders(*L.txs, L.tag, seq, shape, pel * qs, nsteps, op_stripes(shape, L.txs->size()), be, *L.tx);
+    OpSenders senders(*L.txs, L.tag, seq, shape, piece_el * qs, nsteps, op_stripes(shape, L.txs->size()), be, *L.tx);
     RingRx rx(*L.rxs, L.tag, seq, shape, nsteps);
     StepSlots slots(be, rx, senders, ws, nsteps, rxbuf, kNb, [&](size_t G) { return nrx(G) * qs; });
     const StepIo io = step_io(*L.txs, *L.rxs, L.tag, seq, shape);
@@ -247,138 +233,6 @@ int device_quant_lane(QLane &L) {
     const bool lane_copies = max_chunk * qs >= (size_t{4} << 20);
     const PcieQueues pq = lane_copies ? PcieQueues{} : shared_pcie_queues(be, L.device);
     if (!lane_copies && !pq.h2d) return fail(1);
-    if (pm) {
-        // ---- per-piece metadata (one segment: G == g). Payload steps 0 .. ws-1 fill txq[g % 3]; step g+1's payload
-        // is the chunk step g receives, so its pieces are quantized (each with its own min / max and metadata packet)
-        // as soon as they are reduced, while step g still receives; the all-gather forwards received pieces and
-        // metadata packets as they arrive.
-        int cons_rc = 0;
-        auto pfailed = [&] { return cons_rc != 0 || failed(); };
-        // quantizes piece j of payload step gp (its elements [off, off + k) of the chunk at src) and sends its metadata
-        auto emit = [&](size_t gp, size_t j, const uint8_t *chunk, size_t n) -> int {
-            const size_t slot = gp % 3, off = j * pel, k = std::min(pel, n - off);
-            uint8_t *src = const_cast<uint8_t *>(chunk) + off * es;
-            be->minmax(src, k, L.dtype, minmax_out, st);
-            stream_wait_polling(be, st);
-            const QuantMeta m = kernels::make_meta(L.qalgo, L.dtype, L.qtype, minmax_out[0], minmax_out[1]);
-            const auto params = kernels::make_params(m, L.qtype);
-            if (gp + 1 == ws) // the all-gather's payload; parity: own chunk := D(Q(x)), what the others de-quantize
-                be->quantize_setback(txq[slot] + off * qs, src, k, L.dtype, L.qtype, params, st);
-            else
-                be->quantize(txq[slot] + off * qs, src, k, L.dtype, L.qtype, params, st);
-            DevEvent e = record(st);
-            pcie_note(0, k * qs);
-            txready[slot].add(off * qs, (off + k) * qs, e);
-            if (gp == 0) first_payload = e;
-            return send_meta(io, m, *L.tx);
-        };
-        auto publish_payload = [&](size_t gp) -> bool {
-            if (gp >= 3 && !senders.wait(gp - 3)) return false; // txq[gp % 3] was step gp-3's payload
-            txready[gp % 3].clear();
-            publish(gp, txq[gp % 3], &txready[gp % 3]);
-            return true;
-        };
-        for (size_t G = 0; G < nsteps; ++G) {
-            const bool rs = is_rs(G);
-            if (!slots.ensure_posted(G, failed)) return fail(1);
-            if (G == 0) { // own input: every piece's metadata at once
-                if (!publish_payload(0)) return fail(1);
-                const auto [c0, c1] = tx_range(0);
-                for (size_t j = 0; j < npieces(c1 - c0); ++j)
-                    if (int m = emit(0, j, L.dst + c0 * es, c1 - c0)) return fail(m);
-                step_sub_mark('q', 0);
-            }
-            // the next step may start sending what this step produces (payload pieces or forwarded bytes)
-            if (G + 1 < nsteps) {
-                if (G + 1 < ws) {
-                    if (!publish_payload(G + 1)) return fail(1);
-                } else {
-                    publish(G + 1, slots.buf(G), &slots.ready(G));
-                }
-            }
-            fault_point("qring", seq, G, "meta");
-            const size_t n_rx = nrx(G), pb = pel * qs;
-            const bool fwd_meta = !rs && G + 1 < nsteps; // all-gather step whose bytes the next step forwards
-            const bool produce = rs;                      // step G+1's payload is this step's chunk (G+1 <= ws-1)
-            std::vector<QuantMeta> metas;
-            std::vector<size_t> got(npieces(n_rx), 0);
-            size_t next_emit = 0;
-            uint8_t *region = L.dst + rx_range(G).first * es;
-            uint8_t *sink = slots.buf(G);
-            ReadyRanges *fwd = &slots.ready(G);
-            DevEvent step_last = nullptr;
-            bool first = true;
-            auto pull_meta = [&](size_t j) -> int { // metadata packets of this step arrive in piece order
-                while (metas.size() <= j) {
-                    QuantMeta m;
-                    if (int r = recv_meta(io, m, *L.rx, L.aborted, failed)) return r;
-                    if (fwd_meta)
-                        if (int r = send_meta(io, m, *L.tx)) return r;
-                    metas.push_back(m);
-                }
-                return 0;
-            };
-            auto emit_ready = [&]() -> int { // step G+1's pieces, in order, once their bytes are reduced
-                while (produce && next_emit < got.size() &&
-                       got[next_emit] == std::min(pb, n_rx * qs - next_emit * pb)) {
-                    if (int r = emit(G + 1, next_emit, region, n_rx)) return r;
-                    ++next_emit;
-                }
-                return 0;
-            };
-            const int rc = rx.receive(
-                G, qs, pb,
-                [&](size_t a, size_t e) {
-                    if (cons_rc) return;
-                    pcie_note(e - a, 0);
-                    for (size_t sa = a; sa < e;) { // piece by piece (each with its own parameters)
-                        const size_t j = sa / pb, se = std::min(e, (j + 1) * pb), n = (se - sa) / qs;
-                        if ((cons_rc = pull_meta(j)) != 0) return;
-                        const auto params = kernels::make_params(metas[j], L.qtype);
-                        if (rs) {
-                            if (lane_copies) {
-                                be->memcpy_async(rxdev[G % kNb] + sa, sink + sa, se - sa, st);
-                            } else {
-                                be->memcpy_async(rxdev[G % kNb] + sa, sink + sa, se - sa, pq.h2d);
-                                be->stream_wait_event(st, record(pq.h2d));
-                            }
-                            be->dequant_reduce(region + sa / qs * es, rxdev[G % kNb] + sa, n, L.dtype, L.qtype, L.rop,
-                                               params, st);
-                        } else {
-                            fwd->add(sa, se, nullptr);
-                            be->dequant_reduce(region + sa / qs * es, sink + sa, n, L.dtype, L.qtype, ReduceOp::Set,
-                                               params, st);
-                        }
-                        got[j] += se - sa;
-                        sa = se;
-                    }
-                    step_last = record(st);
-                    if (first) {
-                        first = false;
-                        step_sub_mark('f', G);
-                        fault_point("qring", seq, G, "rx");
-                    }
-                    cons_rc = emit_ready();
-                },
-                [&] {
-                    maybe_open_gate();
-                    slots.try_post(G + 1);
-                },
-                pfailed, L.aborted);
-            slots.free_after(G, step_last);
-            if (rc) return fail(cons_rc ? cons_rc : rc);
-            if (cons_rc) return fail(cons_rc);
-            if (npieces(n_rx) > 0)
-                if (int r = pull_meta(npieces(n_rx) - 1)) return fail(r); // (consumed every piece: all pulled)
-            if (produce && next_emit != got.size()) return fail(1); // (every piece was reduced: cannot happen)
-            *L.rx += n_rx * qs;
-            rx.unpost(G);
-            step_mark(rs, rs ? G : G - (ws - 1));
-            fault_point("qring", seq, G, "end");
-        }
-        if (!senders.wait_all()) return fail(1);
-        return 0;
-    }
     for (size_t G = 0; G < nsteps; ++G) {
         const size_t g = G % nps, b = G % kNb;
         const bool rs = is_rs(G);

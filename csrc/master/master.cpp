@@ -985,7 +985,6 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
     pkt.shape.quant_lanes = 4;
     pkt.shape.stripe_min_kib = 256;
     pkt.shape.segment_chunk_mib = 0;
-    pkt.shape.quant_piece_kib = 0xffff; // smallest proposal; 0 (off) if any participant proposes none
     bool seg_any = false;
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;
@@ -996,7 +995,6 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
         pkt.shape.stripes = std::min(pkt.shape.stripes, sh->second.stripes);
         pkt.shape.quant_lanes = std::min(pkt.shape.quant_lanes, sh->second.quant_lanes);
         pkt.shape.stripe_min_kib = std::max(pkt.shape.stripe_min_kib, sh->second.stripe_min_kib);
-        pkt.shape.quant_piece_kib = std::min(pkt.shape.quant_piece_kib, sh->second.quant_piece_kib);
         // smallest non-zero segment (0 = unsegmented only if every proposal says so)
         const uint16_t sg = sh->second.segment_chunk_mib;
         if (sg != 0 && (!seg_any || sg < pkt.shape.segment_chunk_mib)) {
@@ -1004,7 +1002,6 @@ void Master::check_coll_initiate_consensus(uint32_t group, uint64_t tag) {
             seg_any = true;
         }
     }
-    if (pkt.shape.quant_piece_kib == 0xffff) pkt.shape.quant_piece_kib = 0;
     bool stale = false;
     for (auto &[_, c] : clients_) {
         if (c.group != group || c.phase != Phase::Accepted) continue;

@@ -179,16 +179,11 @@ struct WireShape {
     uint8_t quant_lanes = 2;        // PCCL_QUANT_LANES: lanes of a quantized op (1..4)
     uint16_t stripe_min_kib = 8192; // PCCL_STRIPE_MIN_BYTES / 1 KiB: smallest stripe (>= 256 KiB)
     uint16_t segment_chunk_mib = 128; // PCCL_SEGMENT_CHUNK_MIB: largest ring chunk of one segment (0: one segment)
-    // appended (optional; absent = 0): wire bytes / 1 KiB per quantization piece of a small quantized device op, each
-    // piece with its own metadata packet so the reduce-scatter forwards piece by piece (PCCL_QUANT_PIECE_META_KIB);
-    // 0: one metadata packet per ring step
-    uint16_t quant_piece_kib = 0;
     void encode(WBuf &w) const {
         w.u8(stripes);
         w.u8(quant_lanes);
         w.u16(stripe_min_kib);
         w.u16(segment_chunk_mib);
-        w.u16(quant_piece_kib);
     }
     bool decode(RBuf &r) {
         if (!r.ok() || r.remaining() < 6) return false;
@@ -196,7 +191,6 @@ struct WireShape {
         quant_lanes = r.u8();
         stripe_min_kib = r.u16();
         segment_chunk_mib = r.u16();
-        quant_piece_kib = r.ok() && r.remaining() >= 2 ? r.u16() : 0;
         stripes = stripes < 1 ? 1 : (stripes > 16 ? 16 : stripes);
         quant_lanes = quant_lanes < 1 ? 1 : (quant_lanes > 4 ? 4 : quant_lanes);
         if (stripe_min_kib < 256) stripe_min_kib = 256;
@@ -204,7 +198,7 @@ struct WireShape {
     }
     bool operator==(const WireShape &o) const {
         return stripes == o.stripes && quant_lanes == o.quant_lanes && stripe_min_kib == o.stripe_min_kib &&
-               segment_chunk_mib == o.segment_chunk_mib && quant_piece_kib == o.quant_piece_kib;
+               segment_chunk_mib == o.segment_chunk_mib;
     }
 };
 
