@@ -21,10 +21,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PEER = os.path.join(HERE, "workers", "stress_peer.py")
 
 
-def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None):
+def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, stop_p=0.0):
+    """`stop_p`: share of the victims that are SIGSTOPped instead (a hung peer: its sockets stay open, only the
+    liveness protocol notices) and SIGKILLed 4 s later."""
     rng = random.Random(1234)
     stop = tmp_path / "stop"
     procs, killed, signalled = [], 0, set()
+    hung = []  # (process, time to SIGKILL it)
+
+    def hit(victim):
+        if rng.random() < stop_p:
+            victim.send_signal(signal.SIGSTOP)
+            hung.append((victim, time.time() + 4.0))
+        else:
+            victim.send_signal(signal.SIGKILL)
     with local_master() as addr:
         def spawn():
             # stdout to a file: a long soak must never block a peer on a full pipe
@@ -37,6 +47,9 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None):
         t_end = time.time() + duration
         t_report = time.time() + 30
         while time.time() < t_end:
+            for v, t_kill in [h for h in hung if time.time() >= h[1]]:
+                v.send_signal(signal.SIGKILL)
+                hung.remove((v, t_kill))
             # a SIGKILLed GPU process can take a while to exit: never pick (or count) it twice
             alive = [p for p, _ in procs if p.poll() is None and p.pid not in signalled]
             if soak and time.time() >= t_report:  # progress of a long soak (run pytest with -s to see it live)
@@ -47,7 +60,7 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None):
                 time.sleep(rng.uniform(0.5, 2.0))
                 if rng.random() < 0.4 and len(alive) > 2:
                     victim = rng.choice(alive)
-                    victim.send_signal(signal.SIGKILL)
+                    hit(victim)
                     signalled.add(victim.pid)
                     killed += 1
                 if rng.random() < 0.6 and len(alive) < 2 * target:
@@ -56,11 +69,13 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None):
             time.sleep(rng.uniform(2.0, 4.0))
             if len(alive) > 2:
                 victim = rng.choice(alive)
-                victim.send_signal(signal.SIGKILL)
+                hit(victim)
                 signalled.add(victim.pid)
                 killed += 1
             if len([p for p, _ in procs if p.poll() is None and p.pid not in signalled]) < target:
                 spawn()
+        for v, _ in hung:
+            v.send_signal(signal.SIGKILL)
         stop.write_text("1")
         for p, out in procs:
             try:
@@ -95,6 +110,18 @@ def test_random_kill_respawn(tmp_path):
     assert sum(s["ok_ops"] for s in summaries) > 10, summaries
 
 
+def test_random_stop_kill_respawn(tmp_path, monkeypatch):
+    """The same churn with half of the victims hung instead of killed (SIGSTOP, SIGKILLed 4 s later): the master drops a
+    hung peer after PCCL_PEER_TIMEOUT_MS (2 s here) while its sockets are still open, and the survivors keep making
+    progress with exact results."""
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", "2000")
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
+    killed, summaries = _run_stress(tmp_path, duration, 4, soak=duration > 60, stop_p=0.5)
+    assert killed >= 3
+    assert summaries and all(s["bad"] == 0 for s in summaries), summaries
+    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+
+
 @pytest.mark.gpu
 def test_random_kill_respawn_gpu_ipc(tmp_path, hip):
     """Device tensors on cuda:0: the peers reduce over the xGMI/IPC path, so SIGKILLs land during IPC votes and
@@ -114,6 +141,21 @@ def test_random_kill_respawn_gpu_ring(tmp_path, hip):
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
     killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60,
                                     env={"PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "64"})
+    assert killed >= 3
+    assert summaries and all(s["bad"] == 0 for s in summaries), summaries
+    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["ring", "ipc"])
+def test_random_stop_kill_respawn_gpu(tmp_path, hip, monkeypatch, path):
+    """Hung and killed peers at random on cuda:0 (PCCL_PEER_TIMEOUT_MS 2 s): on the TCP device ring with a 64 MiB
+    tensor per step (hangs land mid-pipeline) and on the xGMI path (hangs land around votes and kernels); no wrong
+    result, survivors progress, everyone alive at the end exits cleanly."""
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", "2000")
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
+    env = {"PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "64"} if path == "ring" else None
+    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60, env=env, stop_p=0.5)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
     assert sum(s["ok_ops"] for s in summaries) > 10, summaries
