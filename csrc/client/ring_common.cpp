@@ -700,13 +700,16 @@ void StepSlots::post(size_t g) {
     rx_.post(g, buf_[b], rx_bytes_(g));
 }
 
-bool StepSlots::ensure_posted(size_t g, const std::function<bool()> &failed) {
-    while (!rx_.posted(g)) {
+bool StepSlots::ensure_posted(size_t g, const std::function<bool()> &failed, const std::function<bool()> &aborted) {
+    for (size_t polls = 1; !rx_.posted(g); ++polls) {
         if (can_post(g)) {
             post(g);
             break;
         }
-        if (failed()) return false;
+        // (the slot may wait on forwarded bytes whose sender is blocked on a peer that stopped reading: the wait
+        // also ends on the op's watchdog verdict or the master's abort, polled every ~20 ms)
+        if (failed() || watch_failed()) return false;
+        if (aborted && polls % 1000 == 0 && aborted()) return false;
         std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     return true;

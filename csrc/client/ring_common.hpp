@@ -386,8 +386,9 @@ public:
     ReadyRanges &ready(size_t g) { return ready_[g % n_]; } // received ranges (the all-gather forwards them)
     bool can_post(size_t g) const;
     void post(size_t g);
-    // posts step g's sinks (normally already posted during step g-1), waiting for its slot; false if `failed`
-    bool ensure_posted(size_t g, const std::function<bool()> &failed);
+    // posts step g's sinks (normally already posted during step g-1), waiting for its slot; false if `failed`, the
+    // op's watchdog failed it, or `aborted` (the master's abort poll) reports
+    bool ensure_posted(size_t g, const std::function<bool()> &failed, const std::function<bool()> &aborted = {});
     // posts step g's sinks if not yet posted and its slot is free (non-blocking; from the receive loop)
     bool try_post(size_t g);
     // the last GPU work reading step g's slot

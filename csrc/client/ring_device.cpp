@@ -182,7 +182,7 @@ int device_ring_pipeline(DevRing &R) {
         const size_t g = lstep(G), b = G % kNb, nb = (G + 1) % kNb;
         const bool rs = is_rs(G);
         // 1. step G's sinks (normally posted during step G-1)
-        if (!slots.ensure_posted(G, [&] { return senders.failed(); })) return fail(1);
+        if (!slots.ensure_posted(G, [&] { return senders.failed(); }, R.aborted)) return fail(1);
         // 2. this step's reduce writes txbuf[nb], last read by step G-2's sends
         uint8_t *region = region_of(G);
         const size_t shift = reinterpret_cast<uintptr_t>(region) % 16;

@@ -236,7 +236,7 @@ int device_quant_lane(QLane &L) {
     for (size_t G = 0; G < nsteps; ++G) {
         const size_t g = G % nps, b = G % kNb;
         const bool rs = is_rs(G);
-        if (!slots.ensure_posted(G, failed)) return fail(1);
+        if (!slots.ensure_posted(G, failed, L.aborted)) return fail(1);
         if (g < ws) { // own payload: reduce-scatter steps and the all-gather's first step
             const size_t slot = G % 2;
             const auto [c0, c1] = tx_range(G);
