@@ -24,7 +24,7 @@ PEER = os.path.join(HERE, "workers", "stress_peer.py")
 def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, stop_p=0.0):
     """`stop_p`: share of the victims that are SIGSTOPped instead (a hung peer: its sockets stay open, only the
     liveness protocol notices) and SIGKILLed 4 s later."""
-    rng = random.Random(1234)
+    rng = random.Random(int(os.environ.get("PCCL_STRESS_SEED", "1234")))
     stop = tmp_path / "stop"
     procs, killed, signalled = [], 0, set()
     hung = []  # (process, time to SIGKILL it)
@@ -82,6 +82,8 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, 
                 p.wait(timeout=90)
             except subprocess.TimeoutExpired:
                 p.send_signal(signal.SIGUSR1)  # faulthandler: dump every thread's Python stack
+                time.sleep(1)
+                p.send_signal(signal.SIGUSR2)  # native backtraces of every thread (PCCL_DEBUG_BACKTRACE_SIGNAL)
                 time.sleep(1)
                 p.kill()
                 p.wait()
