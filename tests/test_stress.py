@@ -87,6 +87,13 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, 
                 time.sleep(1)
                 p.kill()
                 p.wait()
+                dump = os.environ.get("PCCL_STRESS_DUMP_DIR")  # every peer's whole output, for the post-mortem
+                if dump:
+                    os.makedirs(dump, exist_ok=True)
+                    for k, (_, o) in enumerate(procs):
+                        o.seek(0)
+                        with open(os.path.join(dump, f"peer{k}.out"), "w") as f:
+                            f.write(o.read())
                 out.seek(0)
                 raise AssertionError("peer did not stop:\n" + out.read()[-6000:])
     summaries = []
