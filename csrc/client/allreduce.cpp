@@ -358,20 +358,23 @@ bool Client::join_async_reduce(uint64_t tag) {
     }
     op->wait();
     op->joined.store(true);
-    if (!op->success) {
-        // Re-establish the ring once per connection revision: every peer sees the same failures, so every peer
-        // performs exactly one establishment round (several concurrent failed ops must not cascade into more).
-        // Ops still in flight keep this peer in the master's COLLECTIVE_COMMUNICATIONS_RUNNING state, where an
-        // establish vote is illegal; the last failed op to be joined performs the round instead.
-        std::lock_guard lock(establish_mtx_);
-        if (conn_revision_.load() == op->revision_at_start && !interrupted_ && !any_collective_running()) {
-            if (!request_and_establish_locked(false)) {
-                LOG(ERR) << "Failed to re-establish P2P connections after abort";
-            }
+    // Re-establish the ring once per connection revision after a failed op: every peer sees the same failures, so
+    // every peer performs exactly one establishment round (several concurrent failed ops must not cascade into more;
+    // reference ccoip_client_handler.cpp:1349-1367). Ops still in flight keep this peer in the master's
+    // COLLECTIVE_COMMUNICATIONS_RUNNING state, where an establish vote is illegal: the round is then left pending and
+    // performed by the next join with nothing running - whether that op failed or succeeded, so a peer whose last
+    // joined op succeeded still joins the round its peers are waiting in.
+    if (op->success && reestablish_pending_.load() == UINT64_MAX) return true; // (the common path takes no lock)
+    std::lock_guard lock(establish_mtx_);
+    if (!op->success && conn_revision_.load() == op->revision_at_start) reestablish_pending_ = op->revision_at_start;
+    if (reestablish_pending_.load() != UINT64_MAX && !interrupted_ && !any_collective_running()) {
+        const bool due = reestablish_pending_.load() == conn_revision_.load();
+        reestablish_pending_ = UINT64_MAX;
+        if (due && !request_and_establish_locked(false)) {
+            LOG(ERR) << "Failed to re-establish P2P connections after abort";
         }
-        return false;
     }
-    return true;
+    return op->success;
 }
 
 bool Client::get_reduce_info(uint64_t tag, ReduceInfo &out) {

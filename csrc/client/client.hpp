@@ -281,6 +281,10 @@ private:
     std::shared_ptr<IpcArena> arena_;
     std::shared_ptr<HierState> hier_;
     std::mutex establish_mtx_; // serializes concurrent re-establishment attempts
+    // a failed op was joined while other ops were still running (no establishment vote possible then): the connection
+    // revision it failed on, or UINT64_MAX; the next join with nothing running performs the round (guarded by
+    // establish_mtx_)
+    std::atomic<uint64_t> reestablish_pending_{UINT64_MAX};
 
     std::atomic<uint64_t> conn_revision_{0};
     std::atomic<size_t> global_ws_{0}, local_ws_{0}, n_groups_{0}, largest_group_{0};
