@@ -71,7 +71,7 @@ class _Run:
         return self.outs
 
 
-def _check_survivor(lines, t_fault, bound_s, world_before=3):
+def _check_survivor(lines, t_fault, bound_s, world_before=3, smaller_ring=True):
     oks = [x for x in lines if "error" not in x and "world" in x]
     assert oks and not any(x.get("bad") for x in oks), lines[-5:]
     errs = [x for x in lines if "error" in x]
@@ -83,7 +83,10 @@ def _check_survivor(lines, t_fault, bound_s, world_before=3):
     assert detect <= bound_s, f"failed op {detect:.2f} s after the fault (bound {bound_s} s)"
     assert oks[0]["world"] == world_before
     after = [x for x in oks if x["t"] > first_err]
-    assert any(x["world"] == world_before - 1 for x in after), "the ring did not re-form without the stopped peer"
+    if smaller_ring and not any(x["world"] < world_before for x in after):
+        print("survivor timeline:", [(round(x["t"] - t_fault, 2), x.get("world", x.get("error", "")[:50]))
+                                     for x in lines if x["t"] > t_fault - 0.5])
+        raise AssertionError("the ring did not re-form without the stopped peer")
     return detect, after
 
 
@@ -170,8 +173,11 @@ def test_blackholed_link_host_ring(monkeypatch):
             continue
         oks_before = [x for x in lines[r] if "world" in x and x["t"] < t_bh]
         assert len(oks_before) >= 3, "no ops before the black hole"
-        detect, after = _check_survivor(lines[r], t_bh, stall_s + 2.0)
-        print(f"peer {r}: failed op {detect:.2f} s after the black hole (dropped: {dropped})")
+        # With a second peer dropped (a reused black connection) both may be admitted again by the survivor's next
+        # update_topology, so it need not run an op in a smaller ring: the ring growing back to 3 is checked below.
+        detect, after = _check_survivor(lines[r], t_bh, stall_s + 2.0, smaller_ring=len(dropped) == 1)
+        print(f"peer {r}: failed op {detect:.2f} s after the black hole (dropped: {dropped}, "
+              f"worlds after: {sorted(set(x['world'] for x in after))})")
         assert any(x["world"] == 3 for x in after), "the dropped peer did not rejoin"
 
 

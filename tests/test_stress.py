@@ -81,19 +81,24 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, 
             try:
                 p.wait(timeout=90)
             except subprocess.TimeoutExpired:
-                p.send_signal(signal.SIGUSR1)  # faulthandler: dump every thread's Python stack
+                # stacks of every peer still running (the one that does not stop may wait for another one)
+                alive = [q for q, _ in procs if q.poll() is None]
+                for q in alive:
+                    q.send_signal(signal.SIGUSR1)  # faulthandler: dump every thread's Python stack
                 time.sleep(1)
-                p.send_signal(signal.SIGUSR2)  # native backtraces of every thread (PCCL_DEBUG_BACKTRACE_SIGNAL)
-                time.sleep(1)
-                p.kill()
-                p.wait()
+                for q in alive:
+                    q.send_signal(signal.SIGUSR2)  # native backtraces of every thread (PCCL_DEBUG_BACKTRACE_SIGNAL)
+                time.sleep(2)
+                for q in alive:
+                    q.kill()
+                    q.wait()
                 dump = os.environ.get("PCCL_STRESS_DUMP_DIR")  # every peer's whole output, for the post-mortem
                 if dump:
                     os.makedirs(dump, exist_ok=True)
-                    for k, (_, o) in enumerate(procs):
+                    for k, (q, o) in enumerate(procs):
                         o.seek(0)
-                        with open(os.path.join(dump, f"peer{k}.out"), "w") as f:
-                            f.write(o.read())
+                        with open(os.path.join(dump, f"peer{k}{'_alive' if q in alive else ''}.out"), "w") as f:
+                            f.write(f"pid {q.pid}\n" + o.read())
                 out.seek(0)
                 raise AssertionError("peer did not stop:\n" + out.read()[-6000:])
     summaries = []
