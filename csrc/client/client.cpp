@@ -5,6 +5,7 @@
 #include <csignal>
 #include <cstring>
 #include <list>
+#include <sstream>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -566,6 +567,24 @@ void Client::liveness_loop() {
             if (master_.send(C2MHeartbeat{})) heartbeats_++;
             l.lock();
             next_hb = now + hb;
+        }
+        // PCCL_CLIENT_DUMP_SEC=N: log this peer's consensus-relevant state every N seconds (diagnosing stuck runs;
+        // the master's counterpart is PCCL_MASTER_DUMP_SEC)
+        static const size_t dump_every = env_size("PCCL_CLIENT_DUMP_SEC", 0);
+        if (dump_every && now - last_dump_ >= std::chrono::seconds(dump_every)) {
+            last_dump_ = now;
+            l.unlock();
+            std::ostringstream os;
+            os << "Client " << uuid_.str() << ": revision " << conn_revision_.load() << " pending-reestablish "
+               << static_cast<int64_t>(reestablish_pending_.load()) << " ops";
+            {
+                std::lock_guard ol(ops_mtx_);
+                for (const auto &[t, op] : ops_)
+                    os << " " << t << (op->done.load() ? (op->success ? ":ok" : ":failed") : ":running")
+                       << (op->joined.load() ? "/joined" : "") << "@" << op->revision_at_start;
+            }
+            LOG(WARN) << os.str();
+            l.lock();
         }
         // a master that has been silent for twice the peer timeout (it sends M2CHeartbeat every heartbeat interval)
         // is lost: closing the connection fails every wait on it instead of hanging the application

@@ -311,6 +311,7 @@ private:
     std::mutex live_mtx_;
     std::condition_variable live_cv_;
     bool live_stop_ = false;
+    std::chrono::steady_clock::time_point last_dump_{}; // PCCL_CLIENT_DUMP_SEC (liveness thread only)
     std::map<const OpState *, Watched> watched_;
     std::thread liveness_thread_;
     std::atomic<uint64_t> stall_reports_{0}, stall_fails_{0}, master_lost_{0}, heartbeats_{0};
