@@ -37,9 +37,8 @@ EventPool &event_pool() {
 
 
 bool Client::abort_received(uint64_t tag) {
-    auto p = master_.receive<M2CCollectiveCommsAbort>([tag](const M2CCollectiveCommsAbort &a) { return a.tag == tag; },
-                                                       0ms);
-    return p.has_value();
+    return master_.peek<M2CCollectiveCommsAbort>(
+        [tag](const M2CCollectiveCommsAbort &a) { return a.tag == tag && a.aborted; });
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -182,7 +181,7 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
     std::snprintf(range_name, sizeof(range_name), "pccl all_reduce tag %llu bytes %zu",
                   static_cast<unsigned long long>(tag), op->req.count * dtype_size(op->req.dtype));
     RoctxRange range(range_name);
-    bool success = false, abort_seen = false;
+    bool success = false;
     uint64_t seq = 0;
     bool commenced = false;
     uint8_t agreed = 0;
@@ -269,33 +268,26 @@ void Client::run_op(const std::shared_ptr<OpState> &op, bool on_caller) {
                 ring::current_watch() = nullptr;
             }
             success = r.first && !r.second;
-            abort_seen = r.second;
             if (success) last_framing_ = !tcp_ring ? 0 : (op->shape.reference ? 2 : 1);
             if (success) fault_point("op_end", seq); // this peer's part is done, the master has no verdict yet
         } else {
             LOG(WARN) << "all-reduce tag " << tag << ": no usable ring (peers lost)";
         }
     }
-    // completion protocol: exactly one Abort(tag) packet per op, then Complete(tag)
+    // completion protocol: exactly one Abort(tag) packet per op, then Complete(tag). The op's polls only peek at the
+    // abort (abort_received), so it is taken here whether or not they saw it: a poll that took it while the op went
+    // on to finish (a step's last sends completing after the poll) left this wait with nothing to receive.
     bool ok = false;
     if (commenced) {
         C2MCollectiveCommsComplete comp;
         comp.tag = tag;
         comp.was_aborted = !success;
         if (master_.send(comp)) {
-            bool aborted = abort_seen;
-            bool got_abort = abort_seen;
-            if (!got_abort) {
-                auto a = master_.receive<M2CCollectiveCommsAbort>(
-                    [tag](const M2CCollectiveCommsAbort &p) { return p.tag == tag; });
-                if (a) {
-                    got_abort = true;
-                    aborted = a->aborted;
-                }
-            }
+            auto a = master_.receive<M2CCollectiveCommsAbort>(
+                [tag](const M2CCollectiveCommsAbort &p) { return p.tag == tag; });
             auto c = master_.receive<M2CCollectiveCommsComplete>(
                 [tag](const M2CCollectiveCommsComplete &p) { return p.tag == tag; });
-            ok = got_abort && c.has_value() && !aborted && success;
+            ok = a.has_value() && c.has_value() && !a->aborted && success;
         }
     }
     if (!ok) {

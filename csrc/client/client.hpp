@@ -252,6 +252,8 @@ private:
     std::pair<bool, bool> ipc_reduce_segmented(OpState &op, const RingView &rv, uint64_t seq, int device,
                                                bool &use_ring);
     std::pair<bool, bool> hier_reduce(OpState &op, const RingView &rv, uint64_t seq, int device);
+    // Whether the master's abort of the running op `tag` has arrived. It only looks: the packet is consumed by the
+    // op's completion protocol (run_op), so a poll from any thread of the op can never take it from that wait.
     bool abort_received(uint64_t tag);
 
     // shared state

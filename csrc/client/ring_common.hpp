@@ -125,8 +125,9 @@ inline bool watch_failed() {
     return w != nullptr && w->failed.load(std::memory_order_acquire);
 }
 
-// Abort state of one op shared by all of its threads: the master's abort packet for a tag is consumed by the first
-// poll that sees it (Client::abort_received), so that poll records it here for every other thread of the op.
+// Abort state of one op shared by all of its threads: the first poll that sees the master's abort packet
+// (Client::abort_received, which leaves it queued for run_op's completion protocol) records it here, so the other
+// threads of the op stop scanning the master queue.
 class OpAbort {
 public:
     explicit OpAbort(std::function<bool()> poll) : poll_(std::move(poll)) {}

@@ -94,6 +94,13 @@ void MasterConnection::rx_loop() {
     LOG(DEBUG) << "Master connection RX loop ended";
 }
 
+bool MasterConnection::contains(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match) {
+    std::lock_guard lock(q_mtx_);
+    for (const auto &it : queue_)
+        if (match(it.id, it.payload)) return true;
+    return false;
+}
+
 bool MasterConnection::take(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match,
                             std::chrono::milliseconds timeout) {
     std::unique_lock lock(q_mtx_);

@@ -56,8 +56,19 @@ public:
         return result;
     }
 
+    // Whether a packet of type P (matching pred) is queued; it stays queued (its owner still receives it).
+    template<typename P>
+    bool peek(const std::function<bool(const P &)> &pred) {
+        return contains([&](uint16_t id, const std::vector<uint8_t> &payload) {
+            if (id != P::kId) return false;
+            auto p = proto::decode_payload<P>(payload.data(), payload.size());
+            return p && pred(*p);
+        });
+    }
+
 private:
     bool send_raw(uint16_t id, const std::vector<uint8_t> &payload);
+    bool contains(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match);
     bool take(const std::function<bool(uint16_t, const std::vector<uint8_t> &)> &match,
               std::chrono::milliseconds timeout);
     void rx_loop();

@@ -455,6 +455,30 @@ TEST(mc_timeout_and_poll) {
     c.join();
 }
 
+// An op's abort polls only look (Client::abort_received): the packet stays queued for its completion protocol, however
+// many threads of the op saw it first
+TEST(mc_peek_leaves_packet_queued) {
+    MasterSide ms;
+    net::MasterConnection c(loop_v4(ms.srv.port()));
+    EXPECT(c.connect() && ms.wait_client());
+    auto is_abort_of = [](uint64_t tag) {
+        return [tag](const proto::M2CCollectiveCommsAbort &a) { return a.tag == tag && a.aborted; };
+    };
+    EXPECT(!c.peek<proto::M2CCollectiveCommsAbort>(is_abort_of(7)));
+    proto::M2CCollectiveCommsAbort ab;
+    ab.tag = 7;
+    ab.aborted = true;
+    ms.send_later(ab);
+    EXPECT(eventually([&] { return c.peek<proto::M2CCollectiveCommsAbort>(is_abort_of(7)); }));
+    EXPECT(c.peek<proto::M2CCollectiveCommsAbort>(is_abort_of(7)));  // still there
+    EXPECT(!c.peek<proto::M2CCollectiveCommsAbort>(is_abort_of(8))); // another op's tag
+    auto a = c.receive<proto::M2CCollectiveCommsAbort>([](const auto &x) { return x.tag == 7; }, 0ms);
+    EXPECT(a && a->aborted);
+    EXPECT(!c.peek<proto::M2CCollectiveCommsAbort>(is_abort_of(7))); // taken by the receive
+    c.interrupt();
+    c.join();
+}
+
 TEST(mc_server_close_unblocks_receiver) {
     auto *ms = new MasterSide();
     net::MasterConnection c(loop_v4(ms->srv.port()));
