@@ -101,27 +101,31 @@ def _run_stress(tmp_path, duration, target, device="cpu", soak=False, env=None, 
                             f.write(f"pid {q.pid}\n" + o.read())
                 out.seek(0)
                 raise AssertionError("peer did not stop:\n" + out.read()[-6000:])
-    summaries = []
+    summaries, progress = [], 0
     for p, out in procs:
         out.seek(0)
         text = out.read()
         out.close()
+        lines = [json.loads(x) for x in text.splitlines() if x.startswith("{")]
+        progress += max([x["progress"] for x in lines if "progress" in x], default=0)
         if p.returncode == -signal.SIGKILL:
             continue
         assert p.returncode == 0, text[-3000:]
-        lines = [json.loads(x) for x in text.splitlines() if x.startswith("{")]
-        assert lines, text[-2000:]
-        summaries.append(lines[-1])
-    return killed, summaries
+        ends = [x for x in lines if "steps" in x or "kicked" in x]
+        assert ends, text[-2000:]
+        summaries.append(ends[-1])
+    print(f"[stress] {killed} hit, {len(procs)} spawned, progress {progress} peer-steps", flush=True)
+    return killed, summaries, progress
 
 
 def test_random_kill_respawn(tmp_path):
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "25"))
     soak = duration > 60
-    killed, summaries = _run_stress(tmp_path, duration, int(os.environ.get("PCCL_STRESS_PEERS", "4")), soak=soak)
+    killed, summaries, progress = _run_stress(tmp_path, duration, int(os.environ.get("PCCL_STRESS_PEERS", "4")),
+                                              soak=soak)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
-    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too
 
 
 def test_random_stop_kill_respawn(tmp_path, monkeypatch):
@@ -130,10 +134,30 @@ def test_random_stop_kill_respawn(tmp_path, monkeypatch):
     progress with exact results."""
     monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", "2000")
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
-    killed, summaries = _run_stress(tmp_path, duration, 4, soak=duration > 60, stop_p=0.5)
+    killed, summaries, progress = _run_stress(tmp_path, duration, 4, soak=duration > 60, stop_p=0.5)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
-    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too
+
+
+HOSTDEV = os.environ.get("PCCL_TEST_HOSTDEV") or os.path.join(os.path.dirname(HERE), "pccl_amd", "lib",
+                                                              "libpccl_hostdev.so")
+
+
+def test_random_stop_kill_respawn_emulated_device(tmp_path, monkeypatch):
+    """The hung / killed peer churn on the device rings, on the CPU: the host-emulated device backend (every pointer is
+    device memory, streams are worker threads) runs the small-message path for the 16-96 KiB tensors and the staged
+    pipeline for a 4 MiB one, with their abort polls - the code a GPU soak hung in when a poll took the master's abort
+    packet and the op still finished (docs/ROUND6_RESPONSE.md)."""
+    if not os.path.exists(HOSTDEV) or os.environ.get("PCCL_DISABLE_HIP") == "1":
+        pytest.skip("libpccl_hostdev.so not built, or device plugins disabled (PCCL_DISABLE_HIP)")
+    monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", "2000")
+    duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
+    env = {"PCCL_HIP_PLUGIN": HOSTDEV, "PCCL_HOSTDEV_ALL_DEVICE": "1", "PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "4"}
+    killed, summaries, progress = _run_stress(tmp_path, duration, 4, soak=duration > 60, env=env, stop_p=0.5)
+    assert killed >= 3
+    assert summaries and all(s["bad"] == 0 for s in summaries), summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too
 
 
 @pytest.mark.gpu
@@ -141,10 +165,10 @@ def test_random_kill_respawn_gpu_ipc(tmp_path, hip):
     """Device tensors on cuda:0: the peers reduce over the xGMI/IPC path, so SIGKILLs land during IPC votes and
     kernels; no wrong result, survivors progress, everyone alive at the end exits cleanly."""
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
-    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60)
+    killed, summaries, progress = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
-    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too
 
 
 @pytest.mark.gpu
@@ -153,11 +177,11 @@ def test_random_kill_respawn_gpu_ring(tmp_path, hip):
     tensor per step next to the small ones, so kills land mid-pipeline (staging copies, fused reduce kernels and
     send-ahead stripes in flight): no wrong result, survivors progress, everyone alive at the end exits cleanly."""
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
-    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60,
+    killed, summaries, progress = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60,
                                     env={"PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "64"})
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
-    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too
 
 
 @pytest.mark.gpu
@@ -169,7 +193,8 @@ def test_random_stop_kill_respawn_gpu(tmp_path, hip, monkeypatch, path):
     monkeypatch.setenv("PCCL_PEER_TIMEOUT_MS", "2000")
     duration = float(os.environ.get("PCCL_STRESS_SECONDS", "30"))
     env = {"PCCL_DISABLE_IPC": "1", "STRESS_BIG_MIB": "64"} if path == "ring" else None
-    killed, summaries = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60, env=env, stop_p=0.5)
+    killed, summaries, progress = _run_stress(tmp_path, duration, 4, device="cuda:0", soak=duration > 60, env=env,
+                                              stop_p=0.5)
     assert killed >= 3
     assert summaries and all(s["bad"] == 0 for s in summaries), summaries
-    assert sum(s["ok_ops"] for s in summaries) > 10, summaries
+    assert progress > 10, (progress, summaries)  # successful steps of every peer of the run, the killed ones too

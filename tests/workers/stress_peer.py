@@ -3,7 +3,8 @@
 Loop: admit pending peers (after joining the background reduce of the previous step) -> sync shared state when the
 topology changed -> launch this step's multi-tensor all-reduce in a background thread (it overlaps the next step's
 "compute") -> join the previous step's reduce. Values are all ones, so every successful op must equal the world size
-it ran with. Runs until <stop_file> exists, then leaves. Prints one JSON summary line.
+it ran with. Runs until <stop_file> exists, then leaves. Prints {"progress": n} after each successful step and one JSON
+summary line at the end.
 """
 import json
 import os
@@ -46,6 +47,7 @@ def main():
         res = all_reduce_multiple_with_retry(comm, tensors, pccl.ReduceOp.SUM, max_in_flight=4, tag_base=tag_base)
         if res.ok:
             ok_ops += 1
+            print(json.dumps({"progress": ok_ops}), flush=True)  # the run's progress counts peers killed later too
             for t in tensors:
                 if not torch.all(t == float(res.world_size)) and not torch.all(t == t[0]):
                     bad += 1
